@@ -1,0 +1,157 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.
+
+ctypes front-ends for the two CPU checkers under oracle/:
+
+* ``RefOracle``  — oracle/_ref/libdgref.so: the reference's own native/native.c
+  compiled unmodified + ref_harness.c (the ground truth; see oracle/Makefile).
+* ``PortOracle`` — oracle/_build/libj2t_oracle.so: our plain-C restatement of
+  the j2t path (oracle/j2t_oracle.c), pinned against RefOracle and the golden
+  fixtures in tests/golden/.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may use
+this module, and only as the checker / reported baseline — never as the thing
+measured or shipped.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _cpu_has_avx2() -> bool:
+    try:
+        with open("/proc/cpuinfo") as fh:
+            return " avx2" in fh.read()
+    except OSError:
+        return False
+
+
+class _Base:
+    def __init__(self, lib: C.CDLL, prefix: str):
+        self.lib = lib
+        self.p = prefix
+        f = getattr(lib, prefix + "desc_create")
+        f.restype = C.c_void_p
+        f.argtypes = [C.c_char_p, C.c_size_t]
+        g = getattr(lib, prefix + "desc_destroy")
+        g.argtypes = [C.c_void_p]
+        j = getattr(lib, prefix + "j2t")
+        j.restype = C.c_uint64
+        j.argtypes = [C.c_void_p, C.c_uint32, C.c_char_p, C.c_size_t, C.c_uint64,
+                      C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]
+        b = getattr(lib, prefix + "j2t_batch")
+        b.restype = C.c_int
+        b.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64,
+                      C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+        self._descs = {}
+
+    def _desc(self, blob: bytes):
+        h = self._descs.get(blob)
+        if h is None:
+            h = getattr(self.lib, self.p + "desc_create")(blob, len(blob))
+            if not h:
+                raise ValueError("bad descriptor blob")
+            self._descs[blob] = h
+        return h
+
+    def j2t(self, flat, json: bytes, flags: int, root: Optional[int] = None) -> Tuple[int, bytes]:
+        """One message -> (packed ret, thrift bytes); bytes are b"" on error."""
+        d = self._desc(flat.blob)
+        root = flat.root_type if root is None else root
+        cap = 16 * len(json) + 65536
+        out = C.create_string_buffer(cap)
+        ol = C.c_size_t(0)
+        ret = getattr(self.lib, self.p + "j2t")(d, root, json, len(json), flags, out, cap, C.byref(ol))
+        if ret != 0:
+            return int(ret), b""
+        if ol.value > cap:
+            raise RuntimeError("oracle output exceeded harness capacity")
+        return 0, out.raw[:ol.value]
+
+    def j2t_batch(self, flat, msgs: Sequence[bytes], flags: int, nthreads: int = 1,
+                  root: Optional[int] = None, slot_factor: int = 4, slot_pad: int = 64):
+        """Batch API over an arena: returns (rets u64[n], outs list[bytes])."""
+        arena, in_off = pack_arena(msgs)
+        return self.j2t_arena(flat, arena, in_off, flags, nthreads, root, slot_factor, slot_pad)
+
+    def j2t_arena(self, flat, arena: np.ndarray, in_off: np.ndarray, flags: int, nthreads: int = 1,
+                  root: Optional[int] = None, slot_factor: int = 4, slot_pad: int = 64,
+                  decode: bool = True):
+        n = len(in_off) - 1
+        lens = np.diff(in_off)
+        out_off = np.zeros(n + 1, dtype=np.uint64)
+        np.cumsum(lens * slot_factor + slot_pad, out=out_off[1:])
+        out = np.zeros(int(out_off[-1]) + 64, dtype=np.uint8)
+        out_len = np.zeros(n, dtype=np.uint32)
+        rets = np.zeros(n, dtype=np.uint64)
+        d = self._desc(flat.blob)
+        root = flat.root_type if root is None else root
+        getattr(self.lib, self.p + "j2t_batch")(
+            d, root, arena.ctypes.data, in_off.ctypes.data, n, flags, out.ctypes.data,
+            out_off.ctypes.data, out_len.ctypes.data, rets.ctypes.data, nthreads)
+        if not decode:
+            return rets, (out, out_off, out_len)
+        outs = []
+        for i in range(n):
+            if rets[i] != 0:
+                outs.append(b"")
+            else:
+                o = int(out_off[i])
+                outs.append(out[o:o + int(out_len[i])].tobytes())
+        return rets, outs
+
+
+def pack_arena(msgs: Sequence[bytes]) -> Tuple[np.ndarray, np.ndarray]:
+    lens = np.fromiter((len(m) for m in msgs), dtype=np.uint64, count=len(msgs))
+    in_off = np.zeros(len(msgs) + 1, dtype=np.uint64)
+    np.cumsum(lens, out=in_off[1:])
+    arena = np.frombuffer(b"".join(msgs) + b"\0" * 64, dtype=np.uint8).copy()
+    return arena, in_off
+
+
+_ref_singleton = None
+_port_singleton = None
+
+
+def ref_lib_path() -> Optional[str]:
+    cand = ["libdgref.so", "libdgref_sse.so"] if _cpu_has_avx2() else ["libdgref_sse.so"]
+    for c in cand:
+        p = os.path.join(HERE, "_ref", c)
+        if os.path.exists(p):
+            return p
+    return None
+
+
+def RefOracle() -> Optional[_Base]:
+    """The reference's own C engine, or None if oracle/_ref was not built."""
+    global _ref_singleton
+    if _ref_singleton is None:
+        p = ref_lib_path()
+        if p is None:
+            return None
+        _ref_singleton = _Base(C.CDLL(p), "dgref_")
+    return _ref_singleton
+
+
+def PortOracle() -> _Base:
+    """Our plain-C restatement (oracle/j2t_oracle.c)."""
+    global _port_singleton
+    if _port_singleton is None:
+        p = os.path.join(HERE, "_build", "libj2t_oracle.so")
+        if not os.path.exists(p):
+            raise FileNotFoundError(f"{p} missing: run `make -C oracle oracle`")
+        _port_singleton = _Base(C.CDLL(p), "dgo_")
+    return _port_singleton
+
+
+def unpack_ret(ret: int) -> Tuple[int, int, int]:
+    """(code, pos, value) exactly as conv/j2t/impl_amd64.go:250-259 decode it."""
+    code = ret & 0xFF
+    pos = (ret >> 8) & 0xFFFFFFFF
+    val = ret >> 40
+    return code, pos, val

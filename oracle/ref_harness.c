@@ -1,0 +1,424 @@
+/*
+ * ORACLE — TEST INFRASTRUCTURE ONLY. Never linked into the product.
+ *
+ * ref_harness.c: drives the REFERENCE's own C engine, compiled unmodified from
+ * where it lies (/root/reference/native/native.c, one translation unit of
+ * #includes, reference native/native.c:17-29), behind a tiny C ABI so tests
+ * and bench.py's cpu_baseline can call it through ctypes.
+ *
+ * The harness does only what the reference's Go layer does around the FSM:
+ *  - rebuild the reference's descriptor structs (native/thrift.h:70-137) from a
+ *    dg_desc v1 blob (include/dgj2t_desc.h): tTypeDesc/tStructDesc/tFieldDesc,
+ *    a FieldIdMap indexed by id, a RequiresBitmap by id sized like
+ *    thrift/utils.go:30-91, and a TrieTree with no positions whose root leaves
+ *    hold every (key, field) pair (trie_get native/map.c:86-132 then does a
+ *    linear scan: result-equivalent to the Go-built trie);
+ *  - emulate BinaryConv.do (conv/j2t/impl.go:38-91): empty body -> STOP byte,
+ *    unquoted STRING root -> json.EncodeString via the reference quote();
+ *  - emulate doNative + handleError's OOM re-entry (conv/j2t/impl_amd64.go:
+ *    40-69,169-247): grow the buffer / caches and call j2t_fsm_exec again;
+ *  - emulate the Do epilogue (conv/j2t/conv.go:70-77): output dropped on error.
+ * Inputs are copied into a buffer with a NUL byte after the last byte so the
+ * reference's reads of src[len] (e.g. check_leading_zero, native/scanning.c:
+ * 781-786) are deterministic; the GPU path defines src[len] == 0 the same way.
+ */
+#include "native.c"
+
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/dgj2t_desc.h"
+
+typedef struct {
+    tTypeDesc *types;
+    tStructDesc *structs;
+    tFieldDesc *fields;
+    tFieldDesc ***idbufs;
+    uint64_t **reqbufs;
+    TrieTree *tries;
+    GoSlice *leaves;
+    Pair **pairs;
+    tDefaultValue *dflts;
+    uint32_t n_types, n_structs, n_fields;
+    uint8_t *blob;
+} RefDesc;
+
+static const char *NAME_BINARY = "binary";
+static const char *NAME_OTHER = "other\0\0\0";
+
+void *dgref_desc_create(const uint8_t *blob_in, size_t len)
+{
+    const dg_desc_hdr *h = (const dg_desc_hdr *)blob_in;
+    if (len < sizeof(dg_desc_hdr) || h->magic != DG_DESC_MAGIC || h->total_len > len)
+        return NULL;
+    RefDesc *d = (RefDesc *)calloc(1, sizeof(RefDesc));
+    d->blob = (uint8_t *)malloc(len);
+    memcpy(d->blob, blob_in, len);
+    const uint8_t *b = d->blob;
+    const dg_type *T = (const dg_type *)(b + h->off_types);
+    const dg_struct *S = (const dg_struct *)(b + h->off_structs);
+    const dg_field *F = (const dg_field *)(b + h->off_fields);
+    const dg_name *N = (const dg_name *)(b + h->off_names);
+    const uint64_t *R = (const uint64_t *)(b + h->off_reqwords);
+    const char *P = (const char *)(b + h->off_pool);
+    d->n_types = h->n_types;
+    d->n_structs = h->n_structs;
+    d->n_fields = h->n_fields;
+    d->types = (tTypeDesc *)calloc(h->n_types + 1, sizeof(tTypeDesc));
+    d->structs = (tStructDesc *)calloc(h->n_structs + 1, sizeof(tStructDesc));
+    d->fields = (tFieldDesc *)calloc(h->n_fields + 1, sizeof(tFieldDesc));
+    d->dflts = (tDefaultValue *)calloc(h->n_fields + 1, sizeof(tDefaultValue));
+    d->idbufs = (tFieldDesc ***)calloc(h->n_structs + 1, sizeof(void *));
+    d->reqbufs = (uint64_t **)calloc(h->n_structs + 1, sizeof(void *));
+    d->tries = (TrieTree *)calloc(h->n_structs + 1, sizeof(TrieTree));
+    d->leaves = (GoSlice *)calloc(h->n_structs + 1, sizeof(GoSlice));
+    d->pairs = (Pair **)calloc(h->n_structs + 1, sizeof(void *));
+
+    for (uint32_t i = 0; i < h->n_types; i++) {
+        tTypeDesc *t = &d->types[i];
+        t->type = T[i].ttype;
+        if (T[i].flags & DG_TF_BINARY) {
+            t->name.buf = NAME_BINARY;
+            t->name.len = 6;
+        } else {
+            t->name.buf = NAME_OTHER;
+            t->name.len = 5;
+        }
+        t->key = T[i].key == DG_NONE ? NULL : &d->types[T[i].key];
+        t->elem = T[i].elem == DG_NONE ? NULL : &d->types[T[i].elem];
+        t->st = T[i].st == DG_NONE ? NULL : &d->structs[T[i].st];
+    }
+    for (uint32_t i = 0; i < h->n_fields; i++) {
+        tFieldDesc *f = &d->fields[i];
+        f->is_request_base = (F[i].flags & DG_FF_REQUEST_BASE) != 0;
+        f->required = F[i].required;
+        f->vm = F[i].vm;
+        f->ID = F[i].id;
+        f->type = &d->types[F[i].type];
+        if (F[i].dflt_len != DG_NONE) {
+            d->dflts[i].thrift_binary.buf = P + F[i].dflt_off;
+            d->dflts[i].thrift_binary.len = F[i].dflt_len;
+            f->default_value = &d->dflts[i];
+        }
+        /* only len != 0 is read (native/thrift.c:725) */
+        f->http_mappings.len = (F[i].flags & DG_FF_HTTP_MAPPING) ? 1 : 0;
+    }
+    for (uint32_t s = 0; s < h->n_structs; s++) {
+        tStructDesc *st = &d->structs[s];
+        const dg_struct *ds = &S[s];
+        uint32_t maxid = 0;
+        for (uint32_t k = 0; k < ds->n_fields; k++)
+            if (F[ds->field_begin + k].id > maxid)
+                maxid = F[ds->field_begin + k].id;
+        /* FieldIDMap: indexed by id */
+        size_t idlen = ds->n_fields ? (size_t)maxid + 1 : 0;
+        d->idbufs[s] = (tFieldDesc **)calloc(idlen + 1, sizeof(void *));
+        for (uint32_t k = 0; k < ds->n_fields; k++)
+            d->idbufs[s][F[ds->field_begin + k].id] = &d->fields[ds->field_begin + k];
+        st->ids.buf = d->idbufs[s];
+        st->ids.len = idlen;
+        st->ids.cap = idlen;
+        /* RequiresBitmap by id: len = max(len(st.Fields), maxid/64+1) words
+         * (thrift/idl.go:679 + RequiresBitmap.Set malloc, thrift/utils.go:46-63) */
+        size_t words = ds->n_fields;
+        if (ds->n_fields && (size_t)maxid / 64 + 1 > words)
+            words = (size_t)maxid / 64 + 1;
+        d->reqbufs[s] = (uint64_t *)calloc(words + 1, sizeof(uint64_t));
+        for (uint32_t k = 0; k < ds->n_fields; k++) {
+            uint64_t w = R[ds->req_begin + k / 64];
+            if ((w >> (k % 64)) & 1) {
+                uint16_t id = F[ds->field_begin + k].id;
+                d->reqbufs[s][id / 64] |= 1ull << (id % 64);
+            }
+        }
+        st->reqs.buf = d->reqbufs[s];
+        st->reqs.len = words;
+        st->hms.len = (ds->flags & DG_SF_HTTP_MAPPING) ? 1 : 0;
+        /* names: trie with zero positions, all pairs in root leaves */
+        uint32_t npairs = 0;
+        for (uint32_t j = 0; j <= ds->name_mask; j++)
+            if (N[ds->name_begin + j].field != DG_NONE)
+                npairs++;
+        d->pairs[s] = (Pair *)calloc(npairs + 1, sizeof(Pair));
+        uint32_t q = 0;
+        TrieTree *tr = &d->tries[s];
+        for (uint32_t j = 0; j <= ds->name_mask; j++) {
+            const dg_name *nm = &N[ds->name_begin + j];
+            if (nm->field == DG_NONE)
+                continue;
+            d->pairs[s][q].val = &d->fields[nm->field];
+            d->pairs[s][q].key.buf = P + nm->key_off;
+            d->pairs[s][q].key.len = nm->key_len;
+            if (nm->key_len == 0)
+                tr->empty = &d->fields[nm->field];
+            q++;
+        }
+        d->leaves[s].buf = (char *)d->pairs[s];
+        d->leaves[s].len = npairs;
+        d->leaves[s].cap = npairs;
+        tr->count = npairs;
+        tr->node.leaves = &d->leaves[s];
+        st->names.trie = npairs ? tr : NULL;
+        st->names.hash = NULL;
+    }
+    return d;
+}
+
+void dgref_desc_destroy(void *p)
+{
+    RefDesc *d = (RefDesc *)p;
+    if (!d)
+        return;
+    for (uint32_t s = 0; s < d->n_structs; s++) {
+        free(d->idbufs[s]);
+        free(d->reqbufs[s]);
+        free(d->pairs[s]);
+    }
+    free(d->types);
+    free(d->structs);
+    free(d->fields);
+    free(d->dflts);
+    free(d->idbufs);
+    free(d->reqbufs);
+    free(d->tries);
+    free(d->leaves);
+    free(d->pairs);
+    free(d->blob);
+    free(d);
+}
+
+/* pooled per-thread machine state (internal/types/types.go:313-338) */
+typedef struct {
+    J2TStateMachine *fsm;
+    char *reqs, *keys, *dbuf;
+    int32_t *fields;
+    size_t reqs_cap, keys_cap, fields_cap;
+    char *buf;
+    size_t buf_cap;
+    char *src;
+    size_t src_cap;
+} RefCtx;
+
+static RefCtx *ctx_new(void)
+{
+    RefCtx *c = (RefCtx *)calloc(1, sizeof(RefCtx));
+    c->fsm = (J2TStateMachine *)calloc(1, sizeof(J2TStateMachine));
+    c->reqs_cap = 1 << 20; /* generous: the OOM re-entry path is exercised only by the reference's own MockConv tests */
+    c->keys_cap = 1024;
+    c->fields_cap = 4096;
+    c->reqs = (char *)malloc(c->reqs_cap);
+    c->keys = (char *)malloc(c->keys_cap);
+    c->fields = (int32_t *)malloc(c->fields_cap * sizeof(int32_t));
+    c->dbuf = (char *)malloc(800);
+    return c;
+}
+
+static void ctx_free(RefCtx *c)
+{
+    free(c->fsm);
+    free(c->reqs);
+    free(c->keys);
+    free(c->fields);
+    free(c->dbuf);
+    free(c->buf);
+    free(c->src);
+    free(c);
+}
+
+static void ensure(char **p, size_t *cap, size_t need)
+{
+    if (*cap < need) {
+        free(*p);
+        *cap = need;
+        *p = (char *)malloc(need);
+    }
+}
+
+/* One BinaryConv.Do. Returns the packed reference ret; *out_len = bytes. */
+static uint64_t ref_do(RefCtx *c, RefDesc *d, uint32_t root, const uint8_t *json, size_t n,
+                       uint64_t flags, uint8_t *out, size_t out_cap, size_t *out_len)
+{
+    *out_len = 0;
+    const tTypeDesc *desc = &d->types[root];
+    if (n == 0) { /* conv/j2t/impl.go:52-82 */
+        if (out_cap >= 1)
+            out[0] = 0;
+        *out_len = 1;
+        return 0;
+    }
+    /* src copy with a NUL sentinel (and quoting for an unquoted STRING root) */
+    size_t slen;
+    if (desc->type == TTYPE_STRING && json[0] != '"') { /* conv/j2t/impl.go:85-88 */
+        ensure(&c->src, &c->src_cap, n * 8 + 16);
+        ssize_t dn = n * 8;
+        c->src[0] = '"';
+        quote((const char *)json, n, c->src + 1, &dn, 0);
+        c->src[1 + dn] = '"';
+        slen = dn + 2;
+    } else {
+        ensure(&c->src, &c->src_cap, n + 16);
+        memcpy(c->src, json, n);
+        slen = n;
+    }
+    memset(c->src + slen, 0, 8);
+
+    size_t want = slen * 16 + 65536;
+    ensure(&c->buf, &c->buf_cap, want);
+    GoSlice buf = {c->buf, 0, c->buf_cap - 64 /* b64decode may write past cap */};
+    GoString src = {c->src, slen};
+
+    J2TStateMachine *fsm = c->fsm;
+    fsm->sp = 1;
+    fsm->vt[0].st = 0;
+    fsm->vt[0].jp = 0;
+    fsm->vt[0].td = desc;
+    fsm->reqs_cache.buf = c->reqs;
+    fsm->reqs_cache.len = 0;
+    fsm->reqs_cache.cap = c->reqs_cap;
+    fsm->key_cache.buf = c->keys;
+    fsm->key_cache.len = 0;
+    fsm->key_cache.cap = c->keys_cap;
+    fsm->field_cache.buf = c->fields;
+    fsm->field_cache.len = 0;
+    fsm->field_cache.cap = c->fields_cap;
+    fsm->jt.dbuf = c->dbuf;
+    fsm->jt.dcap = 800;
+
+    uint64_t ret;
+    for (;;) {
+        ret = j2t_fsm_exec(fsm, &buf, &src, flags);
+        if (ret == 0)
+            break;
+        uint8_t e = ret & 0xff;
+        size_t p = ret >> 8; /* handleError: int(ret >> ERR_WRAP_SHIFT_CODE) */
+        if (e == ERR_OOM_BUF) {
+            size_t nc = buf.cap + (buf.cap >> 1);
+            if (nc < buf.cap + p)
+                nc = buf.cap + p * 2;
+            char *nb = (char *)malloc(nc + 64);
+            memcpy(nb, buf.buf, buf.len);
+            free(c->buf);
+            c->buf = nb;
+            c->buf_cap = nc + 64;
+            buf.buf = nb;
+            buf.cap = nc;
+            continue;
+        }
+        if (e == ERR_OOM_BM || e == ERR_OOM_KEY) {
+            /* GrowReqCache / GrowKeyCache: a bigger cache; reqs copies live
+             * in the old cache are referenced by pointer from the stack, so
+             * keep the old block alive (leaked until ctx_free of next call) */
+            GoSlice *cs = e == ERR_OOM_BM ? &fsm->reqs_cache : &fsm->key_cache;
+            size_t nc = cs->cap * 2 + p;
+            char *nb = (char *)malloc(nc);
+            memcpy(nb, cs->buf, cs->len);
+            /* bitmaps on the stack point into the old cache: rebase them */
+            if (e == ERR_OOM_BM) {
+                for (size_t i = 0; i < fsm->sp; i++) {
+                    J2TState *v = &fsm->vt[i];
+                    if (v->td && v->td->type == TTYPE_STRUCT &&
+                        (J2T_ST(v->st) == J2T_OBJ || J2T_ST(v->st) == J2T_OBJ_0) &&
+                        (char *)v->ex.es.reqs.buf >= cs->buf &&
+                        (char *)v->ex.es.reqs.buf < cs->buf + cs->cap)
+                        v->ex.es.reqs.buf = (uint64_t *)(nb + ((char *)v->ex.es.reqs.buf - cs->buf));
+                }
+                free(c->reqs);
+                c->reqs = nb;
+                c->reqs_cap = nc;
+            } else {
+                free(c->keys);
+                c->keys = nb;
+                c->keys_cap = nc;
+            }
+            cs->buf = nb;
+            cs->cap = nc;
+            continue;
+        }
+        if (e == ERR_OOM_FIELD) {
+            size_t nc = fsm->field_cache.cap + 4096;
+            int32_t *nb = (int32_t *)malloc(nc * sizeof(int32_t));
+            memcpy(nb, fsm->field_cache.buf, fsm->field_cache.len * sizeof(int32_t));
+            free(c->fields);
+            c->fields = nb;
+            c->fields_cap = nc;
+            fsm->field_cache.buf = nb;
+            fsm->field_cache.cap = nc;
+            fsm->vt[fsm->sp - 1].jp = p; /* SetPos */
+            continue;
+        }
+        break; /* real error or host callback (ERR_HM/HM_END/VM_END) */
+    }
+    if (ret != 0)
+        return ret;
+    *out_len = buf.len;
+    if (buf.len <= out_cap)
+        memcpy(out, buf.buf, buf.len);
+    return 0;
+}
+
+static RefCtx *g_ctx;
+
+uint64_t dgref_j2t(void *desc, uint32_t root, const uint8_t *json, size_t n, uint64_t flags,
+                   uint8_t *out, size_t out_cap, size_t *out_len)
+{
+    if (!g_ctx)
+        g_ctx = ctx_new();
+    return ref_do(g_ctx, (RefDesc *)desc, root, json, n, flags, out, out_cap, out_len);
+}
+
+/* ---- batched, multi-threaded driver for the CPU baseline ---- */
+typedef struct {
+    RefDesc *d;
+    uint32_t root;
+    const uint8_t *json;
+    const uint64_t *in_off;
+    uint64_t lo, hi, flags;
+    uint8_t *out;
+    const uint64_t *out_off;
+    uint32_t *out_len;
+    uint64_t *ret;
+} Job;
+
+static void *run_job(void *arg)
+{
+    Job *j = (Job *)arg;
+    RefCtx *c = ctx_new();
+    for (uint64_t i = j->lo; i < j->hi; i++) {
+        size_t ol = 0;
+        uint64_t cap = j->out_off[i + 1] - j->out_off[i];
+        j->ret[i] = ref_do(c, j->d, j->root, j->json + j->in_off[i], j->in_off[i + 1] - j->in_off[i],
+                           j->flags, j->out + j->out_off[i], cap, &ol);
+        j->out_len[i] = (uint32_t)ol;
+    }
+    ctx_free(c);
+    return NULL;
+}
+
+/* Messages [0, n) split into nthreads contiguous byte-balanced shards. */
+int dgref_j2t_batch(void *desc, uint32_t root, const uint8_t *json, const uint64_t *in_off,
+                    uint64_t n, uint64_t flags, uint8_t *out, const uint64_t *out_off,
+                    uint32_t *out_len, uint64_t *ret, int nthreads)
+{
+    if (nthreads < 1)
+        nthreads = 1;
+    Job *jobs = (Job *)calloc(nthreads, sizeof(Job));
+    pthread_t *th = (pthread_t *)calloc(nthreads, sizeof(pthread_t));
+    uint64_t total = in_off[n] - in_off[0];
+    uint64_t lo = 0;
+    for (int t = 0; t < nthreads; t++) {
+        uint64_t target = in_off[0] + total * (uint64_t)(t + 1) / nthreads;
+        uint64_t hi = lo;
+        while (hi < n && (t == nthreads - 1 || in_off[hi] < target))
+            hi++;
+        jobs[t] = (Job){(RefDesc *)desc, root, json, in_off, lo, hi, flags, out, out_off, out_len, ret};
+        lo = hi;
+    }
+    for (int t = 0; t < nthreads; t++)
+        pthread_create(&th[t], NULL, run_job, &jobs[t]);
+    for (int t = 0; t < nthreads; t++)
+        pthread_join(th[t], NULL);
+    free(jobs);
+    free(th);
+    return 0;
+}
