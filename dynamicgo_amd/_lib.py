@@ -1,0 +1,62 @@
+"""ctypes binding of the C ABI (include/dgj2t.h) exported by libdgj2t.so.
+
+The product path has no CPU fallback: if the HIP library is missing or fails
+to load, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libdgj2t.so")
+
+# symbols include/dgj2t.h declares (checked by tests/test_abi.py)
+EXPORTS = ["dg_last_error", "dg_ctx_create", "dg_ctx_destroy", "dg_ctx_stream", "dg_desc_create",
+           "dg_desc_create_device", "dg_desc_destroy", "dg_desc_root", "dg_j2t_batch_device",
+           "dg_slot_bound", "dg_j2t_batch_host", "dg_j2t_do", "dg_bench_device"]
+
+_lib = None
+
+
+class DGError(RuntimeError):
+    pass
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise DGError(f"{LIB_PATH} missing: the HIP transcoder is not built "
+                      "(run __graft_entry__.build() or python -m dynamicgo_amd.build)")
+    L = C.CDLL(LIB_PATH)
+    vp, u32, u64, sz, i32 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_size_t, C.c_int
+    P64 = C.POINTER(C.c_uint64)
+    sig = {
+        "dg_last_error": (C.c_char_p, []),
+        "dg_ctx_create": (i32, [i32, C.POINTER(vp)]),
+        "dg_ctx_destroy": (None, [vp]),
+        "dg_ctx_stream": (vp, [vp]),
+        "dg_desc_create": (i32, [vp, C.c_char_p, sz, C.POINTER(vp)]),
+        "dg_desc_create_device": (i32, [vp, vp, sz, C.POINTER(vp)]),
+        "dg_desc_destroy": (None, [vp]),
+        "dg_desc_root": (u32, [vp]),
+        "dg_j2t_batch_device": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, vp, vp, vp, vp, vp]),
+        "dg_slot_bound": (u64, [u64]),
+        "dg_j2t_batch_host": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, u64, vp, vp, P64]),
+        "dg_j2t_do": (i32, [vp, vp, u32, C.c_char_p, sz, u64, vp, sz, C.POINTER(sz), P64]),
+        "dg_bench_device": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, vp, vp, vp, i32, C.POINTER(C.c_float)]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def check(rc: int):
+    if rc != 0:
+        msg = lib().dg_last_error()
+        raise DGError(f"dgj2t error {rc}: {msg.decode() if msg else ''}")

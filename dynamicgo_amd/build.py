@@ -1,0 +1,50 @@
+"""Build the in-tree native artefacts.
+
+  dynamicgo_amd/libdgj2t.so        HIP kernels + C ABI for gfx950 (the product)
+  oracle/_build/libj2t_oracle.so   plain-C restatement (test infrastructure)
+  oracle/_ref/libdgref*.so         the reference's own native/*.c (test
+                                   infrastructure; only when /root/reference exists)
+
+Usage: python -m dynamicgo_amd.build [--no-oracle]
+"""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "dynamicgo_amd", "csrc")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("DG_OFFLOAD_ARCH", "gfx950")
+
+
+def _run(cmd, cwd=None):
+    print("+", " ".join(cmd), flush=True)
+    subprocess.run(cmd, cwd=cwd, check=True)
+
+
+def build_hip(force=False):
+    out = os.path.join(ROOT, "dynamicgo_amd", "libdgj2t.so")
+    srcs = [os.path.join(CSRC, f) for f in ("j2t_kernel.hip", "j2t_device.h", "dg_tables.h")]
+    srcs += [os.path.join(ROOT, "include", f) for f in ("dgj2t.h", "dgj2t_desc.h")]
+    if not force and os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(s) for s in srcs):
+        return out
+    _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+          "-ffp-contract=off", "-Wno-unused-result", "-o", out, os.path.join(CSRC, "j2t_kernel.hip")])
+    return out
+
+
+def build_oracle():
+    _run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "oracle"])
+    if os.path.isdir("/root/reference/native"):
+        _run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "ref"])
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    build_hip(force="--force" in argv)
+    if "--no-oracle" not in argv:
+        build_oracle()
+
+
+if __name__ == "__main__":
+    main()

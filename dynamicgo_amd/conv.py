@@ -1,0 +1,276 @@
+"""Host-side mirror of conv/j2t's API over the HIP transcoder.
+
+Reference surface (Go):
+  conv.Options                      conv/api.go:52-121
+  j2t.NewBinaryConv(opts)           conv/j2t/conv.go:36
+  (*BinaryConv).Do(ctx, desc, json) conv/j2t/conv.go:53-77
+  (*BinaryConv).DoInto(...)         conv/j2t/conv.go:81-96
+  toFlags(opts)                     conv/j2t/conv.go:98-127
+  explainNativeError(ret, in)       conv/j2t/impl_amd64.go:261-298
+
+Additions for the batched device path: ``BinaryConv.do_batch`` (host arenas)
+and ``BinaryConv.do_device`` (arenas already resident in HBM, torch tensors).
+Every call runs the HIP kernels in libdgj2t.so; there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+from .thrift import FlatDescriptor, TypeDescriptor, flatten, TYPE_NAMES
+
+# flag bits (native/thrift.h:23-32, internal/types/types.go:81-92)
+F_ALLOW_UNKNOWN = 1
+F_WRITE_DEFAULT = 1 << 1
+F_VALUE_MAPPING = 1 << 2
+F_HTTP_MAPPING = 1 << 3
+F_STRING_INT = 1 << 4
+F_WRITE_REQUIRE = 1 << 5
+F_NO_BASE64 = 1 << 6
+F_WRITE_OPTIONAL = 1 << 7
+F_TRACE_BACK = 1 << 8
+F_NO_WRITE_BASE = 1 << 9
+F_VALIDATE_UTF8 = 1 << 16  # extension, off by default
+
+DG_ST_OUT_OVERFLOW = 0xF0
+DG_ST_DEEP = 0xF1
+
+# internal/types/types.go:107-131 ParsingError messages
+_ERR_MSG = {0: "ok", 1: "eof", 2: "invalid char", 3: "invalid escape char", 4: "invalid unicode escape",
+            5: "integer overflow", 6: "invalid number format", 7: "recursion exceeded max depth",
+            8: "float number is infinity", 9: "dismatched type", 10: "required field is not set",
+            11: "unsupported type", 12: "unknown field", 13: "dismatched types", 14: "decode base64 error",
+            16: "out of memory of bitmap", 17: "out of memory of buffer", 18: "out of memory of key",
+            19: "http-mapping", 20: "unsupported value-mapping", 21: "http-mapping end",
+            22: "out of memory of field", 23: "out of memory of field value", 24: "value-mapping end"}
+_J2T_STATES = {0: "J2T_VAL", 1: "J2T_ARR", 2: "J2T_OBJ", 3: "J2T_KEY", 4: "J2T_ELEM", 5: "J2T_ARR_0",
+               6: "J2T_OBJ_0", 16: "J2T_VM"}
+
+
+@dataclass
+class Options:
+    """conv.Options (conv/api.go:52-121), the fields j2t reads."""
+    EnableValueMapping: bool = False
+    EnableHttpMapping: bool = False
+    EnableThriftBase: bool = False
+    String2Int64: bool = False
+    NoBase64Binary: bool = False
+    WriteOptionalField: bool = False
+    WriteDefaultField: bool = False
+    WriteRequireField: bool = False
+    DisallowUnknownField: bool = False
+    ReadHttpValueFallback: bool = False
+    ValidateUTF8: bool = False  # extension (north_star: "UTF-8 validation"), default off
+
+
+def to_flags(o: Options) -> int:
+    """toFlags conv/j2t/conv.go:98-127."""
+    f = 0
+    if o.WriteDefaultField:
+        f |= F_WRITE_DEFAULT
+    if not o.DisallowUnknownField:
+        f |= F_ALLOW_UNKNOWN
+    if o.EnableValueMapping:
+        f |= F_VALUE_MAPPING
+    if o.EnableHttpMapping:
+        f |= F_HTTP_MAPPING
+    if o.String2Int64:
+        f |= F_STRING_INT
+    if o.WriteRequireField:
+        f |= F_WRITE_REQUIRE
+    if o.NoBase64Binary:
+        f |= F_NO_BASE64
+    if o.WriteOptionalField:
+        f |= F_WRITE_OPTIONAL
+    if o.ReadHttpValueFallback:
+        f |= F_TRACE_BACK
+    if o.ValidateUTF8:
+        f |= F_VALIDATE_UTF8
+    return f
+
+
+def unpack_ret(ret: int) -> Tuple[int, int, int]:
+    """(code, pos, value): getErrCode/getPos/getValue conv/j2t/impl_amd64.go:250-259."""
+    return ret & 0xFF, (ret >> 8) & 0xFFFFFFFF, ret >> 40
+
+
+class J2TError(Exception):
+    """A conversion error, carrying the reference's packed status word."""
+
+    def __init__(self, ret: int, msg: str):
+        super().__init__(msg)
+        self.ret = ret
+        self.code, self.pos, self.value = unpack_ret(ret)
+
+
+def _locate(src: bytes, ip: int) -> str:
+    # json.SyntaxError.Locate: a window around the position
+    lo, hi = max(0, ip - 10), min(len(src), ip + 10)
+    return "\n\n\t%s\n\n\t%s^%s\n" % (src[lo:hi].decode("utf-8", "replace"), "." * (ip - lo), "." * (hi - ip))
+
+
+def explain_native_error(ret: int, src: bytes) -> str:
+    """explainNativeError conv/j2t/impl_amd64.go:261-298 (message text)."""
+    e, ip, v = unpack_ret(ret)
+    loc = _locate(src, ip)
+    if e == 2:
+        ch, st = v >> 8, v & 0xFF
+        return "invalid char '%s' for state %s, near %d of %s" % (chr(ch & 0xFF), _J2T_STATES.get(st, st), ip, loc)
+    if e == 6:
+        return "unexpected number type %d, near %d of %s" % (v, ip, loc)
+    if e == 11:
+        return "unsupported thrift type %s, near %d of %s" % (TYPE_NAMES.get(v, v), ip, loc)
+    if e == 20:
+        return "unsupported value-mapping type %d, near %d of %r" % (v, ip, loc)
+    if e == 9:
+        return "expect type %s but got type %d, near %d of %s" % (TYPE_NAMES.get(v >> 8, v >> 8), v & 0xFF, ip, loc)
+    if e == 10:
+        return "missing required field %d, near %d of %s" % (v, ip, loc)
+    if e == 12:
+        n = max(ip - v - 1, 0)
+        return "unknown field '%s', near %d of %s" % (src[n:ip - 1].decode("utf-8", "replace"), ip, loc)
+    if e == 7:
+        return "stack %d overflow, near %d of %s" % (v, ip, loc)
+    if e == 14:
+        return "decode base64 error: illegal base64 data at input byte %d, near %d of %s" % (v, ip, loc)
+    return "native error %r, value %d, near %d of %s" % (_ERR_MSG.get(e, "unknown"), v, ip, loc)
+
+
+class Context:
+    """One HIP device: stream + workspaces (dg_ctx)."""
+
+    def __init__(self, device: int = 0):
+        L = _lib.lib()
+        h = C.c_void_p()
+        _lib.check(L.dg_ctx_create(device, C.byref(h)))
+        self.h = h
+        self.device = device
+        self._descs = {}
+
+    def desc(self, flat: FlatDescriptor):
+        """Device-resident copy of a flattened descriptor (cached by content)."""
+        d = self._descs.get(flat.blob)
+        if d is None:
+            h = C.c_void_p()
+            _lib.check(_lib.lib().dg_desc_create(self.h, flat.blob, len(flat.blob), C.byref(h)))
+            d = h
+            self._descs[flat.blob] = d
+        return d
+
+    def close(self):
+        L = _lib.lib()
+        for d in self._descs.values():
+            L.dg_desc_destroy(d)
+        self._descs.clear()
+        if self.h:
+            L.dg_ctx_destroy(self.h)
+            self.h = None
+
+
+_default_ctx: Optional[Context] = None
+
+
+def default_context() -> Context:
+    global _default_ctx
+    if _default_ctx is None:
+        _default_ctx = Context(0)
+    return _default_ctx
+
+
+class BinaryConv:
+    """j2t.BinaryConv (conv/j2t/conv.go:31-96) on the MI355X."""
+
+    def __init__(self, opts: Optional[Options] = None, ctx: Optional[Context] = None):
+        self.opts = opts or Options()
+        self.ctx = ctx
+        self._flat_cache = {}
+
+    def set_options(self, opts: Options):
+        self.opts = opts
+
+    def _ctx(self) -> Context:
+        if self.ctx is None:
+            self.ctx = default_context()
+        return self.ctx
+
+    def _flat(self, desc) -> FlatDescriptor:
+        if isinstance(desc, FlatDescriptor):
+            return desc
+        f = self._flat_cache.get(id(desc))
+        if f is None:
+            f = flatten(desc)
+            self._flat_cache[id(desc)] = f
+        return f
+
+    def _check_opts(self):
+        if self.opts.EnableHttpMapping:
+            # conv/j2t/conv.go:57-68: HTTP mapping needs a request and Go callbacks
+            raise J2TError(0, "EnableHttpMapping needs host callbacks (out of scope on the GPU path)")
+
+    def do(self, desc, jbytes: bytes) -> Optional[bytes]:
+        """Do: returns Thrift bytes (None for an empty result) or raises J2TError."""
+        outs, rets = self.do_batch(desc, [jbytes])
+        if rets[0] != 0:
+            raise J2TError(int(rets[0]), explain_native_error(int(rets[0]), jbytes))
+        return outs[0] if outs[0] else None
+
+    def do_into(self, desc, jbytes: bytes, buf: bytearray):
+        """DoInto: appends to buf."""
+        out = self.do(desc, jbytes)
+        if out:
+            buf.extend(out)
+
+    def do_batch(self, desc, msgs: Sequence[bytes]) -> Tuple[List[bytes], np.ndarray]:
+        """Batch of independent messages -> (outputs, packed statuses)."""
+        self._check_opts()
+        flat = self._flat(desc)
+        ctx = self._ctx()
+        n = len(msgs)
+        lens = np.fromiter((len(m) for m in msgs), dtype=np.uint64, count=n)
+        in_off = np.zeros(n + 1, dtype=np.uint64)
+        np.cumsum(lens, out=in_off[1:])
+        arena = np.frombuffer(b"".join(msgs) + b"\0" * 16, dtype=np.uint8)
+        rets = np.zeros(max(n, 1), dtype=np.uint64)
+        out_off = np.zeros(n + 1, dtype=np.uint64)
+        cap = int(lens.sum()) * 4 + 64 * n + 64
+        out = np.zeros(cap, dtype=np.uint8)
+        need = C.c_uint64(0)
+        L = _lib.lib()
+        rc = L.dg_j2t_batch_host(ctx.h, ctx.desc(flat), flat.root_type, arena.ctypes.data, in_off.ctypes.data,
+                                 n, to_flags(self.opts), out.ctypes.data, cap, out_off.ctypes.data,
+                                 rets.ctypes.data, C.byref(need))
+        if rc == -3 and need.value > cap:
+            cap = int(need.value) + 64
+            out = np.zeros(cap, dtype=np.uint8)
+            rc = L.dg_j2t_batch_host(ctx.h, ctx.desc(flat), flat.root_type, arena.ctypes.data,
+                                     in_off.ctypes.data, n, to_flags(self.opts), out.ctypes.data, cap,
+                                     out_off.ctypes.data, rets.ctypes.data, C.byref(need))
+        _lib.check(rc)
+        outs = [out[int(out_off[i]):int(out_off[i + 1])].tobytes() for i in range(n)]
+        return outs, rets[:n]
+
+    def do_device(self, desc, json, in_off, out, out_off, out_len, ret, pending=None, stream=None):
+        """Device-resident batch over torch CUDA tensors (uint8/int64/int32).
+
+        json: uint8[>= in_off[-1] + 16]; in_off/out_off: int64[n+1];
+        out: uint8 arena; out_len: int32[n]; ret: int64[n]. Asynchronous on
+        `stream` (a torch.cuda.Stream) or the context's stream.
+        """
+        self._check_opts()
+        flat = self._flat(desc)
+        ctx = self._ctx()
+        n = in_off.numel() - 1
+        s = stream.cuda_stream if stream is not None else None
+        _lib.check(_lib.lib().dg_j2t_batch_device(
+            ctx.h, ctx.desc(flat), flat.root_type, json.data_ptr(), in_off.data_ptr(), n,
+            to_flags(self.opts), out.data_ptr(), out_off.data_ptr(), out_len.data_ptr(), ret.data_ptr(),
+            pending.data_ptr() if pending is not None else None, s))
+
+
+def new_binary_conv(opts: Optional[Options] = None) -> BinaryConv:
+    """j2t.NewBinaryConv (conv/j2t/conv.go:36)."""
+    return BinaryConv(opts)

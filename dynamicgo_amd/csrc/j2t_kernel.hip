@@ -1,0 +1,1086 @@
+/*
+ * j2t_kernel.hip — the MI355X kernels and the C ABI (include/dgj2t.h).
+ *
+ * Kernel map:
+ *  j2t_lane_kernel  one lane per message, stack of FAST_DEPTH frames in
+ *                   registers/scratch; messages that outgrow it are marked
+ *                   DG_ST_DEEP and left to
+ *  j2t_deep_kernel  a small persistent grid that redoes only the DEEP
+ *                   messages with a MAX_RECURSE (4096) stack in workspace.
+ * Both run the same templated FSM (Machine<...>::run) that restates
+ * j2t_fsm_exec (native/thrift.c:765-1187).
+ */
+#include <hip/hip_runtime.h>
+
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+#include <vector>
+
+#include "j2t_device.h"
+
+namespace dg {
+
+constexpr int FAST_DEPTH = 24;      /* frames per lane in the fast kernel */
+constexpr int FAST_SKIP_WORDS = 1;  /* 64 skip levels */
+constexpr int WS_KEYCAP = 1024;     /* unquoted-key buffer per lane (reference key cache: 1 KB) */
+constexpr int WS_REQCAP = 256;      /* multi-word requires arena per lane (words) */
+constexpr int DEEP_THREADS = 256;   /* persistent lanes of the deep kernel */
+constexpr int DEEP_KEYCAP = 1 << 20;
+constexpr int DEEP_REQCAP = 1 << 16;
+
+struct Params {
+    DescView D;
+    uint32_t root;
+    const uint8_t *json;
+    const uint64_t *in_off;
+    uint64_t n;
+    uint64_t flag;
+    uint8_t *out;
+    const uint64_t *out_off;
+    uint32_t *out_len;
+    uint64_t *ret;
+    uint32_t *pending;
+    uint32_t *deep_count; /* DG_ST_DEEP messages appended here by the fast kernel */
+    uint64_t *deep_list;
+    uint8_t *ws;       /* per-lane workspace base */
+    uint64_t ws_stride;/* bytes per lane */
+    uint32_t keycap, reqcap;
+};
+
+/* The FSM of one message. FRAMES: frame storage (private array or workspace). */
+struct Machine {
+    DescView D;
+    Src src;
+    Out out;
+    uint64_t flag;
+    Frame *vt;
+    uint32_t sp, cap;
+    uint64_t *skipbits;
+    uint32_t skipcap;
+    Workspace ws;
+    uint32_t reqlen;
+    uint32_t field_cache_len;
+    JState jt;
+
+    DGI const dg_type &TY(uint32_t t) const { return D.T[t]; }
+
+    DGI uint64_t push(uint32_t st, uint32_t td, int64_t p)
+    {
+        if (sp >= MAX_RECURSE) return pack(E_RECURSE_MAX, sp, (uint64_t)p);
+        if (sp >= cap) return pack0(DG_ST_DEEP, 0);
+        Frame &x = vt[sp++];
+        x.st = st;
+        x.td = td;
+        return 0;
+    }
+
+    /* requires bits of struct frame x (bm_* native/map.c:134-154) */
+    DGI bool bm_is_set(const Frame &x, const dg_struct &sd, uint32_t k) const
+    {
+        if (sd.req_words == 1) return (x.reqs >> k) & 1;
+        return (ws.reqarena[x.roff + (k >> 6)] >> (k & 63)) & 1;
+    }
+    DGI void bm_set_req(Frame &x, const dg_struct &sd, uint32_t k, int req)
+    {
+        uint64_t *w = sd.req_words == 1 ? &x.reqs : &ws.reqarena[x.roff + (k >> 6)];
+        uint64_t m = 1ull << (k & 63);
+        if (req == DG_REQ_DEFAULT || req == DG_REQ_REQUIRED) *w |= m;
+        else if (req == DG_REQ_OPTIONAL) *w &= ~m;
+    }
+
+    /* tb_write_empty native/thrift.c:171-203 */
+    DGI uint64_t write_empty(uint32_t td, int64_t p)
+    {
+        const dg_type &t = TY(td);
+        switch (t.ttype) {
+        case DG_T_BOOL:
+        case DG_T_BYTE: out.w8(0); return 0;
+        case DG_T_I16: out.w16(0); return 0;
+        case DG_T_I32: out.w32(0); return 0;
+        case DG_T_I64:
+        case DG_T_DOUBLE: out.w64(0); return 0;
+        case DG_T_STRING: out.w32(0); return 0;
+        case DG_T_LIST:
+        case DG_T_SET:
+            out.w8(TY(t.elem).ttype);
+            out.w32(0);
+            return 0;
+        case DG_T_MAP:
+            out.w8(TY(t.key).ttype);
+            out.w8(TY(t.elem).ttype);
+            out.w32(0);
+            return 0;
+        case DG_T_STRUCT: out.w8(0); return 0;
+        default: return pack(E_UNSUPPORT_THRIFT_TYPE, t.ttype, (uint64_t)p);
+        }
+    }
+    /* tb_write_default_or_empty native/thrift.c:205-217 */
+    DGI uint64_t write_default_or_empty(const dg_field &f, int64_t p)
+    {
+        if (f.dflt_len != DG_NONE) {
+            out.wbytes(D.P + f.dflt_off, f.dflt_len);
+            return 0;
+        }
+        return write_empty(f.type, p);
+    }
+
+    /* j2t_write_unset_fields native/thrift.c:258-310 */
+    DGN uint64_t write_unset_fields(const Frame &x, const dg_struct &sd, int64_t p)
+    {
+        bool wr = flag & DG_F_WRITE_REQUIRE, wd = flag & DG_F_WRITE_DEFAULT;
+        bool wo = flag & DG_F_WRITE_OPTIONAL, tb = flag & DG_F_TRACE_BACK;
+        for (uint32_t w = 0; w < sd.req_words; w++) {
+            uint64_t bits = sd.req_words == 1 ? x.reqs : ws.reqarena[x.roff + w];
+            while (bits) {
+                uint32_t k = w * 64 + __builtin_ctzll(bits);
+                bits &= bits - 1;
+                const dg_field &f = D.F[sd.field_begin + k];
+                if (f.flags & DG_FF_REQUEST_BASE) continue;
+                if (tb && (f.required == DG_REQ_REQUIRED || sp == 1)) field_cache_len++;
+                else if (!wr && f.required == DG_REQ_REQUIRED)
+                    return pack(E_NULL_REQUIRED, f.id, (uint64_t)p);
+                else if ((wr && f.required == DG_REQ_REQUIRED) || (wd && f.required == DG_REQ_DEFAULT) ||
+                         (wo && f.required == DG_REQ_OPTIONAL)) {
+                    out.w8(TY(f.type).ttype);
+                    out.w16(f.id);
+                    uint64_t r = write_default_or_empty(f, p);
+                    if (r) return r;
+                }
+            }
+        }
+        return 0;
+    }
+
+    /* j2t_number native/thrift.c:312-365 */
+    DGI uint64_t j2t_number(uint32_t td, const Src &s, int64_t &p)
+    {
+        int64_t s0 = p;
+        vnumber(s, p, jt, ws.dbuf);
+        if (jt.vt < 0) return pack((uint32_t)-jt.vt, (uint64_t)s0, (uint64_t)p);
+        bool isint = jt.vt == V_INTEGER;
+        switch (TY(td).ttype) {
+        case DG_T_BYTE: out.w8(isint ? (uint8_t)jt.iv : (uint8_t)cvt32(jt.dv)); return 0;
+        case DG_T_I16: out.w16(isint ? (uint16_t)jt.iv : (uint16_t)cvt32(jt.dv)); return 0;
+        case DG_T_I32: out.w32(isint ? (uint32_t)jt.iv : (uint32_t)cvt32(jt.dv)); return 0;
+        case DG_T_I64: out.w64(isint ? (uint64_t)jt.iv : (uint64_t)cvt64(jt.dv)); return 0;
+        case DG_T_DOUBLE: out.w64((uint64_t)__double_as_longlong(jt.dv)); return 0;
+        }
+        return pack(E_DISMATCH_TYPE, v2(TY(td).ttype, V_INTEGER), (uint64_t)p);
+    }
+
+    /* j2t_string native/thrift.c:367-399 */
+    DGI uint64_t j2t_string(int64_t &p)
+    {
+        int64_t s0 = p;
+        bool esc;
+        int64_t e = advance_string(src, s0, esc);
+        if (e < 0) return pack((uint32_t)-e, (uint64_t)s0, (uint64_t)p);
+        p = e;
+        int64_t n = e - s0 - 1;
+        if (esc) {
+            uint64_t lp = out.alloc(4);
+            OutSink sink{&out, out.len};
+            int64_t l = unquote(src.s + s0, n, sink);
+            if (l < 0) return pack((uint32_t)-l, (uint64_t)s0, (uint64_t)p);
+            out.len += (uint64_t)l;
+            out.put32(lp, (uint32_t)l);
+        } else {
+            out.w32((uint32_t)n);
+            out.wbytes(src.s + s0, (uint64_t)n);
+        }
+        return 0;
+    }
+
+    /* j2t_binary native/thrift.c:401-420 */
+    DGI uint64_t j2t_binary(int64_t &p)
+    {
+        int64_t s0 = p;
+        bool esc;
+        int64_t e = advance_string(src, s0, esc);
+        if (e < 0) return pack((uint32_t)-e, (uint64_t)s0, (uint64_t)p);
+        p = e;
+        int64_t n = e - s0 - 1;
+        uint64_t back = out.alloc(4);
+        int64_t l = b64decode(out, src.s + s0, n);
+        if (l < 0) return pack(E_DECODE_BASE64, (uint64_t)(-l - 1), (uint64_t)p);
+        out.len += (uint64_t)l;
+        out.put32(back, (uint32_t)l);
+        return 0;
+    }
+
+    /* j2t_map_key native/thrift.c:422-447 */
+    DGI uint64_t j2t_map_key(const uint8_t *kp, int64_t kn, uint32_t kt, int64_t p)
+    {
+        switch (TY(kt).ttype) {
+        case DG_T_STRING:
+            out.w32((uint32_t)kn);
+            out.wbytes(kp, (uint64_t)kn);
+            return 0;
+        case DG_T_BYTE:
+        case DG_T_I16:
+        case DG_T_I32:
+        case DG_T_I64:
+        case DG_T_DOUBLE: {
+            Src tmp{kp, kn};
+            int64_t q = 0;
+            return j2t_number(kt, tmp, q);
+        }
+        default:
+            return pack(E_UNSUPPORT_THRIFT_TYPE, TY(kt).ttype, (uint64_t)p);
+        }
+    }
+
+    /* exact-match field lookup (j2t_find_field_key native/thrift.c:449-468) */
+    DGI int32_t find_field(const dg_struct &sd, const uint8_t *k, int64_t kn) const
+    {
+        uint32_t h = DG_NAME_HASH_SEED;
+        for (int64_t i = 0; i < kn; i++) h = DG_NAME_HASH_STEP(h, k[i]);
+        uint32_t j = h & sd.name_mask;
+        for (;;) {
+            const dg_name &nm = D.N[sd.name_begin + j];
+            if (nm.field == DG_NONE) return -1;
+            if (nm.hash == h && nm.key_len == (uint32_t)kn) {
+                const uint8_t *q = D.P + nm.key_off;
+                bool eq = true;
+                for (int64_t i = 0; i < kn; i++) {
+                    if (q[i] != k[i]) {
+                        eq = false;
+                        break;
+                    }
+                }
+                if (eq) return (int32_t)nm.field;
+            }
+            j = (j + 1) & sd.name_mask;
+        }
+    }
+
+    /* j2t_read_key native/thrift.c:470-504 */
+    DGI uint64_t read_key(int64_t &p, const uint8_t *&kp, int64_t &kn)
+    {
+        int64_t s0 = p;
+        bool esc;
+        int64_t e = advance_string(src, s0, esc);
+        if (e < 0) return pack((uint32_t)-e, (uint64_t)s0, (uint64_t)p);
+        p = e;
+        kn = e - s0 - 1;
+        kp = src.s + s0;
+        if (esc) {
+            BufSink sink{ws.keybuf, (int64_t)ws.keycap, false};
+            int64_t l = unquote(kp, kn, sink);
+            if (l < 0) return pack((uint32_t)-l, (uint64_t)s0, (uint64_t)p);
+            if (sink.over) return pack0(DG_ST_DEEP, 0);
+            kp = ws.keybuf;
+            kn = l;
+        }
+        return 0;
+    }
+
+    /* j2t_key native/thrift.c:668-763 */
+    DGI uint64_t j2t_key(int64_t &p, uint32_t dc, bool obj0, uint64_t &unwindPos, int32_t &lastField)
+    {
+        const uint8_t *kp;
+        int64_t kn;
+        uint64_t r = read_key(p, kp, kn);
+        if (r) return r;
+        const dg_type &t = TY(dc);
+        if (t.ttype == DG_T_MAP) {
+            unwindPos = out.len;
+            r = j2t_map_key(kp, kn, t.key, p);
+            if (r) return r;
+            if (obj0) {
+                vt[sp - 1].size = 0;
+                return push(J_ELEM, t.elem, p);
+            }
+            Frame &x = vt[sp - 1];
+            x.st = J_ELEM;
+            x.td = t.elem;
+            return 0;
+        }
+        Frame &pex = obj0 ? vt[sp - 1] : vt[sp - 2];
+        const dg_struct &sd = D.S[t.st];
+        int32_t fi = find_field(sd, kp, kn);
+        if (fi < 0 || ((D.F[fi].flags & DG_FF_REQUEST_BASE) && (flag & DG_F_NO_WRITE_BASE))) {
+            if (fi < 0 && (flag & DG_F_ALLOW_UNKNOWN) == 0) return pack(E_UNKNOWN_FIELD, (uint64_t)kn, (uint64_t)p);
+            if (obj0) return push(J_ELEM | ST_SKIP, DG_NONE, p);
+            Frame &x = vt[sp - 1];
+            x.st = J_ELEM | ST_SKIP;
+            x.td = DG_NONE;
+            return 0;
+        }
+        const dg_field &f = D.F[fi];
+        uint32_t k = (uint32_t)fi - sd.field_begin;
+        if ((flag & DG_F_ENABLE_HM) && (f.flags & DG_FF_HTTP_MAPPING) && !bm_is_set(pex, sd, k)) {
+            if (obj0) return push(J_ELEM | ST_SKIP, f.type, p);
+            Frame &x = vt[sp - 1];
+            x.st = J_ELEM | ST_SKIP;
+            x.td = f.type;
+            return 0;
+        }
+        uint32_t vm = ST_VM;
+        if ((flag & DG_F_ENABLE_VM) == 0 || f.vm == DG_VM_NONE) {
+            vm = ST_FIELD;
+            unwindPos = out.len;
+            lastField = fi;
+            out.w8(TY(f.type).ttype);
+            out.w16(f.id);
+        }
+        if (obj0) {
+            r = push(J_ELEM | vm, f.type, p);
+            if (r) return r;
+        } else {
+            Frame &x = vt[sp - 1];
+            x.st = J_ELEM | vm;
+            x.td = f.type;
+        }
+        vt[sp - 1].f = (uint32_t)fi;
+        /* pex may be vt[sp-2] (obj0) after the push: re-resolve */
+        Frame &px = obj0 ? vt[sp - 2] : vt[sp - 2];
+        bm_set_req(px, sd, k, DG_REQ_OPTIONAL);
+        return 0;
+    }
+
+    /* j2t_field_vm native/thrift.c:506-666 */
+    DGN uint64_t field_vm(int64_t &p, const Frame &x)
+    {
+        const dg_field &f = D.F[x.f];
+        uint8_t ft = TY(f.type).ttype;
+        if (f.vm <= DG_VM_INLINE_MAX) {
+            out.w8(ft);
+            out.w16(f.id);
+            if (f.vm != DG_VM_JSCONV) return pack(E_UNSUPPORT_VM_TYPE, f.vm, (uint64_t)p);
+            uint8_t ch = src.at(p - 1);
+            if (ch == '"') {
+                if (ft == DG_T_STRING) return j2t_string(p);
+                if (src.at(p) == '"') {
+                    uint64_t r = write_default_or_empty(f, p);
+                    if (r) return r;
+                    p += 1;
+                    return 0;
+                }
+            } else {
+                if (ch != '-' && (ch < '0' || ch > '9')) return pack(E_INVAL, sx8_64(ch), (uint64_t)p);
+                p -= 1;
+            }
+            int64_t s0 = p;
+            vnumber(src, p, jt, ws.dbuf);
+            if (jt.vt != V_INTEGER && jt.vt != V_DOUBLE) return pack(E_NUMBER_FMT, (uint64_t)jt.vt, (uint64_t)p);
+            bool isint = jt.vt == V_INTEGER;
+            switch (ft) {
+            case DG_T_STRING:
+                out.w32((uint32_t)(p - s0));
+                out.wbytes(src.s + s0, (uint64_t)(p - s0));
+                return 0;
+            case DG_T_I64: out.w64(isint ? (uint64_t)jt.iv : (uint64_t)cvt64(jt.dv)); break;
+            case DG_T_I32: out.w32(isint ? (uint32_t)jt.iv : (uint32_t)cvt32(jt.dv)); break;
+            case DG_T_I16:
+                out.w16(isint ? (uint16_t)jt.iv : (uint16_t)cvt32(jt.dv));
+                /* the reference misses a break here (native/thrift.c:590-603) */
+                out.w8(isint ? (uint8_t)jt.iv : (uint8_t)cvt32(jt.dv));
+                break;
+            case DG_T_BYTE: out.w8(isint ? (uint8_t)jt.iv : (uint8_t)cvt32(jt.dv)); break;
+            case DG_T_DOUBLE: out.w64((uint64_t)__double_as_longlong(jt.dv)); break;
+            default: return pack(E_UNSUPPORT_THRIFT_TYPE, ft, (uint64_t)p);
+            }
+            if (ch == '"') {
+                if (src.at(p) != '"') return pack(E_INVAL, sx8_64(src.at(p)), (uint64_t)p);
+                p += 1;
+            }
+            return 0;
+        }
+        /* non-inline value mapping: host callback (ERR_VM_END) */
+        p -= 1;
+        int64_t s0 = p;
+        int64_t r = skip_one(src, p, skipbits, skipcap);
+        if (r == SKIP_DEEP) return pack0(DG_ST_DEEP, 0);
+        if (r < 0) return pack((uint32_t)-r, (uint64_t)s0, (uint64_t)p);
+        return pack0(E_VM_END, (uint64_t)p);
+    }
+
+    /* j2t_fsm_exec native/thrift.c:765-1187 */
+    DGI uint64_t run(uint32_t root)
+    {
+        int64_t p = 0;
+        bool null_val = false;
+        uint64_t unwindPos = 0;
+        int32_t lastField = -1;
+        sp = 1;
+        vt[0].st = J_VAL;
+        vt[0].td = root;
+        while (sp) {
+            if (sp >= MAX_RECURSE) return pack(E_RECURSE_MAX, sp, (uint64_t)p);
+            Frame &x = vt[sp - 1];
+            uint32_t dc = x.td;
+            uint32_t st = x.st;
+            uint8_t ch = advance_ns(src, p);
+            switch (st & 0xffff) {
+            default:
+                sp--;
+                break;
+            case J_ARR_0:
+                if (ch == ']') {
+                    out.put32(x.bp, 0);
+                    sp--;
+                    continue;
+                }
+                x.size = 0;
+                x.st = J_ARR;
+                p -= 1;
+                {
+                    uint64_t r = push(J_VAL, TY(dc).elem, p);
+                    if (r) return r;
+                }
+                continue;
+            case J_ARR:
+                if (ch == ']' || ch == ',') {
+                    if (!null_val) x.size += 1;
+                    else null_val = false;
+                    if (ch == ']') {
+                        out.put32(x.bp, x.size);
+                        sp--;
+                        continue;
+                    }
+                    uint64_t r = push(J_VAL, TY(dc).elem, p);
+                    if (r) return r;
+                    continue;
+                }
+                return pack(E_INVAL, v2(sx8(ch), J_ARR), (uint64_t)p);
+            case J_OBJ_0:
+                if (ch == '}') {
+                    const dg_type &t = TY(dc);
+                    if (t.ttype == DG_T_STRUCT) {
+                        const dg_struct &sd = D.S[t.st];
+                        uint64_t r = write_unset_fields(x, sd, p - 1);
+                        if (r) return r;
+                        if (sd.req_words > 1) reqlen -= sd.req_words;
+                        if ((flag & DG_F_ENABLE_HM) && field_cache_len > 0) return pack0(E_HM_END, (uint64_t)p);
+                        out.w8(0);
+                    } else {
+                        out.put32(x.bp, 0);
+                    }
+                    sp--;
+                    continue;
+                }
+                if (ch == '"') {
+                    x.st = J_OBJ;
+                    uint64_t r = j2t_key(p, dc, true, unwindPos, lastField);
+                    if (r) return r;
+                    continue;
+                }
+                return pack(E_INVAL, v2(sx8(ch), J_OBJ_0), (uint64_t)p);
+            case J_OBJ:
+                if (ch == '}') {
+                    const dg_type &t = TY(dc);
+                    if (t.ttype == DG_T_STRUCT) {
+                        const dg_struct &sd = D.S[t.st];
+                        if (null_val) {
+                            null_val = false;
+                            bm_set_req(x, sd, (uint32_t)lastField - sd.field_begin, D.F[lastField].required);
+                            out.len = unwindPos;
+                        }
+                        uint64_t r = write_unset_fields(x, sd, p - 1);
+                        if (r) return r;
+                        if (sd.req_words > 1) reqlen -= sd.req_words;
+                        if ((flag & DG_F_ENABLE_HM) && field_cache_len != 0) return pack0(E_HM_END, (uint64_t)p);
+                        out.w8(0);
+                    } else {
+                        if (!null_val) x.size += 1;
+                        else {
+                            null_val = false;
+                            out.len = unwindPos;
+                        }
+                        out.put32(x.bp, x.size);
+                    }
+                    sp--;
+                    continue;
+                }
+                if (ch == ',') {
+                    const dg_type &t = TY(dc);
+                    if (t.ttype == DG_T_MAP) {
+                        if (!null_val) x.size += 1;
+                        else {
+                            null_val = false;
+                            out.len = unwindPos;
+                        }
+                    } else if (null_val) {
+                        null_val = false;
+                        const dg_struct &sd = D.S[t.st];
+                        bm_set_req(x, sd, (uint32_t)lastField - sd.field_begin, D.F[lastField].required);
+                        out.len = unwindPos;
+                    }
+                    uint64_t r = push(J_KEY, dc, p);
+                    if (r) return r;
+                    continue;
+                }
+                return pack(E_INVAL, v2(sx8(ch), J_OBJ), (uint64_t)p);
+            case J_KEY: {
+                if (ch != '"') return pack(E_INVAL, v2('"', J_KEY), (uint64_t)p);
+                uint64_t r = j2t_key(p, dc, false, unwindPos, lastField);
+                if (r) return r;
+                continue;
+            }
+            case J_ELEM:
+                if (ch != ':') return pack(E_INVAL, v2(':', J_ELEM), (uint64_t)p);
+                x.st = J_VAL | (st & 0xffff0000u);
+                continue;
+            }
+            /* J_VAL, already dropped */
+            if (st & ST_SKIP) {
+                p -= 1;
+                int64_t s0 = p;
+                int64_t r = skip_one(src, p, skipbits, skipcap);
+                if (r == SKIP_DEEP) return pack0(DG_ST_DEEP, 0);
+                if (r < 0) return pack((uint32_t)-r, (uint64_t)s0, (uint64_t)p);
+                continue;
+            }
+            if ((flag & DG_F_ENABLE_VM) && (st & ST_VM)) {
+                uint64_t r = field_vm(p, x);
+                if (r) return r;
+                continue;
+            }
+            const dg_type &t = TY(dc);
+            switch (ch) {
+            case '0': case '1': case '2': case '3': case '4':
+            case '5': case '6': case '7': case '8': case '9': case '-': {
+                p -= 1;
+                uint64_t r = j2t_number(dc, src, p);
+                if (r) return r;
+                break;
+            }
+            case 'n': {
+                int64_t s0 = p;
+                int64_t r = advance_dword(src, p, 1, p - 1, VS_NULL);
+                if (r < 0) return pack((uint32_t)-r, (uint64_t)s0, (uint64_t)p);
+                null_val = true;
+                break;
+            }
+            case 't':
+            case 'f': {
+                int64_t s0 = p;
+                int64_t r = ch == 't' ? advance_dword(src, p, 1, p - 1, VS_TRUE) : advance_dword(src, p, 0, p - 1, VS_ALSE);
+                if (r < 0) return pack((uint32_t)-r, (uint64_t)s0, (uint64_t)p);
+                if (t.ttype != DG_T_BOOL) return pack(E_DISMATCH_TYPE, v2(t.ttype, DG_T_BOOL), (uint64_t)p);
+                out.w8(ch == 't' ? 1 : 0);
+                break;
+            }
+            case '[': {
+                if (t.ttype != DG_T_LIST && t.ttype != DG_T_SET)
+                    return pack(E_DISMATCH_TYPE2, ((uint32_t)t.ttype << 16) | (DG_T_SET << 8) | DG_T_LIST, (uint64_t)p);
+                out.w8(TY(t.elem).ttype);
+                uint64_t bp = out.alloc(4);
+                uint64_t r = push(J_ARR_0, dc, p);
+                if (r) return r;
+                vt[sp - 1].bp = (uint32_t)bp;
+                vt[sp - 1].size = 0;
+                break;
+            }
+            case '{': {
+                if (t.ttype != DG_T_STRUCT && t.ttype != DG_T_MAP)
+                    return pack(E_DISMATCH_TYPE2, ((uint32_t)t.ttype << 16) | (DG_T_MAP << 8) | DG_T_STRUCT, (uint64_t)p);
+                if (t.ttype == DG_T_STRUCT) {
+                    const dg_struct &sd = D.S[t.st];
+                    uint64_t r = push(J_OBJ_0, dc, p);
+                    if (r) return r;
+                    Frame &nx = vt[sp - 1];
+                    /* bm_malloc_reqs native/thrift.c:232-250 */
+                    if (sd.req_words == 1) {
+                        nx.reqs = D.R[sd.req_begin];
+                    } else {
+                        if (reqlen + sd.req_words > ws.reqcap) return pack0(DG_ST_DEEP, 0);
+                        nx.roff = reqlen;
+                        for (uint32_t w = 0; w < sd.req_words; w++) ws.reqarena[reqlen + w] = D.R[sd.req_begin + w];
+                        reqlen += sd.req_words;
+                    }
+                    if ((flag & DG_F_ENABLE_HM) && (sd.flags & DG_SF_HTTP_MAPPING)) return pack0(E_HM, (uint64_t)(p - 1));
+                } else {
+                    out.w8(TY(t.key).ttype);
+                    out.w8(TY(t.elem).ttype);
+                    uint64_t bp = out.alloc(4);
+                    uint64_t r = push(J_OBJ_0, dc, p);
+                    if (r) return r;
+                    vt[sp - 1].bp = (uint32_t)bp;
+                    vt[sp - 1].size = 0;
+                }
+                break;
+            }
+            case '"': {
+                uint64_t r;
+                if (t.ttype == DG_T_STRING) {
+                    if ((flag & DG_F_NO_BASE64) == 0 && (t.flags & DG_TF_BINARY)) r = j2t_binary(p);
+                    else r = j2t_string(p);
+                    if (r) return r;
+                } else if ((flag & DG_F_ENABLE_I2S) && (t.ttype == DG_T_I64 || t.ttype == DG_T_I32 || t.ttype == DG_T_I16 ||
+                                                         t.ttype == DG_T_BYTE || t.ttype == DG_T_DOUBLE)) {
+                    if (src.at(p) == '"') {
+                        r = write_empty(dc, p);
+                        if (r) return r;
+                    } else {
+                        r = j2t_number(dc, src, p);
+                        if (r) return r;
+                        if (p >= src.n) return pack(E_EOF, 0, (uint64_t)p);
+                        if (src.at(p) != '"') return pack(E_INVAL, v2(sx8(src.at(p)), J_VAL), (uint64_t)p);
+                    }
+                    p += 1;
+                } else {
+                    return pack(E_DISMATCH_TYPE, v2(t.ttype, DG_T_STRING), (uint64_t)p);
+                }
+                break;
+            }
+            case 0:
+                return pack(E_EOF, 0, (uint64_t)p);
+            default:
+                return pack(E_INVAL, v2(sx8(ch), J_VAL), (uint64_t)p);
+            }
+        }
+        return 0;
+    }
+};
+
+/* BinaryConv.do prelude/epilogue (conv/j2t/impl.go:38-91, conv.go:70-77) around
+ * the FSM for message i. Returns the status; writes out_len. */
+DGI uint64_t convert_one(const Params &P, uint64_t i, Frame *frames, uint32_t depth, uint64_t *skipbits,
+                         uint32_t skipcap, const Workspace &ws, uint32_t &olen)
+{
+    uint64_t a = P.in_off[i], b = P.in_off[i + 1];
+    uint64_t oa = P.out_off[i], ob = P.out_off[i + 1];
+    Machine m;
+    m.D = P.D;
+    m.src = Src{P.json + a, (int64_t)(b - a)};
+    m.out = Out{P.out + oa, ob - oa, 0};
+    m.flag = P.flag;
+    m.vt = frames;
+    m.cap = depth;
+    m.skipbits = skipbits;
+    m.skipcap = skipcap;
+    m.ws = ws;
+    m.reqlen = 0;
+    m.field_cache_len = 0;
+    uint64_t r;
+    if (b == a) { /* empty body -> STOP (conv/j2t/impl.go:52-82) */
+        m.out.w8(0);
+        r = 0;
+    } else if (P.D.T[P.root].ttype == DG_T_STRING && m.src.s[0] != '"') {
+        /* unquoted STRING root: json.EncodeString then unquote == identity
+         * (conv/j2t/impl.go:85-88; native/parsing.c:28-62 escapes only '"',
+         * '\\' and control bytes, all restored by unquote) */
+        m.out.w32((uint32_t)m.src.n);
+        m.out.wbytes(m.src.s, (uint64_t)m.src.n);
+        r = 0;
+    } else {
+        r = m.run(P.root);
+    }
+    if (r == 0 && m.out.len > m.out.cap) r = pack(DG_ST_OUT_OVERFLOW, m.out.len, 0);
+    olen = r == 0 ? (uint32_t)m.out.len : 0;
+    return r;
+}
+
+DGI Workspace lane_ws(const Params &P, uint64_t lane)
+{
+    Workspace w;
+    uint8_t *base = P.ws + lane * P.ws_stride;
+    w.dbuf = base;
+    w.keybuf = base + DCAP;
+    w.keycap = P.keycap;
+    w.reqarena = (uint64_t *)(base + DCAP + P.keycap);
+    w.reqcap = P.reqcap;
+    w.frames = nullptr;
+    w.skipbits = nullptr;
+    return w;
+}
+
+__global__ __launch_bounds__(256) void j2t_lane_kernel(Params P)
+{
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.n) return;
+    Frame frames[FAST_DEPTH];
+    uint64_t skipbits[FAST_SKIP_WORDS];
+    Workspace ws = lane_ws(P, i);
+    uint32_t olen;
+    uint64_t r = convert_one(P, i, frames, FAST_DEPTH, skipbits, FAST_SKIP_WORDS * 64, ws, olen);
+    P.ret[i] = r;
+    P.out_len[i] = olen;
+    if ((uint8_t)r == DG_ST_OUT_OVERFLOW && P.pending) atomicAdd(P.pending, 1u);
+    if ((uint8_t)r == DG_ST_DEEP) P.deep_list[atomicAdd(P.deep_count, 1u)] = i;
+}
+
+/* Redo the DG_ST_DEEP messages (listed by the fast kernel) with a MAX_RECURSE
+ * stack in workspace. Persistent grid; exits at once when the list is empty. */
+__global__ __launch_bounds__(256) void j2t_deep_kernel(Params P)
+{
+    uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    Workspace ws = lane_ws(P, lane);
+    Frame *frames = (Frame *)(P.ws + lane * P.ws_stride + DCAP + P.keycap + (uint64_t)P.reqcap * 8);
+    uint64_t *skipbits = (uint64_t *)(frames + MAX_RECURSE);
+    uint32_t cnt = *P.deep_count;
+    for (uint64_t k = lane; k < cnt; k += stride) {
+        uint64_t i = P.deep_list[k];
+        uint32_t olen;
+        uint64_t r = convert_one(P, i, frames, MAX_RECURSE, skipbits, MAX_RECURSE, ws, olen);
+        P.ret[i] = r;
+        P.out_len[i] = olen;
+        if ((uint8_t)r == DG_ST_OUT_OVERFLOW && P.pending) atomicAdd(P.pending, 1u);
+    }
+}
+
+}  // namespace dg
+
+/* ========================================================================== */
+/* host side: C ABI                                                            */
+/* ========================================================================== */
+using namespace dg;
+
+static thread_local char g_err[512];
+static int set_err(int code, const char *fmt, ...)
+{
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    va_end(ap);
+    return code;
+}
+#define HIPCHK(x)                                                                              \
+    do {                                                                                       \
+        hipError_t e_ = (x);                                                                   \
+        if (e_ != hipSuccess) return set_err(DG_E_HIP, "%s: %s", #x, hipGetErrorString(e_));  \
+    } while (0)
+
+struct dg_ctx {
+    int device;
+    hipStream_t stream;
+    uint8_t *ws_fast = nullptr;
+    uint64_t ws_fast_lanes = 0;
+    uint32_t *d_deep_count = nullptr;
+    uint64_t *d_deep_list = nullptr;
+    uint8_t *ws_deep = nullptr;
+    uint32_t *d_pending = nullptr;
+    std::mutex mu;
+    /* staging for the host API */
+    uint8_t *d_json = nullptr; uint64_t d_json_cap = 0;
+    uint64_t *d_in_off = nullptr; uint64_t d_in_cap = 0;
+    uint8_t *d_out = nullptr; uint64_t d_out_cap = 0;
+    uint64_t *d_out_off = nullptr; uint64_t d_oo_cap = 0;
+    uint32_t *d_out_len = nullptr; uint64_t d_ol_cap = 0;
+    uint64_t *d_ret = nullptr; uint64_t d_ret_cap = 0;
+};
+
+struct dg_desc {
+    dg_ctx *ctx;
+    uint8_t *d_blob;
+    size_t len;
+    dg_desc_hdr hdr;
+    DescView view;
+};
+
+static const uint64_t FAST_WS_STRIDE = DCAP + WS_KEYCAP + (uint64_t)WS_REQCAP * 8;
+static const uint64_t DEEP_WS_STRIDE = DCAP + DEEP_KEYCAP + (uint64_t)DEEP_REQCAP * 8 +
+                                       (uint64_t)MAX_RECURSE * sizeof(Frame) + MAX_RECURSE / 8;
+
+template <class T>
+static int grow(T *&p, uint64_t &cap, uint64_t want)
+{
+    if (cap >= want) return DG_OK;
+    (void)hipFree(p);
+    p = nullptr;
+    uint64_t nc = std::max<uint64_t>(want, cap * 2);
+    HIPCHK(hipMalloc(&p, nc * sizeof(T)));
+    cap = nc;
+    return DG_OK;
+}
+
+extern "C" {
+
+const char *dg_last_error(void) { return g_err; }
+
+int dg_ctx_create(int device, dg_ctx **out)
+{
+    if (!out) return set_err(DG_E_INVALID, "null out");
+    int ndev = 0;
+    HIPCHK(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return set_err(DG_E_INVALID, "device %d out of range (%d)", device, ndev);
+    HIPCHK(hipSetDevice(device));
+    dg_ctx *c = new dg_ctx();
+    c->device = device;
+    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIPCHK(hipMalloc(&c->ws_deep, DEEP_WS_STRIDE * DEEP_THREADS));
+    HIPCHK(hipMalloc(&c->d_pending, 16));
+    HIPCHK(hipMalloc(&c->d_deep_count, 16));
+    *out = c;
+    return DG_OK;
+}
+
+void dg_ctx_destroy(dg_ctx *c)
+{
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipFree(c->ws_fast);
+    (void)hipFree(c->ws_deep);
+    (void)hipFree(c->d_pending);
+    (void)hipFree(c->d_deep_count);
+    (void)hipFree(c->d_deep_list);
+    (void)hipFree(c->d_json);
+    (void)hipFree(c->d_in_off);
+    (void)hipFree(c->d_out);
+    (void)hipFree(c->d_out_off);
+    (void)hipFree(c->d_out_len);
+    (void)hipFree(c->d_ret);
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+void *dg_ctx_stream(dg_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
+static int desc_finish(dg_ctx *c, const dg_desc_hdr &h, uint8_t *d_blob, size_t len, dg_desc **out)
+{
+    if (h.magic != DG_DESC_MAGIC || h.version != DG_DESC_VERSION || h.total_len > len)
+        return set_err(DG_E_DESC, "bad descriptor blob header");
+    dg_desc *d = new dg_desc();
+    d->ctx = c;
+    d->d_blob = d_blob;
+    d->len = len;
+    d->hdr = h;
+    d->view.T = (const dg_type *)(d_blob + h.off_types);
+    d->view.S = (const dg_struct *)(d_blob + h.off_structs);
+    d->view.F = (const dg_field *)(d_blob + h.off_fields);
+    d->view.N = (const dg_name *)(d_blob + h.off_names);
+    d->view.R = (const uint64_t *)(d_blob + h.off_reqwords);
+    d->view.P = d_blob + h.off_pool;
+    *out = d;
+    return DG_OK;
+}
+
+int dg_desc_create(dg_ctx *c, const void *blob, size_t len, dg_desc **out)
+{
+    if (!c || !blob || !out || len < sizeof(dg_desc_hdr)) return set_err(DG_E_INVALID, "bad args");
+    dg_desc_hdr h;
+    memcpy(&h, blob, sizeof h);
+    if (h.magic != DG_DESC_MAGIC || h.total_len > len) return set_err(DG_E_DESC, "bad descriptor blob");
+    HIPCHK(hipSetDevice(c->device));
+    uint8_t *d_blob;
+    HIPCHK(hipMalloc(&d_blob, len));
+    HIPCHK(hipMemcpy(d_blob, blob, len, hipMemcpyHostToDevice));
+    return desc_finish(c, h, d_blob, len, out);
+}
+
+int dg_desc_create_device(dg_ctx *c, const void *d_src, size_t len, dg_desc **out)
+{
+    if (!c || !d_src || !out || len < sizeof(dg_desc_hdr)) return set_err(DG_E_INVALID, "bad args");
+    HIPCHK(hipSetDevice(c->device));
+    uint8_t *d_blob;
+    HIPCHK(hipMalloc(&d_blob, len));
+    HIPCHK(hipMemcpy(d_blob, d_src, len, hipMemcpyDeviceToDevice));
+    dg_desc_hdr h;
+    HIPCHK(hipMemcpy(&h, d_blob, sizeof h, hipMemcpyDeviceToHost));
+    return desc_finish(c, h, d_blob, len, out);
+}
+
+void dg_desc_destroy(dg_desc *d)
+{
+    if (!d) return;
+    (void)hipFree(d->d_blob);
+    delete d;
+}
+
+uint32_t dg_desc_root(const dg_desc *d) { return d ? d->hdr.root_type : 0; }
+
+uint64_t dg_slot_bound(uint64_t len) { return 4 * len + 64; }
+
+static int ensure_fast_ws(dg_ctx *c, uint64_t lanes)
+{
+    if (c->ws_fast_lanes >= lanes) return DG_OK;
+    (void)hipFree(c->ws_fast);
+    (void)hipFree(c->d_deep_list);
+    c->ws_fast = nullptr;
+    c->d_deep_list = nullptr;
+    uint64_t want = std::max<uint64_t>(lanes, 1 << 16);
+    HIPCHK(hipMalloc(&c->ws_fast, want * FAST_WS_STRIDE));
+    HIPCHK(hipMalloc(&c->d_deep_list, want * 8));
+    c->ws_fast_lanes = want;
+    return DG_OK;
+}
+
+static int launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *json, const uint64_t *in_off,
+                  uint64_t n, uint64_t flags, uint8_t *out, const uint64_t *out_off, uint32_t *out_len,
+                  uint64_t *ret, uint32_t *pending, hipStream_t s)
+{
+    if (n == 0) return DG_OK;
+    if (root >= d->hdr.n_types) return set_err(DG_E_INVALID, "root type %u out of range", root);
+    int rc = ensure_fast_ws(c, n);
+    if (rc) return rc;
+    Params P;
+    P.D = d->view;
+    P.root = root;
+    P.json = json;
+    P.in_off = in_off;
+    P.n = n;
+    P.flag = flags;
+    P.out = out;
+    P.out_off = out_off;
+    P.out_len = out_len;
+    P.ret = ret;
+    P.pending = pending;
+    P.deep_count = c->d_deep_count;
+    P.deep_list = c->d_deep_list;
+    P.ws = c->ws_fast;
+    P.ws_stride = FAST_WS_STRIDE;
+    P.keycap = WS_KEYCAP;
+    P.reqcap = WS_REQCAP;
+    uint64_t blocks = (n + 255) / 256;
+    HIPCHK(hipMemsetAsync(c->d_deep_count, 0, 16, s));
+    hipLaunchKernelGGL(j2t_lane_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, P);
+    HIPCHK(hipGetLastError());
+    Params Q = P;
+    Q.ws = c->ws_deep;
+    Q.ws_stride = DEEP_WS_STRIDE;
+    Q.keycap = DEEP_KEYCAP;
+    Q.reqcap = DEEP_REQCAP;
+    hipLaunchKernelGGL(j2t_deep_kernel, dim3(DEEP_THREADS / 64), dim3(64), 0, s, Q);
+    HIPCHK(hipGetLastError());
+    return DG_OK;
+}
+
+int dg_j2t_batch_device(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *d_json, const uint64_t *d_in_off,
+                        uint64_t n, uint64_t flags, uint8_t *d_out, const uint64_t *d_out_off, uint32_t *d_out_len,
+                        uint64_t *d_ret, uint32_t *d_pending, void *stream)
+{
+    if (!c || !d) return set_err(DG_E_INVALID, "null ctx/desc");
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    return launch(c, d, root, d_json, d_in_off, n, flags, d_out, d_out_off, d_out_len, d_ret, d_pending, s);
+}
+
+int dg_j2t_batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *json, const uint64_t *in_off,
+                      uint64_t n, uint64_t flags, uint8_t *out, uint64_t out_cap, uint64_t *out_off, uint64_t *ret,
+                      uint64_t *out_need)
+{
+    if (!c || !d || (!json && n) || !in_off || !out_off || (!ret && n)) return set_err(DG_E_INVALID, "bad args");
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    int rc;
+    uint64_t base = in_off[0], bytes = in_off[n] - in_off[0];
+    std::vector<uint64_t> ioff(n + 1), soff(n + 1);
+    soff[0] = 0;
+    for (uint64_t i = 0; i <= n; i++) ioff[i] = in_off[i] - base;
+    for (uint64_t i = 0; i < n; i++) soff[i + 1] = soff[i] + dg_slot_bound(ioff[i + 1] - ioff[i]);
+    if ((rc = grow(c->d_json, c->d_json_cap, bytes + 64))) return rc;
+    if ((rc = grow(c->d_in_off, c->d_in_cap, n + 1))) return rc;
+    if ((rc = grow(c->d_out, c->d_out_cap, soff[n] + 64))) return rc;
+    if ((rc = grow(c->d_out_off, c->d_oo_cap, n + 1))) return rc;
+    if ((rc = grow(c->d_out_len, c->d_ol_cap, n + 1))) return rc;
+    if ((rc = grow(c->d_ret, c->d_ret_cap, n + 1))) return rc;
+    hipStream_t s = c->stream;
+    HIPCHK(hipMemcpyAsync(c->d_json, json + base, bytes, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemsetAsync(c->d_json + bytes, 0, 64, s));
+    HIPCHK(hipMemcpyAsync(c->d_in_off, ioff.data(), (n + 1) * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->d_out_off, soff.data(), (n + 1) * 8, hipMemcpyHostToDevice, s));
+    if ((rc = launch(c, d, root, c->d_json, c->d_in_off, n, flags, c->d_out, c->d_out_off, c->d_out_len, c->d_ret,
+                     nullptr, s)))
+        return rc;
+    std::vector<uint32_t> olen(n);
+    HIPCHK(hipMemcpyAsync(ret, c->d_ret, n * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(olen.data(), c->d_out_len, n * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    /* overflowed messages: rerun each with an exact-size slot (GPU) */
+    std::vector<uint64_t> redo;
+    for (uint64_t i = 0; i < n; i++)
+        if ((uint8_t)ret[i] == DG_ST_OUT_OVERFLOW) redo.push_back(i);
+    std::vector<std::vector<uint8_t>> redo_out(redo.size());
+    for (size_t k = 0; k < redo.size(); k++) {
+        uint64_t i = redo[k];
+        uint64_t need = ret[i] >> 40;
+        uint64_t one_in[2] = {0, ioff[i + 1] - ioff[i]};
+        uint64_t one_out[2] = {0, need + 64};
+        uint8_t *d1;
+        uint64_t *d_io, *d_oo, *d_r;
+        uint32_t *d_ol;
+        HIPCHK(hipMalloc(&d1, one_out[1]));
+        HIPCHK(hipMalloc(&d_io, 16));
+        HIPCHK(hipMalloc(&d_oo, 16));
+        HIPCHK(hipMalloc(&d_r, 8));
+        HIPCHK(hipMalloc(&d_ol, 4));
+        HIPCHK(hipMemcpyAsync(d_io, one_in, 16, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(d_oo, one_out, 16, hipMemcpyHostToDevice, s));
+        rc = launch(c, d, root, c->d_json + ioff[i], d_io, 1, flags, d1, d_oo, d_ol, d_r, nullptr, s);
+        if (rc) return rc;
+        uint32_t l1;
+        HIPCHK(hipMemcpyAsync(&ret[i], d_r, 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(&l1, d_ol, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        olen[i] = l1;
+        redo_out[k].resize(l1);
+        if (l1) HIPCHK(hipMemcpy(redo_out[k].data(), d1, l1, hipMemcpyDeviceToHost));
+        (void)hipFree(d1);
+        (void)hipFree(d_io);
+        (void)hipFree(d_oo);
+        (void)hipFree(d_r);
+        (void)hipFree(d_ol);
+    }
+    uint64_t total = 0;
+    out_off[0] = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        if (ret[i] != 0) olen[i] = 0;
+        total += olen[i];
+        out_off[i + 1] = total;
+    }
+    if (out_need) *out_need = total;
+    if (total > out_cap || (!out && total)) return set_err(DG_E_NOMEM, "output needs %llu bytes", (unsigned long long)total);
+    /* D2H of each slot's used prefix (contiguous runs merged) */
+    std::vector<uint8_t> stage(soff[n]);
+    HIPCHK(hipMemcpy(stage.data(), c->d_out, soff[n], hipMemcpyDeviceToHost));
+    size_t rk = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        if (!olen[i]) continue;
+        if (rk < redo.size() && redo[rk] == i) {
+            memcpy(out + out_off[i], redo_out[rk].data(), olen[i]);
+            rk++;
+        } else {
+            memcpy(out + out_off[i], stage.data() + soff[i], olen[i]);
+        }
+        while (rk < redo.size() && redo[rk] < i) rk++;
+    }
+    return DG_OK;
+}
+
+int dg_j2t_do(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *json, size_t len, uint64_t flags,
+              uint8_t *out, size_t out_cap, size_t *out_len, uint64_t *ret)
+{
+    uint64_t in_off[2] = {0, len};
+    uint64_t oo[2];
+    uint64_t need = 0;
+    static const uint8_t empty = 0;
+    int rc = dg_j2t_batch_host(c, d, root, len ? json : &empty, in_off, 1, flags, out, out_cap, oo, ret, &need);
+    if (out_len) *out_len = need;
+    return rc;
+}
+
+int dg_bench_device(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *d_json, const uint64_t *d_in_off,
+                    uint64_t n, uint64_t flags, uint8_t *d_out, const uint64_t *d_out_off, uint32_t *d_out_len,
+                    uint64_t *d_ret, int iters, float *ms)
+{
+    if (!c || !d || iters < 1 || !ms) return set_err(DG_E_INVALID, "bad args");
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    HIPCHK(hipEventRecord(e0, c->stream));
+    for (int k = 0; k < iters; k++) {
+        int rc = launch(c, d, root, d_json, d_in_off, n, flags, d_out, d_out_off, d_out_len, d_ret, c->d_pending,
+                        c->stream);
+        if (rc) return rc;
+    }
+    HIPCHK(hipEventRecord(e1, c->stream));
+    HIPCHK(hipEventSynchronize(e1));
+    HIPCHK(hipEventElapsedTime(ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return DG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,136 @@
+/*
+ * dgj2t.h — C ABI of the MI355X-native batched JSON -> Thrift-binary
+ * transcoder (the conv/j2t hot path of cloudwego/dynamicgo).
+ *
+ * Boundary replaced (reference, Go -> machine code, no cgo):
+ *   J2T_FSM(fsm *types.J2TStateMachine, buf *[]byte, src *string, flag uint64) uint64
+ *     internal/native/dispatch_amd64.go:66-68
+ *   -> uint64_t j2t_fsm_exec(J2TStateMachine*, GoSlice *buf, const GoString *src, uint64_t flag)
+ *     native/thrift.h:202, native/thrift.c:765-1187
+ * and the Go prelude/epilogue around it (BinaryConv.do conv/j2t/impl.go:38-91,
+ * BinaryConv.Do conv/j2t/conv.go:53-77).
+ *
+ * The reference converts ONE message per call, reading Go descriptor structs
+ * in place. This ABI converts a BATCH: a JSON arena with n+1 offsets, against a
+ * descriptor flattened once (include/dgj2t_desc.h) and kept resident on the
+ * device. Per message it returns the Thrift bytes and the reference's packed
+ * status word, bit-identical: code bits 0-7 | pos bits 8-39 | value bits 40-63
+ * (native/thrift.h:223-242, decoded by explainNativeError
+ * conv/j2t/impl_amd64.go:261-298), 0 = success.
+ *
+ * Flags are the reference's j2t flag word (native/thrift.h:23-32,
+ * conv/j2t/conv.go:98-127 toFlags). DG_F_VALIDATE_UTF8 is an opt-in extension
+ * (bit 16) that the reference does not have; off by default.
+ *
+ * All functions return 0 on success and a negative DG_E_* on API failure;
+ * dg_last_error() describes the last failure of the calling thread.
+ */
+#ifndef DGJ2T_H
+#define DGJ2T_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* j2t flag bits (reference native/thrift.h:23-32) */
+#define DG_F_ALLOW_UNKNOWN (1ull << 0)
+#define DG_F_WRITE_DEFAULT (1ull << 1)
+#define DG_F_ENABLE_VM (1ull << 2)
+#define DG_F_ENABLE_HM (1ull << 3)
+#define DG_F_ENABLE_I2S (1ull << 4)
+#define DG_F_WRITE_REQUIRE (1ull << 5)
+#define DG_F_NO_BASE64 (1ull << 6)
+#define DG_F_WRITE_OPTIONAL (1ull << 7)
+#define DG_F_TRACE_BACK (1ull << 8)
+#define DG_F_NO_WRITE_BASE (1ull << 9)
+#define DG_F_VALIDATE_UTF8 (1ull << 16) /* extension: reject invalid UTF-8 in strings */
+
+/* library-internal per-message statuses (code byte values the reference never
+ * produces). The host entry points resolve them before returning; the device
+ * entry point leaves them for the caller and counts them in *d_pending. */
+#define DG_ST_OUT_OVERFLOW 0xF0u /* slot too small; value bits = bytes needed */
+#define DG_ST_DEEP 0xF1u         /* (internal) nesting beyond the fast kernel's stack */
+
+/* API error codes */
+#define DG_OK 0
+#define DG_E_INVALID (-1)
+#define DG_E_HIP (-2)
+#define DG_E_NOMEM (-3)
+#define DG_E_DESC (-4)
+
+typedef struct dg_ctx dg_ctx;
+typedef struct dg_desc dg_desc;
+
+/* Per-thread description of the last failure. */
+const char *dg_last_error(void);
+
+/* A context owns one HIP device, a stream and device workspaces. */
+int dg_ctx_create(int device, dg_ctx **out);
+void dg_ctx_destroy(dg_ctx *ctx);
+/* The context's HIP stream (hipStream_t), for callers that order their own work. */
+void *dg_ctx_stream(dg_ctx *ctx);
+
+/* Upload a dg_desc v1 blob (include/dgj2t_desc.h) to the context's device.
+ * Replaces reading the Go *thrift.TypeDescriptor graph in place
+ * (native/thrift.h:70-137 <-> thrift/descriptor.go:119-267). */
+int dg_desc_create(dg_ctx *ctx, const void *blob, size_t len, dg_desc **out);
+/* Same, for a blob already resident in device memory (e.g. received by an
+ * RCCL broadcast on a non-root rank). */
+int dg_desc_create_device(dg_ctx *ctx, const void *d_blob, size_t len, dg_desc **out);
+void dg_desc_destroy(dg_desc *desc);
+/* Root type index recorded in the blob header. */
+uint32_t dg_desc_root(const dg_desc *desc);
+
+/*
+ * Device-resident batch: every pointer is device memory of ctx's device.
+ *   d_json      JSON arena (at least in_off[n] + 16 readable bytes)
+ *   d_in_off    n+1 u64 offsets into d_json; message i = [in_off[i], in_off[i+1])
+ *   d_out       output arena; message i may use [out_off[i], out_off[i+1])
+ *   d_out_off   n+1 u64 slot bounds (e.g. prefix sum of dg_slot_bound(len))
+ *   d_out_len   n u32: Thrift bytes written for message i (0 on error)
+ *   d_ret       n u64: packed reference status (0 = ok), or DG_ST_OUT_OVERFLOW
+ *   d_pending   optional u32 counter (device), incremented once per message
+ *               left with DG_ST_OUT_OVERFLOW; may be NULL
+ * Enqueued on ctx's stream (or `stream` if non-NULL); asynchronous.
+ * Equivalent, per message, to BinaryConv.Do(ctx, desc, jbytes)
+ * (conv/j2t/conv.go:53-77) with the given flags.
+ */
+int dg_j2t_batch_device(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, const uint8_t *d_json,
+                        const uint64_t *d_in_off, uint64_t n, uint64_t flags, uint8_t *d_out,
+                        const uint64_t *d_out_off, uint32_t *d_out_len, uint64_t *d_ret,
+                        uint32_t *d_pending, void *stream);
+
+/* Output-slot size the device path uses by default for a message of len bytes. */
+uint64_t dg_slot_bound(uint64_t len);
+
+/*
+ * Host batch (pinned or pageable host memory): H2D, kernels, overflow reruns,
+ * D2H with the outputs compacted. On return out holds the n outputs back to
+ * back: message i is out[out_off[i], out_off[i+1]) (empty on error, see ret).
+ * out_cap must be >= the total; *out_need receives the total required (if the
+ * call returns DG_E_NOMEM because out_cap was too small, retry with it).
+ */
+int dg_j2t_batch_host(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, const uint8_t *json,
+                      const uint64_t *in_off, uint64_t n, uint64_t flags, uint8_t *out, uint64_t out_cap,
+                      uint64_t *out_off, uint64_t *ret, uint64_t *out_need);
+
+/* One message, BinaryConv.Do semantics (conv/j2t/conv.go:53-77). *out_len is
+ * the Thrift length; returns the packed status word through *ret. */
+int dg_j2t_do(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, const uint8_t *json, size_t len,
+              uint64_t flags, uint8_t *out, size_t out_cap, size_t *out_len, uint64_t *ret);
+
+/* Timing helper for benchmarks: launch the device batch `iters` times on the
+ * context stream bracketed by HIP events; returns total milliseconds of GPU
+ * time in *ms (events are recorded on the stream the kernels run on). */
+int dg_bench_device(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, const uint8_t *d_json,
+                    const uint64_t *d_in_off, uint64_t n, uint64_t flags, uint8_t *d_out,
+                    const uint64_t *d_out_off, uint32_t *d_out_len, uint64_t *d_ret, int iters,
+                    float *ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DGJ2T_H */

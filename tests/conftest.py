@@ -1,0 +1,44 @@
+import json
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests"), os.path.join(ROOT, "tests", "golden")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP kernels)")
+
+
+class _Flat:
+    def __init__(self, blob, root):
+        self.blob = blob
+        self.root_type = root
+
+
+@pytest.fixture(scope="session")
+def golden():
+    """(rows, flats): the reference-generated fixtures."""
+    with open(os.path.join(GOLDEN, "descs.json")) as fh:
+        d = json.load(fh)
+    flats = {k: _Flat(bytes.fromhex(v["blob"]), v["root"]) for k, v in d.items()}
+    rows = []
+    with open(os.path.join(GOLDEN, "j2t_golden.jsonl")) as fh:
+        for line in fh:
+            r = json.loads(line)
+            rows.append((r["desc"], r["flags"], bytes.fromhex(r["json"]), r["ret"], bytes.fromhex(r["out"])))
+    return rows, flats
+
+
+def gpu_available():
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:
+        return False

@@ -1,0 +1,70 @@
+"""CPU: the oracle restatement against the reference-generated golden vectors
+(and against the reference engine itself when oracle/_ref is built)."""
+import random
+
+import pytest
+
+import oracle
+import fuzz
+from dynamicgo_amd import thrift as T
+from schemas import probe, idl_desc
+
+
+def test_port_oracle_matches_golden(golden):
+    rows, flats = golden
+    port = oracle.PortOracle()
+    bad = []
+    for name, flags, js, ret, out in rows:
+        r, o = port.j2t(flats[name], js, flags)
+        if r != ret or o != out:
+            bad.append((name, flags, js[:80], hex(r), hex(ret)))
+    assert not bad, bad[:5]
+
+
+def test_ref_oracle_matches_golden(golden):
+    ref = oracle.RefOracle()
+    if ref is None:
+        pytest.skip("oracle/_ref not built")
+    rows, flats = golden
+    for name, flags, js, ret, out in rows:
+        r, o = ref.j2t(flats[name], js, flags)
+        assert (r, o) == (ret, out), (name, flags, js[:80])
+
+
+def test_appendix_d_known_answers(golden):
+    """SURVEY.md Appendix D vectors, captured from the reference engine."""
+    rows, _ = golden
+    want = {
+        b'{"A":1,"A":2}': (0, "080001000000010800010000000200"),
+        b'{"D":"xxx"}': (0x30000000a0e, ""),
+        b'{"A":01}': (0x31020000000702, ""),
+        b'{"E":1e400}': (0x50000000a08, ""),
+        b'{"C":[1.0e2, -9223372036854775808, 9223372036854775808]}':
+            (0, "0f00030a0000000300000000000000648000000000000000800000000000000000"),
+        b'{"A":"7"}': (0, "06000100070700"),
+    }
+    got = {js: (ret, out.hex()) for _, _, js, ret, out in rows if js in want}
+    assert got == want
+
+
+def test_reference_payload_sizes(golden):
+    """introduction.md:101,103 — Simple 114 B, Nesting 6455 B of Thrift."""
+    rows, _ = golden
+    sizes = {(n, len(js)): len(out) for n, f, js, r, out in rows if n in ("simple", "nesting") and f == 1 and r == 0}
+    assert sizes[("simple", 236)] == 114
+    assert sizes[("nesting", 11855)] == 6455
+
+
+@pytest.mark.parametrize("seed", [11, 12])
+def test_port_vs_reference_fuzz(seed):
+    ref = oracle.RefOracle()
+    if ref is None:
+        pytest.skip("oracle/_ref not built")
+    port = oracle.PortOracle()
+    rng = random.Random(seed)
+    for td in (probe("D2"), idl_desc("baseline.thrift", "NestingMethod"), idl_desc("example3.thrift", "ExampleMethod")):
+        fl = T.flatten(td)
+        for _ in range(400):
+            m = fuzz.gen_message(rng, td)
+            flags = rng.choice([1, 0, 0x11, 0x5, 0x23, 0x83])
+            assert ref.j2t(fl, m, flags) == port.j2t(fl, m, flags), (m, flags)
