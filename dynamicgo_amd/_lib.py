@@ -30,6 +30,13 @@ def lib() -> C.CDLL:
     if not os.path.exists(LIB_PATH):
         raise DGError(f"{LIB_PATH} missing: the HIP transcoder is not built "
                       "(run __graft_entry__.build() or python -m dynamicgo_amd.build)")
+    # One HIP runtime per process: torch ships its own libamdhip64 (soname
+    # libamdhip64.so.7, file libamdhip64.so). Loading torch first makes our
+    # NEEDED libamdhip64.so.7 resolve to that copy instead of a second runtime.
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
     L = C.CDLL(LIB_PATH)
     vp, u32, u64, sz, i32 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_size_t, C.c_int
     P64 = C.POINTER(C.c_uint64)
