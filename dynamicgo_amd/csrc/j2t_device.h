@@ -61,62 +61,189 @@ struct DescView {
     const uint8_t *P;
 };
 
+/* J2TState (native/thrift.h:164-170) without jp (no re-entry): 16 bytes.
+ * u = J2TExtra: container {bp: low 32, size: high 32}; struct {inline
+ * requires bits, or arena offset in the low 32}; field {field index}. */
 struct Frame {
-    uint32_t st;   /* J_* | ST_* */
-    uint32_t td;   /* type index */
-    uint32_t bp;   /* J2TExtra_Cont.bp: output offset of the size word */
-    uint32_t size; /* J2TExtra_Cont.size */
-    uint64_t reqs; /* J2TExtra_Struct.reqs: inline bits (req_words == 1) */
-    uint32_t roff; /* ... or offset into the lane's reqs arena (req_words > 1) */
-    uint32_t f;    /* J2TExtra_Field.f: global field index */
+    uint32_t st; /* J_* | ST_* */
+    uint32_t td; /* type index */
+    uint64_t u;
 };
+template <class FR> DGI uint32_t fbp(const FR &x) { return (uint32_t)x.u; }
+template <class FR> DGI uint32_t fsize(const FR &x) { return (uint32_t)(x.u >> 32); }
+template <class FR> DGI void set_size(FR &x, uint32_t v) { x.u = (x.u & 0xffffffffull) | ((uint64_t)v << 32); }
+typedef __attribute__((address_space(3))) Frame LFrame;
+
+/* address-space-typed pointers: LDS (ds_*) or global (global_*), never flat */
+typedef __attribute__((address_space(1))) uint8_t gu8;
+typedef __attribute__((address_space(1))) uint64_t gu64;
+typedef const __attribute__((address_space(3))) uint64_t lds_u64;
+typedef const __attribute__((address_space(1))) uint64_t glb_u64;
 
 /* Per-lane workspace in device memory (rare paths only). */
 struct Workspace {
-    uint8_t *dbuf;     /* 800 B big-decimal digits (internal/types/types.go:268) */
-    uint8_t *keybuf;   /* unquoted-key buffer (reference key cache) */
+    gu8 *dbuf;     /* 800 B big-decimal digits (internal/types/types.go:268) */
+    gu8 *keybuf;   /* unquoted-key buffer (reference key cache) */
     uint32_t keycap;
-    uint64_t *reqarena;/* multi-word requires bitmaps */
+    gu64 *reqarena;/* multi-word requires bitmaps */
     uint32_t reqcap;   /* words */
-    Frame *frames;     /* deep stack (deep kernel only) */
-    uint64_t *skipbits;/* deep skip stack (deep kernel only) */
 };
 
-struct Src {
-    const uint8_t *s;
+
+/* One message's bytes, read through a cached, aligned 8-byte window. `w8` is
+ * the 8-aligned word at or below the message start, `off0` the start's byte
+ * offset from it. Reads at i >= n yield 0. Whole aligned words are read, so
+ * up to 7 bytes before/after the message must be readable (arena padding). */
+template <class W>
+struct SrcT {
+    const W *w8;
+    int64_t off0;
     int64_t n;
-    DGI uint8_t at(int64_t i) const { return (uint64_t)i < (uint64_t)n ? s[i] : 0; }
+    int64_t tag;
+    uint64_t word;
+    DGI void init(const W *words, int64_t off, int64_t len)
+    {
+        w8 = words;
+        off0 = off;
+        n = len;
+        tag = -1;
+        word = 0;
+    }
+    DGI uint64_t wordk(int64_t k)
+    {
+        if (k != tag) {
+            tag = k;
+            word = w8[k];
+        }
+        return word;
+    }
+    DGI uint8_t raw(int64_t i)
+    {
+        int64_t b = off0 + i;
+        return (uint8_t)(wordk(b >> 3) >> ((b & 7) << 3));
+    }
+    DGI uint8_t at(int64_t i) { return (uint64_t)i < (uint64_t)n ? raw(i) : 0; }
+    /* 8 bytes at [i, i+8) (caller guarantees i + 8 <= n), first byte lowest */
+    DGI uint64_t get8(int64_t i)
+    {
+        int64_t b = off0 + i;
+        int64_t k = b >> 3;
+        uint32_t sh = (uint32_t)(b & 7) << 3;
+        uint64_t lo = wordk(k);
+        if (sh == 0) return lo;
+        uint64_t hi = wordk(k + 1);
+        return (lo >> sh) | (hi << (64 - sh));
+    }
+    /* sub-view [s0, s0+len) of this message (same memory) */
+    DGI SrcT sub(int64_t s0, int64_t len) const
+    {
+        SrcT r;
+        r.init(w8, off0 + s0, len);
+        return r;
+    }
 };
 
-/* Thrift output with a hard slot bound: writes past `cap` are dropped, `len`
- * keeps counting (the required size is reported on overflow). */
+/* exact per-byte zero flags (0x80 in each zero byte, no false positives) */
+DGI uint64_t zbytes(uint64_t v)
+{
+    const uint64_t M = 0x7F7F7F7F7F7F7F7Full;
+    return ~(((v & M) + M) | v | M);
+}
+
+/* Thrift output with a hard slot bound and 8-byte write combining.
+ * Bytes are assembled in `wbuf` (the word holding position len) and stored
+ * as whole aligned words; back-patches of already-stored words (list/map
+ * sizes, string lengths) go straight to memory. Writes past `cap` are
+ * dropped while `len` keeps counting: the required size is reported on
+ * overflow. */
 struct Out {
-    uint8_t *b;
+    gu8 *b;
     uint64_t cap;
     uint64_t len;
-    DGI void put(uint64_t pos, uint8_t v) { if (pos < cap) b[pos] = v; }
-    DGI uint64_t alloc(uint64_t k) { uint64_t s = len; len += k; return s; }
-    DGI void w8(uint8_t v) { put(len, v); len++; }
-    DGI void w16(uint16_t v) { put(len, v >> 8); put(len + 1, (uint8_t)v); len += 2; }
-    DGI void put32(uint64_t at, uint32_t v)
+    uint64_t wbuf;
+    bool wide; /* slot base 8-aligned: word stores allowed */
+
+    DGI void init(uint8_t *base, uint64_t c)
     {
-        if (at + 4 <= cap) {
-            b[at] = v >> 24; b[at + 1] = v >> 16; b[at + 2] = v >> 8; b[at + 3] = v;
+        b = (gu8 *)(void *)base;
+        cap = c;
+        len = 0;
+        wbuf = 0;
+        wide = ((uintptr_t)base & 7) == 0;
+    }
+    DGI void store_word(uint64_t wi, uint64_t v)
+    {
+        uint64_t a = wi << 3;
+        if (wide && a + 8 <= cap) {
+            *(gu64 *)(b + a) = v;
         } else {
-            put(at, v >> 24); put(at + 1, v >> 16); put(at + 2, v >> 8); put(at + 3, v);
+            for (int k = 0; k < 8; k++)
+                if (a + k < cap) b[a + k] = (uint8_t)(v >> (8 * k));
         }
     }
-    DGI void w32(uint32_t v) { put32(len, v); len += 4; }
-    DGI void w64(uint64_t v) { put32(len, (uint32_t)(v >> 32)); put32(len + 4, (uint32_t)v); len += 8; }
-    DGI void wbytes(const uint8_t *p, uint64_t n)
+    DGI uint64_t load_word(uint64_t wi) const
+    {
+        uint64_t a = wi << 3;
+        if (wide && a + 8 <= cap) return *(const gu64 *)(b + a);
+        uint64_t v = 0;
+        for (int k = 0; k < 8; k++)
+            if (a + k < cap) v |= (uint64_t)b[a + k] << (8 * k);
+        return v;
+    }
+    /* append n (1..8) bytes given little-endian in v (first byte lowest) */
+    DGI void wle(uint64_t v, uint32_t n)
+    {
+        uint32_t used = (uint32_t)(len & 7);
+        uint32_t sh = used << 3;
+        if (n < 8) v &= (1ull << (n << 3)) - 1;
+        uint64_t lo = (wbuf & ((1ull << sh) - 1)) | (v << sh);
+        uint64_t hi = used ? (v >> (64 - sh)) : 0;
+        uint64_t wi = len >> 3;
+        len += n;
+        if (used + n >= 8) {
+            store_word(wi, lo);
+            wbuf = hi;
+        } else {
+            wbuf = lo;
+        }
+    }
+    DGI void w8(uint8_t v) { wle(v, 1); }
+    DGI void w16(uint16_t v) { wle(__builtin_bswap16(v), 2); }
+    DGI void w32(uint32_t v) { wle(__builtin_bswap32(v), 4); }
+    DGI void w64(uint64_t v) { wle(__builtin_bswap64(v), 8); }
+    /* reserve k (<= 8) bytes to be back-patched; returns their position */
+    DGI uint64_t alloc(uint32_t k)
     {
         uint64_t s = len;
-        len += n;
-        if (s + n <= cap) {
-            for (uint64_t i = 0; i < n; i++) b[s + i] = p[i];
-        } else {
-            for (uint64_t i = 0; i < n; i++) put(s + i, p[i]);
+        wle(0, k);
+        return s;
+    }
+    /* overwrite one already-written byte */
+    DGI void patch8(uint64_t q, uint8_t v)
+    {
+        if (q >= (len & ~7ull)) {
+            uint32_t sh = (uint32_t)(q & 7) << 3;
+            wbuf = (wbuf & ~(0xFFull << sh)) | ((uint64_t)v << sh);
+        } else if (q < cap) {
+            b[q] = v;
         }
+    }
+    DGI void put32(uint64_t at, uint32_t v)
+    {
+        patch8(at, v >> 24);
+        patch8(at + 1, v >> 16);
+        patch8(at + 2, v >> 8);
+        patch8(at + 3, v);
+    }
+    /* truncate to x <= len (the reference's buf->len = unwindPos) */
+    DGI void set_len(uint64_t x)
+    {
+        if ((x >> 3) != (len >> 3)) wbuf = (x & 7) ? load_word(x >> 3) : 0;
+        len = x;
+    }
+    DGI void finish()
+    {
+        if (len & 7) store_word(len >> 3, wbuf);
     }
 };
 
@@ -132,14 +259,18 @@ DGI bool isspace_(uint8_t c) { return c == ' ' || c == '\r' || c == '\n' || c ==
 /* advance_ns native/scanning.c:64-105 (+ lspace native/fastbytes.c:25-123):
  * 4 scalar probes, then a scan; note *p is left unchanged when the scan
  * reaches EOF (the reference returns before updating it). */
-DGI uint8_t advance_ns(const Src &s, int64_t &p)
+template <class S>
+DGI uint8_t advance_ns(S &s, int64_t &p)
 {
     int64_t vi = p;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-        if (vi < s.n && !isspace_(s.s[vi])) {
-            p = vi + 1;
-            return s.s[vi];
+        if (vi < s.n) {
+            uint8_t c = s.raw(vi);
+            if (!isspace_(c)) {
+                p = vi + 1;
+                return c;
+            }
         }
         vi++;
     }
@@ -147,14 +278,20 @@ DGI uint8_t advance_ns(const Src &s, int64_t &p)
         p = vi;
         return 0;
     }
-    while (vi < s.n && isspace_(s.s[vi])) vi++;
-    if (vi >= s.n) return 0;
-    p = vi + 1;
-    return s.s[vi];
+    while (vi < s.n) {
+        uint8_t c = s.raw(vi);
+        if (!isspace_(c)) {
+            p = vi + 1;
+            return c;
+        }
+        vi++;
+    }
+    return 0;
 }
 
 /* advance_dword native/scanning.c:107-128 (long vs size_t compare: unsigned) */
-DGI int64_t advance_dword(const Src &s, int64_t &p, int64_t dec, int64_t ret, uint32_t val)
+template <class S>
+DGI int64_t advance_dword(S &s, int64_t &p, int64_t dec, int64_t ret, uint32_t val)
 {
     if ((uint64_t)p > (uint64_t)(s.n + dec - 4)) {
         p = s.n;
@@ -175,20 +312,32 @@ DGI int64_t advance_dword(const Src &s, int64_t &p, int64_t dec, int64_t ret, ui
 }
 
 /* advance_string native/scanning.c:130-375: index after the closing quote;
- * esc = whether a backslash occurs inside the string. */
-DGI int64_t advance_string(const Src &s, int64_t p, bool &esc)
+ * esc = whether a backslash occurs inside the string. 8 bytes per step: the
+ * window word is tested for '"' and '\\' with exact SWAR byte compares. */
+template <class S>
+DGI int64_t advance_string(S &s, int64_t p, bool &esc)
 {
     esc = false;
     if (s.n == p) return -(int64_t)E_EOF;
     int64_t i = p;
     while (i < s.n) {
-        uint8_t c = s.s[i++];
-        if (c == '"') return i;
-        if (c == '\\') {
-            esc = true;
-            if (i >= s.n) return -(int64_t)E_EOF;
-            i++;
+        int64_t b = s.off0 + i;
+        int64_t k = b >> 3;
+        uint64_t w = s.wordk(k);
+        uint64_t m = zbytes(w ^ 0x2222222222222222ull) | zbytes(w ^ 0x5C5C5C5C5C5C5C5Cull);
+        m &= ~0ull << ((b & 7) << 3);
+        int64_t lim = s.n - (k * 8 - s.off0); /* bytes of this word inside the message */
+        if (lim < 8) m &= (1ull << (lim << 3)) - 1;
+        if (m == 0) {
+            i = (k + 1) * 8 - s.off0;
+            continue;
         }
+        int j = __builtin_ctzll(m) >> 3;
+        int64_t pos = k * 8 + j - s.off0;
+        if ((uint8_t)(w >> (j << 3)) == '"') return pos + 1;
+        esc = true;
+        if (pos + 1 >= s.n) return -(int64_t)E_EOF;
+        i = pos + 2;
     }
     return -(int64_t)E_EOF;
 }
@@ -200,12 +349,13 @@ DGI int hexv(uint8_t c)
     if (l >= 'a' && l <= 'f') return l - 'a' + 10;
     return -1;
 }
-DGI bool hex4(const uint8_t *q, uint32_t &v)
+template <class S>
+DGI bool hex4(S &s, int64_t i, uint32_t &v)
 {
     uint32_t r = 0;
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-        int h = hexv(q[i]);
+    for (int k = 0; k < 4; k++) {
+        int h = hexv(s.at(i + k));
         if (h < 0) return false;
         r = (r << 4) | (uint32_t)h;
     }
@@ -213,24 +363,25 @@ DGI bool hex4(const uint8_t *q, uint32_t &v)
     return true;
 }
 
-/* unquote native/parsing.c:702-945 with flags == 0. Writes through `sink`
- * (an Out at a position, or a plain buffer); returns length or -errcode. */
-template <class Sink>
-DGN int64_t unquote(const uint8_t *sp, int64_t nb, Sink &dst)
+/* unquote native/parsing.c:702-945 with flags == 0, over src[s0, s0+nb).
+ * Writes through `dst` (an Out at a position, or a plain buffer); returns
+ * the unquoted length or -errcode. */
+template <class S, class Sink>
+DGI int64_t unquote(S &src, int64_t s0, int64_t nb, Sink &dst)
 {
-    int64_t o = 0;
+    int64_t o = 0, i = s0;
     while (nb > 0) {
-        uint8_t c0 = *sp;
+        uint8_t c0 = src.raw(i);
         if (c0 != '\\') {
             dst(o++, c0);
-            sp++;
+            i++;
             nb--;
             continue;
         }
-        sp += 2;
+        i += 2;
         nb -= 2;
         if (nb < 0) return -(int64_t)E_EOF;
-        uint8_t c = sp[-1];
+        uint8_t c = src.raw(i - 1);
         uint8_t cc;
         switch (c) { /* _UnquoteTab native/parsing.c:565-575 */
         case '/': cc = '/'; break;
@@ -250,8 +401,8 @@ DGN int64_t unquote(const uint8_t *sp, int64_t nb, Sink &dst)
         }
         if (nb < 4) return -(int64_t)E_EOF;
         uint32_t r0, r1;
-        if (!hex4(sp, r0)) return -(int64_t)E_INVAL;
-        sp += 4;
+        if (!hex4(src, i, r0)) return -(int64_t)E_INVAL;
+        i += 4;
         nb -= 4;
         if (r0 <= 0x7f) {
             dst(o++, (uint8_t)r0);
@@ -268,9 +419,9 @@ DGN int64_t unquote(const uint8_t *sp, int64_t nb, Sink &dst)
             dst(o++, 0x80 | (r0 & 0x3f));
             continue;
         }
-        if (nb < 6 || r0 > 0xdbff || sp[0] != '\\' || sp[1] != 'u') return -(int64_t)E_UNICODE;
-        if (!hex4(sp + 2, r1)) return -(int64_t)E_INVAL;
-        sp += 6;
+        if (nb < 6 || r0 > 0xdbff || src.raw(i) != '\\' || src.raw(i + 1) != 'u') return -(int64_t)E_UNICODE;
+        if (!hex4(src, i + 2, r1)) return -(int64_t)E_INVAL;
+        i += 6;
         nb -= 6;
         if (r1 < 0xdc00 || r1 > 0xdfff) return -(int64_t)E_UNICODE;
         r0 = ((r0 - 0xd800) << 10) + (r1 - 0xdc00) + 0x10000;
@@ -284,11 +435,10 @@ DGN int64_t unquote(const uint8_t *sp, int64_t nb, Sink &dst)
 
 struct OutSink {
     Out *o;
-    uint64_t base;
-    DGI void operator()(int64_t i, uint8_t v) { o->put(base + (uint64_t)i, v); }
+    DGI void operator()(int64_t, uint8_t v) { o->w8(v); } /* sequential */
 };
 struct BufSink {
-    uint8_t *b;
+    gu8 *b;
     int64_t cap;
     bool over;
     DGI void operator()(int64_t i, uint8_t v)
@@ -309,14 +459,16 @@ DGI int b64v(uint8_t c)
     return -1;
 }
 
-/* decode_block native/base64.c:539-657; ip/op are offsets. */
-DGI int64_t decode_block(const uint8_t *src, int64_t ie, int64_t &ipp, Out &o, int64_t &op)
+/* decode_block native/base64.c:539-657 over src[s0 + ...]; ipp/op relative;
+ * output appended to o (op counts the decoded bytes). */
+template <class S>
+DGI int64_t decode_block(S &src, int64_t s0, int64_t ie, int64_t &ipp, Out &o, int64_t &op)
 {
     int nb = 0;
     uint32_t v0 = 0;
     int64_t ip = ipp;
     while (nb < 4 && ip < ie) {
-        uint8_t ch = src[ip];
+        uint8_t ch = src.raw(s0 + ip);
         if (ch == '\r' || ch == '\n') {
             ip++;
             continue;
@@ -331,43 +483,47 @@ DGI int64_t decode_block(const uint8_t *src, int64_t ie, int64_t &ipp, Out &o, i
     if (nb < 4) {
         if (ip == ie) return ip - ipp + 1;
         if (nb == 3) {
-            if (src[ip++] != '=') return ip - ipp;
+            if (src.raw(s0 + ip++) != '=') return ip - ipp;
         } else {
             if (ip >= ie - 1) return ip - ipp + 1;
-            if (src[ip++] != '=') return ip - ipp;
-            if (src[ip++] != '=') return ip - ipp;
+            if (src.raw(s0 + ip++) != '=') return ip - ipp;
+            if (src.raw(s0 + ip++) != '=') return ip - ipp;
         }
         if (ip < ie) return ip - ipp + 1;
         v0 <<= 6 * (4 - nb);
     }
-    uint64_t ob = o.len;
-    if (nb >= 4) o.put(ob + op + 2, v0 & 0xff);
-    if (nb >= 3) o.put(ob + op + 1, (v0 >> 8) & 0xff);
-    if (nb >= 2) o.put(ob + op, (v0 >> 16) & 0xff);
+    if (nb >= 2) {
+        /* bytes (v0>>16, v0>>8, v0) of which nb-1 are kept */
+        uint64_t le = ((v0 >> 16) & 0xff) | (((v0 >> 8) & 0xff) << 8) | ((uint64_t)(v0 & 0xff) << 16);
+        o.wle(le, (uint32_t)(nb - 1));
+    } else if (op > 0) {
+        o.set_len(o.len - 1); /* nb == 0 ("==" alone): *opp = op - 1 */
+    }
     ipp = ip;
     op = op + nb - 1;
     return 0;
 }
 
-/* Decodes src[0, nb) at o.len; returns decoded length or (ib - ip - dv) < 0. */
-DGI int64_t b64decode(Out &o, const uint8_t *src, int64_t nb)
+/* Decodes src[s0, s0+nb), appending to o; returns the decoded length or
+ * (ib - ip - dv) < 0 like the reference. */
+template <class S>
+DGI int64_t b64decode(Out &o, S &src, int64_t s0, int64_t nb)
 {
     if (nb == 0) return 0;
     int64_t ip = 0, op = 0;
-    /* fast path: whole 4-char quanta of valid characters (no CR/LF, no pad) */
+    /* whole 4-char quanta of alphabet characters: decode_block on such a
+     * quantum consumes exactly it (the reference's 8/4-byte loops) */
     while (ip + 4 <= nb) {
-        int a = b64v(src[ip]), b = b64v(src[ip + 1]), c = b64v(src[ip + 2]), d = b64v(src[ip + 3]);
+        int a = b64v(src.raw(s0 + ip)), b = b64v(src.raw(s0 + ip + 1));
+        int c = b64v(src.raw(s0 + ip + 2)), d = b64v(src.raw(s0 + ip + 3));
         if ((a | b | c | d) < 0) break;
         uint32_t v = ((uint32_t)a << 18) | ((uint32_t)b << 12) | ((uint32_t)c << 6) | (uint32_t)d;
-        uint64_t at = o.len + op;
-        o.put(at, v >> 16);
-        o.put(at + 1, v >> 8);
-        o.put(at + 2, v);
+        o.wle(((v >> 16) & 0xff) | (((v >> 8) & 0xff) << 8) | ((uint64_t)(v & 0xff) << 16), 3);
         ip += 4;
         op += 3;
     }
     while (ip < nb) {
-        int64_t dv = decode_block(src, nb, ip, o, op);
+        int64_t dv = decode_block(src, s0, nb, ip, o, op);
         if (dv != 0) return -ip - dv;
     }
     return op;
@@ -448,7 +604,7 @@ DGI bool eisel_lemire(uint64_t mant, int exp10, int sgn, double &val)
 /* ---- atof_native: big-decimal slow path native/atof_native.c:17-424 ---- */
 constexpr int DCAP = 800;
 struct Decimal {
-    uint8_t *d;
+    gu8 *d;
     int nd, dp, neg, trunc;
 };
 DGI void dtrim(Decimal &d)
@@ -492,7 +648,7 @@ DGN void right_shift(Decimal &d, uint32_t k)
     d.nd = w;
     dtrim(d);
 }
-DGI bool prefix_is_less(const uint8_t *b, const char *s, int bn)
+DGI bool prefix_is_less(const gu8 *b, const char *s, int bn)
 {
     int i = 0;
     for (; i < bn; i++) {
@@ -557,7 +713,8 @@ DGI int should_roundup(const Decimal &d, int nd)
 __device__ __constant__ static const int POW_TAB[9] = {1, 3, 6, 9, 13, 16, 19, 23, 26};
 
 /* decimal_set + decimal_to_f64 native/atof_native.c:71-416 */
-DGN double atof_native(const Src &src, int64_t s0, int64_t len, uint8_t *dbuf)
+template <class S>
+DGN double atof_native(S src, int64_t s0, int64_t len, gu8 *dbuf)
 {
     Decimal d;
     d.d = dbuf;
@@ -663,7 +820,8 @@ struct JState {
 };
 
 /* vnumber native/scanning.c:958-1083 */
-DGI void vnumber(const Src &src, int64_t &p, JState &ret, uint8_t *dbuf)
+template <class S>
+DGI void vnumber(S &src, int64_t &p, JState &ret, gu8 *dbuf)
 {
     int sgn = 1;
     uint64_t man = 0;
@@ -677,7 +835,7 @@ DGI void vnumber(const Src &src, int64_t &p, JState &ret, uint8_t *dbuf)
         ret.vt = -(int64_t)E_EOF;
         return;
     }
-    uint8_t c = src.s[i];
+    uint8_t c = src.raw(i);
     if (c == '-') {
         i++;
         sgn = -1;
@@ -686,7 +844,7 @@ DGI void vnumber(const Src &src, int64_t &p, JState &ret, uint8_t *dbuf)
             ret.vt = -(int64_t)E_EOF;
             return;
         }
-        c = src.s[i];
+        c = src.raw(i);
     }
     if (c < '0' || c > '9') {
         p = i;
@@ -701,7 +859,7 @@ DGI void vnumber(const Src &src, int64_t &p, JState &ret, uint8_t *dbuf)
         }
     }
     while (i < n) {
-        c = src.s[i];
+        c = src.raw(i);
         if (c < '0' || c > '9') break;
         if (man_nd < 19) {
             man = man * 10 + (c - '0');
@@ -711,7 +869,7 @@ DGI void vnumber(const Src &src, int64_t &p, JState &ret, uint8_t *dbuf)
         i++;
     }
     if (exp10 > 0) trunc = 1;
-    if (i < n && src.s[i] == '.') {
+    if (i < n && src.raw(i) == '.') {
         i++;
         ret.vt = V_DOUBLE;
         if (i >= n) {
@@ -719,7 +877,7 @@ DGI void vnumber(const Src &src, int64_t &p, JState &ret, uint8_t *dbuf)
             ret.vt = -(int64_t)E_EOF;
             return;
         }
-        c = src.s[i];
+        c = src.raw(i);
         if (c < '0' || c > '9') {
             p = i;
             ret.vt = -(int64_t)E_INVAL;
@@ -727,7 +885,7 @@ DGI void vnumber(const Src &src, int64_t &p, JState &ret, uint8_t *dbuf)
         }
     }
     if (man == 0 && exp10 == 0) {
-        while (i < n && src.s[i] == '0') {
+        while (i < n && src.raw(i) == '0') {
             i++;
             exp10--;
         }
@@ -735,7 +893,7 @@ DGI void vnumber(const Src &src, int64_t &p, JState &ret, uint8_t *dbuf)
         man_nd = 0;
     }
     while (i < n && man_nd < 19) {
-        c = src.s[i];
+        c = src.raw(i);
         if (c < '0' || c > '9') break;
         man = man * 10 + (c - '0');
         man_nd++;
@@ -743,12 +901,12 @@ DGI void vnumber(const Src &src, int64_t &p, JState &ret, uint8_t *dbuf)
         i++;
     }
     while (i < n) {
-        c = src.s[i];
+        c = src.raw(i);
         if (c < '0' || c > '9') break;
         trunc = 1;
         i++;
     }
-    if (i < n && (src.s[i] == 'e' || src.s[i] == 'E')) {
+    if (i < n && (src.raw(i) == 'e' || src.raw(i) == 'E')) {
         int esm = 1, exp = 0;
         i++;
         ret.vt = V_DOUBLE;
@@ -757,7 +915,7 @@ DGI void vnumber(const Src &src, int64_t &p, JState &ret, uint8_t *dbuf)
             ret.vt = -(int64_t)E_EOF;
             return;
         }
-        c = src.s[i];
+        c = src.raw(i);
         if (c == '+' || c == '-') {
             esm = c == '+' ? 1 : -1;
             i++;
@@ -766,7 +924,7 @@ DGI void vnumber(const Src &src, int64_t &p, JState &ret, uint8_t *dbuf)
                 ret.vt = -(int64_t)E_EOF;
                 return;
             }
-            c = src.s[i];
+            c = src.raw(i);
         }
         if (c < '0' || c > '9') {
             p = i;
@@ -774,7 +932,7 @@ DGI void vnumber(const Src &src, int64_t &p, JState &ret, uint8_t *dbuf)
             return;
         }
         while (i < n) {
-            c = src.s[i];
+            c = src.raw(i);
             if (c < '0' || c > '9') break;
             if (exp < 10000) exp = exp * 10 + (c - '0');
             i++;
@@ -815,18 +973,19 @@ DGI bool numch(uint8_t c)
 
 /* skip_number native/scanning.c:1317-1535 as the AVX2 build decomposes it:
  * 32-byte blocks while >= 32 bytes remain, then 16-byte blocks, then scalar. */
-DGN int64_t skip_number(const uint8_t *sp, int64_t nb)
+template <class S>
+DGN int64_t skip_number(S src, int64_t base, int64_t nb)
 {
     int64_t di = -1, ei = -1, si = -1;
     int64_t off = 0;
     if (nb == 0) return -1;
-    if (sp[0] == '0' && (nb == 1 || (sp[1] != '.' && sp[1] != 'e' && sp[1] != 'E'))) return 1;
+    if (src.raw(base) == '0' && (nb == 1 || (src.raw(base + 1) != '.' && src.raw(base + 1) != 'e' && src.raw(base + 1) != 'E'))) return 1;
     for (int W = 32; W >= 16; W -= 16) {
         while (nb >= W) {
             uint32_t md = 0, me = 0, ms = 0, v;
             int i = W;
             for (int k = 0; k < W; k++) {
-                uint8_t c = sp[off + k];
+                uint8_t c = src.raw(base + off + k);
                 if (!numch(c)) {
                     i = k;
                     break;
@@ -859,7 +1018,7 @@ DGN int64_t skip_number(const uint8_t *sp, int64_t nb)
         }
     }
     while (nb-- > 0) {
-        uint8_t c = sp[off++];
+        uint8_t c = src.raw(base + off++);
         if (c >= '0' && c <= '9') continue;
         int64_t *iv = c == '.' ? &di : (c == 'e' || c == 'E') ? &ei : (c == '+' || c == '-') ? &si : nullptr;
         if (!iv) {
@@ -878,7 +1037,8 @@ check_index:
     return off;
 }
 
-DGI int64_t skip_string(const Src &s, int64_t &p)
+template <class S>
+DGI int64_t skip_string(S &s, int64_t &p)
 {
     bool esc;
     int64_t q = p - 1;
@@ -898,20 +1058,36 @@ DGI int64_t skip_string(const Src &s, int64_t &p)
 enum { FV = 0, FARR = 1, FOBJ = 2, FKEY = 3, FELEM = 4, FARR0 = 5, FOBJ0 = 6 };
 constexpr int64_t SKIP_DEEP = -0x7fff;
 
-DGN int64_t skip_one(const Src &s, int64_t &p, uint64_t *bits, uint32_t cap)
+struct SkipRes {
+    int64_t r; /* vi >= 0, -errcode, or SKIP_DEEP */
+    int64_t p; /* position after the skip (or at the error) */
+};
+
+/* Levels 0..63 of the container bit-stack live in a register; deeper levels
+ * in `bits` (device workspace, deep pass only). */
+template <class S>
+DGN SkipRes skip_one(S s, int64_t p, gu64 *bits, uint32_t cap)
 {
     uint32_t sp = 1;
     int top = FV;
     int64_t vi = -1;
-    auto below_kind = [&](uint32_t lvl) -> int { return ((bits[lvl >> 6] >> (lvl & 63)) & 1) ? FOBJ : FARR; };
+    uint64_t low = 0;
+    auto below_kind = [&](uint32_t lvl) -> int {
+        uint64_t w = lvl < 64 ? low : bits[(lvl >> 6) - 1];
+        return ((w >> (lvl & 63)) & 1) ? FOBJ : FARR;
+    };
     auto push = [&](int newtop) -> int64_t {
         /* the current top (ARR/OBJ) becomes level sp-1 */
         if (sp >= MAX_RECURSE) return -(int64_t)E_RECURSE_MAX;
         if (sp > cap) return SKIP_DEEP;
         uint32_t lvl = sp - 1;
         uint64_t m = 1ull << (lvl & 63);
-        if (top == FOBJ) bits[lvl >> 6] |= m;
-        else bits[lvl >> 6] &= ~m;
+        if (lvl < 64) {
+            low = top == FOBJ ? (low | m) : (low & ~m);
+        } else {
+            gu64 *w = &bits[(lvl >> 6) - 1];
+            *w = top == FOBJ ? (*w | m) : (*w & ~m);
+        }
         sp++;
         top = newtop;
         return 0;
@@ -934,10 +1110,10 @@ DGN int64_t skip_one(const Src &s, int64_t &p, uint64_t *bits, uint32_t cap)
             }
             if (ch == ',') {
                 int64_t r = push(FV);
-                if (r) return r;
+                if (r) return SkipRes{r, p};
                 continue;
             }
-            return -(int64_t)E_INVAL;
+            return SkipRes{-(int64_t)E_INVAL, p};
         case FOBJ:
             if (ch == '}') {
                 drop();
@@ -945,19 +1121,19 @@ DGN int64_t skip_one(const Src &s, int64_t &p, uint64_t *bits, uint32_t cap)
             }
             if (ch == ',') {
                 int64_t r = push(FKEY);
-                if (r) return r;
+                if (r) return SkipRes{r, p};
                 continue;
             }
-            return -(int64_t)E_INVAL;
+            return SkipRes{-(int64_t)E_INVAL, p};
         case FKEY: {
-            if (ch != '"') return -(int64_t)E_INVAL;
+            if (ch != '"') return SkipRes{-(int64_t)E_INVAL, p};
             top = FELEM;
             int64_t r = skip_string(s, p);
-            if (r < 0) return r;
+            if (r < 0) return SkipRes{r, p};
             continue;
         }
         case FELEM:
-            if (ch != ':') return -(int64_t)E_INVAL;
+            if (ch != ':') return SkipRes{-(int64_t)E_INVAL, p};
             top = FV;
             continue;
         case FARR0:
@@ -975,75 +1151,75 @@ DGN int64_t skip_one(const Src &s, int64_t &p, uint64_t *bits, uint32_t cap)
             if (ch == '"') {
                 top = FOBJ;
                 int64_t r = skip_string(s, p);
-                if (r < 0) return r;
+                if (r < 0) return SkipRes{r, p};
                 r = push(FELEM);
-                if (r) return r;
+                if (r) return SkipRes{r, p};
                 continue;
             }
-            return -(int64_t)E_INVAL;
+            return SkipRes{-(int64_t)E_INVAL, p};
         }
         /* value, with `top` already replaced/dropped as the reference does */
         switch (ch) {
         case '0': case '1': case '2': case '3': case '4':
         case '5': case '6': case '7': case '8': case '9': {
             int64_t i = p - 1; /* skip_positive native/scanning.c:1616-1631 */
-            int64_t r = skip_number(s.s + i, s.n - i);
+            int64_t r = skip_number(s, i, s.n - i);
             if (r < 0) {
                 p -= r + 2;
-                return -(int64_t)E_INVAL;
+                return SkipRes{-(int64_t)E_INVAL, p};
             }
             p += r - 1;
             break;
         }
         case '-': {
             int64_t i = p; /* skip_negative native/scanning.c:1599-1614 */
-            int64_t r = skip_number(s.s + i, s.n - i);
+            int64_t r = skip_number(s, i, s.n - i);
             if (r < 0) {
                 p -= r + 1;
-                return -(int64_t)E_INVAL;
+                return SkipRes{-(int64_t)E_INVAL, p};
             }
             p += r;
             break;
         }
         case 'n': {
             int64_t r = advance_dword(s, p, 1, p - 1, VS_NULL);
-            if (r < 0) return r;
+            if (r < 0) return SkipRes{r, p};
             break;
         }
         case 't': {
             int64_t r = advance_dword(s, p, 1, p - 1, VS_TRUE);
-            if (r < 0) return r;
+            if (r < 0) return SkipRes{r, p};
             break;
         }
         case 'f': {
             int64_t r = advance_dword(s, p, 0, p - 1, VS_ALSE);
-            if (r < 0) return r;
+            if (r < 0) return SkipRes{r, p};
             break;
         }
         case '[': {
             if (sp == 0) { sp = 1; top = FARR0; break; }
             int64_t r = push(FARR0);
-            if (r) return r;
+            if (r) return SkipRes{r, p};
             break;
         }
         case '{': {
             if (sp == 0) { sp = 1; top = FOBJ0; break; }
             int64_t r = push(FOBJ0);
-            if (r) return r;
+            if (r) return SkipRes{r, p};
             break;
         }
         case '"': {
             int64_t r = skip_string(s, p);
-            if (r < 0) return r;
+            if (r < 0) return SkipRes{r, p};
             break;
         }
         case 0:
-            return -(int64_t)E_EOF;
+            return SkipRes{-(int64_t)E_EOF, p};
         default:
-            return -(int64_t)E_INVAL;
+            return SkipRes{-(int64_t)E_INVAL, p};
         }
     }
-    return vi;
+    return SkipRes{vi, p};
 }
 
 }  // namespace dg

@@ -1,13 +1,13 @@
 /*
  * j2t_kernel.hip — the MI355X kernels and the C ABI (include/dgj2t.h).
  *
- * Kernel map:
- *  j2t_lane_kernel  one lane per message, stack of FAST_DEPTH frames in
- *                   registers/scratch; messages that outgrow it are marked
- *                   DG_ST_DEEP and left to
- *  j2t_deep_kernel  a small persistent grid that redoes only the DEEP
- *                   messages with a MAX_RECURSE (4096) stack in workspace.
- * Both run the same templated FSM (Machine<...>::run) that restates
+ * Kernel map (one launch per batch):
+ *  j2t_lane_kernel  one lane per message; the block's JSON span is staged in
+ *                   LDS; stack of FAST_DEPTH frames per lane. Messages that
+ *                   outgrow it are listed as DG_ST_DEEP and the LAST block to
+ *                   finish redoes them (deep_pass) with a MAX_RECURSE (4096)
+ *                   stack in device workspace.
+ * Both run the same templated FSM (Machine<S>::run) that restates
  * j2t_fsm_exec (native/thrift.c:765-1187).
  */
 #include <hip/hip_runtime.h>
@@ -29,7 +29,7 @@ constexpr int FAST_DEPTH = 24;      /* frames per lane in the fast kernel */
 constexpr int FAST_SKIP_WORDS = 1;  /* 64 skip levels */
 constexpr int WS_KEYCAP = 1024;     /* unquoted-key buffer per lane (reference key cache: 1 KB) */
 constexpr int WS_REQCAP = 256;      /* multi-word requires arena per lane (words) */
-constexpr int DEEP_THREADS = 256;   /* persistent lanes of the deep kernel */
+constexpr int DEEP_THREADS = 256;   /* lanes of the deep pass (= LANE_BLOCK) */
 constexpr int DEEP_KEYCAP = 1 << 20;
 constexpr int DEEP_REQCAP = 1 << 16;
 
@@ -52,15 +52,26 @@ struct Params {
     uint32_t keycap, reqcap;
 };
 
-/* The FSM of one message. FRAMES: frame storage (private array or workspace). */
+/* Frame stack: frame k of this lane at base[k * stride] (LDS: frame-major
+ * across the block, so a wave at equal depth touches consecutive slots). */
+template <class FP>
+struct FStack {
+    FP base;
+    uint32_t stride;
+    DGI auto &operator[](uint32_t k) const { return base[k * stride]; }
+};
+
+/* The FSM of one message over source type S (LDS- or global-backed) and
+ * frame storage FP (LDS or device workspace). */
+template <class S, class FP>
 struct Machine {
     DescView D;
-    Src src;
+    S src;
     Out out;
     uint64_t flag;
-    Frame *vt;
+    FStack<FP> vt;
     uint32_t sp, cap;
-    uint64_t *skipbits;
+    gu64 *skipbits;
     uint32_t skipcap;
     Workspace ws;
     uint32_t reqlen;
@@ -73,24 +84,31 @@ struct Machine {
     {
         if (sp >= MAX_RECURSE) return pack(E_RECURSE_MAX, sp, (uint64_t)p);
         if (sp >= cap) return pack0(DG_ST_DEEP, 0);
-        Frame &x = vt[sp++];
+        auto &x = vt[sp++];
         x.st = st;
         x.td = td;
         return 0;
     }
 
     /* requires bits of struct frame x (bm_* native/map.c:134-154) */
-    DGI bool bm_is_set(const Frame &x, const dg_struct &sd, uint32_t k) const
+    template <class FR>
+    DGI bool bm_is_set(const FR &x, const dg_struct &sd, uint32_t k) const
     {
-        if (sd.req_words == 1) return (x.reqs >> k) & 1;
-        return (ws.reqarena[x.roff + (k >> 6)] >> (k & 63)) & 1;
+        if (sd.req_words == 1) return (x.u >> k) & 1;
+        return (ws.reqarena[(uint32_t)x.u + (k >> 6)] >> (k & 63)) & 1;
     }
-    DGI void bm_set_req(Frame &x, const dg_struct &sd, uint32_t k, int req)
+    template <class FR>
+    DGI void bm_set_req(FR &x, const dg_struct &sd, uint32_t k, int req)
     {
-        uint64_t *w = sd.req_words == 1 ? &x.reqs : &ws.reqarena[x.roff + (k >> 6)];
         uint64_t m = 1ull << (k & 63);
-        if (req == DG_REQ_DEFAULT || req == DG_REQ_REQUIRED) *w |= m;
-        else if (req == DG_REQ_OPTIONAL) *w &= ~m;
+        bool set = req == DG_REQ_DEFAULT || req == DG_REQ_REQUIRED;
+        if (!set && req != DG_REQ_OPTIONAL) return;
+        if (sd.req_words == 1) {
+            x.u = set ? (x.u | m) : (x.u & ~m);
+        } else {
+            gu64 *w = &ws.reqarena[(uint32_t)x.u + (k >> 6)];
+            *w = set ? (*w | m) : (*w & ~m);
+        }
     }
 
     /* tb_write_empty native/thrift.c:171-203 */
@@ -123,19 +141,20 @@ struct Machine {
     DGI uint64_t write_default_or_empty(const dg_field &f, int64_t p)
     {
         if (f.dflt_len != DG_NONE) {
-            out.wbytes(D.P + f.dflt_off, f.dflt_len);
+            for (uint32_t i = 0; i < f.dflt_len; i++) out.w8(D.P[f.dflt_off + i]);
             return 0;
         }
         return write_empty(f.type, p);
     }
 
     /* j2t_write_unset_fields native/thrift.c:258-310 */
-    DGN uint64_t write_unset_fields(const Frame &x, const dg_struct &sd, int64_t p)
+    template <class FR>
+    DGI uint64_t write_unset_fields(const FR &x, const dg_struct &sd, int64_t p)
     {
         bool wr = flag & DG_F_WRITE_REQUIRE, wd = flag & DG_F_WRITE_DEFAULT;
         bool wo = flag & DG_F_WRITE_OPTIONAL, tb = flag & DG_F_TRACE_BACK;
         for (uint32_t w = 0; w < sd.req_words; w++) {
-            uint64_t bits = sd.req_words == 1 ? x.reqs : ws.reqarena[x.roff + w];
+            uint64_t bits = sd.req_words == 1 ? x.u : ws.reqarena[(uint32_t)x.u + w];
             while (bits) {
                 uint32_t k = w * 64 + __builtin_ctzll(bits);
                 bits &= bits - 1;
@@ -157,7 +176,8 @@ struct Machine {
     }
 
     /* j2t_number native/thrift.c:312-365 */
-    DGI uint64_t j2t_number(uint32_t td, const Src &s, int64_t &p)
+    template <class S2>
+    DGI uint64_t j2t_number(uint32_t td, S2 &s, int64_t &p)
     {
         int64_t s0 = p;
         vnumber(s, p, jt, ws.dbuf);
@@ -184,16 +204,23 @@ struct Machine {
         int64_t n = e - s0 - 1;
         if (esc) {
             uint64_t lp = out.alloc(4);
-            OutSink sink{&out, out.len};
-            int64_t l = unquote(src.s + s0, n, sink);
+            OutSink sink{&out};
+            int64_t l = unquote(src, s0, n, sink);
             if (l < 0) return pack((uint32_t)-l, (uint64_t)s0, (uint64_t)p);
-            out.len += (uint64_t)l;
             out.put32(lp, (uint32_t)l);
         } else {
             out.w32((uint32_t)n);
-            out.wbytes(src.s + s0, (uint64_t)n);
+            copy_src(s0, n);
         }
         return 0;
+    }
+
+    /* copy src[s0, s0+n) to the output (string bodies, tb_write_string) */
+    DGI void copy_src(int64_t s0, int64_t n)
+    {
+        int64_t i = 0;
+        for (; i + 8 <= n; i += 8) out.wle(src.get8(s0 + i), 8);
+        for (; i < n; i++) out.w8(src.raw(s0 + i));
     }
 
     /* j2t_binary native/thrift.c:401-420 */
@@ -206,29 +233,47 @@ struct Machine {
         p = e;
         int64_t n = e - s0 - 1;
         uint64_t back = out.alloc(4);
-        int64_t l = b64decode(out, src.s + s0, n);
+        int64_t l = b64decode(out, src, s0, n);
         if (l < 0) return pack(E_DECODE_BASE64, (uint64_t)(-l - 1), (uint64_t)p);
-        out.len += (uint64_t)l;
         out.put32(back, (uint32_t)l);
         return 0;
     }
 
+    /* A JSON object key: raw in the source, or unquoted into the lane's key
+     * buffer (the reference's key cache, native/thrift.c:480-498). */
+    struct Key {
+        bool inbuf;
+        int64_t s0;
+        int64_t n;
+        uint32_t hash;
+    };
+    DGI uint8_t key_byte(const Key &k, int64_t i) { return k.inbuf ? ws.keybuf[i] : src.raw(k.s0 + i); }
+
     /* j2t_map_key native/thrift.c:422-447 */
-    DGI uint64_t j2t_map_key(const uint8_t *kp, int64_t kn, uint32_t kt, int64_t p)
+    DGI uint64_t j2t_map_key(const Key &k, uint32_t kt, int64_t p)
     {
         switch (TY(kt).ttype) {
         case DG_T_STRING:
-            out.w32((uint32_t)kn);
-            out.wbytes(kp, (uint64_t)kn);
+            out.w32((uint32_t)k.n);
+            if (k.inbuf) {
+                for (int64_t i = 0; i < k.n; i++) out.w8(ws.keybuf[i]);
+            } else {
+                copy_src(k.s0, k.n);
+            }
             return 0;
         case DG_T_BYTE:
         case DG_T_I16:
         case DG_T_I32:
         case DG_T_I64:
         case DG_T_DOUBLE: {
-            Src tmp{kp, kn};
             int64_t q = 0;
-            return j2t_number(kt, tmp, q);
+            if (k.inbuf) {
+                SrcT<glb_u64> kb;
+                kb.init((glb_u64 *)ws.keybuf, 0, k.n);
+                return j2t_number(kt, kb, q);
+            }
+            S kv = src.sub(k.s0, k.n);
+            return j2t_number(kt, kv, q);
         }
         default:
             return pack(E_UNSUPPORT_THRIFT_TYPE, TY(kt).ttype, (uint64_t)p);
@@ -236,19 +281,17 @@ struct Machine {
     }
 
     /* exact-match field lookup (j2t_find_field_key native/thrift.c:449-468) */
-    DGI int32_t find_field(const dg_struct &sd, const uint8_t *k, int64_t kn) const
+    DGI int32_t find_field(const dg_struct &sd, const Key &k)
     {
-        uint32_t h = DG_NAME_HASH_SEED;
-        for (int64_t i = 0; i < kn; i++) h = DG_NAME_HASH_STEP(h, k[i]);
-        uint32_t j = h & sd.name_mask;
+        uint32_t j = k.hash & sd.name_mask;
         for (;;) {
             const dg_name &nm = D.N[sd.name_begin + j];
             if (nm.field == DG_NONE) return -1;
-            if (nm.hash == h && nm.key_len == (uint32_t)kn) {
+            if (nm.hash == k.hash && nm.key_len == (uint32_t)k.n) {
                 const uint8_t *q = D.P + nm.key_off;
                 bool eq = true;
-                for (int64_t i = 0; i < kn; i++) {
-                    if (q[i] != k[i]) {
+                for (int64_t i = 0; i < k.n; i++) {
+                    if (q[i] != key_byte(k, i)) {
                         eq = false;
                         break;
                     }
@@ -260,54 +303,58 @@ struct Machine {
     }
 
     /* j2t_read_key native/thrift.c:470-504 */
-    DGI uint64_t read_key(int64_t &p, const uint8_t *&kp, int64_t &kn)
+    DGI uint64_t read_key(int64_t &p, Key &k)
     {
         int64_t s0 = p;
         bool esc;
         int64_t e = advance_string(src, s0, esc);
         if (e < 0) return pack((uint32_t)-e, (uint64_t)s0, (uint64_t)p);
         p = e;
-        kn = e - s0 - 1;
-        kp = src.s + s0;
+        k.s0 = s0;
+        k.n = e - s0 - 1;
+        k.inbuf = false;
         if (esc) {
             BufSink sink{ws.keybuf, (int64_t)ws.keycap, false};
-            int64_t l = unquote(kp, kn, sink);
+            int64_t l = unquote(src, s0, k.n, sink);
             if (l < 0) return pack((uint32_t)-l, (uint64_t)s0, (uint64_t)p);
             if (sink.over) return pack0(DG_ST_DEEP, 0);
-            kp = ws.keybuf;
-            kn = l;
+            k.inbuf = true;
+            k.n = l;
         }
+        uint32_t h = DG_NAME_HASH_SEED;
+        for (int64_t i = 0; i < k.n; i++) h = DG_NAME_HASH_STEP(h, key_byte(k, i));
+        k.hash = h;
         return 0;
     }
 
     /* j2t_key native/thrift.c:668-763 */
     DGI uint64_t j2t_key(int64_t &p, uint32_t dc, bool obj0, uint64_t &unwindPos, int32_t &lastField)
     {
-        const uint8_t *kp;
-        int64_t kn;
-        uint64_t r = read_key(p, kp, kn);
+        Key key;
+        uint64_t r = read_key(p, key);
         if (r) return r;
+        int64_t kn = key.n;
         const dg_type &t = TY(dc);
         if (t.ttype == DG_T_MAP) {
             unwindPos = out.len;
-            r = j2t_map_key(kp, kn, t.key, p);
+            r = j2t_map_key(key, t.key, p);
             if (r) return r;
             if (obj0) {
-                vt[sp - 1].size = 0;
+                set_size(vt[sp - 1], 0);
                 return push(J_ELEM, t.elem, p);
             }
-            Frame &x = vt[sp - 1];
+            auto &x = vt[sp - 1];
             x.st = J_ELEM;
             x.td = t.elem;
             return 0;
         }
-        Frame &pex = obj0 ? vt[sp - 1] : vt[sp - 2];
+        auto &pex = vt[obj0 ? sp - 1 : sp - 2];
         const dg_struct &sd = D.S[t.st];
-        int32_t fi = find_field(sd, kp, kn);
+        int32_t fi = find_field(sd, key);
         if (fi < 0 || ((D.F[fi].flags & DG_FF_REQUEST_BASE) && (flag & DG_F_NO_WRITE_BASE))) {
             if (fi < 0 && (flag & DG_F_ALLOW_UNKNOWN) == 0) return pack(E_UNKNOWN_FIELD, (uint64_t)kn, (uint64_t)p);
             if (obj0) return push(J_ELEM | ST_SKIP, DG_NONE, p);
-            Frame &x = vt[sp - 1];
+            auto &x = vt[sp - 1];
             x.st = J_ELEM | ST_SKIP;
             x.td = DG_NONE;
             return 0;
@@ -316,7 +363,7 @@ struct Machine {
         uint32_t k = (uint32_t)fi - sd.field_begin;
         if ((flag & DG_F_ENABLE_HM) && (f.flags & DG_FF_HTTP_MAPPING) && !bm_is_set(pex, sd, k)) {
             if (obj0) return push(J_ELEM | ST_SKIP, f.type, p);
-            Frame &x = vt[sp - 1];
+            auto &x = vt[sp - 1];
             x.st = J_ELEM | ST_SKIP;
             x.td = f.type;
             return 0;
@@ -333,21 +380,20 @@ struct Machine {
             r = push(J_ELEM | vm, f.type, p);
             if (r) return r;
         } else {
-            Frame &x = vt[sp - 1];
+            auto &x = vt[sp - 1];
             x.st = J_ELEM | vm;
             x.td = f.type;
         }
-        vt[sp - 1].f = (uint32_t)fi;
-        /* pex may be vt[sp-2] (obj0) after the push: re-resolve */
-        Frame &px = obj0 ? vt[sp - 2] : vt[sp - 2];
-        bm_set_req(px, sd, k, DG_REQ_OPTIONAL);
+        vt[sp - 1].u = (uint32_t)fi;
+        /* the object frame is vt[sp-2] in both cases once the ELEM is on top */
+        bm_set_req(vt[sp - 2], sd, k, DG_REQ_OPTIONAL);
         return 0;
     }
 
     /* j2t_field_vm native/thrift.c:506-666 */
-    DGN uint64_t field_vm(int64_t &p, const Frame &x)
+    DGI uint64_t field_vm(int64_t &p, uint32_t fidx)
     {
-        const dg_field &f = D.F[x.f];
+        const dg_field &f = D.F[fidx];
         uint8_t ft = TY(f.type).ttype;
         if (f.vm <= DG_VM_INLINE_MAX) {
             out.w8(ft);
@@ -373,7 +419,7 @@ struct Machine {
             switch (ft) {
             case DG_T_STRING:
                 out.w32((uint32_t)(p - s0));
-                out.wbytes(src.s + s0, (uint64_t)(p - s0));
+                copy_src(s0, p - s0);
                 return 0;
             case DG_T_I64: out.w64(isint ? (uint64_t)jt.iv : (uint64_t)cvt64(jt.dv)); break;
             case DG_T_I32: out.w32(isint ? (uint32_t)jt.iv : (uint32_t)cvt32(jt.dv)); break;
@@ -395,9 +441,10 @@ struct Machine {
         /* non-inline value mapping: host callback (ERR_VM_END) */
         p -= 1;
         int64_t s0 = p;
-        int64_t r = skip_one(src, p, skipbits, skipcap);
-        if (r == SKIP_DEEP) return pack0(DG_ST_DEEP, 0);
-        if (r < 0) return pack((uint32_t)-r, (uint64_t)s0, (uint64_t)p);
+        SkipRes sr = skip_one(src, p, skipbits, skipcap);
+        p = sr.p;
+        if (sr.r == SKIP_DEEP) return pack0(DG_ST_DEEP, 0);
+        if (sr.r < 0) return pack((uint32_t)-sr.r, (uint64_t)s0, (uint64_t)p);
         return pack0(E_VM_END, (uint64_t)p);
     }
 
@@ -413,7 +460,7 @@ struct Machine {
         vt[0].td = root;
         while (sp) {
             if (sp >= MAX_RECURSE) return pack(E_RECURSE_MAX, sp, (uint64_t)p);
-            Frame &x = vt[sp - 1];
+            auto &x = vt[sp - 1];
             uint32_t dc = x.td;
             uint32_t st = x.st;
             uint8_t ch = advance_ns(src, p);
@@ -423,11 +470,11 @@ struct Machine {
                 break;
             case J_ARR_0:
                 if (ch == ']') {
-                    out.put32(x.bp, 0);
+                    out.put32(fbp(x), 0);
                     sp--;
                     continue;
                 }
-                x.size = 0;
+                set_size(x, 0);
                 x.st = J_ARR;
                 p -= 1;
                 {
@@ -437,10 +484,10 @@ struct Machine {
                 continue;
             case J_ARR:
                 if (ch == ']' || ch == ',') {
-                    if (!null_val) x.size += 1;
+                    if (!null_val) set_size(x, fsize(x) + 1);
                     else null_val = false;
                     if (ch == ']') {
-                        out.put32(x.bp, x.size);
+                        out.put32(fbp(x), fsize(x));
                         sp--;
                         continue;
                     }
@@ -460,7 +507,7 @@ struct Machine {
                         if ((flag & DG_F_ENABLE_HM) && field_cache_len > 0) return pack0(E_HM_END, (uint64_t)p);
                         out.w8(0);
                     } else {
-                        out.put32(x.bp, 0);
+                        out.put32(fbp(x), 0);
                     }
                     sp--;
                     continue;
@@ -480,7 +527,7 @@ struct Machine {
                         if (null_val) {
                             null_val = false;
                             bm_set_req(x, sd, (uint32_t)lastField - sd.field_begin, D.F[lastField].required);
-                            out.len = unwindPos;
+                            out.set_len(unwindPos);
                         }
                         uint64_t r = write_unset_fields(x, sd, p - 1);
                         if (r) return r;
@@ -488,12 +535,12 @@ struct Machine {
                         if ((flag & DG_F_ENABLE_HM) && field_cache_len != 0) return pack0(E_HM_END, (uint64_t)p);
                         out.w8(0);
                     } else {
-                        if (!null_val) x.size += 1;
+                        if (!null_val) set_size(x, fsize(x) + 1);
                         else {
                             null_val = false;
-                            out.len = unwindPos;
+                            out.set_len(unwindPos);
                         }
-                        out.put32(x.bp, x.size);
+                        out.put32(fbp(x), fsize(x));
                     }
                     sp--;
                     continue;
@@ -501,16 +548,16 @@ struct Machine {
                 if (ch == ',') {
                     const dg_type &t = TY(dc);
                     if (t.ttype == DG_T_MAP) {
-                        if (!null_val) x.size += 1;
+                        if (!null_val) set_size(x, fsize(x) + 1);
                         else {
                             null_val = false;
-                            out.len = unwindPos;
+                            out.set_len(unwindPos);
                         }
                     } else if (null_val) {
                         null_val = false;
                         const dg_struct &sd = D.S[t.st];
                         bm_set_req(x, sd, (uint32_t)lastField - sd.field_begin, D.F[lastField].required);
-                        out.len = unwindPos;
+                        out.set_len(unwindPos);
                     }
                     uint64_t r = push(J_KEY, dc, p);
                     if (r) return r;
@@ -532,13 +579,14 @@ struct Machine {
             if (st & ST_SKIP) {
                 p -= 1;
                 int64_t s0 = p;
-                int64_t r = skip_one(src, p, skipbits, skipcap);
-                if (r == SKIP_DEEP) return pack0(DG_ST_DEEP, 0);
-                if (r < 0) return pack((uint32_t)-r, (uint64_t)s0, (uint64_t)p);
+                SkipRes sr = skip_one(src, p, skipbits, skipcap);
+                p = sr.p;
+                if (sr.r == SKIP_DEEP) return pack0(DG_ST_DEEP, 0);
+                if (sr.r < 0) return pack((uint32_t)-sr.r, (uint64_t)s0, (uint64_t)p);
                 continue;
             }
             if ((flag & DG_F_ENABLE_VM) && (st & ST_VM)) {
-                uint64_t r = field_vm(p, x);
+                uint64_t r = field_vm(p, (uint32_t)x.u);
                 if (r) return r;
                 continue;
             }
@@ -574,8 +622,7 @@ struct Machine {
                 uint64_t bp = out.alloc(4);
                 uint64_t r = push(J_ARR_0, dc, p);
                 if (r) return r;
-                vt[sp - 1].bp = (uint32_t)bp;
-                vt[sp - 1].size = 0;
+                vt[sp - 1].u = (uint32_t)bp;
                 break;
             }
             case '{': {
@@ -585,13 +632,13 @@ struct Machine {
                     const dg_struct &sd = D.S[t.st];
                     uint64_t r = push(J_OBJ_0, dc, p);
                     if (r) return r;
-                    Frame &nx = vt[sp - 1];
+                    auto &nx = vt[sp - 1];
                     /* bm_malloc_reqs native/thrift.c:232-250 */
                     if (sd.req_words == 1) {
-                        nx.reqs = D.R[sd.req_begin];
+                        nx.u = D.R[sd.req_begin];
                     } else {
                         if (reqlen + sd.req_words > ws.reqcap) return pack0(DG_ST_DEEP, 0);
-                        nx.roff = reqlen;
+                        nx.u = reqlen;
                         for (uint32_t w = 0; w < sd.req_words; w++) ws.reqarena[reqlen + w] = D.R[sd.req_begin + w];
                         reqlen += sd.req_words;
                     }
@@ -602,8 +649,7 @@ struct Machine {
                     uint64_t bp = out.alloc(4);
                     uint64_t r = push(J_OBJ_0, dc, p);
                     if (r) return r;
-                    vt[sp - 1].bp = (uint32_t)bp;
-                    vt[sp - 1].size = 0;
+                    vt[sp - 1].u = (uint32_t)bp;
                 }
                 break;
             }
@@ -641,16 +687,16 @@ struct Machine {
 };
 
 /* BinaryConv.do prelude/epilogue (conv/j2t/impl.go:38-91, conv.go:70-77) around
- * the FSM for message i. Returns the status; writes out_len. */
-DGI uint64_t convert_one(const Params &P, uint64_t i, Frame *frames, uint32_t depth, uint64_t *skipbits,
-                         uint32_t skipcap, const Workspace &ws, uint32_t &olen)
+ * the FSM for message i read through `src`. Returns the status; writes olen. */
+template <class S, class FP>
+DGI uint64_t convert_one(const Params &P, uint64_t i, const S &src, FStack<FP> frames, uint32_t depth,
+                         gu64 *skipbits, uint32_t skipcap, const Workspace &ws, uint32_t &olen)
 {
-    uint64_t a = P.in_off[i], b = P.in_off[i + 1];
     uint64_t oa = P.out_off[i], ob = P.out_off[i + 1];
-    Machine m;
+    Machine<S, FP> m;
     m.D = P.D;
-    m.src = Src{P.json + a, (int64_t)(b - a)};
-    m.out = Out{P.out + oa, ob - oa, 0};
+    m.src = src;
+    m.out.init(P.out + oa, ob - oa);
     m.flag = P.flag;
     m.vt = frames;
     m.cap = depth;
@@ -660,19 +706,20 @@ DGI uint64_t convert_one(const Params &P, uint64_t i, Frame *frames, uint32_t de
     m.reqlen = 0;
     m.field_cache_len = 0;
     uint64_t r;
-    if (b == a) { /* empty body -> STOP (conv/j2t/impl.go:52-82) */
+    if (m.src.n == 0) { /* empty body -> STOP (conv/j2t/impl.go:52-82) */
         m.out.w8(0);
         r = 0;
-    } else if (P.D.T[P.root].ttype == DG_T_STRING && m.src.s[0] != '"') {
+    } else if (P.D.T[P.root].ttype == DG_T_STRING && m.src.raw(0) != '"') {
         /* unquoted STRING root: json.EncodeString then unquote == identity
          * (conv/j2t/impl.go:85-88; native/parsing.c:28-62 escapes only '"',
          * '\\' and control bytes, all restored by unquote) */
         m.out.w32((uint32_t)m.src.n);
-        m.out.wbytes(m.src.s, (uint64_t)m.src.n);
+        m.copy_src(0, m.src.n);
         r = 0;
     } else {
         r = m.run(P.root);
     }
+    if (r == 0) m.out.finish();
     if (r == 0 && m.out.len > m.out.cap) r = pack(DG_ST_OUT_OVERFLOW, m.out.len, 0);
     olen = r == 0 ? (uint32_t)m.out.len : 0;
     return r;
@@ -681,50 +728,127 @@ DGI uint64_t convert_one(const Params &P, uint64_t i, Frame *frames, uint32_t de
 DGI Workspace lane_ws(const Params &P, uint64_t lane)
 {
     Workspace w;
-    uint8_t *base = P.ws + lane * P.ws_stride;
+    gu8 *base = (gu8 *)(void *)(P.ws + lane * P.ws_stride);
     w.dbuf = base;
     w.keybuf = base + DCAP;
     w.keycap = P.keycap;
-    w.reqarena = (uint64_t *)(base + DCAP + P.keycap);
+    w.reqarena = (gu64 *)(base + DCAP + P.keycap);
     w.reqcap = P.reqcap;
-    w.frames = nullptr;
-    w.skipbits = nullptr;
     return w;
 }
 
-__global__ __launch_bounds__(256) void j2t_lane_kernel(Params P)
+DGI SrcT<glb_u64> global_src(const Params &P, uint64_t i)
 {
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= P.n) return;
-    Frame frames[FAST_DEPTH];
-    uint64_t skipbits[FAST_SKIP_WORDS];
-    Workspace ws = lane_ws(P, i);
-    uint32_t olen;
-    uint64_t r = convert_one(P, i, frames, FAST_DEPTH, skipbits, FAST_SKIP_WORDS * 64, ws, olen);
+    uint64_t a = P.in_off[i], b = P.in_off[i + 1];
+    SrcT<glb_u64> s;
+    s.init((glb_u64 *)(const void *)(P.json + (a & ~7ull)), (int64_t)(a & 7), (int64_t)(b - a));
+    return s;
+}
+
+DGI void finish(const Params &P, uint64_t i, uint64_t r, uint32_t olen)
+{
     P.ret[i] = r;
     P.out_len[i] = olen;
     if ((uint8_t)r == DG_ST_OUT_OVERFLOW && P.pending) atomicAdd(P.pending, 1u);
-    if ((uint8_t)r == DG_ST_DEEP) P.deep_list[atomicAdd(P.deep_count, 1u)] = i;
 }
 
-/* Redo the DG_ST_DEEP messages (listed by the fast kernel) with a MAX_RECURSE
- * stack in workspace. Persistent grid; exits at once when the list is empty. */
-__global__ __launch_bounds__(256) void j2t_deep_kernel(Params P)
+/* Deep pass: messages that outgrew the fast stack, redone by the LAST block
+ * to finish, with a MAX_RECURSE stack in device workspace. The list and its
+ * counter are published with agent-scope atomics behind each producer
+ * block's release fence; the last block acquires once. */
+DGI void deep_pass(const Params &P, uint32_t *done, uint32_t nblocks)
 {
-    uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    Workspace ws = lane_ws(P, lane);
-    Frame *frames = (Frame *)(P.ws + lane * P.ws_stride + DCAP + P.keycap + (uint64_t)P.reqcap * 8);
-    uint64_t *skipbits = (uint64_t *)(frames + MAX_RECURSE);
-    uint32_t cnt = *P.deep_count;
-    for (uint64_t k = lane; k < cnt; k += stride) {
-        uint64_t i = P.deep_list[k];
-        uint32_t olen;
-        uint64_t r = convert_one(P, i, frames, MAX_RECURSE, skipbits, MAX_RECURSE, ws, olen);
-        P.ret[i] = r;
-        P.out_len[i] = olen;
-        if ((uint8_t)r == DG_ST_OUT_OVERFLOW && P.pending) atomicAdd(P.pending, 1u);
+    __shared__ uint32_t s_last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence(); /* release this block's results */
+        uint32_t prev = __hip_atomic_fetch_add(done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = prev == nblocks - 1;
+        if (s_last) __threadfence(); /* acquire every other block's */
     }
+    __syncthreads();
+    if (!s_last) return;
+    uint32_t cnt = __hip_atomic_load(P.deep_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t lane = threadIdx.x;
+    Workspace ws = lane_ws(P, lane);
+    FStack<Frame *> frames{(Frame *)(P.ws + lane * P.ws_stride + DCAP + P.keycap + (uint64_t)P.reqcap * 8), 1};
+    gu64 *skipbits = (gu64 *)(void *)(frames.base + MAX_RECURSE);
+    for (uint64_t k = lane; k < cnt; k += blockDim.x) {
+        uint64_t i = __hip_atomic_load(&P.deep_list[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t olen;
+        uint64_t r = convert_one(P, i, global_src(P, i), frames, MAX_RECURSE, skipbits, MAX_RECURSE, ws, olen);
+        finish(P, i, r, olen);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) { /* self-reset for the next launch on this context */
+        __hip_atomic_store(P.deep_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+constexpr uint32_t LANE_BLOCK = 256;
+constexpr uint32_t STAGE_BYTES = 64 * 1024; /* LDS staging of the block's JSON bytes */
+constexpr uint32_t LDS_DEPTH = 16;          /* frames per lane in LDS: 16 x 256 x 16 B = 64 KiB */
+
+struct DeepParams {
+    uint8_t *ws;
+    uint64_t ws_stride;
+    uint32_t keycap, reqcap;
+    uint32_t *done;
+};
+
+/* One lane per message. The block's messages are contiguous in the arena:
+ * when their span fits, it is staged into LDS with coalesced 16-byte loads
+ * and every lane parses from LDS through its 8-byte register window. */
+__global__ __launch_bounds__(LANE_BLOCK) __attribute__((amdgpu_waves_per_eu(1, 1))) void j2t_lane_kernel(Params P, DeepParams DP)
+{
+    __shared__ __attribute__((aligned(16))) uint64_t stage[STAGE_BYTES / 8];
+    __shared__ __attribute__((aligned(16))) Frame lframes[LDS_DEPTH * LANE_BLOCK];
+    uint64_t b0 = (uint64_t)blockIdx.x * LANE_BLOCK;
+    uint64_t b1 = b0 + LANE_BLOCK < P.n ? b0 + LANE_BLOCK : P.n;
+    uint64_t lo = P.in_off[b0], hi = P.in_off[b1];
+    uint64_t base = lo & ~15ull;
+    uint64_t words = (hi - base + 15) >> 4;
+    bool staged = words * 16 <= STAGE_BYTES;
+    if (staged) {
+        const uint4 *g = (const uint4 *)(P.json + base);
+        uint4 *l = (uint4 *)stage;
+        for (uint64_t k = threadIdx.x; k < words; k += LANE_BLOCK) l[k] = g[k];
+        __syncthreads();
+    }
+    uint64_t i = b0 + threadIdx.x;
+    if (i < b1) {
+        FStack<LFrame *> frames{(LFrame *)(void *)&lframes[threadIdx.x], LANE_BLOCK};
+        gu64 *skipbits = nullptr; /* 64 skip levels in a register */
+        Workspace ws = lane_ws(P, i);
+        uint32_t olen;
+        uint64_t r;
+        if (staged) {
+            uint64_t a = P.in_off[i], b = P.in_off[i + 1];
+            SrcT<lds_u64> s;
+            s.init((lds_u64 *)(void *)stage, (int64_t)(a - base), (int64_t)(b - a));
+            r = convert_one(P, i, s, frames, LDS_DEPTH, skipbits, 64, ws, olen);
+        } else {
+#ifndef DG_EXP_NO_GLOBAL
+            r = convert_one(P, i, global_src(P, i), frames, LDS_DEPTH, skipbits, 64, ws, olen);
+#else
+            r = pack0(DG_ST_DEEP, 0); olen = 0;
+#endif
+        }
+        finish(P, i, r, olen);
+        if ((uint8_t)r == DG_ST_DEEP) {
+            uint32_t k = __hip_atomic_fetch_add(P.deep_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&P.deep_list[k], i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    Params Q = P;
+    Q.ws = DP.ws;
+    Q.ws_stride = DP.ws_stride;
+    Q.keycap = DP.keycap;
+    Q.reqcap = DP.reqcap;
+#ifndef DG_EXP_NO_DEEP
+    deep_pass(Q, DP.done, gridDim.x);
+#endif
 }
 
 }  // namespace dg
@@ -809,6 +933,7 @@ int dg_ctx_create(int device, dg_ctx **out)
     HIPCHK(hipMalloc(&c->ws_deep, DEEP_WS_STRIDE * DEEP_THREADS));
     HIPCHK(hipMalloc(&c->d_pending, 16));
     HIPCHK(hipMalloc(&c->d_deep_count, 16));
+    HIPCHK(hipMemset(c->d_deep_count, 0, 16)); /* {deep_count, done}: self-reset by each launch */
     *out = c;
     return DG_OK;
 }
@@ -888,7 +1013,7 @@ void dg_desc_destroy(dg_desc *d)
 
 uint32_t dg_desc_root(const dg_desc *d) { return d ? d->hdr.root_type : 0; }
 
-uint64_t dg_slot_bound(uint64_t len) { return 4 * len + 64; }
+uint64_t dg_slot_bound(uint64_t len) { return (4 * len + 64 + 7) & ~7ull; }
 
 static int ensure_fast_ws(dg_ctx *c, uint64_t lanes)
 {
@@ -930,16 +1055,14 @@ static int launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *jso
     P.ws_stride = FAST_WS_STRIDE;
     P.keycap = WS_KEYCAP;
     P.reqcap = WS_REQCAP;
-    uint64_t blocks = (n + 255) / 256;
-    HIPCHK(hipMemsetAsync(c->d_deep_count, 0, 16, s));
-    hipLaunchKernelGGL(j2t_lane_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, P);
-    HIPCHK(hipGetLastError());
-    Params Q = P;
-    Q.ws = c->ws_deep;
-    Q.ws_stride = DEEP_WS_STRIDE;
-    Q.keycap = DEEP_KEYCAP;
-    Q.reqcap = DEEP_REQCAP;
-    hipLaunchKernelGGL(j2t_deep_kernel, dim3(DEEP_THREADS / 64), dim3(64), 0, s, Q);
+    uint64_t blocks = (n + LANE_BLOCK - 1) / LANE_BLOCK;
+    DeepParams DP;
+    DP.ws = c->ws_deep;
+    DP.ws_stride = DEEP_WS_STRIDE;
+    DP.keycap = DEEP_KEYCAP;
+    DP.reqcap = DEEP_REQCAP;
+    DP.done = c->d_deep_count + 1;
+    hipLaunchKernelGGL(j2t_lane_kernel, dim3((uint32_t)blocks), dim3(LANE_BLOCK), 0, s, P, DP);
     HIPCHK(hipGetLastError());
     return DG_OK;
 }
