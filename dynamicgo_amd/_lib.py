@@ -9,7 +9,7 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libdgj2t.so")
+LIB_PATH = os.environ.get("DG_LIB_PATH") or os.path.join(HERE, "libdgj2t.so")
 
 # symbols include/dgj2t.h declares (checked by tests/test_abi.py)
 EXPORTS = ["dg_last_error", "dg_ctx_create", "dg_ctx_destroy", "dg_ctx_stream", "dg_desc_create",

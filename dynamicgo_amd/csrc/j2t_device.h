@@ -23,6 +23,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "../../include/dgj2t.h"
 #include "../../include/dgj2t_desc.h"
 #include "dg_tables.h"
@@ -52,14 +54,46 @@ DGI uint32_t v2(uint32_t vh, uint8_t vl) { return (vh << 8) | vl; }
 DGI uint32_t sx8(uint8_t c) { return (uint32_t)(int32_t)(int8_t)c; } /* (uint32_t)(char) */
 DGI uint64_t sx8_64(uint8_t c) { return (uint64_t)(int64_t)(int8_t)c; }
 
-struct DescView {
-    const dg_type *T;
-    const dg_struct *S;
-    const dg_field *F;
-    const dg_name *N;
-    const uint64_t *R;
-    const uint8_t *P;
+/* The descriptor tables, in global memory (DescView) or copied to LDS by the
+ * kernel prologue (DescViewT<3>); records are read by value. */
+template <int AS>
+struct DescViewT {
+    const __attribute__((address_space(AS))) dg_type *T;
+    const __attribute__((address_space(AS))) dg_struct *S;
+    const __attribute__((address_space(AS))) dg_field *F;
+    const __attribute__((address_space(AS))) dg_name *N;
+    const __attribute__((address_space(AS))) uint64_t *R;
+    const __attribute__((address_space(AS))) uint8_t *P;
 };
+typedef DescViewT<1> DescView;
+
+/* read a descriptor record (multiple of 8 bytes) by value from any address space */
+template <class T, int AS>
+DGI typename std::remove_cv<T>::type ldrec(const __attribute__((address_space(AS))) T *p)
+{
+    static_assert(sizeof(T) % 8 == 0, "record size");
+    const __attribute__((address_space(AS))) uint64_t *q = (const __attribute__((address_space(AS))) uint64_t *)p;
+    uint64_t tmp[sizeof(T) / 8];
+#pragma unroll
+    for (unsigned k = 0; k < sizeof(T) / 8; k++) tmp[k] = q[k];
+    typename std::remove_cv<T>::type v;
+    __builtin_memcpy(&v, tmp, sizeof(T));
+    return v;
+}
+
+/* views of a dg_desc v1 blob at `base` (section offsets from its header) */
+template <int AS>
+DGI DescViewT<AS> desc_view(const __attribute__((address_space(AS))) uint8_t *base, const dg_desc_hdr &h)
+{
+    DescViewT<AS> v;
+    v.T = (const __attribute__((address_space(AS))) dg_type *)(base + h.off_types);
+    v.S = (const __attribute__((address_space(AS))) dg_struct *)(base + h.off_structs);
+    v.F = (const __attribute__((address_space(AS))) dg_field *)(base + h.off_fields);
+    v.N = (const __attribute__((address_space(AS))) dg_name *)(base + h.off_names);
+    v.R = (const __attribute__((address_space(AS))) uint64_t *)(base + h.off_reqwords);
+    v.P = base + h.off_pool;
+    return v;
+}
 
 /* J2TState (native/thrift.h:164-170) without jp (no re-entry): 16 bytes.
  * u = J2TExtra: container {bp: low 32, size: high 32}; struct {inline
@@ -193,6 +227,11 @@ struct Out {
     /* append n (1..8) bytes given little-endian in v (first byte lowest) */
     DGI void wle(uint64_t v, uint32_t n)
     {
+#ifdef DG_ABL_NOOUT
+        len += n;
+        wbuf ^= v;
+        return;
+#endif
         uint32_t used = (uint32_t)(len & 7);
         uint32_t sh = used << 3;
         if (n < 8) v &= (1ull << (n << 3)) - 1;
@@ -509,6 +548,9 @@ DGI int64_t decode_block(S &src, int64_t s0, int64_t ie, int64_t &ipp, Out &o, i
 template <class S>
 DGI int64_t b64decode(Out &o, S &src, int64_t s0, int64_t nb)
 {
+#ifdef DG_ABL_NOB64
+    return (nb / 4) * 3;
+#endif
     if (nb == 0) return 0;
     int64_t ip = 0, op = 0;
     /* whole 4-char quanta of alphabet characters: decode_block on such a
@@ -823,6 +865,23 @@ struct JState {
 template <class S>
 DGI void vnumber(S &src, int64_t &p, JState &ret, gu8 *dbuf)
 {
+#ifdef DG_ABL_NONUM
+    {
+        int64_t i = p;
+        uint64_t acc = 0;
+        while (i < src.n) {
+            uint8_t c = src.raw(i);
+            if (!((c >= '0' && c <= '9') || c == '-' || c == '.' || c == 'e' || c == 'E' || c == '+')) break;
+            acc = acc * 10 + c;
+            i++;
+        }
+        p = i;
+        ret.vt = V_INTEGER;
+        ret.iv = (int64_t)acc;
+        ret.dv = 0;
+        return;
+    }
+#endif
     int sgn = 1;
     uint64_t man = 0;
     int man_nd = 0, exp10 = 0, trunc = 0;

@@ -34,7 +34,6 @@ constexpr int DEEP_KEYCAP = 1 << 20;
 constexpr int DEEP_REQCAP = 1 << 16;
 
 struct Params {
-    DescView D;
     uint32_t root;
     const uint8_t *json;
     const uint64_t *in_off;
@@ -52,6 +51,19 @@ struct Params {
     uint32_t keycap, reqcap;
 };
 
+#ifdef DG_PROFILE
+#define PROF_DECL uint64_t prof[16] = {0};
+#define PROF(k, stmt)                                    \
+    do {                                                 \
+        uint64_t t0_ = __builtin_amdgcn_s_memtime();     \
+        stmt;                                            \
+        prof[k] += __builtin_amdgcn_s_memtime() - t0_;   \
+    } while (0)
+#else
+#define PROF_DECL
+#define PROF(k, stmt) stmt
+#endif
+
 /* Frame stack: frame k of this lane at base[k * stride] (LDS: frame-major
  * across the block, so a wave at equal depth touches consecutive slots). */
 template <class FP>
@@ -63,9 +75,9 @@ struct FStack {
 
 /* The FSM of one message over source type S (LDS- or global-backed) and
  * frame storage FP (LDS or device workspace). */
-template <class S, class FP>
+template <class S, class FP, class DV>
 struct Machine {
-    DescView D;
+    DV D;
     S src;
     Out out;
     uint64_t flag;
@@ -77,8 +89,9 @@ struct Machine {
     uint32_t reqlen;
     uint32_t field_cache_len;
     JState jt;
+    PROF_DECL
 
-    DGI const dg_type &TY(uint32_t t) const { return D.T[t]; }
+    DGI dg_type TY(uint32_t t) const { return ldrec(&D.T[t]); }
 
     DGI uint64_t push(uint32_t st, uint32_t td, int64_t p)
     {
@@ -114,7 +127,7 @@ struct Machine {
     /* tb_write_empty native/thrift.c:171-203 */
     DGI uint64_t write_empty(uint32_t td, int64_t p)
     {
-        const dg_type &t = TY(td);
+        const dg_type t = TY(td);
         switch (t.ttype) {
         case DG_T_BOOL:
         case DG_T_BYTE: out.w8(0); return 0;
@@ -158,7 +171,7 @@ struct Machine {
             while (bits) {
                 uint32_t k = w * 64 + __builtin_ctzll(bits);
                 bits &= bits - 1;
-                const dg_field &f = D.F[sd.field_begin + k];
+                const dg_field f = ldrec(&D.F[sd.field_begin + k]);
                 if (f.flags & DG_FF_REQUEST_BASE) continue;
                 if (tb && (f.required == DG_REQ_REQUIRED || sp == 1)) field_cache_len++;
                 else if (!wr && f.required == DG_REQ_REQUIRED)
@@ -198,19 +211,21 @@ struct Machine {
     {
         int64_t s0 = p;
         bool esc;
-        int64_t e = advance_string(src, s0, esc);
+        int64_t e;
+        PROF(8, e = advance_string(src, s0, esc));
         if (e < 0) return pack((uint32_t)-e, (uint64_t)s0, (uint64_t)p);
         p = e;
         int64_t n = e - s0 - 1;
         if (esc) {
             uint64_t lp = out.alloc(4);
             OutSink sink{&out};
-            int64_t l = unquote(src, s0, n, sink);
+            int64_t l;
+            PROF(9, l = unquote(src, s0, n, sink));
             if (l < 0) return pack((uint32_t)-l, (uint64_t)s0, (uint64_t)p);
             out.put32(lp, (uint32_t)l);
         } else {
-            out.w32((uint32_t)n);
-            copy_src(s0, n);
+            PROF(11, out.w32((uint32_t)n));
+            PROF(10, copy_src(s0, n));
         }
         return 0;
     }
@@ -218,6 +233,10 @@ struct Machine {
     /* copy src[s0, s0+n) to the output (string bodies, tb_write_string) */
     DGI void copy_src(int64_t s0, int64_t n)
     {
+#ifdef DG_ABL_NOSTR
+        out.len += n;
+        return;
+#endif
         int64_t i = 0;
         for (; i + 8 <= n; i += 8) out.wle(src.get8(s0 + i), 8);
         for (; i < n; i++) out.w8(src.raw(s0 + i));
@@ -233,7 +252,8 @@ struct Machine {
         p = e;
         int64_t n = e - s0 - 1;
         uint64_t back = out.alloc(4);
-        int64_t l = b64decode(out, src, s0, n);
+        int64_t l;
+        PROF(12, l = b64decode(out, src, s0, n));
         if (l < 0) return pack(E_DECODE_BASE64, (uint64_t)(-l - 1), (uint64_t)p);
         out.put32(back, (uint32_t)l);
         return 0;
@@ -283,15 +303,17 @@ struct Machine {
     /* exact-match field lookup (j2t_find_field_key native/thrift.c:449-468) */
     DGI int32_t find_field(const dg_struct &sd, const Key &k)
     {
+#ifdef DG_ABL_NOKEY
+        return (int32_t)(sd.field_begin + (k.hash % sd.n_fields));
+#endif
         uint32_t j = k.hash & sd.name_mask;
         for (;;) {
-            const dg_name &nm = D.N[sd.name_begin + j];
+            const dg_name nm = ldrec(&D.N[sd.name_begin + j]);
             if (nm.field == DG_NONE) return -1;
             if (nm.hash == k.hash && nm.key_len == (uint32_t)k.n) {
-                const uint8_t *q = D.P + nm.key_off;
                 bool eq = true;
                 for (int64_t i = 0; i < k.n; i++) {
-                    if (q[i] != key_byte(k, i)) {
+                    if (D.P[nm.key_off + i] != key_byte(k, i)) {
                         eq = false;
                         break;
                     }
@@ -331,10 +353,11 @@ struct Machine {
     DGI uint64_t j2t_key(int64_t &p, uint32_t dc, bool obj0, uint64_t &unwindPos, int32_t &lastField)
     {
         Key key;
-        uint64_t r = read_key(p, key);
+        uint64_t r;
+        PROF(1, r = read_key(p, key));
         if (r) return r;
         int64_t kn = key.n;
-        const dg_type &t = TY(dc);
+        const dg_type t = TY(dc);
         if (t.ttype == DG_T_MAP) {
             unwindPos = out.len;
             r = j2t_map_key(key, t.key, p);
@@ -349,9 +372,10 @@ struct Machine {
             return 0;
         }
         auto &pex = vt[obj0 ? sp - 1 : sp - 2];
-        const dg_struct &sd = D.S[t.st];
-        int32_t fi = find_field(sd, key);
-        if (fi < 0 || ((D.F[fi].flags & DG_FF_REQUEST_BASE) && (flag & DG_F_NO_WRITE_BASE))) {
+        const dg_struct sd = ldrec(&D.S[t.st]);
+        int32_t fi;
+        PROF(2, fi = find_field(sd, key));
+        if (fi < 0 || ((ldrec(&D.F[fi]).flags & DG_FF_REQUEST_BASE) && (flag & DG_F_NO_WRITE_BASE))) {
             if (fi < 0 && (flag & DG_F_ALLOW_UNKNOWN) == 0) return pack(E_UNKNOWN_FIELD, (uint64_t)kn, (uint64_t)p);
             if (obj0) return push(J_ELEM | ST_SKIP, DG_NONE, p);
             auto &x = vt[sp - 1];
@@ -359,7 +383,7 @@ struct Machine {
             x.td = DG_NONE;
             return 0;
         }
-        const dg_field &f = D.F[fi];
+        const dg_field f = ldrec(&D.F[fi]);
         uint32_t k = (uint32_t)fi - sd.field_begin;
         if ((flag & DG_F_ENABLE_HM) && (f.flags & DG_FF_HTTP_MAPPING) && !bm_is_set(pex, sd, k)) {
             if (obj0) return push(J_ELEM | ST_SKIP, f.type, p);
@@ -393,7 +417,7 @@ struct Machine {
     /* j2t_field_vm native/thrift.c:506-666 */
     DGI uint64_t field_vm(int64_t &p, uint32_t fidx)
     {
-        const dg_field &f = D.F[fidx];
+        const dg_field f = ldrec(&D.F[fidx]);
         uint8_t ft = TY(f.type).ttype;
         if (f.vm <= DG_VM_INLINE_MAX) {
             out.w8(ft);
@@ -463,7 +487,8 @@ struct Machine {
             auto &x = vt[sp - 1];
             uint32_t dc = x.td;
             uint32_t st = x.st;
-            uint8_t ch = advance_ns(src, p);
+            uint8_t ch;
+            PROF(0, ch = advance_ns(src, p));
             switch (st & 0xffff) {
             default:
                 sp--;
@@ -498,10 +523,11 @@ struct Machine {
                 return pack(E_INVAL, v2(sx8(ch), J_ARR), (uint64_t)p);
             case J_OBJ_0:
                 if (ch == '}') {
-                    const dg_type &t = TY(dc);
+                    const dg_type t = TY(dc);
                     if (t.ttype == DG_T_STRUCT) {
-                        const dg_struct &sd = D.S[t.st];
-                        uint64_t r = write_unset_fields(x, sd, p - 1);
+                        const dg_struct sd = ldrec(&D.S[t.st]);
+                        uint64_t r;
+                        PROF(6, r = write_unset_fields(x, sd, p - 1));
                         if (r) return r;
                         if (sd.req_words > 1) reqlen -= sd.req_words;
                         if ((flag & DG_F_ENABLE_HM) && field_cache_len > 0) return pack0(E_HM_END, (uint64_t)p);
@@ -521,15 +547,16 @@ struct Machine {
                 return pack(E_INVAL, v2(sx8(ch), J_OBJ_0), (uint64_t)p);
             case J_OBJ:
                 if (ch == '}') {
-                    const dg_type &t = TY(dc);
+                    const dg_type t = TY(dc);
                     if (t.ttype == DG_T_STRUCT) {
-                        const dg_struct &sd = D.S[t.st];
+                        const dg_struct sd = ldrec(&D.S[t.st]);
                         if (null_val) {
                             null_val = false;
-                            bm_set_req(x, sd, (uint32_t)lastField - sd.field_begin, D.F[lastField].required);
+                            bm_set_req(x, sd, (uint32_t)lastField - sd.field_begin, ldrec(&D.F[lastField]).required);
                             out.set_len(unwindPos);
                         }
-                        uint64_t r = write_unset_fields(x, sd, p - 1);
+                        uint64_t r;
+                        PROF(6, r = write_unset_fields(x, sd, p - 1));
                         if (r) return r;
                         if (sd.req_words > 1) reqlen -= sd.req_words;
                         if ((flag & DG_F_ENABLE_HM) && field_cache_len != 0) return pack0(E_HM_END, (uint64_t)p);
@@ -546,7 +573,7 @@ struct Machine {
                     continue;
                 }
                 if (ch == ',') {
-                    const dg_type &t = TY(dc);
+                    const dg_type t = TY(dc);
                     if (t.ttype == DG_T_MAP) {
                         if (!null_val) set_size(x, fsize(x) + 1);
                         else {
@@ -555,8 +582,8 @@ struct Machine {
                         }
                     } else if (null_val) {
                         null_val = false;
-                        const dg_struct &sd = D.S[t.st];
-                        bm_set_req(x, sd, (uint32_t)lastField - sd.field_begin, D.F[lastField].required);
+                        const dg_struct sd = ldrec(&D.S[t.st]);
+                        bm_set_req(x, sd, (uint32_t)lastField - sd.field_begin, ldrec(&D.F[lastField]).required);
                         out.set_len(unwindPos);
                     }
                     uint64_t r = push(J_KEY, dc, p);
@@ -590,12 +617,13 @@ struct Machine {
                 if (r) return r;
                 continue;
             }
-            const dg_type &t = TY(dc);
+            const dg_type t = TY(dc);
             switch (ch) {
             case '0': case '1': case '2': case '3': case '4':
             case '5': case '6': case '7': case '8': case '9': case '-': {
                 p -= 1;
-                uint64_t r = j2t_number(dc, src, p);
+                uint64_t r;
+                PROF(3, r = j2t_number(dc, src, p));
                 if (r) return r;
                 break;
             }
@@ -629,7 +657,7 @@ struct Machine {
                 if (t.ttype != DG_T_STRUCT && t.ttype != DG_T_MAP)
                     return pack(E_DISMATCH_TYPE2, ((uint32_t)t.ttype << 16) | (DG_T_MAP << 8) | DG_T_STRUCT, (uint64_t)p);
                 if (t.ttype == DG_T_STRUCT) {
-                    const dg_struct &sd = D.S[t.st];
+                    const dg_struct sd = ldrec(&D.S[t.st]);
                     uint64_t r = push(J_OBJ_0, dc, p);
                     if (r) return r;
                     auto &nx = vt[sp - 1];
@@ -656,8 +684,8 @@ struct Machine {
             case '"': {
                 uint64_t r;
                 if (t.ttype == DG_T_STRING) {
-                    if ((flag & DG_F_NO_BASE64) == 0 && (t.flags & DG_TF_BINARY)) r = j2t_binary(p);
-                    else r = j2t_string(p);
+                    if ((flag & DG_F_NO_BASE64) == 0 && (t.flags & DG_TF_BINARY)) PROF(5, r = j2t_binary(p));
+                    else PROF(4, r = j2t_string(p));
                     if (r) return r;
                 } else if ((flag & DG_F_ENABLE_I2S) && (t.ttype == DG_T_I64 || t.ttype == DG_T_I32 || t.ttype == DG_T_I16 ||
                                                          t.ttype == DG_T_BYTE || t.ttype == DG_T_DOUBLE)) {
@@ -688,13 +716,13 @@ struct Machine {
 
 /* BinaryConv.do prelude/epilogue (conv/j2t/impl.go:38-91, conv.go:70-77) around
  * the FSM for message i read through `src`. Returns the status; writes olen. */
-template <class S, class FP>
-DGI uint64_t convert_one(const Params &P, uint64_t i, const S &src, FStack<FP> frames, uint32_t depth,
+template <class S, class FP, class DV>
+DGI uint64_t convert_one(const Params &P, const DV &dv, uint64_t i, const S &src, FStack<FP> frames, uint32_t depth,
                          gu64 *skipbits, uint32_t skipcap, const Workspace &ws, uint32_t &olen)
 {
     uint64_t oa = P.out_off[i], ob = P.out_off[i + 1];
-    Machine<S, FP> m;
-    m.D = P.D;
+    Machine<S, FP, DV> m;
+    m.D = dv;
     m.src = src;
     m.out.init(P.out + oa, ob - oa);
     m.flag = P.flag;
@@ -709,7 +737,7 @@ DGI uint64_t convert_one(const Params &P, uint64_t i, const S &src, FStack<FP> f
     if (m.src.n == 0) { /* empty body -> STOP (conv/j2t/impl.go:52-82) */
         m.out.w8(0);
         r = 0;
-    } else if (P.D.T[P.root].ttype == DG_T_STRING && m.src.raw(0) != '"') {
+    } else if (dv.T[P.root].ttype == DG_T_STRING && m.src.raw(0) != '"') {
         /* unquoted STRING root: json.EncodeString then unquote == identity
          * (conv/j2t/impl.go:85-88; native/parsing.c:28-62 escapes only '"',
          * '\\' and control bytes, all restored by unquote) */
@@ -717,7 +745,16 @@ DGI uint64_t convert_one(const Params &P, uint64_t i, const S &src, FStack<FP> f
         m.copy_src(0, m.src.n);
         r = 0;
     } else {
+#ifdef DG_PROFILE
+        uint64_t t0 = __builtin_amdgcn_s_memtime();
         r = m.run(P.root);
+        m.prof[7] = __builtin_amdgcn_s_memtime() - t0;
+        for (int k = 0; k < 16; k++) *(uint64_t *)(P.out + oa + 8 * k) = m.prof[k];
+        olen = 128;
+        return 0;
+#else
+        r = m.run(P.root);
+#endif
     }
     if (r == 0) m.out.finish();
     if (r == 0 && m.out.len > m.out.cap) r = pack(DG_ST_OUT_OVERFLOW, m.out.len, 0);
@@ -756,7 +793,8 @@ DGI void finish(const Params &P, uint64_t i, uint64_t r, uint32_t olen)
  * to finish, with a MAX_RECURSE stack in device workspace. The list and its
  * counter are published with agent-scope atomics behind each producer
  * block's release fence; the last block acquires once. */
-DGI void deep_pass(const Params &P, uint32_t *done, uint32_t nblocks)
+template <class DV>
+DGI void deep_pass(const Params &P, const DV &dv, uint32_t *done, uint32_t nblocks)
 {
     __shared__ uint32_t s_last;
     __syncthreads();
@@ -776,7 +814,7 @@ DGI void deep_pass(const Params &P, uint32_t *done, uint32_t nblocks)
     for (uint64_t k = lane; k < cnt; k += blockDim.x) {
         uint64_t i = __hip_atomic_load(&P.deep_list[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         uint32_t olen;
-        uint64_t r = convert_one(P, i, global_src(P, i), frames, MAX_RECURSE, skipbits, MAX_RECURSE, ws, olen);
+        uint64_t r = convert_one(P, dv, i, global_src(P, i), frames, MAX_RECURSE, skipbits, MAX_RECURSE, ws, olen);
         finish(P, i, r, olen);
     }
     __syncthreads();
@@ -788,22 +826,28 @@ DGI void deep_pass(const Params &P, uint32_t *done, uint32_t nblocks)
 
 constexpr uint32_t LANE_BLOCK = 256;
 constexpr uint32_t STAGE_BYTES = 64 * 1024; /* LDS staging of the block's JSON bytes */
-constexpr uint32_t LDS_DEPTH = 16;          /* frames per lane in LDS: 16 x 256 x 16 B = 64 KiB */
+constexpr uint32_t LDS_DEPTH = 8;           /* frames per lane in LDS: 8 x 256 x 16 B = 32 KiB */
+constexpr uint32_t DESC_LDS_BYTES = 48 * 1024; /* descriptors up to this size are copied to LDS */
 
 struct DeepParams {
     uint8_t *ws;
     uint64_t ws_stride;
     uint32_t keycap, reqcap;
     uint32_t *done;
+    const uint8_t *blob; /* descriptor blob (device) */
+    dg_desc_hdr hdr;
 };
 
 /* One lane per message. The block's messages are contiguous in the arena:
  * when their span fits, it is staged into LDS with coalesced 16-byte loads
- * and every lane parses from LDS through its 8-byte register window. */
+ * and every lane parses from LDS through its 8-byte register window. With
+ * LDS_DESC the descriptor tables are copied to LDS too. */
+template <bool LDS_DESC>
 __global__ __launch_bounds__(LANE_BLOCK) __attribute__((amdgpu_waves_per_eu(1, 1))) void j2t_lane_kernel(Params P, DeepParams DP)
 {
     __shared__ __attribute__((aligned(16))) uint64_t stage[STAGE_BYTES / 8];
     __shared__ __attribute__((aligned(16))) Frame lframes[LDS_DEPTH * LANE_BLOCK];
+    __shared__ __attribute__((aligned(16))) uint64_t ldesc[LDS_DESC ? DESC_LDS_BYTES / 8 : 2];
     uint64_t b0 = (uint64_t)blockIdx.x * LANE_BLOCK;
     uint64_t b1 = b0 + LANE_BLOCK < P.n ? b0 + LANE_BLOCK : P.n;
     uint64_t lo = P.in_off[b0], hi = P.in_off[b1];
@@ -814,8 +858,17 @@ __global__ __launch_bounds__(LANE_BLOCK) __attribute__((amdgpu_waves_per_eu(1, 1
         const uint4 *g = (const uint4 *)(P.json + base);
         uint4 *l = (uint4 *)stage;
         for (uint64_t k = threadIdx.x; k < words; k += LANE_BLOCK) l[k] = g[k];
-        __syncthreads();
     }
+    if constexpr (LDS_DESC) {
+        const uint4 *g = (const uint4 *)DP.blob;
+        uint4 *l = (uint4 *)ldesc;
+        for (uint32_t k = threadIdx.x; k < (DP.hdr.total_len + 15) / 16; k += LANE_BLOCK) l[k] = g[k];
+    }
+    __syncthreads();
+    auto dv = [&]() {
+        if constexpr (LDS_DESC) return desc_view<3>((const __attribute__((address_space(3))) uint8_t *)(void *)ldesc, DP.hdr);
+        else return desc_view<1>((const __attribute__((address_space(1))) uint8_t *)(const void *)DP.blob, DP.hdr);
+    }();
     uint64_t i = b0 + threadIdx.x;
     if (i < b1) {
         FStack<LFrame *> frames{(LFrame *)(void *)&lframes[threadIdx.x], LANE_BLOCK};
@@ -827,13 +880,9 @@ __global__ __launch_bounds__(LANE_BLOCK) __attribute__((amdgpu_waves_per_eu(1, 1
             uint64_t a = P.in_off[i], b = P.in_off[i + 1];
             SrcT<lds_u64> s;
             s.init((lds_u64 *)(void *)stage, (int64_t)(a - base), (int64_t)(b - a));
-            r = convert_one(P, i, s, frames, LDS_DEPTH, skipbits, 64, ws, olen);
+            r = convert_one(P, dv, i, s, frames, LDS_DEPTH, skipbits, 64, ws, olen);
         } else {
-#ifndef DG_EXP_NO_GLOBAL
-            r = convert_one(P, i, global_src(P, i), frames, LDS_DEPTH, skipbits, 64, ws, olen);
-#else
-            r = pack0(DG_ST_DEEP, 0); olen = 0;
-#endif
+            r = convert_one(P, dv, i, global_src(P, i), frames, LDS_DEPTH, skipbits, 64, ws, olen);
         }
         finish(P, i, r, olen);
         if ((uint8_t)r == DG_ST_DEEP) {
@@ -846,9 +895,7 @@ __global__ __launch_bounds__(LANE_BLOCK) __attribute__((amdgpu_waves_per_eu(1, 1
     Q.ws_stride = DP.ws_stride;
     Q.keycap = DP.keycap;
     Q.reqcap = DP.reqcap;
-#ifndef DG_EXP_NO_DEEP
-    deep_pass(Q, DP.done, gridDim.x);
-#endif
+    deep_pass(Q, dv, DP.done, gridDim.x);
 }
 
 }  // namespace dg
@@ -897,7 +944,6 @@ struct dg_desc {
     uint8_t *d_blob;
     size_t len;
     dg_desc_hdr hdr;
-    DescView view;
 };
 
 static const uint64_t FAST_WS_STRIDE = DCAP + WS_KEYCAP + (uint64_t)WS_REQCAP * 8;
@@ -962,19 +1008,13 @@ void *dg_ctx_stream(dg_ctx *c) { return c ? (void *)c->stream : nullptr; }
 
 static int desc_finish(dg_ctx *c, const dg_desc_hdr &h, uint8_t *d_blob, size_t len, dg_desc **out)
 {
-    if (h.magic != DG_DESC_MAGIC || h.version != DG_DESC_VERSION || h.total_len > len)
+    if (h.magic != DG_DESC_MAGIC || h.version < 1 || h.version > DG_DESC_VERSION || h.total_len > len)
         return set_err(DG_E_DESC, "bad descriptor blob header");
     dg_desc *d = new dg_desc();
     d->ctx = c;
     d->d_blob = d_blob;
     d->len = len;
     d->hdr = h;
-    d->view.T = (const dg_type *)(d_blob + h.off_types);
-    d->view.S = (const dg_struct *)(d_blob + h.off_structs);
-    d->view.F = (const dg_field *)(d_blob + h.off_fields);
-    d->view.N = (const dg_name *)(d_blob + h.off_names);
-    d->view.R = (const uint64_t *)(d_blob + h.off_reqwords);
-    d->view.P = d_blob + h.off_pool;
     *out = d;
     return DG_OK;
 }
@@ -1038,7 +1078,6 @@ static int launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *jso
     int rc = ensure_fast_ws(c, n);
     if (rc) return rc;
     Params P;
-    P.D = d->view;
     P.root = root;
     P.json = json;
     P.in_off = in_off;
@@ -1062,7 +1101,12 @@ static int launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *jso
     DP.keycap = DEEP_KEYCAP;
     DP.reqcap = DEEP_REQCAP;
     DP.done = c->d_deep_count + 1;
-    hipLaunchKernelGGL(j2t_lane_kernel, dim3((uint32_t)blocks), dim3(LANE_BLOCK), 0, s, P, DP);
+    DP.blob = d->d_blob;
+    DP.hdr = d->hdr;
+    if (d->hdr.total_len <= DESC_LDS_BYTES)
+        hipLaunchKernelGGL(j2t_lane_kernel<true>, dim3((uint32_t)blocks), dim3(LANE_BLOCK), 0, s, P, DP);
+    else
+        hipLaunchKernelGGL(j2t_lane_kernel<false>, dim3((uint32_t)blocks), dim3(LANE_BLOCK), 0, s, P, DP);
     HIPCHK(hipGetLastError());
     return DG_OK;
 }

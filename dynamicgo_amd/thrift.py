@@ -249,6 +249,21 @@ def flatten(root: TypeDescriptor) -> FlatDescriptor:
         pool_index[b] = off
         return off
 
+    key_index: Dict[bytes, int] = {}
+
+    def pool_key(b: bytes) -> int:
+        # keys: 8-aligned and zero-padded so the fast path compares whole words
+        if b in key_index:
+            return key_index[b]
+        while len(pool) % 8:
+            pool.append(0)
+        off = len(pool)
+        pool.extend(b)
+        while len(pool) % 8 or len(pool) == off:
+            pool.append(0)
+        key_index[b] = off
+        return off
+
     type_rows = []
     for t in types:
         flags = 1 if t.is_binary() else 0
@@ -270,12 +285,15 @@ def flatten(root: TypeDescriptor) -> FlatDescriptor:
         findex = {id(f): fbegin + i for i, f in enumerate(fields)}
         for f in fields:
             fl = (1 if f.is_request_base else 0) | (2 if f.http_mappings else 0)
+            if sd.names.get(f.alias) is f:
+                fl |= 4  # DG_FF_ALIAS_SELF
             if f.default_value is not None:
                 doff, dlen = pool_put(bytes(f.default_value)), len(f.default_value)
             else:
                 doff, dlen = 0, DG_NONE
-            field_rows.append(_st.pack(FIELD_FMT, f.id, f.required, fl, f.vm, 0,
-                                       tindex[id(f.type)], doff, dlen, 0))
+            ak = f.alias.encode()
+            field_rows.append(_st.pack(FIELD_FMT, f.id, f.required, fl, f.vm, len(ak),
+                                       tindex[id(f.type)], doff, dlen, pool_key(ak)))
         # requires bits by field index
         nw = max(1, (len(fields) + 63) // 64)
         words = [0] * nw
@@ -295,7 +313,7 @@ def flatten(root: TypeDescriptor) -> FlatDescriptor:
             j = h & (size - 1)
             while slots[j] is not None:
                 j = (j + 1) & (size - 1)
-            slots[j] = (h, pool_put(kb), len(kb), findex[id(sd.ids[f.id])])
+            slots[j] = (h, pool_key(kb), len(kb), findex[id(sd.ids[f.id])])
         nbegin = len(name_rows)
         for s in slots:
             name_rows.append(_st.pack(NAME_FMT, *(s if s else (0, 0, 0, DG_NONE))))
@@ -317,7 +335,7 @@ def flatten(root: TypeDescriptor) -> FlatDescriptor:
     offs.append(len(body))
     body.extend(pool)
     _align8(body)
-    hdr = _st.pack(HDR_FMT, DG_DESC_MAGIC, 1, len(body), root_idx,
+    hdr = _st.pack(HDR_FMT, DG_DESC_MAGIC, 2, len(body), root_idx,
                    len(type_rows), offs[0], len(struct_rows), offs[1],
                    len(field_rows), offs[2], len(name_rows), offs[3],
                    len(req_words), offs[4], len(pool), offs[5])

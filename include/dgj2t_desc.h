@@ -16,7 +16,8 @@
  *   fields[n_fields]    dg_field   24 B  (per struct: contiguous, sorted by field id)
  *   names[n_names]      dg_name    16 B  (per struct: open-addressing table, power of 2)
  *   reqwords[n_reqw]    u64              (per struct: initial requires bits by field INDEX)
- *   pool[pool_len]      bytes            (name keys, IDL default-value Thrift bytes)
+ *   pool[pool_len]      bytes            (name keys 8-aligned and zero-padded to a
+ *                                         multiple of 8, IDL default-value Thrift bytes)
  *
  * Semantics pinned to the reference:
  *  - field-name lookup = exact match on the key bytes; keys are alias and name,
@@ -35,7 +36,7 @@
 #include <stdint.h>
 
 #define DG_DESC_MAGIC 0x31444744u /* "DGD1" */
-#define DG_DESC_VERSION 1u
+#define DG_DESC_VERSION 2u /* v2: alias key per field, 8-aligned keys (v1 blobs still accepted) */
 #define DG_NONE 0xffffffffu
 
 /* Thrift wire type codes (reference native/thrift.h:45-63). */
@@ -64,6 +65,8 @@
 /* dg_field.flags */
 #define DG_FF_REQUEST_BASE 1u /* FieldDescriptor.isRequestBase */
 #define DG_FF_HTTP_MAPPING 2u /* len(FieldDescriptor.httpMappings) != 0 */
+#define DG_FF_ALIAS_SELF 4u   /* the field's alias key resolves to this field in the name map
+                                 (lets the fast path confirm a predicted key by one compare) */
 
 /* dg_field.vm (reference native/thrift.h:64-67) */
 #define DG_VM_NONE 0
@@ -111,11 +114,11 @@ typedef struct dg_field {
     int8_t required;      /* DG_REQ_* (FieldDescriptor.required) */
     uint8_t flags;        /* DG_FF_* */
     uint16_t vm;          /* value-mapping type, DG_VM_* */
-    uint16_t _pad;
+    uint16_t key_len;     /* alias key length (bytes) */
     uint32_t type;        /* type index */
     uint32_t dflt_off;    /* pool offset of the IDL default value as Thrift bytes */
     uint32_t dflt_len;    /* DG_NONE = no default value */
-    uint32_t _pad2;
+    uint32_t key_off;     /* pool offset of the alias key (8-aligned, zero-padded) */
 } dg_field;
 
 typedef struct dg_name {

@@ -33,5 +33,5 @@ def test_descriptor_blob_layout():
     from dynamicgo_amd.thrift import flatten
     fl = flatten(simple_desc())
     hdr = struct.unpack("<16I", fl.blob[:64])
-    assert hdr[0] == 0x31444744 and hdr[1] == 1 and hdr[2] == len(fl.blob)
+    assert hdr[0] == 0x31444744 and hdr[1] == 2 and hdr[2] == len(fl.blob)
     assert hdr[4] >= 7 and hdr[6] == 1 and hdr[8] == 6  # types, 1 struct, 6 fields
