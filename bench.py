@@ -113,13 +113,9 @@ def main():
     L = _lib.lib()
     ctx = conv.Context(local)
     if dist:
-        nb = torch.tensor([len(flat.blob)], dtype=torch.int64, device=dev)
-        torch.distributed.broadcast(nb, 0)
-        blob = torch.empty(int(nb.item()), dtype=torch.uint8, device=dev)
-        if rank == 0:
-            blob.copy_(torch.frombuffer(bytearray(flat.blob), dtype=torch.uint8))
-        torch.distributed.broadcast(blob, 0)
+        from dynamicgo_amd import dist as D
         import ctypes as C
+        blob = D.broadcast_blob(flat.blob if rank == 0 else None, dev)  # RCCL over xGMI
         h = C.c_void_p()
         _lib.check(L.dg_desc_create_device(ctx.h, blob.data_ptr(), blob.numel(), C.byref(h)))
         ctx._descs[flat.blob] = h
@@ -129,7 +125,7 @@ def main():
     n = len(msgs)
     lens = np.diff(off).astype(np.int64)
     slots = np.zeros(n + 1, dtype=np.int64)
-    np.cumsum(lens * 4 + 64, out=slots[1:])
+    np.cumsum((lens * 4 + 64 + 7) & ~7, out=slots[1:])  # dg_slot_bound: 8-aligned slots
     d_json = torch.from_numpy(arena).to(dev)
     d_in = torch.from_numpy(off.astype(np.int64)).to(dev)
     d_out = torch.empty(int(slots[-1]) + 64, dtype=torch.uint8, device=dev)
@@ -146,9 +142,11 @@ def main():
                                          d_out.data_ptr(), d_oo.data_ptr(), d_ol.data_ptr(), d_ret.data_ptr(),
                                          d_pend.data_ptr(), stream.cuda_stream))
 
+    ctx.stats(reset=True)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    bails, deeps = ctx.stats(reset=True)
     # correctness of what we time: every message converted, none left pending
     rets = d_ret.cpu().numpy()
     ok = int((rets == 0).sum())
@@ -203,7 +201,9 @@ def main():
                        "avg_json_bytes": round(json_bytes / n, 1), "msgs_per_s": round(msgs_per_s),
                        "thrift_bytes_per_rank": thrift_bytes, "flags": flags,
                        "parallelism": f"dp{world} (independent shards, descriptor RCCL-broadcast)",
-                       "ok_msgs_per_rank": ok},
+                       "ok_msgs_per_rank": ok,
+                       "exact_path_msgs_per_step": bails / max(1, args.warmup),
+                       "deep_msgs_per_step": deeps / max(1, args.warmup)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "kernel_ms": round(gpu_ms, 5), "alg_bytes_per_launch": alg_bytes},

@@ -22,14 +22,32 @@ def _run(cmd, cwd=None):
     subprocess.run(cmd, cwd=cwd, check=True)
 
 
-def build_hip(force=False):
-    out = os.path.join(ROOT, "dynamicgo_amd", "libdgj2t.so")
-    srcs = [os.path.join(CSRC, f) for f in ("j2t_kernel.hip", "j2t_device.h", "dg_tables.h")]
+UNITS = ("j2t_kern_lds.hip", "j2t_kern_glb.hip", "j2t_host.hip")
+HEADERS = ("j2t_machine.h", "j2t_device.h", "j2t_fast.h", "dg_tables.h")
+
+
+def build_hip(force=False, extra_flags=(), out=None):
+    """Compile the translation units in parallel (one hipcc each), then link."""
+    out = out or os.path.join(ROOT, "dynamicgo_amd", "libdgj2t.so")
+    srcs = [os.path.join(CSRC, f) for f in UNITS + HEADERS]
     srcs += [os.path.join(ROOT, "include", f) for f in ("dgj2t.h", "dgj2t_desc.h")]
     if not force and os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(s) for s in srcs):
         return out
-    _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-          "-ffp-contract=off", "-Wno-unused-result", "-o", out, os.path.join(CSRC, "j2t_kernel.hip")])
+    objdir = os.path.join(ROOT, "build", "obj" + ("_" + str(abs(hash(tuple(extra_flags)))) if extra_flags else ""))
+    os.makedirs(objdir, exist_ok=True)
+    common = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
+              "-Wno-unused-result", *extra_flags]
+    procs, objs = [], []
+    for u in UNITS:
+        o = os.path.join(objdir, u.replace(".hip", ".o"))
+        cmd = common + ["-c", "-o", o, os.path.join(CSRC, u)]
+        print("+", " ".join(cmd), flush=True)
+        procs.append((u, subprocess.Popen(cmd)))
+        objs.append(o)
+    failed = [u for u, p in procs if p.wait() != 0]
+    if failed:
+        raise RuntimeError(f"hipcc failed on {failed}")
+    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out, *objs])
     return out
 
 

@@ -161,6 +161,13 @@ class Context:
             self._descs[flat.blob] = d
         return d
 
+    def stats(self, reset: bool = False):
+        """(bails, deeps): messages the fast path handed to the exact machine
+        and messages redone with the deep stack, since the last reset."""
+        b, d = C.c_uint64(0), C.c_uint64(0)
+        _lib.check(_lib.lib().dg_ctx_stats(self.h, C.byref(b), C.byref(d), int(reset)))
+        return int(b.value), int(d.value)
+
     def close(self):
         L = _lib.lib()
         for d in self._descs.values():

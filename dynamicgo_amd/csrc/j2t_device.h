@@ -546,13 +546,8 @@ DGI int64_t decode_block(S &src, int64_t s0, int64_t ie, int64_t &ipp, Out &o, i
 /* Decodes src[s0, s0+nb), appending to o; returns the decoded length or
  * (ib - ip - dv) < 0 like the reference. */
 template <class S>
-DGI int64_t b64decode(Out &o, S &src, int64_t s0, int64_t nb)
+DGI int64_t b64decode_from(Out &o, S &src, int64_t s0, int64_t nb, int64_t ip, int64_t op)
 {
-#ifdef DG_ABL_NOB64
-    return (nb / 4) * 3;
-#endif
-    if (nb == 0) return 0;
-    int64_t ip = 0, op = 0;
     /* whole 4-char quanta of alphabet characters: decode_block on such a
      * quantum consumes exactly it (the reference's 8/4-byte loops) */
     while (ip + 4 <= nb) {
@@ -569,6 +564,15 @@ DGI int64_t b64decode(Out &o, S &src, int64_t s0, int64_t nb)
         if (dv != 0) return -ip - dv;
     }
     return op;
+}
+template <class S>
+DGI int64_t b64decode(Out &o, S &src, int64_t s0, int64_t nb)
+{
+#ifdef DG_ABL_NOB64
+    return (nb / 4) * 3;
+#endif
+    if (nb == 0) return 0;
+    return b64decode_from(o, src, s0, nb, 0, 0);
 }
 
 /* ====================================================================== */

@@ -1,0 +1,730 @@
+/*
+ * j2t_fast.h — the fast path of the lane-per-message transcoder.
+ *
+ * The exact machine (j2t_kernel.hip, Machine<>) restates j2t_fsm_exec state by
+ * state, error word by error word. Almost every production message takes only
+ * a small, error-free part of that automaton, so the kernel first runs this
+ * leaner converter, which accepts exactly the inputs on which it can produce
+ * the reference's output and BAILS on everything else (any error, unusual
+ * flags, escaped keys, deep nesting, >64-field structs, numbers needing the
+ * big-decimal slow path, output-slot overflow). A bailed message is redone
+ * from scratch by the exact machine, so results are bit-identical either way
+ * and error words always come from the exact machine.
+ *
+ * What makes it faster than the state-by-state FSM:
+ *  - the innermost container lives in registers (LDS holds only parents);
+ *  - object keys are matched against a PREDICTED field (the one after the
+ *    previous field, dg_field.key_off/key_len in descriptor v2) by 8-byte word
+ *    compares; the hash table is only probed on a miss;
+ *  - digits are scanned and accumulated 8 at a time (SWAR), base64 is decoded
+ *    8 characters -> 6 bytes at a time, escaped strings are copied in runs
+ *    between backslashes.
+ *
+ * Reference semantics reproduced here: j2t_fsm_exec native/thrift.c:765-1187
+ * (container/null/unset handling), vnumber native/scanning.c:958-1083,
+ * unquote native/parsing.c:702-945, b64decode native/base64.c:659-817.
+ */
+#pragma once
+#include "j2t_device.h"
+
+namespace dg {
+
+constexpr uint32_t FK_STRUCT = 1, FK_MAP = 2, FK_LIST = 3;
+constexpr uint32_t FAST_LDS_DEPTH = 8; /* parent frames per lane in LDS */
+
+/* one parent container of the fast path (16 B) */
+struct FFrame {
+    uint32_t a; /* struct: struct index; map/list: element type */
+    uint32_t b; /* kind | (hint or count) << 2 */
+    uint64_t u; /* struct: requires bits; list: size position; map: size position | key type << 32 */
+};
+typedef __attribute__((address_space(3))) FFrame LFFrame;
+typedef const __attribute__((address_space(3))) double lds_f64;
+
+/* flags the fast path handles itself; any other flag bit -> bail at entry */
+constexpr uint64_t FAST_FLAGS = DG_F_ALLOW_UNKNOWN | DG_F_WRITE_DEFAULT | DG_F_ENABLE_VM | DG_F_ENABLE_I2S |
+                                DG_F_WRITE_REQUIRE | DG_F_NO_BASE64 | DG_F_WRITE_OPTIONAL | DG_F_NO_WRITE_BASE;
+
+/* small power tables, copied to LDS by the kernel prologue */
+struct FastTabs {
+    const __attribute__((address_space(3))) uint64_t *p10u; /* 10^k, k = 0..19 */
+    lds_f64 *p10d;                                          /* 1e0 .. 1e22 */
+};
+
+/* ---- SWAR helpers ---- */
+
+/* leading ASCII digits among the 8 bytes at src[i..] (bytes at >= n excluded);
+ * x = the bytes XOR '0' (digit values in the digit bytes) */
+template <class S>
+DGI uint32_t digits8(S &src, int64_t i, uint64_t &x)
+{
+    const uint64_t H = 0x8080808080808080ull;
+    uint64_t w = src.get8(i);
+    x = w ^ 0x3030303030303030ull;
+    uint64_t nd = (((x & 0x7F7F7F7F7F7F7F7Full) + 0x7676767676767676ull) | x) & H;
+    int64_t lim = src.n - i;
+    if (lim < 8) nd |= lim <= 0 ? H : (H & (~0ull << (lim << 3)));
+    return nd ? (uint32_t)__builtin_ctzll(nd) >> 3 : 8u;
+}
+
+/* value of the first t (1..8) digits of x */
+DGI uint64_t swar_val(uint64_t x, uint32_t t)
+{
+    uint64_t y = t >= 8 ? x : x << ((8 - t) << 3);
+    y = ((y & 0x0F0F0F0F0F0F0F0Full) * 2561) >> 8;
+    y = ((y & 0x00FF00FF00FF00FFull) * 6553601) >> 16;
+    return ((y & 0x0000FFFF0000FFFFull) * 42949672960001ull) >> 32;
+}
+
+/* man = man * 10^t + (first t digits), t = min(k, 19 - nd) (the reference's
+ * `if (man_nd < 19)` digit cap); returns t */
+DGI uint32_t acc_digits(uint64_t &man, int &nd, uint64_t x, uint32_t k, const FastTabs &tb)
+{
+    uint32_t room = (uint32_t)(19 - nd);
+    uint32_t t = k < room ? k : room;
+    if (t) {
+        man = man * tb.p10u[t] + swar_val(x, t);
+        nd += (int)t;
+    }
+    return t;
+}
+
+/* is_atof_exact (native/scanning.c:883-926) with the powers in LDS */
+DGI bool atof_exact_l(uint64_t man, int exp, int sgn, double &val, const FastTabs &tb)
+{
+    val = (double)man;
+    if (man >> 52 != 0) return false;
+    val = with_sign(val, sgn);
+    if (exp == 0 || man == 0) return true;
+    if (exp > 0 && exp <= 15 + 22) {
+        if (exp > 22) {
+            val = __dmul_rn(val, tb.p10d[exp - 22]);
+            exp = 22;
+        }
+        if (val > 1e15 || val < -1e15) return false;
+        val = __dmul_rn(val, tb.p10d[exp]);
+        return true;
+    }
+    if (exp < 0 && exp >= -22) {
+        val = __ddiv_rn(val, tb.p10d[-exp]);
+        return true;
+    }
+    return false;
+}
+
+/* vnumber (native/scanning.c:958-1083) on the success paths; false = the
+ * reference would error or need atof_native -> bail. */
+template <class S>
+DGI bool fast_vnumber(S &src, int64_t &p, const FastTabs &tb, int64_t &iv, double &dv, bool &isint)
+{
+    int64_t i = p;
+    uint8_t c = src.at(i);
+    int sgn = 1;
+    if (c == '-') {
+        sgn = -1;
+        c = src.at(++i);
+    }
+    if ((uint8_t)(c - '0') > 9) return false;
+    isint = true;
+    iv = 0;
+    dv = 0.0;
+    if (c == '0') {
+        uint8_t c1 = src.at(i + 1);
+        if (c1 != '.' && c1 != 'e' && c1 != 'E') {
+            p = i + 1;
+            return true;
+        }
+    }
+    uint64_t man = 0;
+    int nd = 0, exp10 = 0;
+    bool trunc = false, dbl = false;
+    uint64_t x;
+    for (;;) { /* integer digits */
+        uint32_t k = digits8(src, i, x);
+        uint32_t t = acc_digits(man, nd, x, k, tb);
+        exp10 += (int)(k - t);
+        i += k;
+        if (k < 8) break;
+    }
+    if (exp10 > 0) trunc = true;
+    if (src.at(i) == '.') {
+        i++;
+        dbl = true;
+        if ((uint8_t)(src.at(i) - '0') > 9) return false;
+    }
+    if (man == 0 && exp10 == 0) {
+        while (src.at(i) == '0') {
+            i++;
+            exp10--;
+        }
+        nd = 0;
+    }
+    while (nd < 19) { /* fraction digits up to the cap */
+        uint32_t k = digits8(src, i, x);
+        uint32_t t = acc_digits(man, nd, x, k, tb);
+        exp10 -= (int)t;
+        i += t;
+        if (t < 8) break;
+    }
+    for (;;) { /* digits beyond the cap */
+        uint32_t k = digits8(src, i, x);
+        if (k) trunc = true;
+        i += k;
+        if (k < 8) break;
+    }
+    c = src.at(i);
+    if (c == 'e' || c == 'E') {
+        int esm = 1, e = 0;
+        dbl = true;
+        c = src.at(++i);
+        if (c == '+' || c == '-') {
+            esm = c == '+' ? 1 : -1;
+            c = src.at(++i);
+        }
+        if ((uint8_t)(c - '0') > 9) return false;
+        while ((uint8_t)(c - '0') <= 9) {
+            if (e < 10000) e = e * 10 + (c - '0');
+            c = src.at(++i);
+        }
+        exp10 += e * esm;
+    } else if (!dbl) {
+        /* is_overflow native/scanning.c:950-956 */
+        bool ovf = exp10 != 0 || ((man >> 63) == 1 && (((uint64_t)(int64_t)sgn) & man) != (1ull << 63));
+        if (!ovf) {
+            iv = (int64_t)(man * (uint64_t)(int64_t)sgn);
+            dv = with_sign((double)man, sgn);
+            p = i;
+            return true;
+        }
+    }
+    /* atof_fast native/scanning.c:928-948; atof_native -> bail */
+    double val;
+    if (!atof_exact_l(man, exp10, sgn, val, tb)) {
+        if (!eisel_lemire(man, exp10, sgn, val)) return false;
+        if (trunc) {
+            double vu;
+            if (!eisel_lemire(man + 1, exp10, sgn, vu) || vu != val) return false;
+        }
+    }
+    if ((__double_as_longlong(val) << 1) == 0xFFE0000000000000ull) return false; /* ERR_FLOAT_INF */
+    isint = false;
+    dv = val;
+    p = i;
+    return true;
+}
+
+/* j2t_number's writes (native/thrift.c:312-365) */
+DGI bool emit_number(Out &out, uint8_t tt, bool isint, int64_t iv, double dv)
+{
+    switch (tt) {
+    case DG_T_BYTE: out.w8(isint ? (uint8_t)iv : (uint8_t)cvt32(dv)); return true;
+    case DG_T_I16: out.w16(isint ? (uint16_t)iv : (uint16_t)cvt32(dv)); return true;
+    case DG_T_I32: out.w32(isint ? (uint32_t)iv : (uint32_t)cvt32(dv)); return true;
+    case DG_T_I64: out.w64(isint ? (uint64_t)iv : (uint64_t)cvt64(dv)); return true;
+    case DG_T_DOUBLE: out.w64((uint64_t)__double_as_longlong(dv)); return true;
+    }
+    return false;
+}
+
+/* copy src[s0, s0+n) to the output, 8 bytes per step */
+template <class S>
+DGI void fast_copy(S &src, int64_t s0, int64_t n, Out &out)
+{
+    int64_t i = 0;
+    for (; i + 8 <= n; i += 8) out.wle(src.get8(s0 + i), 8);
+    if (i < n) out.wle(src.get8(s0 + i), (uint32_t)(n - i));
+}
+
+/* 4 hex digits at src[i..i+4) */
+template <class S>
+DGI bool hex4w(S &src, int64_t i, uint32_t &v)
+{
+    uint32_t w = (uint32_t)src.get8(i);
+    uint32_t r = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        int h = hexv((uint8_t)(w >> (8 * k)));
+        if (h < 0) return false;
+        r = (r << 4) | (uint32_t)h;
+    }
+    v = r;
+    return true;
+}
+
+/* unquote (native/parsing.c:702-945, flags 0) of src[s0, s0+nb) appended to
+ * out: runs between backslashes are copied as words. false = error. */
+template <class S>
+DGI bool fast_unquote(S &src, int64_t s0, int64_t nb, Out &out)
+{
+    int64_t i = s0, end = s0 + nb;
+    while (i < end) {
+        uint64_t w = src.get8(i);
+        int64_t rem = end - i;
+        uint64_t m = zbytes(w ^ 0x5C5C5C5C5C5C5C5Cull);
+        if (rem < 8) m &= (1ull << (rem << 3)) - 1;
+        if (m == 0) {
+            uint32_t k = rem < 8 ? (uint32_t)rem : 8u;
+            out.wle(w, k);
+            i += k;
+            continue;
+        }
+        uint32_t j = (uint32_t)__builtin_ctzll(m) >> 3;
+        if (j) out.wle(w, j);
+        i += j;
+        if (end - i < 2) return false;
+        uint8_t c = src.at(i + 1);
+        uint8_t cc;
+        switch (c) { /* _UnquoteTab native/parsing.c:565-575 */
+        case '/': cc = '/'; break;
+        case '"': cc = '"'; break;
+        case 'b': cc = '\b'; break;
+        case 'f': cc = '\f'; break;
+        case 'n': cc = '\n'; break;
+        case 'r': cc = '\r'; break;
+        case 't': cc = '\t'; break;
+        case '\\': cc = '\\'; break;
+        case 'u': cc = 0; break;
+        default: return false;
+        }
+        if (c != 'u') {
+            out.w8(cc);
+            i += 2;
+            continue;
+        }
+        if (end - i < 6) return false;
+        uint32_t r0, r1;
+        if (!hex4w(src, i + 2, r0)) return false;
+        i += 6;
+        if (r0 <= 0x7f) {
+            out.w8((uint8_t)r0);
+        } else if (r0 <= 0x7ff) {
+            out.wle((0xc0 | (r0 >> 6)) | ((0x80 | (r0 & 0x3f)) << 8), 2);
+        } else if (r0 < 0xd800 || r0 > 0xdfff) {
+            out.wle((0xe0 | (r0 >> 12)) | ((0x80 | ((r0 >> 6) & 0x3f)) << 8) | ((0x80 | (r0 & 0x3f)) << 16), 3);
+        } else {
+            if (end - i < 6 || r0 > 0xdbff || src.at(i) != '\\' || src.at(i + 1) != 'u') return false;
+            if (!hex4w(src, i + 2, r1)) return false;
+            if (r1 < 0xdc00 || r1 > 0xdfff) return false;
+            i += 6;
+            r0 = ((r0 - 0xd800) << 10) + (r1 - 0xdc00) + 0x10000;
+            out.wle((0xf0 | (r0 >> 18)) | ((0x80 | ((r0 >> 12) & 0x3f)) << 8) | ((0x80 | ((r0 >> 6) & 0x3f)) << 16) |
+                        ((uint64_t)(0x80 | (r0 & 0x3f)) << 24),
+                    4);
+        }
+    }
+    return true;
+}
+
+/* j2t_string (native/thrift.c:367-399); p is just past the opening quote */
+template <class S>
+DGI bool fast_string(S &src, int64_t &p, Out &out)
+{
+    int64_t s0 = p;
+    bool esc;
+    int64_t e = advance_string(src, s0, esc);
+    if (e < 0) return false;
+    p = e;
+    int64_t nb = e - 1 - s0;
+    if (!esc) {
+        out.w32((uint32_t)nb);
+        fast_copy(src, s0, nb, out);
+        return true;
+    }
+    uint64_t lp = out.alloc(4);
+    uint64_t st = out.len;
+    if (!fast_unquote(src, s0, nb, out)) return false;
+    out.put32(lp, (uint32_t)(out.len - st));
+    return true;
+}
+
+/* 8 base64 characters -> 6 bytes (little-endian in *o); false if any is not
+ * in the standard alphabet */
+DGI bool b64_8(uint64_t w, uint64_t &o)
+{
+    const uint64_t H = 0x8080808080808080ull, L = 0x0101010101010101ull, M7 = 0x7F7F7F7F7F7F7F7Full;
+    if (w & H) return false;
+#define DG_GE(lo) ((w + (uint64_t)(0x80 - (lo)) * L) & H)
+    uint64_t up = DG_GE('A') & ~DG_GE('Z' + 1);
+    uint64_t lw = DG_GE('a') & ~DG_GE('z' + 1);
+    uint64_t dg = DG_GE('0') & ~DG_GE('9' + 1);
+#undef DG_GE
+    uint64_t pl = zbytes(w ^ 0x2B2B2B2B2B2B2B2Bull);
+    uint64_t sl = zbytes(w ^ 0x2F2F2F2F2F2F2F2Full);
+    if ((up | lw | dg | pl | sl) != H) return false;
+    /* per-byte offsets: 'A'->0 (-65), 'a'->26 (-71), '0'->52 (+4), '+'->62 (+19), '/'->63 (+16) */
+    uint64_t off = (((up >> 7) * 0xFF) & (0xBFull * L)) | (((lw >> 7) * 0xFF) & (0xB9ull * L)) |
+                   (((dg >> 7) * 0xFF) & (0x04ull * L)) | (((pl >> 7) * 0xFF) & (0x13ull * L)) |
+                   (((sl >> 7) * 0xFF) & (0x10ull * L));
+    uint64_t v = ((w & M7) + (off & M7)) ^ ((w ^ off) & H); /* bytewise add mod 256 */
+    uint64_t a = ((v & 0x003F003F003F003Full) << 6) | ((v >> 8) & 0x003F003F003F003Full);
+    uint64_t b = ((a & 0x00000FFF00000FFFull) << 12) | ((a >> 16) & 0x00000FFF00000FFFull);
+    o = (uint64_t)(__builtin_bswap32((uint32_t)b) >> 8) | ((uint64_t)(__builtin_bswap32((uint32_t)(b >> 32)) >> 8) << 24);
+    return true;
+}
+
+/* j2t_binary (native/thrift.c:401-420) */
+template <class S>
+DGI bool fast_binary(S &src, int64_t &p, Out &out)
+{
+    int64_t s0 = p;
+    bool esc;
+    int64_t e = advance_string(src, s0, esc);
+    if (e < 0 || esc) return false; /* '\\' is outside the alphabet: decode error */
+    p = e;
+    int64_t nb = e - 1 - s0;
+    uint64_t lp = out.alloc(4);
+    int64_t ip = 0, op = 0;
+    while (ip + 8 <= nb) {
+        uint64_t o;
+        if (!b64_8(src.get8(s0 + ip), o)) break;
+        out.wle(o, 6);
+        ip += 8;
+        op += 6;
+    }
+    if (ip < nb) {
+        op = b64decode_from(out, src, s0, nb, ip, op);
+        if (op < 0) return false;
+    }
+    out.put32(lp, (uint32_t)op);
+    return true;
+}
+
+/* key bytes src[k0, k0+kn) == the zero-padded 8-aligned pool key at pk */
+template <class S, int AS>
+DGI bool key_eq(S &src, int64_t k0, uint32_t kn, const __attribute__((address_space(AS))) uint64_t *pk)
+{
+    for (uint32_t j = 0; j < kn; j += 8) {
+        uint64_t a = src.get8(k0 + j);
+        uint32_t rem = kn - j;
+        if (rem < 8) a &= (1ull << (rem << 3)) - 1;
+        if (a != pk[j >> 3]) return false;
+    }
+    return true;
+}
+
+/* the fast converter over one message; true = out holds the reference's
+ * output, false = bail to the exact machine */
+template <class S, class DV>
+DGI bool fast_convert(const DV &D, S &src, Out &out, uint64_t flag, uint32_t root, LFFrame *fr, uint32_t fstride,
+                      const FastTabs &tb)
+{
+    /* empty body and unquoted STRING roots are the prelude's business (convert_one) */
+    if (src.n == 0 || ldrec(&D.T[root]).ttype == DG_T_STRING) return false;
+    int64_t p = 0;
+    uint32_t sp = 0;                  /* open containers */
+    uint32_t ca = 0, ck = 0, cb = 0;  /* innermost: a, kind, hint/count */
+    uint64_t cu = 0;                  /* innermost: reqs or size position */
+    bool null_val = false;
+    uint64_t unwind = 0;
+    uint32_t lastf = 0;
+    uint32_t td = root;
+    uint8_t c;
+
+#define FAST_PUSH(na, nk, nu)                                             \
+    do {                                                                  \
+        if (sp) {                                                         \
+            if (sp > FAST_LDS_DEPTH) return false;                        \
+            LFFrame &f_ = fr[(sp - 1) * fstride];                         \
+            f_.a = ca;                                                    \
+            f_.b = ck | (cb << 2);                                        \
+            f_.u = cu;                                                    \
+        }                                                                 \
+        sp++;                                                             \
+        ca = (na);                                                        \
+        ck = (nk);                                                        \
+        cb = 0;                                                           \
+        cu = (nu);                                                        \
+    } while (0)
+#define FAST_POP()                                                        \
+    do {                                                                  \
+        if (--sp) {                                                       \
+            const LFFrame &f_ = fr[(sp - 1) * fstride];                   \
+            ca = f_.a;                                                    \
+            ck = f_.b & 3;                                                \
+            cb = f_.b >> 2;                                               \
+            cu = f_.u;                                                    \
+        }                                                                 \
+    } while (0)
+
+    for (;;) {
+        /* ---------------- a value of type td ---------------- */
+        c = src.at(p++);
+        while (c <= ' ') {
+            if (!isspace_(c)) return false;
+            c = src.at(p++);
+        }
+        const dg_type t = ldrec(&D.T[td]);
+        bool opened = false; /* a container was opened: look for its first key/element */
+        switch (c) {
+        case '"':
+            if (t.ttype != DG_T_STRING) return false;
+            if ((flag & DG_F_NO_BASE64) == 0 && (t.flags & DG_TF_BINARY)) {
+                if (!fast_binary(src, p, out)) return false;
+            } else {
+                if (!fast_string(src, p, out)) return false;
+            }
+            break;
+        case '0': case '1': case '2': case '3': case '4':
+        case '5': case '6': case '7': case '8': case '9': case '-': {
+            p -= 1;
+            int64_t iv;
+            double dv;
+            bool isint;
+            if (!fast_vnumber(src, p, tb, iv, dv, isint)) return false;
+            if (!emit_number(out, t.ttype, isint, iv, dv)) return false;
+            break;
+        }
+        case 't':
+            if (p + 3 > src.n || (uint32_t)src.get8(p - 1) != VS_TRUE || t.ttype != DG_T_BOOL) return false;
+            p += 3;
+            out.w8(1);
+            break;
+        case 'f':
+            if (p + 4 > src.n || (uint32_t)src.get8(p) != VS_ALSE || t.ttype != DG_T_BOOL) return false;
+            p += 4;
+            out.w8(0);
+            break;
+        case 'n':
+            if (p + 3 > src.n || (uint32_t)src.get8(p - 1) != VS_NULL || sp == 0) return false;
+            p += 3;
+            null_val = true;
+            break;
+        case '[': {
+            if (t.ttype != DG_T_LIST && t.ttype != DG_T_SET) return false;
+            out.w8(ldrec(&D.T[t.elem]).ttype);
+            uint64_t bp = out.alloc(4);
+            FAST_PUSH(t.elem, FK_LIST, bp);
+            opened = true;
+            break;
+        }
+        case '{':
+            if (t.ttype == DG_T_STRUCT) {
+                const dg_struct sd = ldrec(&D.S[t.st]);
+                if (sd.req_words != 1) return false;
+                FAST_PUSH(t.st, FK_STRUCT, D.R[sd.req_begin]);
+            } else if (t.ttype == DG_T_MAP) {
+                out.wle(ldrec(&D.T[t.key]).ttype | ((uint32_t)ldrec(&D.T[t.elem]).ttype << 8), 2);
+                uint64_t bp = out.alloc(4);
+                FAST_PUSH(t.elem, FK_MAP, bp | ((uint64_t)t.key << 32));
+            } else {
+                return false;
+            }
+            opened = true;
+            break;
+        default:
+            return false;
+        }
+
+        /* ------------- after a value / an opening bracket ------------- */
+        bool first = opened;
+        for (;;) {
+            if (sp == 0) {
+                out.finish();
+                return out.len <= out.cap;
+            }
+            c = src.at(p++);
+            while (c <= ' ') {
+                if (!isspace_(c)) return false;
+                c = src.at(p++);
+            }
+            if (ck == FK_LIST) {
+                if (first) {
+                    first = false;
+                    if (c == ']') { /* size 0 already written */
+                        FAST_POP();
+                        continue;
+                    }
+                    p -= 1;
+                    td = ca;
+                    break;
+                }
+                if (null_val) null_val = false;
+                else cb++;
+                if (c == ',') {
+                    td = ca;
+                    break;
+                }
+                if (c != ']') return false;
+                out.put32(cu, cb);
+                FAST_POP();
+                continue;
+            }
+            /* objects: struct or map */
+            if (first) {
+                first = false;
+                if (c == '}') {
+                    if (ck == FK_MAP) {
+                        FAST_POP();
+                        continue;
+                    }
+                    goto close_struct;
+                }
+            } else if (ck == FK_MAP) {
+                if (null_val) {
+                    null_val = false;
+                    out.set_len(unwind);
+                } else {
+                    cb++;
+                }
+                if (c == '}') {
+                    out.put32((uint32_t)cu, cb);
+                    FAST_POP();
+                    continue;
+                }
+                if (c != ',') return false;
+                c = src.at(p++);
+                while (c <= ' ') {
+                    if (!isspace_(c)) return false;
+                    c = src.at(p++);
+                }
+            } else {
+                if (null_val) { /* native/thrift.c:1016-1032 */
+                    null_val = false;
+                    const dg_field f = ldrec(&D.F[lastf]);
+                    const dg_struct sd = ldrec(&D.S[ca]);
+                    uint64_t m = 1ull << (lastf - sd.field_begin);
+                    if (f.required == DG_REQ_DEFAULT || f.required == DG_REQ_REQUIRED) cu |= m;
+                    else if (f.required == DG_REQ_OPTIONAL) cu &= ~m;
+                    out.set_len(unwind);
+                }
+                if (c == '}') goto close_struct;
+                if (c != ',') return false;
+                c = src.at(p++);
+                while (c <= ' ') {
+                    if (!isspace_(c)) return false;
+                    c = src.at(p++);
+                }
+            }
+            /* a key */
+            if (c != '"') return false;
+            {
+                int64_t k0 = p;
+                bool esc;
+                int64_t e = advance_string(src, k0, esc);
+                if (e < 0 || esc) return false;
+                p = e;
+                uint32_t kn = (uint32_t)(e - 1 - k0);
+                c = src.at(p++);
+                while (c <= ' ') {
+                    if (!isspace_(c)) return false;
+                    c = src.at(p++);
+                }
+                if (c != ':') return false;
+                if (ck == FK_MAP) { /* j2t_map_key native/thrift.c:422-447 */
+                    unwind = out.len;
+                    const uint8_t kt = ldrec(&D.T[(uint32_t)(cu >> 32)]).ttype;
+                    if (kt == DG_T_STRING) {
+                        out.w32(kn);
+                        fast_copy(src, k0, kn, out);
+                    } else {
+                        S ks = src.sub(k0, kn);
+                        int64_t q = 0, iv;
+                        double dv;
+                        bool isint;
+                        if (!fast_vnumber(ks, q, tb, iv, dv, isint)) return false;
+                        if (!emit_number(out, kt, isint, iv, dv)) return false;
+                    }
+                    td = ca;
+                    break;
+                }
+                /* struct field: predicted, then hashed (j2t_key native/thrift.c:668-763) */
+                const dg_struct sd = ldrec(&D.S[ca]);
+                int32_t fi = -1;
+                dg_field f;
+                if (cb < sd.n_fields) {
+                    f = ldrec(&D.F[sd.field_begin + cb]);
+                    if ((f.flags & DG_FF_ALIAS_SELF) && f.key_len == kn &&
+                        key_eq(src, k0, kn, (decltype(&D.R[0]))(&D.P[f.key_off])))
+                        fi = (int32_t)(sd.field_begin + cb);
+                }
+                if (fi < 0) {
+                    uint32_t h = DG_NAME_HASH_SEED;
+                    for (uint32_t j = 0; j < kn; j++) h = DG_NAME_HASH_STEP(h, src.raw(k0 + j));
+                    for (uint32_t s = h & sd.name_mask;; s = (s + 1) & sd.name_mask) {
+                        const dg_name nm = ldrec(&D.N[sd.name_begin + s]);
+                        if (nm.field == DG_NONE) break;
+                        if (nm.hash == h && nm.key_len == kn &&
+                            key_eq(src, k0, kn, (decltype(&D.R[0]))(&D.P[nm.key_off]))) {
+                            fi = (int32_t)nm.field;
+                            break;
+                        }
+                    }
+                    if (fi >= 0) f = ldrec(&D.F[fi]);
+                }
+                if (fi < 0 || ((f.flags & DG_FF_REQUEST_BASE) && (flag & DG_F_NO_WRITE_BASE))) {
+                    if (fi < 0 && (flag & DG_F_ALLOW_UNKNOWN) == 0) return false;
+                    /* skip the value (skip_one native/scanning.c:1134-1631) */
+                    c = src.at(p++);
+                    while (c <= ' ') {
+                        if (!isspace_(c)) return false;
+                        c = src.at(p++);
+                    }
+                    p -= 1;
+                    SkipRes sr = skip_one(src, p, nullptr, 64);
+                    if (sr.r < 0) return false;
+                    p = sr.p;
+                    continue; /* back to "after a value" */
+                }
+                if ((flag & DG_F_ENABLE_VM) && f.vm != DG_VM_NONE) return false;
+                uint32_t k = (uint32_t)fi - sd.field_begin;
+                unwind = out.len;
+                lastf = (uint32_t)fi;
+                const dg_type ft = ldrec(&D.T[f.type]);
+                out.wle((uint32_t)ft.ttype | ((uint32_t)__builtin_bswap16(f.id) << 8), 3);
+                cu &= ~(1ull << k);
+                cb = k + 1;
+                td = f.type;
+                break;
+            }
+        close_struct: { /* j2t_write_unset_fields native/thrift.c:258-310, then STOP */
+            const dg_struct sd = ldrec(&D.S[ca]);
+            uint64_t bits = cu;
+            bool wr = flag & DG_F_WRITE_REQUIRE, wd = flag & DG_F_WRITE_DEFAULT, wo = flag & DG_F_WRITE_OPTIONAL;
+            while (bits) {
+                uint32_t k = __builtin_ctzll(bits);
+                bits &= bits - 1;
+                const dg_field f = ldrec(&D.F[sd.field_begin + k]);
+                if (f.flags & DG_FF_REQUEST_BASE) continue;
+                if (!wr && f.required == DG_REQ_REQUIRED) return false; /* ERR_NULL_REQUIRED */
+                if ((wr && f.required == DG_REQ_REQUIRED) || (wd && f.required == DG_REQ_DEFAULT) ||
+                    (wo && f.required == DG_REQ_OPTIONAL)) {
+                    const dg_type ft = ldrec(&D.T[f.type]);
+                    out.wle((uint32_t)ft.ttype | ((uint32_t)__builtin_bswap16(f.id) << 8), 3);
+                    if (f.dflt_len != DG_NONE) {
+                        for (uint32_t j = 0; j < f.dflt_len; j++) out.w8(D.P[f.dflt_off + j]);
+                        continue;
+                    }
+                    switch (ft.ttype) { /* tb_write_empty native/thrift.c:171-203 */
+                    case DG_T_BOOL:
+                    case DG_T_BYTE: out.w8(0); break;
+                    case DG_T_I16: out.w16(0); break;
+                    case DG_T_I32:
+                    case DG_T_STRING: out.w32(0); break;
+                    case DG_T_I64:
+                    case DG_T_DOUBLE: out.w64(0); break;
+                    case DG_T_LIST:
+                    case DG_T_SET:
+                        out.w8(ldrec(&D.T[ft.elem]).ttype);
+                        out.w32(0);
+                        break;
+                    case DG_T_MAP:
+                        out.w8(ldrec(&D.T[ft.key]).ttype);
+                        out.w8(ldrec(&D.T[ft.elem]).ttype);
+                        out.w32(0);
+                        break;
+                    case DG_T_STRUCT: out.w8(0); break;
+                    default: return false;
+                    }
+                }
+            }
+            out.w8(0);
+            FAST_POP();
+            continue;
+        }
+        }
+    }
+#undef FAST_PUSH
+#undef FAST_POP
+}
+
+}  // namespace dg

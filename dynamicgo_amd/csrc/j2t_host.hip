@@ -1,0 +1,388 @@
+/*
+ * j2t_host.hip — the C ABI (include/dgj2t.h): contexts, descriptors, batch
+ * launches and the host-buffer entry points. Kernels: j2t_machine.h.
+ */
+#include <hip/hip_runtime.h>
+
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+#include <vector>
+
+#include "j2t_machine.h"
+
+/* ========================================================================== */
+/* host side: C ABI                                                            */
+/* ========================================================================== */
+using namespace dg;
+
+static thread_local char g_err[512];
+static int set_err(int code, const char *fmt, ...)
+{
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    va_end(ap);
+    return code;
+}
+#define HIPCHK(x)                                                                              \
+    do {                                                                                       \
+        hipError_t e_ = (x);                                                                   \
+        if (e_ != hipSuccess) return set_err(DG_E_HIP, "%s: %s", #x, hipGetErrorString(e_));  \
+    } while (0)
+
+struct dg_ctx {
+    int device;
+    hipStream_t stream;
+    uint8_t *ws_fast = nullptr;
+    uint64_t ws_fast_lanes = 0;
+    uint32_t *d_deep_count = nullptr;
+    uint64_t *d_deep_list = nullptr;
+    uint8_t *ws_deep = nullptr;
+    uint32_t *d_pending = nullptr;
+    unsigned long long *d_stats = nullptr; /* {bails, deeps} since the last dg_ctx_stats reset */
+    std::mutex mu;
+    /* staging for the host API */
+    uint8_t *d_json = nullptr; uint64_t d_json_cap = 0;
+    uint64_t *d_in_off = nullptr; uint64_t d_in_cap = 0;
+    uint8_t *d_out = nullptr; uint64_t d_out_cap = 0;
+    uint64_t *d_out_off = nullptr; uint64_t d_oo_cap = 0;
+    uint32_t *d_out_len = nullptr; uint64_t d_ol_cap = 0;
+    uint64_t *d_ret = nullptr; uint64_t d_ret_cap = 0;
+};
+
+struct dg_desc {
+    dg_ctx *ctx;
+    uint8_t *d_blob;
+    size_t len;
+    dg_desc_hdr hdr;
+};
+
+static const uint64_t FAST_WS_STRIDE = DCAP + WS_KEYCAP + (uint64_t)WS_REQCAP * 8;
+static const uint64_t DEEP_WS_STRIDE = DCAP + DEEP_KEYCAP + (uint64_t)DEEP_REQCAP * 8 +
+                                       (uint64_t)MAX_RECURSE * sizeof(Frame) + MAX_RECURSE / 8;
+
+template <class T>
+static int grow(T *&p, uint64_t &cap, uint64_t want)
+{
+    if (cap >= want) return DG_OK;
+    (void)hipFree(p);
+    p = nullptr;
+    uint64_t nc = std::max<uint64_t>(want, cap * 2);
+    HIPCHK(hipMalloc(&p, nc * sizeof(T)));
+    cap = nc;
+    return DG_OK;
+}
+
+extern "C" {
+
+const char *dg_last_error(void) { return g_err; }
+
+int dg_ctx_create(int device, dg_ctx **out)
+{
+    if (!out) return set_err(DG_E_INVALID, "null out");
+    int ndev = 0;
+    HIPCHK(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return set_err(DG_E_INVALID, "device %d out of range (%d)", device, ndev);
+    HIPCHK(hipSetDevice(device));
+    dg_ctx *c = new dg_ctx();
+    c->device = device;
+    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIPCHK(hipMalloc(&c->ws_deep, DEEP_WS_STRIDE * DEEP_THREADS));
+    HIPCHK(hipMalloc(&c->d_pending, 16));
+    HIPCHK(hipMalloc(&c->d_deep_count, 16));
+    HIPCHK(hipMemset(c->d_deep_count, 0, 16)); /* {deep_count, done}: self-reset by each launch */
+    HIPCHK(hipMalloc(&c->d_stats, 16));
+    HIPCHK(hipMemset(c->d_stats, 0, 16));
+    *out = c;
+    return DG_OK;
+}
+
+void dg_ctx_destroy(dg_ctx *c)
+{
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipFree(c->ws_fast);
+    (void)hipFree(c->ws_deep);
+    (void)hipFree(c->d_pending);
+    (void)hipFree(c->d_deep_count);
+    (void)hipFree(c->d_stats);
+    (void)hipFree(c->d_deep_list);
+    (void)hipFree(c->d_json);
+    (void)hipFree(c->d_in_off);
+    (void)hipFree(c->d_out);
+    (void)hipFree(c->d_out_off);
+    (void)hipFree(c->d_out_len);
+    (void)hipFree(c->d_ret);
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+void *dg_ctx_stream(dg_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
+static int desc_finish(dg_ctx *c, const dg_desc_hdr &h, uint8_t *d_blob, size_t len, dg_desc **out)
+{
+    if (h.magic != DG_DESC_MAGIC || h.version < 1 || h.version > DG_DESC_VERSION || h.total_len > len)
+        return set_err(DG_E_DESC, "bad descriptor blob header");
+    dg_desc *d = new dg_desc();
+    d->ctx = c;
+    d->d_blob = d_blob;
+    d->len = len;
+    d->hdr = h;
+    *out = d;
+    return DG_OK;
+}
+
+int dg_desc_create(dg_ctx *c, const void *blob, size_t len, dg_desc **out)
+{
+    if (!c || !blob || !out || len < sizeof(dg_desc_hdr)) return set_err(DG_E_INVALID, "bad args");
+    dg_desc_hdr h;
+    memcpy(&h, blob, sizeof h);
+    if (h.magic != DG_DESC_MAGIC || h.total_len > len) return set_err(DG_E_DESC, "bad descriptor blob");
+    HIPCHK(hipSetDevice(c->device));
+    uint8_t *d_blob;
+    HIPCHK(hipMalloc(&d_blob, len));
+    HIPCHK(hipMemcpy(d_blob, blob, len, hipMemcpyHostToDevice));
+    return desc_finish(c, h, d_blob, len, out);
+}
+
+int dg_desc_create_device(dg_ctx *c, const void *d_src, size_t len, dg_desc **out)
+{
+    if (!c || !d_src || !out || len < sizeof(dg_desc_hdr)) return set_err(DG_E_INVALID, "bad args");
+    HIPCHK(hipSetDevice(c->device));
+    uint8_t *d_blob;
+    HIPCHK(hipMalloc(&d_blob, len));
+    HIPCHK(hipMemcpy(d_blob, d_src, len, hipMemcpyDeviceToDevice));
+    dg_desc_hdr h;
+    HIPCHK(hipMemcpy(&h, d_blob, sizeof h, hipMemcpyDeviceToHost));
+    return desc_finish(c, h, d_blob, len, out);
+}
+
+void dg_desc_destroy(dg_desc *d)
+{
+    if (!d) return;
+    (void)hipFree(d->d_blob);
+    delete d;
+}
+
+uint32_t dg_desc_root(const dg_desc *d) { return d ? d->hdr.root_type : 0; }
+
+int dg_ctx_stats(dg_ctx *c, uint64_t *bails, uint64_t *deeps, int reset)
+{
+    if (!c) return set_err(DG_E_INVALID, "null ctx");
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipDeviceSynchronize());
+    unsigned long long h[2];
+    HIPCHK(hipMemcpy(h, c->d_stats, sizeof h, hipMemcpyDeviceToHost));
+    if (bails) *bails = h[0];
+    if (deeps) *deeps = h[1];
+    if (reset) HIPCHK(hipMemset(c->d_stats, 0, sizeof h));
+    return DG_OK;
+}
+
+uint64_t dg_slot_bound(uint64_t len) { return (4 * len + 64 + 7) & ~7ull; }
+
+static int ensure_fast_ws(dg_ctx *c, uint64_t lanes)
+{
+    if (c->ws_fast_lanes >= lanes) return DG_OK;
+    (void)hipFree(c->ws_fast);
+    (void)hipFree(c->d_deep_list);
+    c->ws_fast = nullptr;
+    c->d_deep_list = nullptr;
+    uint64_t want = std::max<uint64_t>(lanes, 1 << 16);
+    HIPCHK(hipMalloc(&c->ws_fast, want * FAST_WS_STRIDE));
+    HIPCHK(hipMalloc(&c->d_deep_list, want * 8));
+    c->ws_fast_lanes = want;
+    return DG_OK;
+}
+
+static int launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *json, const uint64_t *in_off,
+                  uint64_t n, uint64_t flags, uint8_t *out, const uint64_t *out_off, uint32_t *out_len,
+                  uint64_t *ret, uint32_t *pending, hipStream_t s)
+{
+    if (n == 0) return DG_OK;
+    if (root >= d->hdr.n_types) return set_err(DG_E_INVALID, "root type %u out of range", root);
+    int rc = ensure_fast_ws(c, n);
+    if (rc) return rc;
+    Params P;
+    P.root = root;
+    P.json = json;
+    P.in_off = in_off;
+    P.n = n;
+    P.flag = flags;
+    P.out = out;
+    P.out_off = out_off;
+    P.out_len = out_len;
+    P.ret = ret;
+    P.pending = pending;
+    P.deep_count = c->d_deep_count;
+    P.deep_list = c->d_deep_list;
+    P.ws = c->ws_fast;
+    P.ws_stride = FAST_WS_STRIDE;
+    P.keycap = WS_KEYCAP;
+    P.reqcap = WS_REQCAP;
+    P.fast = d->hdr.version >= 2 && (flags & ~FAST_FLAGS) == 0;
+    P.stats = c->d_stats;
+    uint64_t blocks = (n + LANE_BLOCK - 1) / LANE_BLOCK;
+    DeepParams DP;
+    DP.ws = c->ws_deep;
+    DP.ws_stride = DEEP_WS_STRIDE;
+    DP.keycap = DEEP_KEYCAP;
+    DP.reqcap = DEEP_REQCAP;
+    DP.done = c->d_deep_count + 1;
+    DP.blob = d->d_blob;
+    DP.hdr = d->hdr;
+    if (d->hdr.total_len <= DESC_LDS_BYTES)
+        launch_lane_kernel_lds(dim3((uint32_t)blocks), s, P, DP);
+    else
+        launch_lane_kernel_glb(dim3((uint32_t)blocks), s, P, DP);
+    HIPCHK(hipGetLastError());
+    return DG_OK;
+}
+
+int dg_j2t_batch_device(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *d_json, const uint64_t *d_in_off,
+                        uint64_t n, uint64_t flags, uint8_t *d_out, const uint64_t *d_out_off, uint32_t *d_out_len,
+                        uint64_t *d_ret, uint32_t *d_pending, void *stream)
+{
+    if (!c || !d) return set_err(DG_E_INVALID, "null ctx/desc");
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    return launch(c, d, root, d_json, d_in_off, n, flags, d_out, d_out_off, d_out_len, d_ret, d_pending, s);
+}
+
+int dg_j2t_batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *json, const uint64_t *in_off,
+                      uint64_t n, uint64_t flags, uint8_t *out, uint64_t out_cap, uint64_t *out_off, uint64_t *ret,
+                      uint64_t *out_need)
+{
+    if (!c || !d || (!json && n) || !in_off || !out_off || (!ret && n)) return set_err(DG_E_INVALID, "bad args");
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    int rc;
+    uint64_t base = in_off[0], bytes = in_off[n] - in_off[0];
+    std::vector<uint64_t> ioff(n + 1), soff(n + 1);
+    soff[0] = 0;
+    for (uint64_t i = 0; i <= n; i++) ioff[i] = in_off[i] - base;
+    for (uint64_t i = 0; i < n; i++) soff[i + 1] = soff[i] + dg_slot_bound(ioff[i + 1] - ioff[i]);
+    if ((rc = grow(c->d_json, c->d_json_cap, bytes + 64))) return rc;
+    if ((rc = grow(c->d_in_off, c->d_in_cap, n + 1))) return rc;
+    if ((rc = grow(c->d_out, c->d_out_cap, soff[n] + 64))) return rc;
+    if ((rc = grow(c->d_out_off, c->d_oo_cap, n + 1))) return rc;
+    if ((rc = grow(c->d_out_len, c->d_ol_cap, n + 1))) return rc;
+    if ((rc = grow(c->d_ret, c->d_ret_cap, n + 1))) return rc;
+    hipStream_t s = c->stream;
+    HIPCHK(hipMemcpyAsync(c->d_json, json + base, bytes, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemsetAsync(c->d_json + bytes, 0, 64, s));
+    HIPCHK(hipMemcpyAsync(c->d_in_off, ioff.data(), (n + 1) * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->d_out_off, soff.data(), (n + 1) * 8, hipMemcpyHostToDevice, s));
+    if ((rc = launch(c, d, root, c->d_json, c->d_in_off, n, flags, c->d_out, c->d_out_off, c->d_out_len, c->d_ret,
+                     nullptr, s)))
+        return rc;
+    std::vector<uint32_t> olen(n);
+    HIPCHK(hipMemcpyAsync(ret, c->d_ret, n * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(olen.data(), c->d_out_len, n * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    /* overflowed messages: rerun each with an exact-size slot (GPU) */
+    std::vector<uint64_t> redo;
+    for (uint64_t i = 0; i < n; i++)
+        if ((uint8_t)ret[i] == DG_ST_OUT_OVERFLOW) redo.push_back(i);
+    std::vector<std::vector<uint8_t>> redo_out(redo.size());
+    for (size_t k = 0; k < redo.size(); k++) {
+        uint64_t i = redo[k];
+        uint64_t need = ret[i] >> 40;
+        uint64_t one_in[2] = {0, ioff[i + 1] - ioff[i]};
+        uint64_t one_out[2] = {0, need + 64};
+        uint8_t *d1;
+        uint64_t *d_io, *d_oo, *d_r;
+        uint32_t *d_ol;
+        HIPCHK(hipMalloc(&d1, one_out[1]));
+        HIPCHK(hipMalloc(&d_io, 16));
+        HIPCHK(hipMalloc(&d_oo, 16));
+        HIPCHK(hipMalloc(&d_r, 8));
+        HIPCHK(hipMalloc(&d_ol, 4));
+        HIPCHK(hipMemcpyAsync(d_io, one_in, 16, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(d_oo, one_out, 16, hipMemcpyHostToDevice, s));
+        rc = launch(c, d, root, c->d_json + ioff[i], d_io, 1, flags, d1, d_oo, d_ol, d_r, nullptr, s);
+        if (rc) return rc;
+        uint32_t l1;
+        HIPCHK(hipMemcpyAsync(&ret[i], d_r, 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(&l1, d_ol, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        olen[i] = l1;
+        redo_out[k].resize(l1);
+        if (l1) HIPCHK(hipMemcpy(redo_out[k].data(), d1, l1, hipMemcpyDeviceToHost));
+        (void)hipFree(d1);
+        (void)hipFree(d_io);
+        (void)hipFree(d_oo);
+        (void)hipFree(d_r);
+        (void)hipFree(d_ol);
+    }
+    uint64_t total = 0;
+    out_off[0] = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        if (ret[i] != 0) olen[i] = 0;
+        total += olen[i];
+        out_off[i + 1] = total;
+    }
+    if (out_need) *out_need = total;
+    if (total > out_cap || (!out && total)) return set_err(DG_E_NOMEM, "output needs %llu bytes", (unsigned long long)total);
+    /* D2H of each slot's used prefix (contiguous runs merged) */
+    std::vector<uint8_t> stage(soff[n]);
+    HIPCHK(hipMemcpy(stage.data(), c->d_out, soff[n], hipMemcpyDeviceToHost));
+    size_t rk = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        if (!olen[i]) continue;
+        if (rk < redo.size() && redo[rk] == i) {
+            memcpy(out + out_off[i], redo_out[rk].data(), olen[i]);
+            rk++;
+        } else {
+            memcpy(out + out_off[i], stage.data() + soff[i], olen[i]);
+        }
+        while (rk < redo.size() && redo[rk] < i) rk++;
+    }
+    return DG_OK;
+}
+
+int dg_j2t_do(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *json, size_t len, uint64_t flags,
+              uint8_t *out, size_t out_cap, size_t *out_len, uint64_t *ret)
+{
+    uint64_t in_off[2] = {0, len};
+    uint64_t oo[2];
+    uint64_t need = 0;
+    static const uint8_t empty = 0;
+    int rc = dg_j2t_batch_host(c, d, root, len ? json : &empty, in_off, 1, flags, out, out_cap, oo, ret, &need);
+    if (out_len) *out_len = need;
+    return rc;
+}
+
+int dg_bench_device(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *d_json, const uint64_t *d_in_off,
+                    uint64_t n, uint64_t flags, uint8_t *d_out, const uint64_t *d_out_off, uint32_t *d_out_len,
+                    uint64_t *d_ret, int iters, float *ms)
+{
+    if (!c || !d || iters < 1 || !ms) return set_err(DG_E_INVALID, "bad args");
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    HIPCHK(hipEventRecord(e0, c->stream));
+    for (int k = 0; k < iters; k++) {
+        int rc = launch(c, d, root, d_json, d_in_off, n, flags, d_out, d_out_off, d_out_len, d_ret, c->d_pending,
+                        c->stream);
+        if (rc) return rc;
+    }
+    HIPCHK(hipEventRecord(e1, c->stream));
+    HIPCHK(hipEventSynchronize(e1));
+    HIPCHK(hipEventElapsedTime(ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return DG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,9 @@
+/* j2t_lane_kernel instantiation: descriptor tables copied to LDS (blobs <= DESC_LDS_BYTES). */
+#include "j2t_machine.h"
+
+namespace dg {
+void launch_lane_kernel_lds(dim3 grid, hipStream_t s, const Params &P, const DeepParams &DP)
+{
+    hipLaunchKernelGGL(j2t_lane_kernel<true>, grid, dim3(LANE_BLOCK), 0, s, P, DP);
+}
+}  // namespace dg

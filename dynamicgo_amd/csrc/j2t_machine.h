@@ -1,27 +1,26 @@
 /*
- * j2t_kernel.hip — the MI355X kernels and the C ABI (include/dgj2t.h).
+ * j2t_machine.h — the exact machine and the lane kernel (device side).
  *
  * Kernel map (one launch per batch):
  *  j2t_lane_kernel  one lane per message; the block's JSON span is staged in
- *                   LDS; stack of FAST_DEPTH frames per lane. Messages that
- *                   outgrow it are listed as DG_ST_DEEP and the LAST block to
- *                   finish redoes them (deep_pass) with a MAX_RECURSE (4096)
- *                   stack in device workspace.
- * Both run the same templated FSM (Machine<S>::run) that restates
- * j2t_fsm_exec (native/thrift.c:765-1187).
+ *                   LDS. Phase 1: each lane runs the fast path (j2t_fast.h) on
+ *                   its own message. Phase 2: the messages the fast path
+ *                   bailed on are compacted onto the first lanes and redone by
+ *                   the exact machine (Machine<S>::run, a restatement of
+ *                   j2t_fsm_exec native/thrift.c:765-1187) with a stack of
+ *                   LDS_DEPTH frames; messages that outgrow it are listed as
+ *                   DG_ST_DEEP and the LAST block to finish redoes them
+ *                   (deep_pass) with a MAX_RECURSE (4096) stack in device
+ *                   workspace.
+ * The kernel is instantiated in j2t_kern_lds.hip (descriptor copied to LDS)
+ * and j2t_kern_glb.hip (descriptor read from global memory), so the two
+ * compile in parallel; j2t_host.hip holds the C ABI.
  */
+#pragma once
 #include <hip/hip_runtime.h>
 
-#include <stdarg.h>
-#include <stdio.h>
-#include <stdlib.h>
-#include <string.h>
-
-#include <algorithm>
-#include <mutex>
-#include <vector>
-
 #include "j2t_device.h"
+#include "j2t_fast.h"
 
 namespace dg {
 
@@ -49,6 +48,8 @@ struct Params {
     uint8_t *ws;       /* per-lane workspace base */
     uint64_t ws_stride;/* bytes per lane */
     uint32_t keycap, reqcap;
+    uint32_t fast;     /* run the fast path first (descriptor v2, flags within FAST_FLAGS) */
+    unsigned long long *stats; /* {messages bailed to the exact machine, messages redone deep} */
 };
 
 #ifdef DG_PROFILE
@@ -807,6 +808,7 @@ DGI void deep_pass(const Params &P, const DV &dv, uint32_t *done, uint32_t nbloc
     __syncthreads();
     if (!s_last) return;
     uint32_t cnt = __hip_atomic_load(P.deep_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0 && cnt) atomicAdd(&P.stats[1], (unsigned long long)cnt);
     uint64_t lane = threadIdx.x;
     Workspace ws = lane_ws(P, lane);
     FStack<Frame *> frames{(Frame *)(P.ws + lane * P.ws_stride + DCAP + P.keycap + (uint64_t)P.reqcap * 8), 1};
@@ -845,9 +847,13 @@ struct DeepParams {
 template <bool LDS_DESC>
 __global__ __launch_bounds__(LANE_BLOCK) __attribute__((amdgpu_waves_per_eu(1, 1))) void j2t_lane_kernel(Params P, DeepParams DP)
 {
-    __shared__ __attribute__((aligned(16))) uint64_t stage[STAGE_BYTES / 8];
+    __shared__ __attribute__((aligned(16))) uint64_t stage[STAGE_BYTES / 8 + 2]; /* +16 B: word reads past the end */
     __shared__ __attribute__((aligned(16))) Frame lframes[LDS_DEPTH * LANE_BLOCK];
     __shared__ __attribute__((aligned(16))) uint64_t ldesc[LDS_DESC ? DESC_LDS_BYTES / 8 : 2];
+    __shared__ uint64_t s_p10u[20];
+    __shared__ double s_p10d[23];
+    __shared__ uint32_t s_nbail;
+    __shared__ uint16_t s_bail[LANE_BLOCK];
     uint64_t b0 = (uint64_t)blockIdx.x * LANE_BLOCK;
     uint64_t b1 = b0 + LANE_BLOCK < P.n ? b0 + LANE_BLOCK : P.n;
     uint64_t lo = P.in_off[b0], hi = P.in_off[b1];
@@ -864,30 +870,69 @@ __global__ __launch_bounds__(LANE_BLOCK) __attribute__((amdgpu_waves_per_eu(1, 1
         uint4 *l = (uint4 *)ldesc;
         for (uint32_t k = threadIdx.x; k < (DP.hdr.total_len + 15) / 16; k += LANE_BLOCK) l[k] = g[k];
     }
+    if (threadIdx.x < 20) {
+        uint64_t v = 1;
+        for (uint32_t k = 0; k < threadIdx.x; k++) v *= 10;
+        s_p10u[threadIdx.x] = v;
+    }
+    if (threadIdx.x < 23) s_p10d[threadIdx.x] = P10[threadIdx.x];
+    if (threadIdx.x == 0) s_nbail = 0;
     __syncthreads();
     auto dv = [&]() {
         if constexpr (LDS_DESC) return desc_view<3>((const __attribute__((address_space(3))) uint8_t *)(void *)ldesc, DP.hdr);
         else return desc_view<1>((const __attribute__((address_space(1))) uint8_t *)(const void *)DP.blob, DP.hdr);
     }();
     uint64_t i = b0 + threadIdx.x;
+    /* phase 1: the fast path on this lane's own message */
     if (i < b1) {
+        bool done = false;
+        if (P.fast) {
+            uint64_t oa = P.out_off[i], ob = P.out_off[i + 1];
+            Out out;
+            out.init(P.out + oa, ob - oa);
+            FastTabs tb{(const __attribute__((address_space(3))) uint64_t *)(void *)s_p10u,
+                        (lds_f64 *)(void *)s_p10d};
+            LFFrame *ff = (LFFrame *)(void *)&lframes[threadIdx.x];
+            if (staged) {
+                uint64_t a = P.in_off[i], b = P.in_off[i + 1];
+                SrcT<lds_u64> s;
+                s.init((lds_u64 *)(void *)stage, (int64_t)(a - base), (int64_t)(b - a));
+                done = fast_convert(dv, s, out, P.flag, P.root, ff, LANE_BLOCK, tb);
+            } else {
+                SrcT<glb_u64> s = global_src(P, i);
+                done = fast_convert(dv, s, out, P.flag, P.root, ff, LANE_BLOCK, tb);
+            }
+            if (done) finish(P, i, 0, (uint32_t)out.len);
+        }
+        if (!done) {
+            uint32_t k = atomicAdd(&s_nbail, 1u);
+            s_bail[k] = (uint16_t)threadIdx.x;
+        }
+    }
+    __syncthreads();
+    /* phase 2: the exact machine on the block's bailed messages, compacted
+     * onto the first lanes */
+    uint32_t nbail = s_nbail;
+    if (threadIdx.x == 0 && nbail && P.fast) atomicAdd(&P.stats[0], (unsigned long long)nbail);
+    if (threadIdx.x < nbail) {
+        uint64_t j = b0 + s_bail[threadIdx.x];
         FStack<LFrame *> frames{(LFrame *)(void *)&lframes[threadIdx.x], LANE_BLOCK};
         gu64 *skipbits = nullptr; /* 64 skip levels in a register */
-        Workspace ws = lane_ws(P, i);
+        Workspace ws = lane_ws(P, j);
         uint32_t olen;
         uint64_t r;
         if (staged) {
-            uint64_t a = P.in_off[i], b = P.in_off[i + 1];
+            uint64_t a = P.in_off[j], b = P.in_off[j + 1];
             SrcT<lds_u64> s;
             s.init((lds_u64 *)(void *)stage, (int64_t)(a - base), (int64_t)(b - a));
-            r = convert_one(P, dv, i, s, frames, LDS_DEPTH, skipbits, 64, ws, olen);
+            r = convert_one(P, dv, j, s, frames, LDS_DEPTH, skipbits, 64, ws, olen);
         } else {
-            r = convert_one(P, dv, i, global_src(P, i), frames, LDS_DEPTH, skipbits, 64, ws, olen);
+            r = convert_one(P, dv, j, global_src(P, j), frames, LDS_DEPTH, skipbits, 64, ws, olen);
         }
-        finish(P, i, r, olen);
+        finish(P, j, r, olen);
         if ((uint8_t)r == DG_ST_DEEP) {
             uint32_t k = __hip_atomic_fetch_add(P.deep_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&P.deep_list[k], i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&P.deep_list[k], j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     Params Q = P;
@@ -898,356 +943,8 @@ __global__ __launch_bounds__(LANE_BLOCK) __attribute__((amdgpu_waves_per_eu(1, 1
     deep_pass(Q, dv, DP.done, gridDim.x);
 }
 
+/* launchers, one per translation unit */
+void launch_lane_kernel_lds(dim3 grid, hipStream_t s, const Params &P, const DeepParams &DP);
+void launch_lane_kernel_glb(dim3 grid, hipStream_t s, const Params &P, const DeepParams &DP);
+
 }  // namespace dg
-
-/* ========================================================================== */
-/* host side: C ABI                                                            */
-/* ========================================================================== */
-using namespace dg;
-
-static thread_local char g_err[512];
-static int set_err(int code, const char *fmt, ...)
-{
-    va_list ap;
-    va_start(ap, fmt);
-    vsnprintf(g_err, sizeof g_err, fmt, ap);
-    va_end(ap);
-    return code;
-}
-#define HIPCHK(x)                                                                              \
-    do {                                                                                       \
-        hipError_t e_ = (x);                                                                   \
-        if (e_ != hipSuccess) return set_err(DG_E_HIP, "%s: %s", #x, hipGetErrorString(e_));  \
-    } while (0)
-
-struct dg_ctx {
-    int device;
-    hipStream_t stream;
-    uint8_t *ws_fast = nullptr;
-    uint64_t ws_fast_lanes = 0;
-    uint32_t *d_deep_count = nullptr;
-    uint64_t *d_deep_list = nullptr;
-    uint8_t *ws_deep = nullptr;
-    uint32_t *d_pending = nullptr;
-    std::mutex mu;
-    /* staging for the host API */
-    uint8_t *d_json = nullptr; uint64_t d_json_cap = 0;
-    uint64_t *d_in_off = nullptr; uint64_t d_in_cap = 0;
-    uint8_t *d_out = nullptr; uint64_t d_out_cap = 0;
-    uint64_t *d_out_off = nullptr; uint64_t d_oo_cap = 0;
-    uint32_t *d_out_len = nullptr; uint64_t d_ol_cap = 0;
-    uint64_t *d_ret = nullptr; uint64_t d_ret_cap = 0;
-};
-
-struct dg_desc {
-    dg_ctx *ctx;
-    uint8_t *d_blob;
-    size_t len;
-    dg_desc_hdr hdr;
-};
-
-static const uint64_t FAST_WS_STRIDE = DCAP + WS_KEYCAP + (uint64_t)WS_REQCAP * 8;
-static const uint64_t DEEP_WS_STRIDE = DCAP + DEEP_KEYCAP + (uint64_t)DEEP_REQCAP * 8 +
-                                       (uint64_t)MAX_RECURSE * sizeof(Frame) + MAX_RECURSE / 8;
-
-template <class T>
-static int grow(T *&p, uint64_t &cap, uint64_t want)
-{
-    if (cap >= want) return DG_OK;
-    (void)hipFree(p);
-    p = nullptr;
-    uint64_t nc = std::max<uint64_t>(want, cap * 2);
-    HIPCHK(hipMalloc(&p, nc * sizeof(T)));
-    cap = nc;
-    return DG_OK;
-}
-
-extern "C" {
-
-const char *dg_last_error(void) { return g_err; }
-
-int dg_ctx_create(int device, dg_ctx **out)
-{
-    if (!out) return set_err(DG_E_INVALID, "null out");
-    int ndev = 0;
-    HIPCHK(hipGetDeviceCount(&ndev));
-    if (device < 0 || device >= ndev) return set_err(DG_E_INVALID, "device %d out of range (%d)", device, ndev);
-    HIPCHK(hipSetDevice(device));
-    dg_ctx *c = new dg_ctx();
-    c->device = device;
-    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    HIPCHK(hipMalloc(&c->ws_deep, DEEP_WS_STRIDE * DEEP_THREADS));
-    HIPCHK(hipMalloc(&c->d_pending, 16));
-    HIPCHK(hipMalloc(&c->d_deep_count, 16));
-    HIPCHK(hipMemset(c->d_deep_count, 0, 16)); /* {deep_count, done}: self-reset by each launch */
-    *out = c;
-    return DG_OK;
-}
-
-void dg_ctx_destroy(dg_ctx *c)
-{
-    if (!c) return;
-    (void)hipSetDevice(c->device);
-    (void)hipStreamSynchronize(c->stream);
-    (void)hipFree(c->ws_fast);
-    (void)hipFree(c->ws_deep);
-    (void)hipFree(c->d_pending);
-    (void)hipFree(c->d_deep_count);
-    (void)hipFree(c->d_deep_list);
-    (void)hipFree(c->d_json);
-    (void)hipFree(c->d_in_off);
-    (void)hipFree(c->d_out);
-    (void)hipFree(c->d_out_off);
-    (void)hipFree(c->d_out_len);
-    (void)hipFree(c->d_ret);
-    (void)hipStreamDestroy(c->stream);
-    delete c;
-}
-
-void *dg_ctx_stream(dg_ctx *c) { return c ? (void *)c->stream : nullptr; }
-
-static int desc_finish(dg_ctx *c, const dg_desc_hdr &h, uint8_t *d_blob, size_t len, dg_desc **out)
-{
-    if (h.magic != DG_DESC_MAGIC || h.version < 1 || h.version > DG_DESC_VERSION || h.total_len > len)
-        return set_err(DG_E_DESC, "bad descriptor blob header");
-    dg_desc *d = new dg_desc();
-    d->ctx = c;
-    d->d_blob = d_blob;
-    d->len = len;
-    d->hdr = h;
-    *out = d;
-    return DG_OK;
-}
-
-int dg_desc_create(dg_ctx *c, const void *blob, size_t len, dg_desc **out)
-{
-    if (!c || !blob || !out || len < sizeof(dg_desc_hdr)) return set_err(DG_E_INVALID, "bad args");
-    dg_desc_hdr h;
-    memcpy(&h, blob, sizeof h);
-    if (h.magic != DG_DESC_MAGIC || h.total_len > len) return set_err(DG_E_DESC, "bad descriptor blob");
-    HIPCHK(hipSetDevice(c->device));
-    uint8_t *d_blob;
-    HIPCHK(hipMalloc(&d_blob, len));
-    HIPCHK(hipMemcpy(d_blob, blob, len, hipMemcpyHostToDevice));
-    return desc_finish(c, h, d_blob, len, out);
-}
-
-int dg_desc_create_device(dg_ctx *c, const void *d_src, size_t len, dg_desc **out)
-{
-    if (!c || !d_src || !out || len < sizeof(dg_desc_hdr)) return set_err(DG_E_INVALID, "bad args");
-    HIPCHK(hipSetDevice(c->device));
-    uint8_t *d_blob;
-    HIPCHK(hipMalloc(&d_blob, len));
-    HIPCHK(hipMemcpy(d_blob, d_src, len, hipMemcpyDeviceToDevice));
-    dg_desc_hdr h;
-    HIPCHK(hipMemcpy(&h, d_blob, sizeof h, hipMemcpyDeviceToHost));
-    return desc_finish(c, h, d_blob, len, out);
-}
-
-void dg_desc_destroy(dg_desc *d)
-{
-    if (!d) return;
-    (void)hipFree(d->d_blob);
-    delete d;
-}
-
-uint32_t dg_desc_root(const dg_desc *d) { return d ? d->hdr.root_type : 0; }
-
-uint64_t dg_slot_bound(uint64_t len) { return (4 * len + 64 + 7) & ~7ull; }
-
-static int ensure_fast_ws(dg_ctx *c, uint64_t lanes)
-{
-    if (c->ws_fast_lanes >= lanes) return DG_OK;
-    (void)hipFree(c->ws_fast);
-    (void)hipFree(c->d_deep_list);
-    c->ws_fast = nullptr;
-    c->d_deep_list = nullptr;
-    uint64_t want = std::max<uint64_t>(lanes, 1 << 16);
-    HIPCHK(hipMalloc(&c->ws_fast, want * FAST_WS_STRIDE));
-    HIPCHK(hipMalloc(&c->d_deep_list, want * 8));
-    c->ws_fast_lanes = want;
-    return DG_OK;
-}
-
-static int launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *json, const uint64_t *in_off,
-                  uint64_t n, uint64_t flags, uint8_t *out, const uint64_t *out_off, uint32_t *out_len,
-                  uint64_t *ret, uint32_t *pending, hipStream_t s)
-{
-    if (n == 0) return DG_OK;
-    if (root >= d->hdr.n_types) return set_err(DG_E_INVALID, "root type %u out of range", root);
-    int rc = ensure_fast_ws(c, n);
-    if (rc) return rc;
-    Params P;
-    P.root = root;
-    P.json = json;
-    P.in_off = in_off;
-    P.n = n;
-    P.flag = flags;
-    P.out = out;
-    P.out_off = out_off;
-    P.out_len = out_len;
-    P.ret = ret;
-    P.pending = pending;
-    P.deep_count = c->d_deep_count;
-    P.deep_list = c->d_deep_list;
-    P.ws = c->ws_fast;
-    P.ws_stride = FAST_WS_STRIDE;
-    P.keycap = WS_KEYCAP;
-    P.reqcap = WS_REQCAP;
-    uint64_t blocks = (n + LANE_BLOCK - 1) / LANE_BLOCK;
-    DeepParams DP;
-    DP.ws = c->ws_deep;
-    DP.ws_stride = DEEP_WS_STRIDE;
-    DP.keycap = DEEP_KEYCAP;
-    DP.reqcap = DEEP_REQCAP;
-    DP.done = c->d_deep_count + 1;
-    DP.blob = d->d_blob;
-    DP.hdr = d->hdr;
-    if (d->hdr.total_len <= DESC_LDS_BYTES)
-        hipLaunchKernelGGL(j2t_lane_kernel<true>, dim3((uint32_t)blocks), dim3(LANE_BLOCK), 0, s, P, DP);
-    else
-        hipLaunchKernelGGL(j2t_lane_kernel<false>, dim3((uint32_t)blocks), dim3(LANE_BLOCK), 0, s, P, DP);
-    HIPCHK(hipGetLastError());
-    return DG_OK;
-}
-
-int dg_j2t_batch_device(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *d_json, const uint64_t *d_in_off,
-                        uint64_t n, uint64_t flags, uint8_t *d_out, const uint64_t *d_out_off, uint32_t *d_out_len,
-                        uint64_t *d_ret, uint32_t *d_pending, void *stream)
-{
-    if (!c || !d) return set_err(DG_E_INVALID, "null ctx/desc");
-    std::lock_guard<std::mutex> g(c->mu);
-    HIPCHK(hipSetDevice(c->device));
-    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-    return launch(c, d, root, d_json, d_in_off, n, flags, d_out, d_out_off, d_out_len, d_ret, d_pending, s);
-}
-
-int dg_j2t_batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *json, const uint64_t *in_off,
-                      uint64_t n, uint64_t flags, uint8_t *out, uint64_t out_cap, uint64_t *out_off, uint64_t *ret,
-                      uint64_t *out_need)
-{
-    if (!c || !d || (!json && n) || !in_off || !out_off || (!ret && n)) return set_err(DG_E_INVALID, "bad args");
-    std::lock_guard<std::mutex> g(c->mu);
-    HIPCHK(hipSetDevice(c->device));
-    int rc;
-    uint64_t base = in_off[0], bytes = in_off[n] - in_off[0];
-    std::vector<uint64_t> ioff(n + 1), soff(n + 1);
-    soff[0] = 0;
-    for (uint64_t i = 0; i <= n; i++) ioff[i] = in_off[i] - base;
-    for (uint64_t i = 0; i < n; i++) soff[i + 1] = soff[i] + dg_slot_bound(ioff[i + 1] - ioff[i]);
-    if ((rc = grow(c->d_json, c->d_json_cap, bytes + 64))) return rc;
-    if ((rc = grow(c->d_in_off, c->d_in_cap, n + 1))) return rc;
-    if ((rc = grow(c->d_out, c->d_out_cap, soff[n] + 64))) return rc;
-    if ((rc = grow(c->d_out_off, c->d_oo_cap, n + 1))) return rc;
-    if ((rc = grow(c->d_out_len, c->d_ol_cap, n + 1))) return rc;
-    if ((rc = grow(c->d_ret, c->d_ret_cap, n + 1))) return rc;
-    hipStream_t s = c->stream;
-    HIPCHK(hipMemcpyAsync(c->d_json, json + base, bytes, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemsetAsync(c->d_json + bytes, 0, 64, s));
-    HIPCHK(hipMemcpyAsync(c->d_in_off, ioff.data(), (n + 1) * 8, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(c->d_out_off, soff.data(), (n + 1) * 8, hipMemcpyHostToDevice, s));
-    if ((rc = launch(c, d, root, c->d_json, c->d_in_off, n, flags, c->d_out, c->d_out_off, c->d_out_len, c->d_ret,
-                     nullptr, s)))
-        return rc;
-    std::vector<uint32_t> olen(n);
-    HIPCHK(hipMemcpyAsync(ret, c->d_ret, n * 8, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(olen.data(), c->d_out_len, n * 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    /* overflowed messages: rerun each with an exact-size slot (GPU) */
-    std::vector<uint64_t> redo;
-    for (uint64_t i = 0; i < n; i++)
-        if ((uint8_t)ret[i] == DG_ST_OUT_OVERFLOW) redo.push_back(i);
-    std::vector<std::vector<uint8_t>> redo_out(redo.size());
-    for (size_t k = 0; k < redo.size(); k++) {
-        uint64_t i = redo[k];
-        uint64_t need = ret[i] >> 40;
-        uint64_t one_in[2] = {0, ioff[i + 1] - ioff[i]};
-        uint64_t one_out[2] = {0, need + 64};
-        uint8_t *d1;
-        uint64_t *d_io, *d_oo, *d_r;
-        uint32_t *d_ol;
-        HIPCHK(hipMalloc(&d1, one_out[1]));
-        HIPCHK(hipMalloc(&d_io, 16));
-        HIPCHK(hipMalloc(&d_oo, 16));
-        HIPCHK(hipMalloc(&d_r, 8));
-        HIPCHK(hipMalloc(&d_ol, 4));
-        HIPCHK(hipMemcpyAsync(d_io, one_in, 16, hipMemcpyHostToDevice, s));
-        HIPCHK(hipMemcpyAsync(d_oo, one_out, 16, hipMemcpyHostToDevice, s));
-        rc = launch(c, d, root, c->d_json + ioff[i], d_io, 1, flags, d1, d_oo, d_ol, d_r, nullptr, s);
-        if (rc) return rc;
-        uint32_t l1;
-        HIPCHK(hipMemcpyAsync(&ret[i], d_r, 8, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipMemcpyAsync(&l1, d_ol, 4, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-        olen[i] = l1;
-        redo_out[k].resize(l1);
-        if (l1) HIPCHK(hipMemcpy(redo_out[k].data(), d1, l1, hipMemcpyDeviceToHost));
-        (void)hipFree(d1);
-        (void)hipFree(d_io);
-        (void)hipFree(d_oo);
-        (void)hipFree(d_r);
-        (void)hipFree(d_ol);
-    }
-    uint64_t total = 0;
-    out_off[0] = 0;
-    for (uint64_t i = 0; i < n; i++) {
-        if (ret[i] != 0) olen[i] = 0;
-        total += olen[i];
-        out_off[i + 1] = total;
-    }
-    if (out_need) *out_need = total;
-    if (total > out_cap || (!out && total)) return set_err(DG_E_NOMEM, "output needs %llu bytes", (unsigned long long)total);
-    /* D2H of each slot's used prefix (contiguous runs merged) */
-    std::vector<uint8_t> stage(soff[n]);
-    HIPCHK(hipMemcpy(stage.data(), c->d_out, soff[n], hipMemcpyDeviceToHost));
-    size_t rk = 0;
-    for (uint64_t i = 0; i < n; i++) {
-        if (!olen[i]) continue;
-        if (rk < redo.size() && redo[rk] == i) {
-            memcpy(out + out_off[i], redo_out[rk].data(), olen[i]);
-            rk++;
-        } else {
-            memcpy(out + out_off[i], stage.data() + soff[i], olen[i]);
-        }
-        while (rk < redo.size() && redo[rk] < i) rk++;
-    }
-    return DG_OK;
-}
-
-int dg_j2t_do(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *json, size_t len, uint64_t flags,
-              uint8_t *out, size_t out_cap, size_t *out_len, uint64_t *ret)
-{
-    uint64_t in_off[2] = {0, len};
-    uint64_t oo[2];
-    uint64_t need = 0;
-    static const uint8_t empty = 0;
-    int rc = dg_j2t_batch_host(c, d, root, len ? json : &empty, in_off, 1, flags, out, out_cap, oo, ret, &need);
-    if (out_len) *out_len = need;
-    return rc;
-}
-
-int dg_bench_device(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *d_json, const uint64_t *d_in_off,
-                    uint64_t n, uint64_t flags, uint8_t *d_out, const uint64_t *d_out_off, uint32_t *d_out_len,
-                    uint64_t *d_ret, int iters, float *ms)
-{
-    if (!c || !d || iters < 1 || !ms) return set_err(DG_E_INVALID, "bad args");
-    std::lock_guard<std::mutex> g(c->mu);
-    HIPCHK(hipSetDevice(c->device));
-    hipEvent_t e0, e1;
-    HIPCHK(hipEventCreate(&e0));
-    HIPCHK(hipEventCreate(&e1));
-    HIPCHK(hipEventRecord(e0, c->stream));
-    for (int k = 0; k < iters; k++) {
-        int rc = launch(c, d, root, d_json, d_in_off, n, flags, d_out, d_out_off, d_out_len, d_ret, c->d_pending,
-                        c->stream);
-        if (rc) return rc;
-    }
-    HIPCHK(hipEventRecord(e1, c->stream));
-    HIPCHK(hipEventSynchronize(e1));
-    HIPCHK(hipEventElapsedTime(ms, e0, e1));
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-    return DG_OK;
-}
-
-}  // extern "C"

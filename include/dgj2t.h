@@ -47,6 +47,7 @@ extern "C" {
 #define DG_F_TRACE_BACK (1ull << 8)
 #define DG_F_NO_WRITE_BASE (1ull << 9)
 #define DG_F_VALIDATE_UTF8 (1ull << 16) /* extension: reject invalid UTF-8 in strings */
+#define DG_F_NO_FAST_PATH (1ull << 17)  /* extension: run every message on the exact machine (testing) */
 
 /* library-internal per-message statuses (code byte values the reference never
  * produces). The host entry points resolve them before returning; the device
@@ -72,8 +73,13 @@ int dg_ctx_create(int device, dg_ctx **out);
 void dg_ctx_destroy(dg_ctx *ctx);
 /* The context's HIP stream (hipStream_t), for callers that order their own work. */
 void *dg_ctx_stream(dg_ctx *ctx);
+/* Diagnostics (no reference counterpart): messages the kernel's fast path
+ * handed to the exact machine, and messages redone with the 4096-deep stack,
+ * summed over this context's launches since the last reset. Synchronizes the
+ * device. */
+int dg_ctx_stats(dg_ctx *ctx, uint64_t *bails, uint64_t *deeps, int reset);
 
-/* Upload a dg_desc v1 blob (include/dgj2t_desc.h) to the context's device.
+/* Upload a dg_desc blob (v1 or v2) (include/dgj2t_desc.h) to the context's device.
  * Replaces reading the Go *thrift.TypeDescriptor graph in place
  * (native/thrift.h:70-137 <-> thrift/descriptor.go:119-267). */
 int dg_desc_create(dg_ctx *ctx, const void *blob, size_t len, dg_desc **out);

@@ -17,7 +17,10 @@ def _checker():
     return oracle.RefOracle() or oracle.PortOracle()
 
 
-def _run_rows(rows, flats):
+NO_FAST = 1 << 17  # DG_F_NO_FAST_PATH: every message on the exact machine
+
+
+def _run_rows(rows, flats, extra=0):
     """Group golden rows by (desc, flags) and run each group as one batch."""
     groups = {}
     for i, (name, flags, js, ret, out) in enumerate(rows):
@@ -27,7 +30,7 @@ def _run_rows(rows, flats):
         cv = conv.BinaryConv(conv.Options())
         cv.opts = conv.Options()
         msgs = [rows[i][2] for i in idx]
-        outs, rets = _raw_batch(flats[name], msgs, flags)
+        outs, rets = _raw_batch(flats[name], msgs, flags | extra)
         for k, i in enumerate(idx):
             exp_ret, exp_out = rows[i][3], rows[i][4]
             if int(rets[k]) != exp_ret or outs[k] != exp_out:
@@ -53,9 +56,10 @@ def _raw_batch(flat, msgs, flags):
     return [out[int(oo[i]):int(oo[i + 1])].tobytes() for i in range(n)], rets
 
 
-def test_golden_vectors(golden):
+@pytest.mark.parametrize("extra", [0, NO_FAST], ids=["fast+exact", "exact-only"])
+def test_golden_vectors(golden, extra):
     rows, flats = golden
-    bad = _run_rows(rows, flats)
+    bad = _run_rows(rows, flats, extra)
     assert not bad, bad[:8]
 
 
@@ -71,25 +75,47 @@ def test_fuzz_vs_oracle(which):
     fl = T.flatten(td)
     chk = _checker()
     rng = random.Random(hash(which) & 0xffff)
-    for flags in (0x1, 0x0, 0x11, 0x5, 0x23, 0x83, 0x41, 0x100):
-        msgs = [fuzz.gen_message(rng, td) for _ in range(300)]
+    for flags in (0x1, 0x0, 0x11, 0x5, 0x23, 0x83, 0x41, 0x100, 0x201, NO_FAST | 0x1, NO_FAST | 0x83):
+        msgs = [fuzz.gen_message(rng, td, mutate_p=rng.random() < 0.5) for _ in range(300)]
         outs, rets = _raw_batch(fl, msgs, flags)
         for m, o, r in zip(msgs, outs, rets):
             er, eo = chk.j2t(fl, m, flags)
             assert (int(r), o) == (er, eo), (which, hex(flags), m)
 
 
-def test_c2_full_batch_vs_oracle():
-    """The bench workload at full size (65 536 messages), byte-exact."""
-    td = W.simple_desc()
-    fl = T.flatten(td)
-    msgs = W.gen_flat_batch(random.Random(42), 65536)
+@pytest.mark.parametrize("cfg", ["c2", "c3"])
+def test_full_batch_vs_oracle(cfg):
+    """The bench workloads at full size (65 536 messages), byte-exact, and all
+    of them on the fast path (what bench.py measures)."""
+    td, gen, seed = {"c2": (W.simple_desc, W.gen_flat_batch, 42),
+                     "c3": (W.nesting_i64_desc, W.gen_nested_batch, 43)}[cfg]
+    fl = T.flatten(td())
+    msgs = gen(random.Random(seed), 65536)
+    ctx = conv.default_context()
+    ctx.stats(reset=True)
     outs, rets = _raw_batch(fl, msgs, 1)
+    bails, deeps = ctx.stats(reset=True)
     chk = _checker()
     a, off = W.arena(msgs)
     er, eo = chk.j2t_arena(fl, a, off, 1, nthreads=8)
     assert (np.asarray(rets) == er).all()
     assert outs == eo
+    assert (bails, deeps) == (0, 0)
+
+
+def test_large_messages_vs_oracle():
+    """C4-shaped messages (too large to stage in LDS: global-source path)."""
+    fl = T.flatten(W.large_desc())
+    rng = random.Random(44)
+    msgs = W.gen_large_batch(rng, 24, blob_bytes=6000, n_values=300) + W.gen_large_batch(rng, 8)
+    ctx = conv.default_context()
+    ctx.stats(reset=True)
+    outs, rets = _raw_batch(fl, msgs, 1)
+    bails, _ = ctx.stats(reset=True)
+    chk = _checker()
+    for m, o, r in zip(msgs, outs, rets):
+        assert (int(r), o) == chk.j2t(fl, m, 1)
+    assert bails == 0
 
 
 def test_deep_nesting_routes_to_deep_kernel():
