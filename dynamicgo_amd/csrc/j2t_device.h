@@ -487,6 +487,53 @@ struct BufSink {
     }
 };
 
+/* Extension DG_F_VALIDATE_UTF8: offset of the first invalid UTF-8 sequence in
+ * src[s0, s0+n) as utf8_validate (native/utf8.c:101-212) defines validity, or
+ * -1. ASCII runs are skipped 8 bytes at a time. */
+template <class S>
+DGI int64_t utf8_check(S &src, int64_t s0, int64_t n)
+{
+    int64_t i = 0;
+    while (i < n) {
+        if (i + 8 <= n) {
+            uint64_t hb = src.get8(s0 + i) & 0x8080808080808080ull;
+            if (hb == 0) {
+                i += 8;
+                continue;
+            }
+            i += __builtin_ctzll(hb) >> 3;
+        } else if (src.raw(s0 + i) < 0x80) {
+            i++;
+            continue;
+        }
+        uint8_t c = src.raw(s0 + i);
+        int size;
+        uint8_t lo = 0x80, hi = 0xBF;
+        if (c >= 0xC2 && c <= 0xDF) {
+            size = 2;
+        } else if (c >= 0xE0 && c <= 0xEF) {
+            size = 3;
+            if (c == 0xE0) lo = 0xA0;
+            else if (c == 0xED) hi = 0x9F;
+        } else if (c >= 0xF0 && c <= 0xF4) {
+            size = 4;
+            if (c == 0xF0) lo = 0x90;
+            else if (c == 0xF4) hi = 0x8F;
+        } else {
+            return i;
+        }
+        if (n - i < size) return i;
+        uint8_t c1 = src.raw(s0 + i + 1);
+        if (c1 < lo || c1 > hi) return i;
+        for (int k = 2; k < size; k++) {
+            uint8_t ck = src.raw(s0 + i + k);
+            if (ck < 0x80 || ck > 0xBF) return i;
+        }
+        i += size;
+    }
+    return -1;
+}
+
 /* ---- base64: b64decode(mode=0) native/base64.c:659-817 ---- */
 DGI int b64v(uint8_t c)
 {

@@ -217,6 +217,10 @@ struct Machine {
         if (e < 0) return pack((uint32_t)-e, (uint64_t)s0, (uint64_t)p);
         p = e;
         int64_t n = e - s0 - 1;
+        if (flag & DG_F_VALIDATE_UTF8) {
+            int64_t u = utf8_check(src, s0, n);
+            if (u >= 0) return pack(E_INVAL, src.raw(s0 + u), (uint64_t)(s0 + u));
+        }
         if (esc) {
             uint64_t lp = out.alloc(4);
             OutSink sink{&out};
@@ -355,11 +359,16 @@ struct Machine {
     {
         Key key;
         uint64_t r;
+        int64_t ks = p;
         PROF(1, r = read_key(p, key));
         if (r) return r;
         int64_t kn = key.n;
         const dg_type t = TY(dc);
         if (t.ttype == DG_T_MAP) {
+            if ((flag & DG_F_VALIDATE_UTF8) && TY(t.key).ttype == DG_T_STRING) {
+                int64_t u = utf8_check(src, ks, p - ks - 1);
+                if (u >= 0) return pack(E_INVAL, src.raw(ks + u), (uint64_t)(ks + u));
+            }
             unwindPos = out.len;
             r = j2t_map_key(key, t.key, p);
             if (r) return r;

@@ -20,7 +20,12 @@
  *
  * Flags are the reference's j2t flag word (native/thrift.h:23-32,
  * conv/j2t/conv.go:98-127 toFlags). DG_F_VALIDATE_UTF8 is an opt-in extension
- * (bit 16) that the reference does not have; off by default.
+ * (bit 16) that the reference does not have; off by default. With it, the raw
+ * JSON bytes of every string written as a Thrift STRING (string values and
+ * STRING map keys; not binary fields, not field-name keys) must be valid UTF-8
+ * as utf8_validate (native/utf8.c:101-212) defines it; otherwise the message
+ * fails with ERR_INVAL (2), value = the first byte of the invalid sequence,
+ * pos = its offset.
  *
  * All functions return 0 on success and a negative DG_E_* on API failure;
  * dg_last_error() describes the last failure of the calling thread.

@@ -41,6 +41,7 @@ enum { V_EOF = 1, V_DOUBLE = 8, V_INTEGER = 9 };
 #define F_WRITE_OPTIONAL (1ull << 7)
 #define F_TRACE_BACK (1ull << 8)
 #define F_NO_WRITE_BASE (1ull << 9)
+#define F_VALIDATE_UTF8 (1ull << 16) /* extension, see utf8_check */
 /* J2T states native/thrift.h:204-221 */
 enum { J_VAL = 0, J_ARR = 1, J_OBJ = 2, J_KEY = 3, J_ELEM = 4, J_ARR_0 = 5, J_OBJ_0 = 6 };
 #define ST_FIELD (1u << 16)
@@ -1260,6 +1261,50 @@ static uint64_t j2t_number(M *m, uint32_t td, const Src *src, int64_t *p)
     return PACK(E_DISMATCH_TYPE, V2(TY(m, td)->ttype, V_INTEGER), (uint64_t)*p);
 }
 
+/* Extension F_VALIDATE_UTF8 (bit 16, no reference counterpart): the raw JSON
+ * bytes of every string written as a Thrift STRING (string values and STRING
+ * map keys) must be valid UTF-8 as utf8_validate (native/utf8.c:101-212)
+ * defines it. Returns -1 if valid, else the offset of the first invalid
+ * sequence; the caller reports ERR_INVAL, value = that byte, pos = its offset. */
+static int64_t utf8_check(const uint8_t *s, int64_t n)
+{
+    int64_t i = 0;
+    while (i < n) {
+        uint8_t c = s[i];
+        if (c < 0x80) {
+            i++;
+            continue;
+        }
+        int size;
+        uint8_t lo = 0x80, hi = 0xBF;
+        if (c >= 0xC2 && c <= 0xDF)
+            size = 2;
+        else if (c >= 0xE0 && c <= 0xEF) {
+            size = 3;
+            if (c == 0xE0)
+                lo = 0xA0;
+            else if (c == 0xED)
+                hi = 0x9F;
+        } else if (c >= 0xF0 && c <= 0xF4) {
+            size = 4;
+            if (c == 0xF0)
+                lo = 0x90;
+            else if (c == 0xF4)
+                hi = 0x8F;
+        } else
+            return i;
+        if (n - i < size)
+            return i;
+        if (s[i + 1] < lo || s[i + 1] > hi)
+            return i;
+        for (int k = 2; k < size; k++)
+            if (s[i + k] < 0x80 || s[i + k] > 0xBF)
+                return i;
+        i += size;
+    }
+    return -1;
+}
+
 /* j2t_string native/thrift.c:367-399 */
 static uint64_t j2t_string(M *m, int64_t *p)
 {
@@ -1270,6 +1315,11 @@ static uint64_t j2t_string(M *m, int64_t *p)
         return PACK(-e, (uint64_t)s, (uint64_t)*p);
     *p = e;
     int64_t n = e - s - 1;
+    if (m->flag & F_VALIDATE_UTF8) {
+        int64_t r = utf8_check(src->s + s, n);
+        if (r >= 0)
+            return PACK(E_INVAL, (uint64_t)src->s[s + r], (uint64_t)(s + r));
+    }
     if (ep >= s && ep < e) {
         size_t lp = bmalloc(m->buf, 4);
         size_t o = bmalloc(m->buf, n);
@@ -1389,13 +1439,18 @@ static inline void bm_set_req(M *m, uint32_t reqs, uint32_t k, int req)
 static uint64_t j2t_key(M *m, int64_t *p, uint32_t dc, bool obj0, size_t *unwindPos,
                         const dg_field **lastField, Frame *vt)
 {
-    const uint8_t *sp;
-    int64_t kn;
+    const uint8_t *sp = NULL;
+    int64_t kn = 0, ks = *p;
     uint64_t r = j2t_read_key(m, p, &sp, &kn);
     if (r)
         return r;
     const dg_type *t = TY(m, dc);
     if (t->ttype == DG_T_MAP) {
+        if ((m->flag & F_VALIDATE_UTF8) && TY(m, t->key)->ttype == DG_T_STRING) {
+            int64_t u = utf8_check(m->src->s + ks, *p - ks - 1);
+            if (u >= 0)
+                return PACK(E_INVAL, (uint64_t)m->src->s[ks + u], (uint64_t)(ks + u));
+        }
         *unwindPos = m->buf->len;
         r = j2t_map_key(m, sp, kn, t->key, *p);
         if (r)

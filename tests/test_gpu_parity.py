@@ -189,3 +189,24 @@ def test_device_resident_api_torch():
         er, eo = chk.j2t(fl, m, 1)
         assert int(ret[i]) == er
         assert o[slots[i]:slots[i] + ol[i]].tobytes() == eo
+
+
+def test_utf8_validation_extension_vs_port_oracle():
+    """DG_F_VALIDATE_UTF8 (bit 16, extension): GPU vs the port oracle on
+    strings with valid and invalid UTF-8 in values and map keys."""
+    rng = random.Random(16)
+    pieces = [b"a", b"\xc3\xa9", b"\xe4\xb8\xad", b"\xf0\x9f\x98\x80", b"\xff", b"\xc0\x80", b"\xed\xa0\x80",
+              b"\xe4\xb8", b"\\n", b"\\u00e9", b" ", b"0123456789"]
+
+    def s():
+        return b'"' + b"".join(rng.choice(pieces) for _ in range(rng.randint(0, 12))) + b'"'
+    fl = T.flatten(W.nesting_i64_desc())
+    msgs = []
+    for _ in range(400):
+        msgs.append(b'{"String":' + s() + b',"MapStringString":{' + s() + b":" + s() + b'},"ListString":[' +
+                    s() + b"," + s() + b'],"Binary":' + s() + b"}")
+    chk = oracle.PortOracle()
+    for flags in (0x1 | 1 << 16, 0x1 | 1 << 16 | NO_FAST):
+        outs, rets = _raw_batch(fl, msgs, flags)
+        for m, o, r in zip(msgs, outs, rets):
+            assert (int(r), o) == chk.j2t(fl, m, flags), m

@@ -68,3 +68,38 @@ def test_port_vs_reference_fuzz(seed):
             m = fuzz.gen_message(rng, td)
             flags = rng.choice([1, 0, 0x11, 0x5, 0x23, 0x83])
             assert ref.j2t(fl, m, flags) == port.j2t(fl, m, flags), (m, flags)
+
+
+UTF8_FLAG = 1 << 16  # DG_F_VALIDATE_UTF8 (extension; no reference counterpart)
+
+UTF8_CASES = [  # (string body bytes, offset of the first invalid sequence or None)
+    (b"abc", None), ("é中文😀".encode(), None), (b"a\\u00e9\\n", None), (b"", None),
+    (b"a\xff", 1), (b"\xc0\x80", 0), (b"\xc1\xbf", 0), (b"\xed\xa0\x80", 0), (b"\xe0\x80\x80", 0),
+    (b"\xf0\x80\x80\x80", 0), (b"\xf4\x90\x80\x80", 0), (b"\xf5\x80\x80\x80", 0), (b"xy\xe4\xb8", 2),
+    (b"\xe4\xb8\xad\x80", 3), (b"12345678\xc3", 8), (b"\xef\xbf\xbf", None), (b"\xf4\x8f\xbf\xbf", None),
+]
+
+
+def _pack(code, value, pos):
+    return ((value << 40) | (pos << 8) | code) & (2**64 - 1)
+
+
+@pytest.mark.parametrize("body,bad", UTF8_CASES)
+def test_utf8_validation_extension(body, bad):
+    """DG_F_VALIDATE_UTF8 on the port oracle: valid strings convert exactly as
+    without the flag; the first invalid sequence (utf8_validate semantics,
+    native/utf8.c:101-212) gives ERR_INVAL at its offset. Parity unpinned by
+    construction (the reference has no such flag): pinned to the definition
+    above and to the flag-off output on valid input."""
+    chk = oracle.PortOracle()
+    fl = T.flatten(idl_desc("baseline.thrift", "SimpleMethod"))
+    pre = b'{"StringField":"'
+    msg = pre + body + b'"}'
+    r0 = chk.j2t(fl, msg, 1)
+    r1 = chk.j2t(fl, msg, 1 | UTF8_FLAG)
+    if bad is None:
+        assert r1 == r0
+    else:
+        assert r1 == (_pack(2, body[bad], len(pre) + bad), b"")
+    # binary fields are base64 text, not validated
+    assert chk.j2t(fl, b'{"BinaryField":"\xff"}', 1 | UTF8_FLAG) == chk.j2t(fl, b'{"BinaryField":"\xff"}', 1)
