@@ -12,7 +12,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DG_LIB_PATH") or os.path.join(HERE, "libdgj2t.so")
 
 # symbols include/dgj2t.h declares (checked by tests/test_abi.py)
-EXPORTS = ["dg_last_error", "dg_ctx_create", "dg_ctx_destroy", "dg_ctx_stream", "dg_ctx_stats", "dg_desc_create",
+EXPORTS = ["dg_last_error", "dg_ctx_create", "dg_ctx_destroy", "dg_ctx_stream", "dg_ctx_stats", "dg_ctx_counters",
+           "dg_desc_create",
            "dg_desc_create_device", "dg_desc_destroy", "dg_desc_root", "dg_j2t_batch_device",
            "dg_slot_bound", "dg_j2t_batch_host", "dg_j2t_do", "dg_bench_device"]
 
@@ -46,6 +47,7 @@ def lib() -> C.CDLL:
         "dg_ctx_destroy": (None, [vp]),
         "dg_ctx_stream": (vp, [vp]),
         "dg_ctx_stats": (i32, [vp, P64, P64, i32]),
+        "dg_ctx_counters": (i32, [vp, P64, i32, i32]),
         "dg_desc_create": (i32, [vp, C.c_char_p, sz, C.POINTER(vp)]),
         "dg_desc_create_device": (i32, [vp, vp, sz, C.POINTER(vp)]),
         "dg_desc_destroy": (None, [vp]),

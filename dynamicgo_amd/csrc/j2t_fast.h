@@ -213,8 +213,9 @@ DGI bool fast_vnumber(S &src, int64_t &p, const FastTabs &tb, int64_t &iv, doubl
     return true;
 }
 
-/* j2t_number's writes (native/thrift.c:312-365) */
-DGI bool emit_number(Out &out, uint8_t tt, bool isint, int64_t iv, double dv)
+/* j2t_number's writes (native/thrift.c:312-365); O = any byte writer */
+template <class O>
+DGI bool emit_number(O &out, uint8_t tt, bool isint, int64_t iv, double dv)
 {
     switch (tt) {
     case DG_T_BYTE: out.w8(isint ? (uint8_t)iv : (uint8_t)cvt32(dv)); return true;
@@ -227,8 +228,8 @@ DGI bool emit_number(Out &out, uint8_t tt, bool isint, int64_t iv, double dv)
 }
 
 /* copy src[s0, s0+n) to the output, 8 bytes per step */
-template <class S>
-DGI void fast_copy(S &src, int64_t s0, int64_t n, Out &out)
+template <class S, class O>
+DGI void fast_copy(S &src, int64_t s0, int64_t n, O &out)
 {
     int64_t i = 0;
     for (; i + 8 <= n; i += 8) out.wle(src.get8(s0 + i), 8);
@@ -253,8 +254,8 @@ DGI bool hex4w(S &src, int64_t i, uint32_t &v)
 
 /* unquote (native/parsing.c:702-945, flags 0) of src[s0, s0+nb) appended to
  * out: runs between backslashes are copied as words. false = error. */
-template <class S>
-DGI bool fast_unquote(S &src, int64_t s0, int64_t nb, Out &out)
+template <class S, class O>
+DGI bool fast_unquote(S &src, int64_t s0, int64_t nb, O &out)
 {
     int64_t i = s0, end = s0 + nb;
     while (i < end) {

@@ -13,7 +13,7 @@
 #include <mutex>
 #include <vector>
 
-#include "j2t_machine.h"
+#include "j2t_wave.h"
 
 /* ========================================================================== */
 /* host side: C ABI                                                            */
@@ -45,6 +45,13 @@ struct dg_ctx {
     uint8_t *ws_deep = nullptr;
     uint32_t *d_pending = nullptr;
     unsigned long long *d_stats = nullptr; /* {bails, deeps} since the last dg_ctx_stats reset */
+    uint32_t *d_bail_count = nullptr;      /* [0] wave kernel bails, [1] large messages (self-reset) */
+    uint32_t *d_bail_list = nullptr;
+    uint64_t bail_cap = 0;
+    uint32_t *d_big_list = nullptr;
+    uint64_t big_cap = 0;
+    int n_cu = 0;
+    uint8_t *ws_wave = nullptr;
     std::mutex mu;
     /* staging for the host API */
     uint8_t *d_json = nullptr; uint64_t d_json_cap = 0;
@@ -96,8 +103,12 @@ int dg_ctx_create(int device, dg_ctx **out)
     HIPCHK(hipMalloc(&c->d_pending, 16));
     HIPCHK(hipMalloc(&c->d_deep_count, 16));
     HIPCHK(hipMemset(c->d_deep_count, 0, 16)); /* {deep_count, done}: self-reset by each launch */
-    HIPCHK(hipMalloc(&c->d_stats, 16));
-    HIPCHK(hipMemset(c->d_stats, 0, 16));
+    HIPCHK(hipMalloc(&c->d_stats, 16 * 8));
+    HIPCHK(hipMemset(c->d_stats, 0, 16 * 8));
+    HIPCHK(hipMalloc(&c->d_bail_count, 16));
+    HIPCHK(hipMemset(c->d_bail_count, 0, 16));
+    HIPCHK(hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device));
+    HIPCHK(hipMalloc(&c->ws_wave, (size_t)c->n_cu * WV_BLOCKS_PER_CU * WV_WAVES * DCAP));
     *out = c;
     return DG_OK;
 }
@@ -112,6 +123,10 @@ void dg_ctx_destroy(dg_ctx *c)
     (void)hipFree(c->d_pending);
     (void)hipFree(c->d_deep_count);
     (void)hipFree(c->d_stats);
+    (void)hipFree(c->d_bail_count);
+    (void)hipFree(c->d_bail_list);
+    (void)hipFree(c->d_big_list);
+    (void)hipFree(c->ws_wave);
     (void)hipFree(c->d_deep_list);
     (void)hipFree(c->d_json);
     (void)hipFree(c->d_in_off);
@@ -186,6 +201,17 @@ int dg_ctx_stats(dg_ctx *c, uint64_t *bails, uint64_t *deeps, int reset)
     return DG_OK;
 }
 
+int dg_ctx_counters(dg_ctx *c, uint64_t *out, int n, int reset)
+{
+    if (!c || !out || n < 0 || n > 16) return set_err(DG_E_INVALID, "bad args");
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpy(out, c->d_stats, (size_t)n * 8, hipMemcpyDeviceToHost));
+    if (reset) HIPCHK(hipMemset(c->d_stats, 0, 16 * 8));
+    return DG_OK;
+}
+
 uint64_t dg_slot_bound(uint64_t len) { return (4 * len + 64 + 7) & ~7ull; }
 
 static int ensure_fast_ws(dg_ctx *c, uint64_t lanes)
@@ -210,12 +236,20 @@ static int launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *jso
     if (root >= d->hdr.n_types) return set_err(DG_E_INVALID, "root type %u out of range", root);
     int rc = ensure_fast_ws(c, n);
     if (rc) return rc;
+    const bool no_wave = (flags & DG_F_NO_WAVE_PATH) != 0;
+    flags &= ~DG_F_NO_WAVE_PATH;
     Params P;
     P.root = root;
     P.json = json;
     P.in_off = in_off;
     P.n = n;
     P.flag = flags;
+    P.list = nullptr;
+    P.list_count = nullptr;
+    P.reset2 = nullptr;
+    P.big_list = nullptr;
+    P.big_count = nullptr;
+    P.big_max = 0;
     P.out = out;
     P.out_off = out_off;
     P.out_len = out_len;
@@ -238,10 +272,46 @@ static int launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *jso
     DP.done = c->d_deep_count + 1;
     DP.blob = d->d_blob;
     DP.hdr = d->hdr;
-    if (d->hdr.total_len <= DESC_LDS_BYTES)
-        launch_lane_kernel_lds(dim3((uint32_t)blocks), s, P, DP);
-    else
-        launch_lane_kernel_glb(dim3((uint32_t)blocks), s, P, DP);
+    const bool wave = P.fast && !no_wave && d->hdr.total_len <= WV_DESC && d->hdr.total_len <= DESC_LDS_BYTES;
+    auto lane_launch = [&](dim3 g, const Params &Q) {
+        if (d->hdr.total_len <= DESC_LDS_BYTES) launch_lane_kernel_lds(g, s, Q, DP);
+        else launch_lane_kernel_glb(g, s, Q, DP);
+    };
+    if (!wave) {
+        lane_launch(dim3((uint32_t)blocks), P);
+    } else {
+        /* 1. lane kernel: small messages (lane fast path + exact machine);
+         *    messages longer than big_max are listed for the wave kernel
+         * 2. wave kernel: the listed ones, one wavefront per message
+         * 3. lane kernel in list mode: the wave kernel's bails, exact machine */
+        if ((rc = grow(c->d_bail_list, c->bail_cap, n))) return rc;
+        if ((rc = grow(c->d_big_list, c->big_cap, n))) return rc;
+        const char *wm = getenv("DG_WAVE_MIN"); /* messages longer than this go to the wave kernel */
+        const uint64_t big_max = wm ? strtoull(wm, nullptr, 10) : (uint64_t)WV_MIN_DEFAULT;
+        Params P1 = P;
+        P1.big_list = c->d_big_list;
+        P1.big_count = c->d_bail_count + 1;
+        P1.big_max = big_max;
+        lane_launch(dim3((uint32_t)blocks), P1);
+        HIPCHK(hipGetLastError());
+        WaveParams W;
+        W.blob = d->d_blob;
+        W.hdr = d->hdr;
+        W.bail_count = c->d_bail_count;
+        W.bail_list = c->d_bail_list;
+        W.list = c->d_big_list;
+        W.list_count = c->d_bail_count + 1;
+        W.ws = c->ws_wave;
+        uint64_t wblocks = std::min<uint64_t>((n + WV_WAVES - 1) / WV_WAVES, (uint64_t)c->n_cu * WV_BLOCKS_PER_CU);
+        launch_wave_kernel(dim3((uint32_t)wblocks), s, P, W);
+        HIPCHK(hipGetLastError());
+        Params P3 = P;
+        P3.list = c->d_bail_list;
+        P3.list_count = c->d_bail_count;
+        P3.reset2 = c->d_bail_count + 1;
+        P3.fast = 0;
+        lane_launch(dim3((uint32_t)std::min<uint64_t>(blocks, 32)), P3);
+    }
     HIPCHK(hipGetLastError());
     return DG_OK;
 }

@@ -50,6 +50,12 @@ struct Params {
     uint32_t keycap, reqcap;
     uint32_t fast;     /* run the fast path first (descriptor v2, flags within FAST_FLAGS) */
     unsigned long long *stats; /* {messages bailed to the exact machine, messages redone deep} */
+    const uint32_t *list;      /* list mode: convert only these messages (exact machine) */
+    uint32_t *list_count;      /* device count of `list` (self-reset by the last block) */
+    uint32_t *reset2;          /* another counter the last block resets (list mode: the large-message count) */
+    uint32_t *big_list;        /* messages longer than big_max are left to the wave kernel via this list */
+    uint32_t *big_count;
+    uint64_t big_max;
 };
 
 #ifdef DG_PROFILE
@@ -830,6 +836,8 @@ DGI void deep_pass(const Params &P, const DV &dv, uint32_t *done, uint32_t nbloc
     }
     __syncthreads();
     if (threadIdx.x == 0) { /* self-reset for the next launch on this context */
+        if (P.list_count) __hip_atomic_store(P.list_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (P.reset2) __hip_atomic_store(P.reset2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(P.deep_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -863,6 +871,45 @@ __global__ __launch_bounds__(LANE_BLOCK) __attribute__((amdgpu_waves_per_eu(1, 1
     __shared__ double s_p10d[23];
     __shared__ uint32_t s_nbail;
     __shared__ uint16_t s_bail[LANE_BLOCK];
+    __shared__ uint32_t s_cnt;
+    if (P.list) {
+        /* list mode: the messages the wave kernel bailed on, on the exact
+         * machine only, grid-strided over the device-side count */
+        if constexpr (LDS_DESC) {
+            const uint4 *g = (const uint4 *)DP.blob;
+            uint4 *l = (uint4 *)ldesc;
+            for (uint32_t k = threadIdx.x; k < (DP.hdr.total_len + 15) / 16; k += LANE_BLOCK) l[k] = g[k];
+        }
+        if (threadIdx.x == 0) {
+            s_cnt = __hip_atomic_load(P.list_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (blockIdx.x == 0 && s_cnt) atomicAdd(&P.stats[0], (unsigned long long)s_cnt);
+        }
+        __syncthreads();
+        auto dvl = [&]() {
+            if constexpr (LDS_DESC) return desc_view<3>((const __attribute__((address_space(3))) uint8_t *)(void *)ldesc, DP.hdr);
+            else return desc_view<1>((const __attribute__((address_space(1))) uint8_t *)(const void *)DP.blob, DP.hdr);
+        }();
+        const uint32_t cnt = s_cnt;
+        for (uint64_t k = (uint64_t)blockIdx.x * LANE_BLOCK + threadIdx.x; k < cnt; k += (uint64_t)gridDim.x * LANE_BLOCK) {
+            uint64_t j = P.list[k];
+            FStack<LFrame *> frames{(LFrame *)(void *)&lframes[threadIdx.x], LANE_BLOCK};
+            Workspace ws = lane_ws(P, j);
+            uint32_t olen;
+            uint64_t r = convert_one(P, dvl, j, global_src(P, j), frames, LDS_DEPTH, nullptr, 64, ws, olen);
+            finish(P, j, r, olen);
+            if ((uint8_t)r == DG_ST_DEEP) {
+                uint32_t q = __hip_atomic_fetch_add(P.deep_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&P.deep_list[q], j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        Params Q = P;
+        Q.ws = DP.ws;
+        Q.ws_stride = DP.ws_stride;
+        Q.keycap = DP.keycap;
+        Q.reqcap = DP.reqcap;
+        deep_pass(Q, dvl, DP.done, gridDim.x);
+        return;
+    }
     uint64_t b0 = (uint64_t)blockIdx.x * LANE_BLOCK;
     uint64_t b1 = b0 + LANE_BLOCK < P.n ? b0 + LANE_BLOCK : P.n;
     uint64_t lo = P.in_off[b0], hi = P.in_off[b1];
@@ -895,7 +942,12 @@ __global__ __launch_bounds__(LANE_BLOCK) __attribute__((amdgpu_waves_per_eu(1, 1
     /* phase 1: the fast path on this lane's own message */
     if (i < b1) {
         bool done = false;
-        if (P.fast) {
+        if (P.big_list && P.in_off[i + 1] - P.in_off[i] > P.big_max) {
+            /* a large message: the wave kernel (one wavefront per message) takes it */
+            uint32_t q = __hip_atomic_fetch_add(P.big_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&P.big_list[q], (uint32_t)i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            done = true;
+        } else if (P.fast) {
             uint64_t oa = P.out_off[i], ob = P.out_off[i + 1];
             Out out;
             out.init(P.out + oa, ob - oa);

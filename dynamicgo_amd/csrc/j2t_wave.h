@@ -1,0 +1,1051 @@
+/*
+ * j2t_wave.h — the wave-per-message, token-parallel transcoder (gfx950).
+ *
+ * Why: one lane per message gives 65 536 lanes = one wave per SIMD for a 64K
+ * batch (and 64 waves in total for 4K large messages), so the lane kernel is
+ * latency-bound by construction. Here a whole wavefront converts ONE message,
+ * and the work inside the message is spread over the 64 lanes:
+ *
+ *  1. Structural scan (simdjson's stage 1 mapped onto a wavefront): 64 lanes
+ *     x 4 bytes are classified per step through a 256-entry class table in
+ *     LDS; backslash escapes, the in-string mask and scalar runs are carried
+ *     across lanes with ballots and popcounts. Tokens ({ } [ ] : , string,
+ *     scalar) are compacted into a per-wave token ring in LDS (kind | pos),
+ *     and the terminator of every string/scalar writes the token's end.
+ *  2. Pages of 64 tokens, one token per lane:
+ *     - depth by ballot prefix counts, parent = the last opener one level up
+ *       (per-level ballots; parents from earlier pages come from a level
+ *       stack), grammar checked against the neighbouring tokens;
+ *     - Thrift types resolved level by level (keys are hashed and looked up
+ *       in parallel), output length of every token (field headers, container
+ *       headers, scalars, strings, unset fields + STOP at '}');
+ *     - one wave prefix sum gives every token its output offset, and all
+ *       tokens write their bytes at once (byte-exact stores); list/map sizes
+ *       are LDS atomic counters written by the closing bracket.
+ *
+ * Scope: the error-free common grammar, exactly like the lane fast path
+ * (j2t_fast.h). Anything else (every error, escaped keys, duplicate keys,
+ * >64-field structs, nesting beyond WV_MAXD, big-decimal numbers, non-canonical
+ * base64, flags outside FAST_FLAGS, non-container roots) BAILS: the message is
+ * appended to a list that the lane kernel's exact machine (Machine<S>::run,
+ * the restatement of j2t_fsm_exec native/thrift.c:765-1187) converts from
+ * scratch. Results are therefore bit-identical to the reference either way;
+ * the wave path decides speed, never output.
+ *
+ * Reference semantics reproduced (cited where used): container headers and
+ * back-patched sizes native/thrift.c:132-162, 810-875, 1093-1133; null
+ * handling native/thrift.c:942-947, 996-1032; unset fields
+ * native/thrift.c:258-310 + 171-217; key lookup native/thrift.c:668-763;
+ * numbers native/scanning.c:958-1083 + native/thrift.c:312-365; strings
+ * native/thrift.c:367-399 + native/parsing.c:702-945; binary
+ * native/thrift.c:401-420 + native/base64.c:539-817; skipping
+ * native/scanning.c:1134-1572.
+ */
+#pragma once
+#include "j2t_machine.h"
+
+namespace dg {
+
+constexpr uint32_t WV_WAVES = 4;               /* waves (= messages in flight) per block */
+constexpr uint32_t WV_RING = 512;              /* token ring per wave */
+constexpr uint32_t WV_RMASK = WV_RING - 1;
+constexpr uint32_t WV_CHUNK = 256;             /* bytes classified per scan step: 64 lanes x 4 */
+constexpr uint32_t WV_MAXD = 16;               /* container levels handled on the wave path */
+constexpr uint32_t WV_LA = 2;                  /* token lookahead kept unconsumed while scanning */
+constexpr uint32_t WV_NOEND = 0xFFFFFFFFu;     /* string not closed (yet) */
+constexpr uint32_t WV_POSMASK = (1u << 29) - 1;
+constexpr uint32_t WV_MSG = 4096;              /* messages up to this (minus 16) are staged in LDS */
+constexpr uint32_t WV_DESC = 16384;            /* the wave path needs the descriptor in LDS */
+constexpr uint32_t WV_LONG = 192;              /* strings longer than this are copied/decoded by the whole wave */
+constexpr uint32_t WV_BLOCKS_PER_CU = 2;       /* persistent grid: 2 blocks x 4 waves per CU */
+constexpr uint32_t WV_MIN_DEFAULT = 8192;      /* messages longer than this go to the wave kernel (DG_WAVE_MIN) */
+
+/* token kinds (3 bits, stored above the 29-bit position) */
+enum : uint32_t {
+    K_LBRACE = 0, K_RBRACE = 1, K_LBRACK = 2, K_RBRACK = 3, K_COLON = 4, K_COMMA = 5, K_STRING = 6, K_SCALAR = 7,
+    K_NONE = 8
+};
+/* byte classes (LDS table); the low 3 bits give a structural byte's kind */
+constexpr uint8_t C_STRUCT = 0x08, C_WS = 0x10, C_QUOTE = 0x20, C_BS = 0x40;
+
+/* trec[] values for keys */
+constexpr uint32_t TR_SKIP = 0xFFFFFFFFu, TR_MAPKEY = 0xFFFFFFFEu;
+
+/* one open container (32 B): in-page openers at crec[lane], earlier pages'
+ * openers at crec[64 + level] */
+struct CRec {
+    uint32_t type;   /* dg type index */
+    uint32_t flags;  /* CF_* */
+    uint32_t outpos; /* output offset of its header (relative to the slot) */
+    uint32_t count;  /* list/map: elements written (LDS atomic) */
+    uint64_t seen;   /* struct: fields that occurred (by index; LDS atomic) */
+    uint64_t nulldr; /* struct: DEFAULT/REQUIRED fields that occurred as null */
+};
+constexpr uint32_t CF_SKIP = 1, CF_OBJ = 2, CF_STRUCT = 4, CF_MAP = 8, CF_LIST = 16;
+
+struct WaveLds {
+    uint32_t tpos[WV_RING]; /* kind << 29 | position */
+    uint32_t tend[WV_RING]; /* string: closing quote position; scalar: one past its last byte */
+    uint32_t trec[WV_RING]; /* key: field index / TR_* */
+    CRec crec[64 + WV_MAXD + 1];
+};
+
+struct WaveParams {
+    const uint8_t *blob; /* descriptor blob (device) */
+    dg_desc_hdr hdr;
+    uint32_t *bail_count; /* out: messages left to the exact machine */
+    uint32_t *bail_list;
+    const uint32_t *list; /* in: the messages to convert (the lane kernel's large ones) */
+    const uint32_t *list_count;
+    uint8_t *ws;          /* DCAP bytes of big-decimal digits per wave of the grid */
+};
+
+#ifdef DG_WPROF
+/* phase timers (cycles, summed over waves) -> P.stats[2 + k] */
+#define WP_DECL uint64_t wp_t = __builtin_readcyclecounter(); uint64_t wp_acc[10] = {0};
+#define WP(k) do { uint64_t t_ = __builtin_readcyclecounter(); wp_acc[k] += t_ - wp_t; wp_t = t_; } while (0)
+#define WP_FLUSH() do { if (lane == 0) for (int k_ = 0; k_ < 10; k_++) atomicAdd(&P.stats[2 + k_], (unsigned long long)wp_acc[k_]); } while (0)
+#else
+#define WP_DECL
+#define WP(k)
+#define WP_FLUSH()
+#endif
+
+/* ---------------- wavefront helpers ---------------- */
+DGI uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+DGI uint32_t popc(uint64_t x) { return (uint32_t)__builtin_popcountll(x); }
+DGI uint32_t msb(uint64_t x) { return 63u - (uint32_t)__builtin_clzll(x); }
+DGI uint32_t wave_or(uint32_t v)
+{
+#pragma unroll
+    for (int d = 32; d; d >>= 1) v |= (uint32_t)__shfl_xor((int)v, d);
+    return v;
+}
+/* inclusive prefix sum over the 64 lanes */
+DGI uint32_t wave_incl_sum(uint32_t v, uint32_t lane)
+{
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        uint32_t u = (uint32_t)__shfl_up((int)v, d);
+        if (lane >= d) v += u;
+    }
+    return v;
+}
+template <class T>
+DGI T uni(T v) /* wave-uniform value -> SGPR */
+{
+    return (T)__builtin_amdgcn_readfirstlane((int)v);
+}
+
+/* ---------------- byte-exact output ---------------- */
+typedef __attribute__((address_space(1))) uint32_t gu32;
+typedef __attribute__((address_space(1))) uint16_t gu16;
+
+/* store bytes [lo, hi) of the little-endian word v at the 8-aligned w */
+DGI void store_part(gu8 *w, uint64_t v, uint32_t lo, uint32_t hi)
+{
+    uint32_t i = lo;
+    while (i < hi) {
+        uint32_t r = hi - i;
+        if ((i & 7) == 0 && r >= 8) {
+            *(gu64 *)w = v;
+            i += 8;
+        } else if ((i & 3) == 0 && r >= 4) {
+            *(gu32 *)(w + i) = (uint32_t)(v >> (i * 8));
+            i += 4;
+        } else if ((i & 1) == 0 && r >= 2) {
+            *(gu16 *)(w + i) = (uint16_t)(v >> (i * 8));
+            i += 2;
+        } else {
+            w[i] = (uint8_t)(v >> (i * 8));
+            i += 1;
+        }
+    }
+}
+
+/* A writer that owns exactly [start, start + written): whole aligned words
+ * inside the range are stored as 8-byte words, the partial words at both
+ * ends byte-exactly, so neighbouring tokens can write concurrently. */
+struct WOut {
+    gu8 *wa;       /* 8-aligned address of the current word */
+    uint32_t lo;   /* first owned byte of the current word (first word only) */
+    uint32_t used; /* bytes of the current word filled */
+    uint64_t wbuf;
+    uint64_t len;  /* bytes written */
+    bool dry;      /* count only (lengths before the offsets are known) */
+    DGI void init(gu8 *p)
+    {
+        uintptr_t a = (uintptr_t)(void *)p;
+        wa = (gu8 *)(void *)(a & ~(uintptr_t)7);
+        lo = used = (uint32_t)(a & 7);
+        wbuf = 0;
+        len = 0;
+        dry = false;
+    }
+    DGI void init_dry()
+    {
+        wa = nullptr;
+        lo = used = 0;
+        wbuf = 0;
+        len = 0;
+        dry = true;
+    }
+    DGI void wle(uint64_t v, uint32_t n)
+    {
+        if (dry) {
+            len += n;
+            return;
+        }
+        if (n < 8) v &= (1ull << (n << 3)) - 1;
+        uint32_t sh = used << 3;
+        uint64_t lo_w = wbuf | (used ? (v << sh) : v);
+        uint64_t hi_w = used ? (v >> (64 - sh)) : 0;
+        len += n;
+        if (used + n >= 8) {
+            if (lo == 0) *(gu64 *)wa = lo_w;
+            else store_part(wa, lo_w, lo, 8);
+            wa += 8;
+            lo = 0;
+            wbuf = hi_w;
+            used = used + n - 8;
+        } else {
+            wbuf = lo_w;
+            used += n;
+        }
+    }
+    DGI void w8(uint8_t v) { wle(v, 1); }
+    DGI void w16(uint16_t v) { wle(__builtin_bswap16(v), 2); }
+    DGI void w32(uint32_t v) { wle(__builtin_bswap32(v), 4); }
+    DGI void w64(uint64_t v) { wle(__builtin_bswap64(v), 8); }
+    DGI void finish()
+    {
+        if (!dry && used > lo) store_part(wa, wbuf, lo, used);
+    }
+};
+
+/* a writer that only counts (output lengths before the offsets are known) */
+struct CountOut_unused {
+    uint64_t len = 0;
+    DGI void wle(uint64_t, uint32_t n) { len += n; }
+    DGI void w8(uint8_t) { len += 1; }
+    DGI void w16(uint16_t) { len += 2; }
+    DGI void w32(uint32_t) { len += 4; }
+    DGI void w64(uint64_t) { len += 8; }
+};
+
+/* big-endian u32 at an arbitrary byte address, byte-exact */
+DGI void put_be32(gu8 *p, uint32_t v)
+{
+    WOut w;
+    w.init(p);
+    w.w32(v);
+    w.finish();
+}
+
+DGI uint32_t num_size(uint8_t tt)
+{
+    switch (tt) {
+    case DG_T_BYTE: return 1;
+    case DG_T_I16: return 2;
+    case DG_T_I32: return 4;
+    case DG_T_I64:
+    case DG_T_DOUBLE: return 8;
+    }
+    return 0;
+}
+
+/* any '\\' in src[s0, s0+n) */
+template <class S>
+DGI bool has_bslash(S &src, int64_t s0, int64_t n)
+{
+    for (int64_t i = 0; i < n; i += 8) {
+        uint64_t m = zbytes(src.get8(s0 + i) ^ 0x5C5C5C5C5C5C5C5Cull);
+        int64_t rem = n - i;
+        if (rem < 8) m &= (1ull << (rem << 3)) - 1;
+        if (m) return true;
+    }
+    return false;
+}
+
+/* decoded length of a standard-padded base64 body of nb chars (nb % 4 == 0),
+ * or -1 for a shape the wave path leaves to the exact machine */
+template <class S>
+DGI int64_t b64_len(S &src, int64_t s0, int64_t nb)
+{
+    if (nb == 0) return 0;
+    if (nb & 3) return -1;
+    uint8_t c2 = src.raw(s0 + nb - 2), c3 = src.raw(s0 + nb - 1);
+    int64_t pad = c3 == '=' ? (c2 == '=' ? 2 : 1) : 0;
+    return nb / 4 * 3 - pad;
+}
+
+/* b64decode (native/base64.c:659-817, mode 0) of a body of nb chars whose
+ * length b64_len accepted: 8 chars -> 6 bytes per step (b64_8), then whole
+ * quanta; a final quantum "xx==" / "xxx=" keeps the top 1 / 2 bytes like
+ * decode_block (native/base64.c:600-631). false = anything else (\r, \n,
+ * '=' inside, characters outside the alphabet): left to the exact machine. */
+template <class S, class O>
+DGI bool b64_decode_wave(S &src, int64_t s0, int64_t nb, O &out)
+{
+    int64_t ip = 0;
+    uint64_t o;
+    while (ip + 8 <= nb && b64_8(src.get8(s0 + ip), o)) {
+        out.wle(o, 6);
+        ip += 8;
+    }
+    while (ip < nb) {
+        int a = b64v(src.raw(s0 + ip)), b = b64v(src.raw(s0 + ip + 1));
+        uint8_t c2 = src.raw(s0 + ip + 2), c3 = src.raw(s0 + ip + 3);
+        int c = b64v(c2), d = b64v(c3);
+        bool last = ip + 4 == nb;
+        if (a < 0 || b < 0) return false;
+        uint32_t v = ((uint32_t)a << 18) | ((uint32_t)b << 12);
+        uint32_t keep = 3;
+        if (c >= 0 && d >= 0) {
+            v |= ((uint32_t)c << 6) | (uint32_t)d;
+        } else if (last && c >= 0 && c3 == '=') {
+            v |= (uint32_t)c << 6;
+            keep = 2;
+        } else if (last && c2 == '=' && c3 == '=') {
+            keep = 1;
+        } else {
+            return false;
+        }
+        out.wle(((v >> 16) & 0xff) | (((v >> 8) & 0xff) << 8) | ((uint64_t)(v & 0xff) << 16), keep);
+        ip += 4;
+    }
+    return true;
+}
+
+/* j2t_write_unset_fields (native/thrift.c:258-310) for one struct instance
+ * whose remaining requires bits are `bits`: false = ERR_NULL_REQUIRED (bail) */
+template <class DV, class O>
+DGI bool unset_fields(const DV &D, const dg_struct &sd, uint64_t bits, uint64_t flag, O &out)
+{
+    bool wr = flag & DG_F_WRITE_REQUIRE, wd = flag & DG_F_WRITE_DEFAULT, wo = flag & DG_F_WRITE_OPTIONAL;
+    while (bits) {
+        uint32_t k = __builtin_ctzll(bits);
+        bits &= bits - 1;
+        const dg_field f = ldrec(&D.F[sd.field_begin + k]);
+        if (f.flags & DG_FF_REQUEST_BASE) continue;
+        if (!wr && f.required == DG_REQ_REQUIRED) return false;
+        if ((wr && f.required == DG_REQ_REQUIRED) || (wd && f.required == DG_REQ_DEFAULT) ||
+            (wo && f.required == DG_REQ_OPTIONAL)) {
+            const dg_type ft = ldrec(&D.T[f.type]);
+            out.wle((uint32_t)ft.ttype | ((uint32_t)__builtin_bswap16(f.id) << 8), 3);
+            if (f.dflt_len != DG_NONE) {
+                for (uint32_t j = 0; j < f.dflt_len; j++) out.w8(D.P[f.dflt_off + j]);
+                continue;
+            }
+            switch (ft.ttype) { /* tb_write_empty native/thrift.c:171-203 */
+            case DG_T_BOOL:
+            case DG_T_BYTE: out.w8(0); break;
+            case DG_T_I16: out.w16(0); break;
+            case DG_T_I32:
+            case DG_T_STRING: out.w32(0); break;
+            case DG_T_I64:
+            case DG_T_DOUBLE: out.w64(0); break;
+            case DG_T_LIST:
+            case DG_T_SET:
+                out.w8(ldrec(&D.T[ft.elem]).ttype);
+                out.w32(0);
+                break;
+            case DG_T_MAP:
+                out.w8(ldrec(&D.T[ft.key]).ttype);
+                out.w8(ldrec(&D.T[ft.elem]).ttype);
+                out.w32(0);
+                break;
+            case DG_T_STRUCT: out.w8(0); break;
+            default: return false;
+            }
+        }
+    }
+    return true;
+}
+
+/* field lookup j2t_key (native/thrift.c:668-763) by the struct's name table:
+ * global field index or -1 */
+template <class S, class DV>
+DGI int32_t wv_lookup(const DV &D, const dg_struct &sd, S &src, int64_t k0, uint32_t kn)
+{
+    uint32_t h = DG_NAME_HASH_SEED;
+    for (uint32_t j = 0; j < kn; j++) h = DG_NAME_HASH_STEP(h, src.raw(k0 + j));
+    for (uint32_t s = h & sd.name_mask;; s = (s + 1) & sd.name_mask) {
+        const dg_name nm = ldrec(&D.N[sd.name_begin + s]);
+        if (nm.field == DG_NONE) return -1;
+        if (nm.hash == h && nm.key_len == kn && key_eq(src, k0, kn, (decltype(&D.R[0]))(&D.P[nm.key_off])))
+            return (int32_t)nm.field;
+    }
+}
+
+/* src[s0, s0+nb) -> dst, by the 64 lanes of the wave: lane l stores the
+ * 8-aligned destination words l, l+64, ... (partial end words byte-exactly) */
+template <class S>
+DGI void coop_copy(S &src, int64_t s0, int64_t nb, gu8 *dst, uint32_t lane)
+{
+    const uintptr_t da = (uintptr_t)(void *)dst, wb = da & ~(uintptr_t)7;
+    const uint32_t lead = (uint32_t)(da - wb);
+    const int64_t nw = (int64_t)(lead + nb + 7) >> 3;
+    for (int64_t k = lane; k < nw; k += 64) {
+        int64_t off = k * 8 - (int64_t)lead; /* string offset of the word's first byte */
+        uint32_t lo = off < 0 ? (uint32_t)-off : 0u;
+        int64_t rem = nb - off;
+        uint32_t hi = rem < 8 ? (uint32_t)rem : 8u;
+        uint64_t v = off < 0 ? src.get8(s0) << (lo * 8) : src.get8(s0 + off);
+        gu8 *w = (gu8 *)(void *)(wb + (uintptr_t)k * 8);
+        if (lo == 0 && hi == 8) *(gu64 *)w = v;
+        else store_part(w, v, lo, hi);
+    }
+}
+
+/* base64 body src[s0, s0+nb) (nb % 4 == 0) -> dst, by the 64 lanes: 8 chars ->
+ * 6 bytes per lane and step, the last 4..8 chars (padding) by lane 0 */
+template <class S>
+DGI bool coop_b64(S &src, int64_t s0, int64_t nb, gu8 *dst, uint32_t want, uint32_t lane)
+{
+    const int64_t full = nb >= 8 ? (nb - 4) >> 3 : 0;
+    bool ok = true;
+    for (int64_t g = lane; g < full; g += 64) {
+        uint64_t o;
+        if (!b64_8(src.get8(s0 + 8 * g), o)) ok = false;
+        WOut w;
+        w.init(dst + 6 * g);
+        w.wle(o, 6);
+        w.finish();
+    }
+    if (lane == 0) {
+        WOut w;
+        w.init(dst + 6 * full);
+        if (!b64_decode_wave(src, s0 + 8 * full, nb - 8 * full, w)) ok = false;
+        w.finish();
+        if (w.len + 6 * (uint64_t)full != want) ok = false;
+    }
+    return ok;
+}
+
+/* the exact number parser, out of line (rare: keeps the kernel small) */
+__device__ __noinline__ void vnumber_slow(SrcT<const uint64_t> src, int64_t &p, JState &js, gu8 *dbuf)
+{
+    vnumber(src, p, js, dbuf);
+}
+
+/* ---------------- stage 1: structural scan of one chunk ---------------- */
+struct ScanState {
+    uint32_t produced;   /* tokens appended to the ring so far */
+    uint32_t esc_carry;  /* an escape is pending at the chunk boundary */
+    uint32_t str_carry;  /* inside a string at the chunk boundary */
+    uint32_t scal_carry; /* the chunk's last byte was a scalar byte */
+};
+
+template <class LW, class WP>
+DGI void scan_chunk(WP wbase, int64_t head, int64_t len, uint32_t chunk, ScanState &st, LW &L,
+                    const __attribute__((address_space(3))) uint8_t *cls, uint32_t lane, uint64_t lt)
+{
+    int64_t wi = (int64_t)chunk * 64 + lane;
+    int64_t p0 = wi * 4 - head; /* message position of this lane's byte 0 */
+    uint32_t x = p0 < len ? wbase[wi] : 0x20202020u;
+    uint32_t q = 0, bs = 0, sm = 0, ws = 0, knib = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) {
+        int64_t p = p0 + j;
+        uint8_t c = cls[(x >> (8 * j)) & 0xff];
+        if (p < 0 || p >= len) c = C_WS;
+        q |= (uint32_t)((c >> 5) & 1) << j;
+        bs |= (uint32_t)((c >> 6) & 1) << j;
+        sm |= (uint32_t)((c >> 3) & 1) << j;
+        ws |= (uint32_t)((c >> 4) & 1) << j;
+        knib |= (uint32_t)(c & 7) << (3 * j);
+    }
+    /* escapes: byte j is escaped when an odd backslash run precedes it. The
+     * carry into a lane comes from the nearest lane below that is not all
+     * backslashes (a 4-backslash lane passes its carry through unchanged). */
+    uint32_t e0 = 0, e1 = 1, m0 = 0, m1 = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) {
+        uint32_t b = (bs >> j) & 1;
+        if (e0) { m0 |= 1u << j; e0 = 0; } else e0 = b;
+        if (e1) { m1 |= 1u << j; e1 = 0; } else e1 = b;
+    }
+    uint64_t nab = ballot(bs != 0xF);
+    uint64_t c0b = ballot(e0 != 0);
+    uint64_t below = nab & lt;
+    uint32_t cin = below ? (uint32_t)(c0b >> msb(below)) & 1 : st.esc_carry;
+    uint32_t escaped = cin ? m1 : m0;
+    uint32_t cout = cin ? e1 : e0;
+    /* in-string mask: prefix xor of unescaped quotes, carried by popcounts */
+    uint32_t uq = q & ~escaped;
+    uint32_t px = (uq ^ (uq << 1) ^ (uq << 2) ^ (uq << 3)) & 0xF;
+    uint64_t pb = ballot(__builtin_popcount(uq) & 1);
+    uint32_t sin = (popc(pb & lt) + st.str_carry) & 1;
+    uint32_t instr = sin ? (px ^ 0xF) : px; /* bit j: inside a string after byte j */
+    uint32_t openq = uq & instr, closeq = uq & ~instr & 0xF;
+    uint32_t outside = ~(instr | uq) & 0xF;
+    uint32_t stm = sm & outside;
+    uint32_t scal = outside & ~ws & ~sm;
+    uint64_t sb3 = ballot(scal & 8);
+    uint32_t prevs = lane ? (uint32_t)(sb3 >> (lane - 1)) & 1 : st.scal_carry;
+    uint32_t sprev = ((scal << 1) | prevs) & 0xF;
+    uint32_t sstart = scal & ~sprev;
+    uint32_t send = ~scal & sprev & 0xF;
+    uint32_t tok = stm | openq | sstart;
+    uint32_t term = closeq | send;
+    uint32_t cnt = (uint32_t)__builtin_popcount(tok);
+    uint64_t b0 = ballot(cnt & 1), b1 = ballot(cnt & 2), b2 = ballot(cnt & 4);
+    uint32_t pre = popc(b0 & lt) + 2 * popc(b1 & lt) + 4 * popc(b2 & lt);
+    uint32_t total = popc(b0) + 2 * popc(b1) + 4 * popc(b2);
+    uint32_t k = st.produced + pre;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) {
+        if ((tok >> j) & 1) {
+            uint32_t kind = ((stm >> j) & 1) ? (knib >> (3 * j)) & 7 : ((openq >> j) & 1) ? K_STRING : K_SCALAR;
+            L.tpos[k & WV_RMASK] = (kind << 29) | (uint32_t)(p0 + j);
+            L.tend[k & WV_RMASK] = WV_NOEND;
+            k++;
+        }
+    }
+    /* terminators, after every token write of the chunk: the token a
+     * terminator ends is the last token strictly before it */
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) {
+        if ((term >> j) & 1) {
+            uint32_t kb = st.produced + pre + (uint32_t)__builtin_popcount(tok & ((1u << j) - 1));
+            L.tend[(kb - 1) & WV_RMASK] = (uint32_t)(p0 + j);
+        }
+    }
+    st.produced += total;
+    st.esc_carry = (uint32_t)__builtin_amdgcn_readlane((int)cout, 63);
+    st.str_carry = (st.str_carry + popc(pb)) & 1;
+    st.scal_carry = (uint32_t)(sb3 >> 63) & 1;
+}
+
+/* ---------------- one message ---------------- */
+typedef const __attribute__((address_space(3))) uint32_t lds_u32;
+
+template <class S, class WP, class DV, class LW>
+DGI bool wave_run(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L, S src, WP wbase, int64_t head,
+                  int64_t len, const __attribute__((address_space(3))) uint8_t *cls, const FastTabs &tb, uint32_t lane,
+                  gu8 *dbuf)
+{
+    const uint64_t flag = P.flag;
+    uint64_t oa = P.out_off[m];
+    uint64_t cap = P.out_off[m + 1] - oa;
+    gu8 *ob = (gu8 *)(void *)(P.out + oa);
+    uint32_t nchunks = (uint32_t)((len + head + WV_CHUNK - 1) / WV_CHUNK);
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    const uint64_t le = lt | (1ull << lane);
+
+    WP_DECL
+    ScanState ss{0, 0, 0, 0};
+    uint32_t scanned = 0, consumed = 0;
+    int32_t depth = 0;
+    uint64_t O = 0;
+    bool rootdone = false;
+
+    for (;;) {
+        while (scanned < nchunks && ss.produced - consumed < 64 + WV_LA) {
+            scan_chunk(wbase, head, len, scanned, ss, L, cls, lane, lt);
+            scanned++;
+            if (scanned == nchunks && ss.scal_carry) {
+                if (lane == 0) L.tend[(ss.produced - 1) & WV_RMASK] = (uint32_t)len;
+            }
+        }
+        WP(0);
+        uint32_t avail = ss.produced - consumed;
+        if (scanned < nchunks) avail -= WV_LA;
+        if (avail == 0) break;
+        const uint32_t np = avail < 64 ? avail : 64;
+
+        /* ---------- a page: token t = consumed + lane ---------- */
+        const uint32_t t = consumed + lane;
+        const bool act = lane < np;
+        const uint32_t tp = act ? L.tpos[t & WV_RMASK] : 0;
+        const uint32_t kind = act ? tp >> 29 : K_NONE;
+        const int64_t pos = tp & WV_POSMASK;
+        const bool op = kind == K_LBRACE || kind == K_LBRACK;
+        const bool cl = kind == K_RBRACE || kind == K_RBRACK;
+        const uint64_t bo = ballot(op), bc = ballot(cl);
+        const int32_t dafter = depth + (int32_t)popc(bo & le) - (int32_t)popc(bc & le);
+        const uint64_t bend = ballot(cl && dafter == 0);
+        const bool alive = act && (bend == 0 || lane <= (uint32_t)__builtin_ctzll(bend));
+        const int32_t level = op ? dafter - 1 : dafter;
+        const int32_t plev = cl ? level : level - 1; /* level of the parent opener */
+        bool bad = alive && level >= (int32_t)WV_MAXD;
+        if (t == 0 && !op) bad = true; /* the root must be an object or array */
+        if (ballot(bad)) return false;
+
+        WP(1);
+        /* parent: the last opener at level plev before t (in this page), else
+         * the level stack */
+        int32_t par = -1;
+        {
+            uint32_t need = wave_or(alive && plev >= 0 ? 1u << plev : 0u);
+            uint32_t have = wave_or(alive && op ? 1u << level : 0u);
+            for (uint32_t lm = uni(need & have); lm; lm &= lm - 1) {
+                int32_t Lv = __builtin_ctz(lm);
+                uint64_t mo = ballot(alive && op && level == Lv) & lt;
+                if (plev == Lv && mo) par = (int32_t)msb(mo);
+            }
+        }
+        const uint32_t ci = par >= 0 ? (uint32_t)par : 64u + (uint32_t)(plev < 0 ? 0 : plev);
+        const uint32_t pkind = (uint32_t)__shfl((int)kind, par >= 0 ? par : 0);
+        bool pobj = false;
+        if (alive && plev >= 0) pobj = par >= 0 ? pkind == K_LBRACE : (L.crec[ci].flags & CF_OBJ) != 0;
+
+        /* grammar against the neighbouring tokens */
+        const uint32_t kp = (alive && t >= 1) ? L.tpos[(t - 1) & WV_RMASK] >> 29 : K_NONE;
+        const uint32_t kp2 = (alive && t >= 2) ? L.tpos[(t - 2) & WV_RMASK] >> 29 : K_NONE;
+        const uint32_t tpn = (alive && t + 1 < ss.produced) ? L.tpos[(t + 1) & WV_RMASK] : (K_NONE << 29);
+        const uint32_t kn = tpn >> 29;
+        const bool keyish = kind == K_STRING && pobj && (kp == K_LBRACE || kp == K_COMMA);
+        const bool isval = (kind == K_STRING && !keyish) || kind == K_SCALAR || op;
+        const bool vend = kp == K_SCALAR || kp == K_RBRACE || kp == K_RBRACK ||
+                          (kp == K_STRING && !(pobj && (kp2 == K_LBRACE || kp2 == K_COMMA)));
+        if (alive) {
+            bool ok;
+            if (t == 0) ok = true;
+            else if (keyish) ok = kn == K_COLON;
+            else if (isval) ok = pobj ? kp == K_COLON : (kp == K_LBRACK || kp == K_COMMA);
+            else if (kind == K_COLON) ok = pobj && kp == K_STRING && (kp2 == K_LBRACE || kp2 == K_COMMA);
+            else if (kind == K_COMMA) ok = vend;
+            else if (kind == K_RBRACE) ok = pobj && (kp == K_LBRACE || vend);
+            else ok = !pobj && (kp == K_LBRACK || vend); /* K_RBRACK */
+            bad |= !ok;
+        }
+        const uint32_t te = (alive && (kind == K_STRING || kind == K_SCALAR)) ? L.tend[t & WV_RMASK] : 0;
+        if (alive && kind == K_STRING && te == WV_NOEND) bad = true; /* EOF inside a string */
+        if (ballot(bad)) return false;
+
+        WP(2);
+        /* types, level by level: keys first (they need their struct), then
+         * values (they need their key or container) */
+        uint32_t ty = DG_NONE; /* value: type index; struct key: field index */
+        bool skip = false;
+        {
+            uint32_t lv = wave_or(alive ? 1u << level : 0u);
+            for (lv = uni(lv); lv; lv &= lv - 1) {
+                const int32_t Lv = __builtin_ctz(lv);
+                const bool me = alive && level == Lv;
+                if (me && keyish) {
+                    const uint32_t pf = L.crec[ci].flags, pt = L.crec[ci].type;
+                    uint32_t rec = TR_MAPKEY;
+                    if (pf & CF_SKIP) {
+                        skip = true;
+                        rec = TR_SKIP;
+                    } else if (pf & CF_STRUCT) {
+                        const dg_struct sd = ldrec(&D.S[ldrec(&D.T[pt]).st]);
+                        int64_t k0 = pos + 1;
+                        uint32_t kn2 = (uint32_t)(te - k0);
+                        int32_t fi = has_bslash(src, k0, kn2) ? -2 : wv_lookup(D, sd, src, k0, kn2);
+                        if (fi == -2) {
+                            bad = true; /* escaped key: exact machine */
+                            rec = TR_SKIP;
+                        } else if (fi < 0) {
+                            if ((flag & DG_F_ALLOW_UNKNOWN) == 0) bad = true;
+                            skip = true;
+                            rec = TR_SKIP;
+                        } else {
+                            const dg_field f = ldrec(&D.F[fi]);
+                            if ((flag & DG_F_ENABLE_VM) && f.vm != DG_VM_NONE) bad = true;
+                            if ((f.flags & DG_FF_REQUEST_BASE) && (flag & DG_F_NO_WRITE_BASE)) {
+                                skip = true;
+                                rec = TR_SKIP;
+                            } else {
+                                rec = (uint32_t)fi;
+                                ty = (uint32_t)fi;
+                            }
+                        }
+                    }
+                    L.trec[t & WV_RMASK] = rec;
+                }
+                if (me && isval) {
+                    if (t == 0) {
+                        ty = P.root;
+                    } else {
+                        const uint32_t pf = L.crec[ci].flags, pt = L.crec[ci].type;
+                        if (pf & CF_SKIP) {
+                            skip = true;
+                        } else if (pf & CF_STRUCT) {
+                            uint32_t kr = L.trec[(t - 2) & WV_RMASK];
+                            if (kr >= D_nf) skip = true; /* TR_SKIP (never TR_MAPKEY in a struct) */
+                            else ty = ldrec(&D.F[kr]).type;
+                        } else {
+                            ty = ldrec(&D.T[pt]).elem;
+                        }
+                    }
+                    if (op) {
+                        CRec c;
+                        c.type = ty;
+                        c.flags = (kind == K_LBRACE ? CF_OBJ : 0u) | (skip ? CF_SKIP : 0u);
+                        c.outpos = 0;
+                        c.count = 0;
+                        c.seen = 0;
+                        c.nulldr = 0;
+                        if (!skip) {
+                            const dg_type ct = ldrec(&D.T[ty]);
+                            if (kind == K_LBRACE) {
+                                if (ct.ttype == DG_T_STRUCT) {
+                                    c.flags |= CF_STRUCT;
+                                    if (ldrec(&D.S[ct.st]).req_words != 1) bad = true;
+                                } else if (ct.ttype == DG_T_MAP) {
+                                    c.flags |= CF_MAP;
+                                } else {
+                                    bad = true;
+                                }
+                            } else {
+                                if (ct.ttype == DG_T_LIST || ct.ttype == DG_T_SET) c.flags |= CF_LIST;
+                                else bad = true;
+                            }
+                        }
+                        L.crec[lane] = c;
+                    }
+                }
+                /* a mistyped container must not feed the next level */
+                if (ballot(bad)) return false;
+            }
+        }
+
+        WP(3);
+        /* lengths, part A: keys and values (with the LDS atomics that count
+         * elements and record struct fields). Every heavy helper has ONE call
+         * site below (I-cache: the kernel must stay small). */
+        uint32_t ln = 0;
+        bool isint = false, isnull = false, esc = false, isbin = false;
+        int64_t iv = 0;
+        double dv = 0.0;
+        uint8_t tt = 0;
+        int64_t ns = -1, nn = 0; /* number text to parse */
+        bool slow = false;
+        bool whole = true;       /* the number must span all of it */
+        int64_t cs = 0, cn = 0;  /* string body (copy / unquote / base64) */
+        uint64_t hv = 0;         /* header bytes (little-endian) and count */
+        uint32_t hn = 0;
+        if (alive && !skip && keyish) {
+            const uint32_t pf = L.crec[ci].flags, pt = L.crec[ci].type;
+            const uint32_t tv = L.tpos[(t + 2) & WV_RMASK];
+            isnull = (tv >> 29) == K_SCALAR && src.at(tv & WV_POSMASK) == 'n';
+            if (pf & CF_STRUCT) { /* native/thrift.c:668-763 + null unwinding 1016-1032 */
+                const dg_field f = ldrec(&D.F[ty]);
+                const dg_struct sd = ldrec(&D.S[ldrec(&D.T[pt]).st]);
+                uint64_t bit = 1ull << (ty - sd.field_begin);
+                uint64_t old = __hip_atomic_fetch_or(&L.crec[ci].seen, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (old & bit) bad = true; /* duplicate key: exact machine keeps the order semantics */
+                if (isnull && f.required != DG_REQ_OPTIONAL)
+                    __hip_atomic_fetch_or(&L.crec[ci].nulldr, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                tt = ldrec(&D.T[f.type]).ttype;
+                hv = (uint32_t)tt | ((uint32_t)__builtin_bswap16(f.id) << 8);
+                hn = 3;
+            } else { /* map key, j2t_map_key native/thrift.c:422-447: parsed even when
+                      * the value turns out null (a bad key errors first) */
+                if (!isnull) atomicAdd(&L.crec[ci].count, 1u);
+                cs = pos + 1;
+                cn = te - cs;
+                tt = ldrec(&D.T[ldrec(&D.T[pt]).key]).ttype;
+                esc = has_bslash(src, cs, cn);
+                if (esc) bad = true;
+                if (tt == DG_T_STRING) {
+                    hv = __builtin_bswap32((uint32_t)cn);
+                    hn = 4;
+                } else {
+                    ns = cs;
+                    nn = cn;
+                    whole = false; /* trailing key text is ignored */
+                    cn = 0;
+                }
+            }
+        } else if (alive && !skip && isval) {
+            const dg_type vt = ldrec(&D.T[ty]);
+            tt = vt.ttype;
+            const bool inlist = t != 0 && (L.crec[ci].flags & CF_LIST);
+            if (kind == K_SCALAR) {
+                ns = pos;
+                nn = te - pos;
+            } else if (kind == K_STRING) {
+                cs = pos + 1;
+                cn = te - cs;
+                if (tt != DG_T_STRING) bad = true;
+                isbin = (flag & DG_F_NO_BASE64) == 0 && (vt.flags & DG_TF_BINARY);
+                if (!isbin) esc = has_bslash(src, cs, cn);
+                hn = 4;
+            } else if (kind == K_LBRACE) {
+                if (L.crec[lane].flags & CF_MAP) {
+                    hv = ldrec(&D.T[vt.key]).ttype | ((uint32_t)ldrec(&D.T[vt.elem]).ttype << 8);
+                    hn = 2;
+                    ln = 4; /* + size, written by the '}' */
+                }
+            } else { /* K_LBRACK */
+                hv = ldrec(&D.T[vt.elem]).ttype;
+                hn = 1;
+                ln = 4;
+            }
+            if (inlist) {
+                /* a null element is not counted; checked on the text here */
+                if (!(kind == K_SCALAR && src.at(pos) == 'n')) atomicAdd(&L.crec[ci].count, 1u);
+            }
+        } else if (alive && skip && kind == K_SCALAR) {
+            ns = pos; /* skip_one validates skipped scalars (native/scanning.c:1134-1330) */
+            nn = te - pos;
+        }
+        /* scalars: literals inline, numbers through the one parser */
+        if (ns >= 0) {
+            const uint8_t c0 = src.at(ns);
+            if (whole && (c0 == 'n' || c0 == 't' || c0 == 'f')) {
+                const uint32_t w4 = (uint32_t)src.get8(ns + (c0 == 'f'));
+                const uint32_t want = c0 == 'n' ? VS_NULL : c0 == 't' ? VS_TRUE : VS_ALSE;
+                if (nn != 4 + (c0 == 'f') || w4 != want) bad = true;
+                if (c0 == 'n') {
+                    isnull = true;
+                } else if (!skip) {
+                    if (tt != DG_T_BOOL) bad = true;
+                    hv = c0 == 't';
+                    hn = 1;
+                }
+            } else {
+                S ks = src.sub(ns, nn);
+                int64_t q = 0;
+                if (!fast_vnumber(ks, q, tb, iv, dv, isint)) slow = true;
+                else if (whole && q != nn) bad = true;
+                if (!skip && !num_size(tt)) bad = true;
+            }
+        }
+        /* numbers the fast parser declines (errors, big-decimal cases): the
+         * reference's vnumber (native/scanning.c:958-1083, atof_native
+         * native/atof_native.c:418-424), one lane at a time with the wave's
+         * 800-byte digit buffer */
+        for (uint64_t sm = ballot(slow && !bad); sm; sm &= sm - 1) {
+            if (lane == (uint32_t)__builtin_ctzll(sm)) {
+                JState js;
+                int64_t q = 0;
+                vnumber_slow(src.sub(ns, nn), q, js, dbuf);
+                if (js.vt < 0 || (whole && q != nn)) {
+                    bad = true;
+                } else {
+                    isint = js.vt == V_INTEGER;
+                    iv = js.iv;
+                    dv = js.dv;
+                }
+            }
+        }
+        /* strings: length of the body */
+        if (alive && !skip && !isnull && hn == 4 && isval) {
+            if (isbin) {
+                int64_t bl = b64_len(src, cs, cn);
+                if (bl < 0) bad = true;
+                ln = (uint32_t)bl;
+            } else if (esc) {
+                WOut co;
+                co.init_dry();
+                if (!fast_unquote(src, cs, cn, co)) bad = true;
+                ln = (uint32_t)co.len;
+            } else {
+                ln = (uint32_t)cn;
+            }
+            hv = __builtin_bswap32(ln);
+        }
+        if (keyish && hn == 4) ln = (uint32_t)cn; /* string map key body */
+        if (isnull) {
+            hn = 0;
+            ln = 0;
+        }
+        if (!isnull && ns >= 0 && !skip && hn == 0) ln = num_size(tt);
+        WP(4);
+        /* part B: closing brackets, once every atomic of the page is in */
+        uint64_t reqs = 0;
+        dg_struct csd;
+        if (alive && cl) {
+            const uint32_t pf = L.crec[ci].flags;
+            if (!(pf & CF_SKIP) && (pf & CF_STRUCT)) {
+                csd = ldrec(&D.S[ldrec(&D.T[L.crec[ci].type]).st]);
+                reqs = (D.R[csd.req_begin] & ~L.crec[ci].seen) | L.crec[ci].nulldr;
+                if (reqs) {
+                    WOut co;
+                    co.init_dry();
+                    if (!unset_fields(D, csd, reqs, flag, co)) bad = true;
+                    ln = (uint32_t)co.len;
+                }
+                hv = 0; /* STOP after the unset fields */
+                hn = 1;
+            }
+        }
+        if (ballot(bad)) return false;
+        ln += hn;
+
+        WP(5);
+        /* output offsets */
+        const uint32_t incl = wave_incl_sum(ln, lane);
+        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        const uint64_t opos = O + incl - ln;
+        if (O + tot > cap) return false; /* slot overflow: the exact machine reports it */
+        if (alive && op) L.crec[lane].outpos = (uint32_t)opos;
+
+        /* emit: header, then the body, through one writer per lane */
+        bool deferred = false;
+        {
+            WOut w;
+            w.init(ob + opos);
+            const bool live = alive && !skip && !isnull;
+            if (live && cl && hn == 1 && reqs) unset_fields(D, csd, reqs, flag, w); /* before the STOP */
+            if (live && hn) w.wle(hv, hn);
+            if (live && ns >= 0 && hn == 0) emit_number(w, tt, isint, iv, dv);
+            if (live && cn > (int64_t)WV_LONG && isval && (isbin || !esc)) deferred = true; /* whole wave, below */
+            else if (live && isbin) {
+                if (!b64_decode_wave(src, cs, cn, w)) bad = true;
+            } else if (live && esc && isval) {
+                fast_unquote(src, cs, cn, w);
+            } else if (live && cn > 0) {
+                fast_copy(src, cs, cn, w);
+            }
+            w.finish();
+            if (live && !op && !deferred && w.len != ln) bad = true;
+        }
+        if (alive && cl) {
+            const uint32_t pf = L.crec[ci].flags;
+            if (!(pf & CF_SKIP) && !(pf & CF_STRUCT))
+                put_be32(ob + L.crec[ci].outpos + ((pf & CF_MAP) ? 2 : 1), L.crec[ci].count);
+        }
+        WP(6);
+        /* long strings: one at a time, by all 64 lanes */
+        for (uint64_t dm = ballot(deferred); dm; dm &= dm - 1) {
+            const int l = (int)__builtin_ctzll(dm);
+            const int64_t s0 = (int64_t)__builtin_amdgcn_readlane((int)pos, l) + 1;
+            const int64_t nb = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)te, l) - s0;
+            const uint64_t d0 = (((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(opos >> 32), l)) << 32) |
+                                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)opos, l);
+            const uint32_t want = (uint32_t)__builtin_amdgcn_readlane((int)ln, l) - 4;
+            gu8 *dst = ob + d0 + 4;
+            if (__builtin_amdgcn_readlane((int)isbin, l)) {
+                if (!coop_b64(src, s0, nb, dst, want, lane)) bad = true;
+            } else {
+                coop_copy(src, s0, nb, dst, lane);
+            }
+        }
+        if (ballot(bad)) return false;
+        O += tot;
+
+        WP(7);
+        /* carry the last opener of every level into the level stack */
+        {
+            uint32_t have = uni(wave_or(alive && op ? 1u << level : 0u));
+            for (; have; have &= have - 1) {
+                int32_t Lv = __builtin_ctz(have);
+                uint64_t mo = ballot(alive && op && level == Lv);
+                uint32_t last = msb(mo);
+                if (lane < 8) {
+                    const __attribute__((address_space(3))) uint32_t *s =
+                        (const __attribute__((address_space(3))) uint32_t *)&L.crec[last];
+                    __attribute__((address_space(3))) uint32_t *d =
+                        (__attribute__((address_space(3))) uint32_t *)&L.crec[64 + Lv];
+                    d[lane] = s[lane];
+                }
+            }
+        }
+        WP(8);
+        depth = __builtin_amdgcn_readlane(dafter, (int)np - 1);
+        consumed += np;
+        if (bend) {
+            rootdone = true;
+            break;
+        }
+    }
+    WP_FLUSH();
+    if (!rootdone) return false;
+    if (lane == 0) {
+        P.ret[m] = 0;
+        P.out_len[m] = (uint32_t)O;
+    }
+    return true;
+}
+
+/* one message: staged in the wave's LDS buffer when it fits, else read from
+ * global memory through the same code */
+template <class DV, class LW>
+DGI bool wave_convert(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L,
+                      __attribute__((address_space(3))) uint64_t *mbuf,
+                      const __attribute__((address_space(3))) uint8_t *cls, const FastTabs &tb, uint32_t lane, gu8 *dbuf)
+{
+    uint64_t a = P.in_off[m], b = P.in_off[m + 1];
+    int64_t len = (int64_t)(b - a);
+    if (len <= 0 || len > (int64_t)WV_POSMASK) return false;
+    const dg_type rt = ldrec(&D.T[P.root]);
+    if (rt.ttype != DG_T_STRUCT && rt.ttype != DG_T_MAP && rt.ttype != DG_T_LIST && rt.ttype != DG_T_SET) return false;
+    const int64_t head = (int64_t)(a & 7);
+    const uint64_t words = (uint64_t)(len + head + 7) >> 3;
+    /* one instantiation for both cases (I-cache): generic (flat) pointers */
+    const uint64_t *base;
+    if (words + 2 <= WV_MSG / 8) {
+        const glb_u64 *g = (const glb_u64 *)(const void *)(P.json + (a & ~7ull));
+        for (uint64_t k = lane; k < words; k += 64) mbuf[k] = g[k];
+        if (lane < 2) mbuf[words + lane] = 0;
+        base = (const uint64_t *)(void *)mbuf;
+    } else {
+        base = (const uint64_t *)(const void *)(P.json + (a & ~7ull));
+    }
+    SrcT<const uint64_t> s;
+    s.init(base, head, len);
+    return wave_run(P, D, D_nf, m, L, s, (const uint32_t *)base, head, len, cls, tb, lane, dbuf);
+}
+
+/* Persistent grid, one wavefront per message at a time. The messages are
+ * the lane kernel's large ones (W.list) or, without a list, all of them.
+ * The descriptor is copied to LDS once per block; messages that fit are
+ * staged in the wave's LDS buffer. Bailed messages are listed for the exact
+ * machine (j2t_lane_kernel in list mode). */
+template <int V> /* instantiated in j2t_kern_wave.hip only */
+__global__ __launch_bounds__(64 * WV_WAVES) void j2t_wave_kernel(Params P, WaveParams W)
+{
+    __shared__ __attribute__((aligned(16))) WaveLds wl[WV_WAVES];
+    __shared__ __attribute__((aligned(16))) uint64_t s_msg[WV_WAVES][WV_MSG / 8];
+    __shared__ __attribute__((aligned(16))) uint64_t s_desc[WV_DESC / 8];
+    __shared__ uint8_t s_cls[256];
+    __shared__ uint64_t s_p10u[20];
+    __shared__ double s_p10d[23];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t total = W.list ? (uint64_t)__hip_atomic_load((uint32_t *)W.list_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                  : P.n;
+    if ((uint64_t)blockIdx.x * WV_WAVES >= total) return;
+    {
+        const uint4 *g = (const uint4 *)W.blob;
+        uint4 *l = (uint4 *)s_desc;
+        for (uint32_t k = tid; k < (W.hdr.total_len + 15) / 16; k += 64 * WV_WAVES) l[k] = g[k];
+    }
+    {
+        uint32_t c = tid;
+        uint8_t k = 0;
+        switch (c) {
+        case '{': k = C_STRUCT | K_LBRACE; break;
+        case '}': k = C_STRUCT | K_RBRACE; break;
+        case '[': k = C_STRUCT | K_LBRACK; break;
+        case ']': k = C_STRUCT | K_RBRACK; break;
+        case ':': k = C_STRUCT | K_COLON; break;
+        case ',': k = C_STRUCT | K_COMMA; break;
+        case ' ': case '\t': case '\n': case '\r': k = C_WS; break;
+        case '"': k = C_QUOTE; break;
+        case '\\': k = C_BS; break;
+        }
+        if (c < 256) s_cls[c] = k;
+    }
+    if (tid < 20) {
+        uint64_t v = 1;
+        for (uint32_t k = 0; k < tid; k++) v *= 10;
+        s_p10u[tid] = v;
+    }
+    if (tid < 23) s_p10d[tid] = P10[tid];
+    __syncthreads();
+    const uint32_t wave = tid >> 6, lane = tid & 63;
+    const auto dv = desc_view<3>((const __attribute__((address_space(3))) uint8_t *)(void *)s_desc, W.hdr);
+    FastTabs tb{(const __attribute__((address_space(3))) uint64_t *)(void *)s_p10u, (lds_f64 *)(void *)s_p10d};
+    const __attribute__((address_space(3))) uint8_t *cls = (const __attribute__((address_space(3))) uint8_t *)(void *)s_cls;
+    __attribute__((address_space(3))) uint64_t *mbuf = (__attribute__((address_space(3))) uint64_t *)(void *)s_msg[wave];
+    gu8 *dbuf = (gu8 *)(void *)(W.ws + ((uint64_t)blockIdx.x * WV_WAVES + wave) * DCAP);
+    for (uint64_t k = (uint64_t)blockIdx.x * WV_WAVES + wave; k < total; k += (uint64_t)gridDim.x * WV_WAVES) {
+        const uint64_t m = W.list ? (uint64_t)W.list[k] : k;
+        bool ok = wave_convert(P, dv, W.hdr.n_fields, m, wl[wave], mbuf, cls, tb, lane, dbuf);
+        if (!ok && lane == 0) {
+            uint32_t q = atomicAdd(W.bail_count, 1u);
+            W.bail_list[q] = (uint32_t)m;
+        }
+    }
+}
+
+void launch_wave_kernel(dim3 grid, hipStream_t s, const Params &P, const WaveParams &W);
+
+}  // namespace dg

@@ -53,6 +53,7 @@ extern "C" {
 #define DG_F_NO_WRITE_BASE (1ull << 9)
 #define DG_F_VALIDATE_UTF8 (1ull << 16) /* extension: reject invalid UTF-8 in strings */
 #define DG_F_NO_FAST_PATH (1ull << 17)  /* extension: run every message on the exact machine (testing) */
+#define DG_F_NO_WAVE_PATH (1ull << 18)  /* extension: skip the wave-per-message kernel, lane kernel only (testing) */
 
 /* library-internal per-message statuses (code byte values the reference never
  * produces). The host entry points resolve them before returning; the device
@@ -83,6 +84,10 @@ void *dg_ctx_stream(dg_ctx *ctx);
  * summed over this context's launches since the last reset. Synchronizes the
  * device. */
 int dg_ctx_stats(dg_ctx *ctx, uint64_t *bails, uint64_t *deeps, int reset);
+
+/* Diagnostics: the context's n (<= 16) raw device counters: [0] bails, [1]
+ * deep redos, [2..11] wave-kernel phase cycles in a -DDG_WPROF build. */
+int dg_ctx_counters(dg_ctx *ctx, uint64_t *out, int n, int reset);
 
 /* Upload a dg_desc blob (v1 or v2) (include/dgj2t_desc.h) to the context's device.
  * Replaces reading the Go *thrift.TypeDescriptor graph in place

@@ -18,6 +18,7 @@ def _checker():
 
 
 NO_FAST = 1 << 17  # DG_F_NO_FAST_PATH: every message on the exact machine
+NO_WAVE = 1 << 18  # DG_F_NO_WAVE_PATH: lane kernel (lane fast path + exact machine) only
 
 
 def _run_rows(rows, flats, extra=0):
@@ -56,9 +57,13 @@ def _raw_batch(flat, msgs, flags):
     return [out[int(oo[i]):int(oo[i + 1])].tobytes() for i in range(n)], rets
 
 
-@pytest.mark.parametrize("extra", [0, NO_FAST], ids=["fast+exact", "exact-only"])
-def test_golden_vectors(golden, extra):
+@pytest.mark.parametrize("extra", [0, NO_WAVE, NO_FAST, "wave-all"],
+                         ids=["hybrid", "lane-fast+exact", "exact-only", "wave-all"])
+def test_golden_vectors(golden, extra, monkeypatch):
     rows, flats = golden
+    if extra == "wave-all":
+        monkeypatch.setenv("DG_WAVE_MIN", "0")
+        extra = 0
     bad = _run_rows(rows, flats, extra)
     assert not bad, bad[:8]
 
@@ -75,7 +80,8 @@ def test_fuzz_vs_oracle(which):
     fl = T.flatten(td)
     chk = _checker()
     rng = random.Random(hash(which) & 0xffff)
-    for flags in (0x1, 0x0, 0x11, 0x5, 0x23, 0x83, 0x41, 0x100, 0x201, NO_FAST | 0x1, NO_FAST | 0x83):
+    for flags in (0x1, 0x0, 0x11, 0x5, 0x23, 0x83, 0x41, 0x100, 0x201, NO_FAST | 0x1, NO_FAST | 0x83,
+                  NO_WAVE | 0x1, NO_WAVE | 0x83):
         msgs = [fuzz.gen_message(rng, td, mutate_p=rng.random() < 0.5) for _ in range(300)]
         outs, rets = _raw_batch(fl, msgs, flags)
         for m, o, r in zip(msgs, outs, rets):
