@@ -7,7 +7,7 @@ converts its own batch of the configured workload (weak scaling; messages are
 independent, no data-path collective); the flattened descriptor is broadcast
 once from rank 0 over RCCL.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c1]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5|c1]
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 
 Prints ONE JSON line (rank 0). `value` = total JSON bytes converted by all
@@ -38,6 +38,7 @@ CONFIGS = {
     "c3": ("C3: 65536 nested NestingI64 messages (list<string> + map<i64,Simple>), seed 43", 65536),
     "c4": ("C4: 4096 large messages (48 KiB base64 binary + 1024 doubles), seed 44", 4096),
     "c1": ("C1: the reference's Simple payload x 65536 (236 B each)", 65536),
+    "c5": ("C5: mixed 90% flat / 9.5% nested / 0.5% large, 131072 per GPU (1M over 8), seed 45", 131072),
 }
 
 
@@ -50,6 +51,8 @@ def make_batch(cfg: str, rank: int):
         return W.large_desc(), W.gen_large_batch(random.Random(44 + 1000 * rank), CONFIGS[cfg][1])
     if cfg == "c1":
         return W.simple_desc(), [W.c1_simple_json()] * CONFIGS[cfg][1]
+    if cfg == "c5":
+        return W.mixed_desc(), W.gen_mixed_batch(random.Random(45 + 1000 * rank), CONFIGS[cfg][1])
     raise ValueError(cfg)
 
 
@@ -85,6 +88,78 @@ def cpu_baseline(flat, arena, off, flags, budget_s: float = 12.0):
                       f"{cores} threads of '{model}' (nproc={os.cpu_count()})"}
 
 
+def e2e_host_path(L, ctx, dh, root, flags, arena, off, dev, chunks: int = 8, reps: int = 5):
+    """End-to-end from host memory (HTTP bodies in) to host memory (Thrift out):
+    pinned H2D of each chunk's JSON + offsets, conversion, device-side packing
+    of the outputs (dg_pack_device), D2H of the packed bytes + out_len + ret.
+    Chunks alternate between two streams so copies overlap conversion.
+    Returns GB/s of JSON in (best of reps) and the serial breakdown."""
+    n = len(off) - 1
+    bounds = np.linspace(0, n, chunks + 1).astype(np.int64)
+    C = []
+    for c in range(chunks):
+        a, b = int(bounds[c]), int(bounds[c + 1])
+        lo, hi = int(off[a]), int(off[b])
+        o = (off[a:b + 1] - off[a]).astype(np.int64)
+        lens = np.diff(o)
+        slots = np.zeros(b - a + 1, dtype=np.int64)
+        np.cumsum((lens * 4 + 64 + 7) & ~7, out=slots[1:])
+        h_json = torch.from_numpy(np.concatenate([arena[lo:hi], np.zeros(64, np.uint8)])).pin_memory()
+        h_in = torch.from_numpy(o).pin_memory()
+        C.append(dict(n=b - a, h_json=h_json, h_in=h_in,
+                      d_json=torch.empty_like(h_json, device=dev), d_in=torch.empty_like(h_in, device=dev),
+                      d_out=torch.empty(int(slots[-1]) + 64, dtype=torch.uint8, device=dev),
+                      d_oo=torch.from_numpy(slots).to(dev), d_ol=torch.zeros(b - a, dtype=torch.int32, device=dev),
+                      d_ret=torch.zeros(b - a, dtype=torch.int64, device=dev),
+                      d_doff=torch.zeros(b - a + 1, dtype=torch.int64, device=dev),
+                      d_pack=torch.empty(int(slots[-1]) + 64, dtype=torch.uint8, device=dev),
+                      h_ol=torch.empty(b - a, dtype=torch.int32).pin_memory(),
+                      h_ret=torch.empty(b - a, dtype=torch.int64).pin_memory()))
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+
+    def run(sizes):
+        for k, c in enumerate(C):
+            st = streams[k % 2]
+            with torch.cuda.stream(st):
+                c["d_json"].copy_(c["h_json"], non_blocking=True)
+                c["d_in"].copy_(c["h_in"], non_blocking=True)
+                _lib.check(L.dg_j2t_batch_device(ctx.h, dh, root, c["d_json"].data_ptr(), c["d_in"].data_ptr(), c["n"],
+                                                 flags, c["d_out"].data_ptr(), c["d_oo"].data_ptr(), c["d_ol"].data_ptr(),
+                                                 c["d_ret"].data_ptr(), None, st.cuda_stream))
+                torch.cumsum(c["d_ol"], 0, dtype=torch.int64, out=c["d_doff"][1:])
+                _lib.check(L.dg_pack_device(ctx.h, c["d_out"].data_ptr(), c["d_oo"].data_ptr(), c["d_ol"].data_ptr(),
+                                            c["n"], c["d_pack"].data_ptr(), c["d_doff"].data_ptr(), st.cuda_stream))
+                c["h_ol"].copy_(c["d_ol"], non_blocking=True)
+                c["h_ret"].copy_(c["d_ret"], non_blocking=True)
+                if sizes is not None:
+                    c["h_pack"][:sizes[k]].copy_(c["d_pack"][:sizes[k]], non_blocking=True)
+        for st in streams:
+            st.synchronize()
+
+    run(None)  # warm-up: learn each chunk's packed size (deterministic)
+    sizes = [int(c["h_ol"].to(torch.int64).sum()) for c in C]
+    for c, sz in zip(C, sizes):
+        c["h_pack"] = torch.empty(max(sz, 1), dtype=torch.uint8).pin_memory()
+    best = None
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run(sizes)
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    # what came back is what the kernel wrote: packed bytes == the slots' used prefixes
+    c = C[0]
+    slots_h, oo_h, ol_h = c["d_out"].cpu().numpy(), c["d_oo"].cpu().numpy(), c["h_ol"].numpy()
+    want = b"".join(slots_h[int(oo_h[i]):int(oo_h[i]) + int(ol_h[i])].tobytes() for i in range(c["n"]))
+    if c["h_pack"][:sizes[0]].numpy().tobytes() != want[:sizes[0]]:
+        raise RuntimeError("e2e: packed output differs from the device slots")
+    json_bytes = int(off[-1] - off[0])
+    return {"value": round(json_bytes / best / 1e9, 3), "unit": "GB/s", "ms": round(best * 1e3, 3),
+            "thrift_bytes": sum(sizes), "chunks": chunks, "streams": 2,
+            "method": "pinned H2D (JSON+offsets) -> convert -> dg_pack_device -> D2H (packed Thrift + out_len + ret), "
+                      "chunks alternating over 2 streams, wall clock, best of %d" % reps}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -92,6 +167,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory end-to-end measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -124,6 +200,7 @@ def main():
     arena, off = W.arena(msgs)
     n = len(msgs)
     lens = np.diff(off).astype(np.int64)
+    max_len = int(lens.max())  # known to the host that built the arena (dg_j2t_batch_device_ml)
     slots = np.zeros(n + 1, dtype=np.int64)
     np.cumsum((lens * 4 + 64 + 7) & ~7, out=slots[1:])  # dg_slot_bound: 8-aligned slots
     d_json = torch.from_numpy(arena).to(dev)
@@ -138,9 +215,9 @@ def main():
     torch.cuda.set_stream(stream)
 
     def step():
-        _lib.check(L.dg_j2t_batch_device(ctx.h, dh, flat.root_type, d_json.data_ptr(), d_in.data_ptr(), n, flags,
+        _lib.check(L.dg_j2t_batch_device_ml(ctx.h, dh, flat.root_type, d_json.data_ptr(), d_in.data_ptr(), n, flags,
                                          d_out.data_ptr(), d_oo.data_ptr(), d_ol.data_ptr(), d_ret.data_ptr(),
-                                         d_pend.data_ptr(), stream.cuda_stream))
+                                         d_pend.data_ptr(), stream.cuda_stream, max_len))
 
     ctx.stats(reset=True)
     for _ in range(args.warmup):
@@ -185,6 +262,9 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(flat, arena, off, flags)
+    e2e = None
+    if rank == 0 and not args.no_e2e:
+        e2e = e2e_host_path(L, ctx, dh, flat.root_type, flags, arena, off, dev)
 
     traffic = None
     tp = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
@@ -208,6 +288,7 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "kernel_ms": round(gpu_ms, 5), "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
+            "e2e_host": e2e,
         }
         print(json.dumps(line), flush=True)
     if dist:

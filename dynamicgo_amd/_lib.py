@@ -15,7 +15,8 @@ LIB_PATH = os.environ.get("DG_LIB_PATH") or os.path.join(HERE, "libdgj2t.so")
 EXPORTS = ["dg_last_error", "dg_ctx_create", "dg_ctx_destroy", "dg_ctx_stream", "dg_ctx_stats", "dg_ctx_counters",
            "dg_desc_create",
            "dg_desc_create_device", "dg_desc_destroy", "dg_desc_root", "dg_j2t_batch_device",
-           "dg_slot_bound", "dg_j2t_batch_host", "dg_j2t_do", "dg_bench_device"]
+           "dg_j2t_batch_device_ml",
+           "dg_slot_bound", "dg_j2t_batch_host", "dg_j2t_do", "dg_pack_device", "dg_bench_device"]
 
 _lib = None
 
@@ -53,9 +54,11 @@ def lib() -> C.CDLL:
         "dg_desc_destroy": (None, [vp]),
         "dg_desc_root": (u32, [vp]),
         "dg_j2t_batch_device": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, vp, vp, vp, vp, vp]),
+        "dg_j2t_batch_device_ml": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, vp, vp, vp, vp, vp, u64]),
         "dg_slot_bound": (u64, [u64]),
         "dg_j2t_batch_host": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, u64, vp, vp, P64]),
         "dg_j2t_do": (i32, [vp, vp, u32, C.c_char_p, sz, u64, vp, sz, C.POINTER(sz), P64]),
+        "dg_pack_device": (i32, [vp, vp, vp, vp, u64, vp, vp, vp]),
         "dg_bench_device": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, vp, vp, vp, i32, C.POINTER(C.c_float)]),
     }
     for name, (res, args) in sig.items():

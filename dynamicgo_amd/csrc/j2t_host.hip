@@ -45,7 +45,7 @@ struct dg_ctx {
     uint8_t *ws_deep = nullptr;
     uint32_t *d_pending = nullptr;
     unsigned long long *d_stats = nullptr; /* {bails, deeps} since the last dg_ctx_stats reset */
-    uint32_t *d_bail_count = nullptr;      /* [0] wave kernel bails, [1] large messages (self-reset) */
+    uint32_t *d_bail_count = nullptr;      /* [0] wave kernel bails, [1] large messages, [2] wave queue (self-reset) */
     uint32_t *d_bail_list = nullptr;
     uint64_t bail_cap = 0;
     uint32_t *d_big_list = nullptr;
@@ -230,7 +230,7 @@ static int ensure_fast_ws(dg_ctx *c, uint64_t lanes)
 
 static int launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *json, const uint64_t *in_off,
                   uint64_t n, uint64_t flags, uint8_t *out, const uint64_t *out_off, uint32_t *out_len,
-                  uint64_t *ret, uint32_t *pending, hipStream_t s)
+                  uint64_t *ret, uint32_t *pending, hipStream_t s, uint64_t max_len = 0)
 {
     if (n == 0) return DG_OK;
     if (root >= d->hdr.n_types) return set_err(DG_E_INVALID, "root type %u out of range", root);
@@ -272,7 +272,10 @@ static int launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *jso
     DP.done = c->d_deep_count + 1;
     DP.blob = d->d_blob;
     DP.hdr = d->hdr;
-    const bool wave = P.fast && !no_wave && d->hdr.total_len <= WV_DESC && d->hdr.total_len <= DESC_LDS_BYTES;
+    const char *wm = getenv("DG_WAVE_MIN"); /* messages longer than this go to the wave kernel */
+    const uint64_t big_max = wm ? strtoull(wm, nullptr, 10) : (uint64_t)WV_MIN_DEFAULT;
+    const bool wave = P.fast && !no_wave && d->hdr.total_len <= WV_DESC && d->hdr.total_len <= DESC_LDS_BYTES &&
+                      (max_len == 0 || max_len > big_max);
     auto lane_launch = [&](dim3 g, const Params &Q) {
         if (d->hdr.total_len <= DESC_LDS_BYTES) launch_lane_kernel_lds(g, s, Q, DP);
         else launch_lane_kernel_glb(g, s, Q, DP);
@@ -286,8 +289,6 @@ static int launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *jso
          * 3. lane kernel in list mode: the wave kernel's bails, exact machine */
         if ((rc = grow(c->d_bail_list, c->bail_cap, n))) return rc;
         if ((rc = grow(c->d_big_list, c->big_cap, n))) return rc;
-        const char *wm = getenv("DG_WAVE_MIN"); /* messages longer than this go to the wave kernel */
-        const uint64_t big_max = wm ? strtoull(wm, nullptr, 10) : (uint64_t)WV_MIN_DEFAULT;
         Params P1 = P;
         P1.big_list = c->d_big_list;
         P1.big_count = c->d_bail_count + 1;
@@ -302,6 +303,7 @@ static int launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *jso
         W.list = c->d_big_list;
         W.list_count = c->d_bail_count + 1;
         W.ws = c->ws_wave;
+        W.queue = c->d_bail_count + 2;
         uint64_t wblocks = std::min<uint64_t>((n + WV_WAVES - 1) / WV_WAVES, (uint64_t)c->n_cu * WV_BLOCKS_PER_CU);
         launch_wave_kernel(dim3((uint32_t)wblocks), s, P, W);
         HIPCHK(hipGetLastError());
@@ -325,6 +327,17 @@ int dg_j2t_batch_device(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     return launch(c, d, root, d_json, d_in_off, n, flags, d_out, d_out_off, d_out_len, d_ret, d_pending, s);
+}
+
+int dg_j2t_batch_device_ml(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *d_json, const uint64_t *d_in_off,
+                           uint64_t n, uint64_t flags, uint8_t *d_out, const uint64_t *d_out_off, uint32_t *d_out_len,
+                           uint64_t *d_ret, uint32_t *d_pending, void *stream, uint64_t max_len)
+{
+    if (!c || !d) return set_err(DG_E_INVALID, "null ctx/desc");
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    return launch(c, d, root, d_json, d_in_off, n, flags, d_out, d_out_off, d_out_len, d_ret, d_pending, s, max_len);
 }
 
 int dg_j2t_batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *json, const uint64_t *in_off,
@@ -351,8 +364,10 @@ int dg_j2t_batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
     HIPCHK(hipMemsetAsync(c->d_json + bytes, 0, 64, s));
     HIPCHK(hipMemcpyAsync(c->d_in_off, ioff.data(), (n + 1) * 8, hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(c->d_out_off, soff.data(), (n + 1) * 8, hipMemcpyHostToDevice, s));
+    uint64_t max_len = 1;
+    for (uint64_t i = 0; i < n; i++) max_len = std::max<uint64_t>(max_len, ioff[i + 1] - ioff[i]);
     if ((rc = launch(c, d, root, c->d_json, c->d_in_off, n, flags, c->d_out, c->d_out_off, c->d_out_len, c->d_ret,
-                     nullptr, s)))
+                     nullptr, s, max_len)))
         return rc;
     std::vector<uint32_t> olen(n);
     HIPCHK(hipMemcpyAsync(ret, c->d_ret, n * 8, hipMemcpyDeviceToHost, s));
@@ -429,6 +444,19 @@ int dg_j2t_do(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *json, s
     int rc = dg_j2t_batch_host(c, d, root, len ? json : &empty, in_off, 1, flags, out, out_cap, oo, ret, &need);
     if (out_len) *out_len = need;
     return rc;
+}
+
+int dg_pack_device(dg_ctx *c, const uint8_t *d_out, const uint64_t *d_out_off, const uint32_t *d_out_len, uint64_t n,
+                   uint8_t *d_dst, const uint64_t *d_dst_off, void *stream)
+{
+    if (!c || (n && (!d_out || !d_out_off || !d_out_len || !d_dst || !d_dst_off))) return set_err(DG_E_INVALID, "bad args");
+    if (n == 0) return DG_OK;
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    uint64_t blocks = std::min<uint64_t>((n + 3) / 4, (uint64_t)c->n_cu * 8);
+    launch_pack_kernel(dim3((uint32_t)blocks), s, d_out, d_out_off, d_out_len, n, d_dst, d_dst_off);
+    HIPCHK(hipGetLastError());
+    return DG_OK;
 }
 
 int dg_bench_device(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *d_json, const uint64_t *d_in_off,

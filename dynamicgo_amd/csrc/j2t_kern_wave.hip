@@ -6,4 +6,9 @@ void launch_wave_kernel(dim3 grid, hipStream_t s, const Params &P, const WavePar
 {
     hipLaunchKernelGGL(j2t_wave_kernel<0>, grid, dim3(64 * WV_WAVES), 0, s, P, W);
 }
+void launch_pack_kernel(dim3 grid, hipStream_t s, const uint8_t *out, const uint64_t *out_off, const uint32_t *out_len,
+                        uint64_t n, uint8_t *dst, const uint64_t *dst_off)
+{
+    hipLaunchKernelGGL(dg_pack_kernel<0>, grid, dim3(256), 0, s, out, out_off, out_len, n, dst, dst_off);
+}
 }  // namespace dg

@@ -52,7 +52,7 @@ struct Params {
     unsigned long long *stats; /* {messages bailed to the exact machine, messages redone deep} */
     const uint32_t *list;      /* list mode: convert only these messages (exact machine) */
     uint32_t *list_count;      /* device count of `list` (self-reset by the last block) */
-    uint32_t *reset2;          /* another counter the last block resets (list mode: the large-message count) */
+    uint32_t *reset2;          /* two more counters the last block resets (list mode: large-message count, wave queue) */
     uint32_t *big_list;        /* messages longer than big_max are left to the wave kernel via this list */
     uint32_t *big_count;
     uint64_t big_max;
@@ -837,7 +837,10 @@ DGI void deep_pass(const Params &P, const DV &dv, uint32_t *done, uint32_t nbloc
     __syncthreads();
     if (threadIdx.x == 0) { /* self-reset for the next launch on this context */
         if (P.list_count) __hip_atomic_store(P.list_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (P.reset2) __hip_atomic_store(P.reset2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (P.reset2) {
+            __hip_atomic_store(P.reset2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(P.reset2 + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         __hip_atomic_store(P.deep_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }

@@ -58,7 +58,8 @@ constexpr uint32_t WV_MSG = 4096;              /* messages up to this (minus 16)
 constexpr uint32_t WV_DESC = 16384;            /* the wave path needs the descriptor in LDS */
 constexpr uint32_t WV_LONG = 192;              /* strings longer than this are copied/decoded by the whole wave */
 constexpr uint32_t WV_BLOCKS_PER_CU = 2;       /* persistent grid: 2 blocks x 4 waves per CU */
-constexpr uint32_t WV_MIN_DEFAULT = 8192;      /* messages longer than this go to the wave kernel (DG_WAVE_MIN) */
+constexpr uint32_t WV_MIN_DEFAULT = 512; 
+constexpr uint32_t WV_REQMASKS = 64;           /* per-struct REQUIRED-field masks kept in LDS */      /* messages longer than this go to the wave kernel (DG_WAVE_MIN) */
 
 /* token kinds (3 bits, stored above the 29-bit position) */
 enum : uint32_t {
@@ -98,6 +99,7 @@ struct WaveParams {
     const uint32_t *list; /* in: the messages to convert (the lane kernel's large ones) */
     const uint32_t *list_count;
     uint8_t *ws;          /* DCAP bytes of big-decimal digits per wave of the grid */
+    uint32_t *queue;      /* next list entry to take (zero at launch; reset by the list-mode lane kernel) */
 };
 
 #ifdef DG_WPROF
@@ -141,26 +143,21 @@ DGI T uni(T v) /* wave-uniform value -> SGPR */
 typedef __attribute__((address_space(1))) uint32_t gu32;
 typedef __attribute__((address_space(1))) uint16_t gu16;
 
-/* store bytes [lo, hi) of the little-endian word v at the 8-aligned w */
+/* store bytes [lo, hi) of the little-endian word v at the 8-aligned w:
+ * at most 6 naturally aligned stores, straight-line (no divergent loop) */
 DGI void store_part(gu8 *w, uint64_t v, uint32_t lo, uint32_t hi)
 {
-    uint32_t i = lo;
-    while (i < hi) {
-        uint32_t r = hi - i;
-        if ((i & 7) == 0 && r >= 8) {
-            *(gu64 *)w = v;
-            i += 8;
-        } else if ((i & 3) == 0 && r >= 4) {
-            *(gu32 *)(w + i) = (uint32_t)(v >> (i * 8));
-            i += 4;
-        } else if ((i & 1) == 0 && r >= 2) {
-            *(gu16 *)(w + i) = (uint16_t)(v >> (i * 8));
-            i += 2;
-        } else {
-            w[i] = (uint8_t)(v >> (i * 8));
-            i += 1;
-        }
+    if (lo == 0 && hi == 8) {
+        *(gu64 *)w = v;
+        return;
     }
+    uint32_t i = lo;
+    if ((i & 1) && i < hi) { w[i] = (uint8_t)(v >> (i * 8)); i += 1; }
+    if ((i & 2) && i + 2 <= hi) { *(gu16 *)(w + i) = (uint16_t)(v >> (i * 8)); i += 2; }
+    if ((i & 4) && i + 4 <= hi) { *(gu32 *)(w + i) = (uint32_t)(v >> (i * 8)); i += 4; }
+    if (i + 4 <= hi) { *(gu32 *)(w + i) = (uint32_t)(v >> (i * 8)); i += 4; }
+    if (i + 2 <= hi) { *(gu16 *)(w + i) = (uint16_t)(v >> (i * 8)); i += 2; }
+    if (i < hi) w[i] = (uint8_t)(v >> (i * 8));
 }
 
 /* A writer that owns exactly [start, start + written): whole aligned words
@@ -366,10 +363,8 @@ DGI bool unset_fields(const DV &D, const dg_struct &sd, uint64_t bits, uint64_t 
 /* field lookup j2t_key (native/thrift.c:668-763) by the struct's name table:
  * global field index or -1 */
 template <class S, class DV>
-DGI int32_t wv_lookup(const DV &D, const dg_struct &sd, S &src, int64_t k0, uint32_t kn)
+DGI int32_t wv_lookup(const DV &D, const dg_struct &sd, S &src, int64_t k0, uint32_t kn, uint32_t h)
 {
-    uint32_t h = DG_NAME_HASH_SEED;
-    for (uint32_t j = 0; j < kn; j++) h = DG_NAME_HASH_STEP(h, src.raw(k0 + j));
     for (uint32_t s = h & sd.name_mask;; s = (s + 1) & sd.name_mask) {
         const dg_name nm = ldrec(&D.N[sd.name_begin + s]);
         if (nm.field == DG_NONE) return -1;
@@ -524,7 +519,7 @@ typedef const __attribute__((address_space(3))) uint32_t lds_u32;
 template <class S, class WP, class DV, class LW>
 DGI bool wave_run(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L, S src, WP wbase, int64_t head,
                   int64_t len, const __attribute__((address_space(3))) uint8_t *cls, const FastTabs &tb, uint32_t lane,
-                  gu8 *dbuf)
+                  gu8 *dbuf, const __attribute__((address_space(3))) uint64_t *reqmask)
 {
     const uint64_t flag = P.flag;
     uint64_t oa = P.out_off[m];
@@ -616,6 +611,20 @@ DGI bool wave_run(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L
         if (ballot(bad)) return false;
 
         WP(2);
+        /* key hashes, once (the rounds below only probe) */
+        uint32_t khash = DG_NAME_HASH_SEED;
+        bool kesc = false;
+        if (alive && keyish) {
+            const int64_t k0 = pos + 1, kl = te - k0;
+            kesc = has_bslash(src, k0, kl);
+            for (int64_t j = 0; j < kl; j += 8) {
+                uint64_t w = src.get8(k0 + j);
+                const int64_t r = kl - j < 8 ? kl - j : 8;
+#pragma unroll
+                for (int b = 0; b < 8; b++)
+                    if (b < r) khash = DG_NAME_HASH_STEP(khash, (uint8_t)(w >> (8 * b)));
+            }
+        }
         /* types, level by level: keys first (they need their struct), then
          * values (they need their key or container) */
         uint32_t ty = DG_NONE; /* value: type index; struct key: field index */
@@ -633,9 +642,7 @@ DGI bool wave_run(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L
                         rec = TR_SKIP;
                     } else if (pf & CF_STRUCT) {
                         const dg_struct sd = ldrec(&D.S[ldrec(&D.T[pt]).st]);
-                        int64_t k0 = pos + 1;
-                        uint32_t kn2 = (uint32_t)(te - k0);
-                        int32_t fi = has_bslash(src, k0, kn2) ? -2 : wv_lookup(D, sd, src, k0, kn2);
+                        int32_t fi = kesc ? -2 : wv_lookup(D, sd, src, pos + 1, (uint32_t)(te - pos - 1), khash);
                         if (fi == -2) {
                             bad = true; /* escaped key: exact machine */
                             rec = TR_SKIP;
@@ -856,6 +863,13 @@ DGI bool wave_run(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L
             if (!(pf & CF_SKIP) && (pf & CF_STRUCT)) {
                 csd = ldrec(&D.S[ldrec(&D.T[L.crec[ci].type]).st]);
                 reqs = (D.R[csd.req_begin] & ~L.crec[ci].seen) | L.crec[ci].nulldr;
+                const uint32_t sidx = ldrec(&D.T[L.crec[ci].type]).st;
+                if (!(flag & (DG_F_WRITE_REQUIRE | DG_F_WRITE_DEFAULT | DG_F_WRITE_OPTIONAL)) && sidx < WV_REQMASKS) {
+                    /* nothing is written for unset fields: only a missing
+                     * REQUIRED one matters (ERR_NULL_REQUIRED, native/thrift.c:286-290) */
+                    if (reqs & reqmask[sidx]) bad = true;
+                    reqs = 0;
+                }
                 if (reqs) {
                     WOut co;
                     co.init_dry();
@@ -960,7 +974,8 @@ DGI bool wave_run(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L
 template <class DV, class LW>
 DGI bool wave_convert(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L,
                       __attribute__((address_space(3))) uint64_t *mbuf,
-                      const __attribute__((address_space(3))) uint8_t *cls, const FastTabs &tb, uint32_t lane, gu8 *dbuf)
+                      const __attribute__((address_space(3))) uint8_t *cls, const FastTabs &tb, uint32_t lane, gu8 *dbuf,
+                      const __attribute__((address_space(3))) uint64_t *reqmask)
 {
     uint64_t a = P.in_off[m], b = P.in_off[m + 1];
     int64_t len = (int64_t)(b - a);
@@ -981,7 +996,7 @@ DGI bool wave_convert(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, L
     }
     SrcT<const uint64_t> s;
     s.init(base, head, len);
-    return wave_run(P, D, D_nf, m, L, s, (const uint32_t *)base, head, len, cls, tb, lane, dbuf);
+    return wave_run(P, D, D_nf, m, L, s, (const uint32_t *)base, head, len, cls, tb, lane, dbuf, reqmask);
 }
 
 /* Persistent grid, one wavefront per message at a time. The messages are
@@ -996,6 +1011,7 @@ __global__ __launch_bounds__(64 * WV_WAVES) void j2t_wave_kernel(Params P, WaveP
     __shared__ __attribute__((aligned(16))) uint64_t s_msg[WV_WAVES][WV_MSG / 8];
     __shared__ __attribute__((aligned(16))) uint64_t s_desc[WV_DESC / 8];
     __shared__ uint8_t s_cls[256];
+    __shared__ uint64_t s_reqmask[WV_REQMASKS];
     __shared__ uint64_t s_p10u[20];
     __shared__ double s_p10d[23];
     const uint32_t tid = threadIdx.x;
@@ -1030,15 +1046,34 @@ __global__ __launch_bounds__(64 * WV_WAVES) void j2t_wave_kernel(Params P, WaveP
     }
     if (tid < 23) s_p10d[tid] = P10[tid];
     __syncthreads();
-    const uint32_t wave = tid >> 6, lane = tid & 63;
     const auto dv = desc_view<3>((const __attribute__((address_space(3))) uint8_t *)(void *)s_desc, W.hdr);
+    if (tid < WV_REQMASKS && tid < W.hdr.n_structs) {
+        /* REQUIRED fields per struct (request-base fields are never written
+         * nor checked, native/thrift.c:270-272) */
+        const dg_struct sd = ldrec(&dv.S[tid]);
+        uint64_t mk = 0;
+        for (uint32_t k = 0; k < sd.n_fields && k < 64; k++) {
+            const dg_field f = ldrec(&dv.F[sd.field_begin + k]);
+            if (f.required == DG_REQ_REQUIRED && !(f.flags & DG_FF_REQUEST_BASE)) mk |= 1ull << k;
+        }
+        s_reqmask[tid] = mk;
+    }
+    __syncthreads();
+    const uint32_t wave = tid >> 6, lane = tid & 63;
     FastTabs tb{(const __attribute__((address_space(3))) uint64_t *)(void *)s_p10u, (lds_f64 *)(void *)s_p10d};
     const __attribute__((address_space(3))) uint8_t *cls = (const __attribute__((address_space(3))) uint8_t *)(void *)s_cls;
     __attribute__((address_space(3))) uint64_t *mbuf = (__attribute__((address_space(3))) uint64_t *)(void *)s_msg[wave];
     gu8 *dbuf = (gu8 *)(void *)(W.ws + ((uint64_t)blockIdx.x * WV_WAVES + wave) * DCAP);
-    for (uint64_t k = (uint64_t)blockIdx.x * WV_WAVES + wave; k < total; k += (uint64_t)gridDim.x * WV_WAVES) {
+    /* dynamic work queue: message sizes vary by 100x (C5), so waves take the
+     * next message when they finish one instead of a fixed stride */
+    for (;;) {
+        uint32_t kq = 0;
+        if (lane == 0) kq = __hip_atomic_fetch_add(W.queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t k = (uint32_t)__builtin_amdgcn_readfirstlane((int)kq);
+        if (k >= total) break;
         const uint64_t m = W.list ? (uint64_t)W.list[k] : k;
-        bool ok = wave_convert(P, dv, W.hdr.n_fields, m, wl[wave], mbuf, cls, tb, lane, dbuf);
+        bool ok = wave_convert(P, dv, W.hdr.n_fields, m, wl[wave], mbuf, cls, tb, lane, dbuf,
+                               (const __attribute__((address_space(3))) uint64_t *)(void *)s_reqmask);
         if (!ok && lane == 0) {
             uint32_t q = atomicAdd(W.bail_count, 1u);
             W.bail_list[q] = (uint32_t)m;
@@ -1046,6 +1081,27 @@ __global__ __launch_bounds__(64 * WV_WAVES) void j2t_wave_kernel(Params P, WaveP
     }
 }
 
+/* Output packing for the device->host copy: message i's out_len[i] bytes
+ * move from its slot (out + out_off[i], 8-aligned) to dst + dst_off[i]
+ * (dst_off = exclusive prefix sum of out_len), one wavefront per message,
+ * byte-exact at the shared edge words. */
+template <int V>
+__global__ __launch_bounds__(256) void dg_pack_kernel(const uint8_t *out, const uint64_t *out_off,
+                                                      const uint32_t *out_len, uint64_t n, uint8_t *dst,
+                                                      const uint64_t *dst_off)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < n; i += (uint64_t)gridDim.x * 4) {
+        const uint32_t nb = out_len[i];
+        if (!nb) continue;
+        SrcT<const uint64_t> s;
+        s.init((const uint64_t *)(const void *)(out + out_off[i]), 0, nb);
+        coop_copy(s, 0, nb, (gu8 *)(void *)(dst + dst_off[i]), lane);
+    }
+}
+
 void launch_wave_kernel(dim3 grid, hipStream_t s, const Params &P, const WaveParams &W);
+void launch_pack_kernel(dim3 grid, hipStream_t s, const uint8_t *out, const uint64_t *out_off, const uint32_t *out_len,
+                        uint64_t n, uint8_t *dst, const uint64_t *dst_off);
 
 }  // namespace dg

@@ -119,6 +119,15 @@ int dg_j2t_batch_device(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, co
                         const uint64_t *d_out_off, uint32_t *d_out_len, uint64_t *d_ret,
                         uint32_t *d_pending, void *stream);
 
+/* The same with the batch's longest message length (0 = unknown). The host
+ * that built the arena knows it for free; with it the library schedules only
+ * the kernels the batch needs (all messages short: the lane kernel alone,
+ * no wave-kernel / exact-list launches). */
+int dg_j2t_batch_device_ml(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, const uint8_t *d_json,
+                           const uint64_t *d_in_off, uint64_t n, uint64_t flags, uint8_t *d_out,
+                           const uint64_t *d_out_off, uint32_t *d_out_len, uint64_t *d_ret,
+                           uint32_t *d_pending, void *stream, uint64_t max_len);
+
 /* Output-slot size the device path uses by default for a message of len bytes. */
 uint64_t dg_slot_bound(uint64_t len);
 
@@ -141,6 +150,15 @@ int dg_j2t_do(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, const uint8_
 /* Timing helper for benchmarks: launch the device batch `iters` times on the
  * context stream bracketed by HIP events; returns total milliseconds of GPU
  * time in *ms (events are recorded on the stream the kernels run on). */
+/* Pack the converted messages for the device->host copy: message i's
+ * d_out_len[i] bytes move from its slot (d_out + d_out_off[i]) to
+ * d_dst + d_dst_off[i], where d_dst_off is the exclusive prefix sum of
+ * d_out_len (caller-computed, e.g. one scan kernel). Stream-ordered; errored
+ * messages have out_len 0. The Go side then hands (dst, dst_off) to the NIC
+ * path without per-message copies. */
+int dg_pack_device(dg_ctx *ctx, const uint8_t *d_out, const uint64_t *d_out_off, const uint32_t *d_out_len, uint64_t n,
+                   uint8_t *d_dst, const uint64_t *d_dst_off, void *stream);
+
 int dg_bench_device(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, const uint8_t *d_json,
                     const uint64_t *d_in_off, uint64_t n, uint64_t flags, uint8_t *d_out,
                     const uint64_t *d_out_off, uint32_t *d_out_len, uint64_t *d_ret, int iters,
