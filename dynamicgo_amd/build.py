@@ -22,8 +22,8 @@ def _run(cmd, cwd=None):
     subprocess.run(cmd, cwd=cwd, check=True)
 
 
-UNITS = ("j2t_kern_wave.hip", "j2t_kern_lds.hip", "j2t_kern_glb.hip", "j2t_host.hip")
-HEADERS = ("j2t_wave.h", "j2t_machine.h", "j2t_device.h", "j2t_fast.h", "dg_tables.h")
+UNITS = ("j2t_kern_wave.hip", "j2t_kern_small.hip", "j2t_kern_lds.hip", "j2t_kern_glb.hip", "j2t_host.hip")
+HEADERS = ("j2t_small.h", "j2t_wave.h", "j2t_machine.h", "j2t_device.h", "j2t_fast.h", "dg_tables.h")
 
 
 def build_hip(force=False, extra_flags=(), out=None):

@@ -13,7 +13,7 @@
 #include <mutex>
 #include <vector>
 
-#include "j2t_wave.h"
+#include "j2t_small.h"
 
 /* ========================================================================== */
 /* host side: C ABI                                                            */
@@ -280,7 +280,52 @@ static int launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *jso
         if (d->hdr.total_len <= DESC_LDS_BYTES) launch_lane_kernel_lds(g, s, Q, DP);
         else launch_lane_kernel_glb(g, s, Q, DP);
     };
-    if (!wave) {
+    const char *sm_env = getenv("DG_SMALL_MPW"); /* 0: lane kernel (in-kernel exact machine) */
+    const int mpw = sm_env ? atoi(sm_env) : 64;
+    const bool small = P.fast && !no_wave && mpw > 0 && d->hdr.total_len <= SM_DESC;
+    if (small) {
+        /* 1. small kernel: lane-per-message fast path; declines -> bail list,
+         *    messages longer than big_max -> big list (when the batch has any)
+         * 2. wave kernel over the big list
+         * 3. lane kernel in list mode: the exact machine on the bail list */
+        if ((rc = grow(c->d_bail_list, c->bail_cap, n))) return rc;
+        if ((rc = grow(c->d_big_list, c->big_cap, n))) return rc;
+        const bool need_wave = max_len == 0 || max_len > big_max;
+        Params P1 = P;
+        if (need_wave) {
+            P1.big_list = c->d_big_list;
+            P1.big_count = c->d_bail_count + 1;
+            P1.big_max = big_max;
+        }
+        SmallParams S;
+        S.blob = d->d_blob;
+        S.hdr = d->hdr;
+        S.bail_count = c->d_bail_count;
+        S.bail_list = c->d_bail_list;
+        const uint64_t mpb = (uint64_t)SM_WAVES * (uint64_t)(mpw == 64 ? 64 : mpw == 16 ? 16 : 32);
+        launch_small_kernel(mpw, dim3((uint32_t)((n + mpb - 1) / mpb)), s, P1, S);
+        HIPCHK(hipGetLastError());
+        if (need_wave) {
+            WaveParams W;
+            W.blob = d->d_blob;
+            W.hdr = d->hdr;
+            W.bail_count = c->d_bail_count;
+            W.bail_list = c->d_bail_list;
+            W.list = c->d_big_list;
+            W.list_count = c->d_bail_count + 1;
+            W.ws = c->ws_wave;
+            W.queue = c->d_bail_count + 2;
+            uint64_t wblocks = std::min<uint64_t>((n + WV_WAVES - 1) / WV_WAVES, (uint64_t)c->n_cu * WV_BLOCKS_PER_CU);
+            launch_wave_kernel(dim3((uint32_t)wblocks), s, P, W);
+            HIPCHK(hipGetLastError());
+        }
+        Params P3 = P;
+        P3.list = c->d_bail_list;
+        P3.list_count = c->d_bail_count;
+        P3.reset2 = c->d_bail_count + 1;
+        P3.fast = 0;
+        lane_launch(dim3((uint32_t)std::min<uint64_t>(blocks, 16)), P3);
+    } else if (!wave) {
         lane_launch(dim3((uint32_t)blocks), P);
     } else {
         /* 1. lane kernel: small messages (lane fast path + exact machine);

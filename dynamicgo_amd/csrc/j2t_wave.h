@@ -432,13 +432,31 @@ struct ScanState {
     uint32_t scal_carry; /* the chunk's last byte was a scalar byte */
 };
 
-template <class LW, class WP>
-DGI void scan_chunk(WP wbase, int64_t head, int64_t len, uint32_t chunk, ScanState &st, LW &L,
+/* this lane's 4 bytes of chunk `chunk` (spaces past the end) */
+template <class WP>
+DGI uint32_t chunk_word(WP wbase, int64_t head, int64_t len, uint32_t chunk, uint32_t lane)
+{
+    int64_t wi = (int64_t)chunk * 64 + lane;
+    return wi * 4 - head < len ? wbase[wi] : 0x20202020u;
+}
+
+template <class LW>
+DGI void scan_chunk(uint32_t x, int64_t head, int64_t len, uint32_t chunk, ScanState &st, LW &L,
                     const __attribute__((address_space(3))) uint8_t *cls, uint32_t lane, uint64_t lt)
 {
     int64_t wi = (int64_t)chunk * 64 + lane;
     int64_t p0 = wi * 4 - head; /* message position of this lane's byte 0 */
-    uint32_t x = p0 < len ? wbase[wi] : 0x20202020u;
+    /* string interior without a quote or backslash anywhere in the chunk
+     * (long strings, base64 blobs): no tokens, carries unchanged */
+    if (st.str_carry) {
+        const uint32_t M = 0x7F7F7F7Fu;
+        uint32_t vq = x ^ 0x22222222u, vb = x ^ 0x5C5C5C5Cu;
+        uint32_t z = ~(((vq & M) + M) | vq | M) | ~(((vb & M) + M) | vb | M);
+        if (!ballot(z != 0)) {
+            st.esc_carry = 0;
+            return;
+        }
+    }
     uint32_t q = 0, bs = 0, sm = 0, ws = 0, knib = 0;
 #pragma unroll
     for (uint32_t j = 0; j < 4; j++) {
@@ -536,9 +554,12 @@ DGI bool wave_run(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L
     uint64_t O = 0;
     bool rootdone = false;
 
+    uint32_t xnext = chunk_word(wbase, head, len, 0, lane); /* loads run one chunk ahead */
     for (;;) {
         while (scanned < nchunks && ss.produced - consumed < 64 + WV_LA) {
-            scan_chunk(wbase, head, len, scanned, ss, L, cls, lane, lt);
+            const uint32_t xcur = xnext;
+            if (scanned + 1 < nchunks) xnext = chunk_word(wbase, head, len, scanned + 1, lane);
+            scan_chunk(xcur, head, len, scanned, ss, L, cls, lane, lt);
             scanned++;
             if (scanned == nchunks && ss.scal_carry) {
                 if (lane == 0) L.tend[(ss.produced - 1) & WV_RMASK] = (uint32_t)len;
