@@ -16,7 +16,7 @@ for C in FETCH_SIZE WRITE_SIZE; do
   cd /tmp && timeout -k 10 300 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $OUT/pmc_$C -o run -- python3 $ROOT/bench.py --no-cpu-baseline --no-e2e --steps 5 --warmup 2 > $OUT/pmc_$C.log 2>&1 || { echo "pmc $C failed"; tail -5 $OUT/pmc_$C.log; exit 1; }
 done
 cd $ROOT
-python3 tools/traffic.py $(find $OUT/pmc_FETCH_SIZE -name "*counter_collection.csv") $(find $OUT/pmc_WRITE_SIZE -name "*counter_collection.csv") j2t_small_kernel profiles/traffic_c2.json || exit 1
+python3 tools/traffic.py $(find $OUT/pmc_FETCH_SIZE -name "*counter_collection.csv") $(find $OUT/pmc_WRITE_SIZE -name "*counter_collection.csv") j2t_small_kernel $OUT/traffic_c2.json && cp $OUT/traffic_c2.json profiles/ || exit 1
 step bench-c2
 bash tools/gpu_bench.sh $TAG/c2 --config c2 > $OUT/c2.txt 2>&1 || { cat $OUT/c2.txt; exit 1; }
 for CFG in c3 c4 c5; do
