@@ -404,8 +404,13 @@ DGI bool key_eq(S &src, int64_t k0, uint32_t kn, const __attribute__((address_sp
 }
 
 /* the fast converter over one message; true = out holds the reference's
- * output, false = bail to the exact machine */
-template <class S, class DV>
+ * output, false = bail to the exact machine.
+ * LEAN (the small kernel): also bail on unknown-field skips, non-string map
+ * keys and default/empty writes for unset fields. Those need skip_one, a
+ * second vnumber and the tb_write_empty switch; leaving them to the list
+ * pass (which runs the full fast path, then the exact machine) cuts the
+ * small kernel's registers and SGPR spills (C2: 93 -> 83 us/launch). */
+template <bool LEAN = false, class S, class DV>
 DGI bool fast_convert(const DV &D, S &src, Out &out, uint64_t flag, uint32_t root, LFFrame *fr, uint32_t fstride,
                       const FastTabs &tb)
 {
@@ -618,6 +623,7 @@ DGI bool fast_convert(const DV &D, S &src, Out &out, uint64_t flag, uint32_t roo
                         out.w32(kn);
                         fast_copy(src, k0, kn, out);
                     } else {
+                        if constexpr (LEAN) return false;
                         S ks = src.sub(k0, kn);
                         int64_t q = 0, iv;
                         double dv;
@@ -661,6 +667,7 @@ DGI bool fast_convert(const DV &D, S &src, Out &out, uint64_t flag, uint32_t roo
                         c = src.at(p++);
                     }
                     p -= 1;
+                    if constexpr (LEAN) return false; /* the list pass skips it */
                     SkipRes sr = skip_one(src, p, nullptr, 64);
                     if (sr.r < 0) return false;
                     p = sr.p;
@@ -689,6 +696,7 @@ DGI bool fast_convert(const DV &D, S &src, Out &out, uint64_t flag, uint32_t roo
                 if (!wr && f.required == DG_REQ_REQUIRED) return false; /* ERR_NULL_REQUIRED */
                 if ((wr && f.required == DG_REQ_REQUIRED) || (wd && f.required == DG_REQ_DEFAULT) ||
                     (wo && f.required == DG_REQ_OPTIONAL)) {
+                    if constexpr (LEAN) return false;
                     const dg_type ft = ldrec(&D.T[f.type]);
                     out.wle((uint32_t)ft.ttype | ((uint32_t)__builtin_bswap16(f.id) << 8), 3);
                     if (f.dflt_len != DG_NONE) {

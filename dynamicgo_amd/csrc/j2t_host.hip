@@ -322,8 +322,7 @@ static int launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *jso
         Params P3 = P;
         P3.list = c->d_bail_list;
         P3.list_count = c->d_bail_count;
-        P3.reset2 = c->d_bail_count + 1;
-        P3.fast = 0;
+        P3.reset2 = c->d_bail_count + 1; /* P3.fast stays set: the small kernel's declines try the full fast path */
         lane_launch(dim3((uint32_t)std::min<uint64_t>(blocks, 16)), P3);
     } else if (!wave) {
         lane_launch(dim3((uint32_t)blocks), P);

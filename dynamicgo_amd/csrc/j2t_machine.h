@@ -887,6 +887,14 @@ __global__ __launch_bounds__(LANE_BLOCK) __attribute__((amdgpu_waves_per_eu(1, 1
             s_cnt = __hip_atomic_load(P.list_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (blockIdx.x == 0 && s_cnt) atomicAdd(&P.stats[0], (unsigned long long)s_cnt);
         }
+        if (P.fast) {
+            if (threadIdx.x < 20) {
+                uint64_t v = 1;
+                for (uint32_t k = 0; k < threadIdx.x; k++) v *= 10;
+                s_p10u[threadIdx.x] = v;
+            }
+            if (threadIdx.x < 23) s_p10d[threadIdx.x] = P10[threadIdx.x];
+        }
         __syncthreads();
         auto dvl = [&]() {
             if constexpr (LDS_DESC) return desc_view<3>((const __attribute__((address_space(3))) uint8_t *)(void *)ldesc, DP.hdr);
@@ -895,6 +903,19 @@ __global__ __launch_bounds__(LANE_BLOCK) __attribute__((amdgpu_waves_per_eu(1, 1
         const uint32_t cnt = s_cnt;
         for (uint64_t k = (uint64_t)blockIdx.x * LANE_BLOCK + threadIdx.x; k < cnt; k += (uint64_t)gridDim.x * LANE_BLOCK) {
             uint64_t j = P.list[k];
+            if (P.fast) {
+                /* the small kernel's declines: the full fast path first (unknown-field
+                 * skips, numeric map keys, default writes), then the exact machine */
+                Out out;
+                out.init(P.out + P.out_off[j], P.out_off[j + 1] - P.out_off[j]);
+                FastTabs tb{(const __attribute__((address_space(3))) uint64_t *)(void *)s_p10u,
+                            (lds_f64 *)(void *)s_p10d};
+                SrcT<glb_u64> s = global_src(P, j);
+                if (fast_convert(dvl, s, out, P.flag, P.root, (LFFrame *)(void *)&lframes[threadIdx.x], LANE_BLOCK, tb)) {
+                    finish(P, j, 0, (uint32_t)out.len);
+                    continue;
+                }
+            }
             FStack<LFrame *> frames{(LFrame *)(void *)&lframes[threadIdx.x], LANE_BLOCK};
             Workspace ws = lane_ws(P, j);
             uint32_t olen;

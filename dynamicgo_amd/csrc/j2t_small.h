@@ -91,10 +91,10 @@ __global__ __launch_bounds__(64 * SM_WAVES) __attribute__((amdgpu_waves_per_eu(D
     if (staged) {
         SrcT<lds_u64> s;
         s.init((lds_u64 *)(void *)stage, (int64_t)(a - base), (int64_t)(b - a));
-        done = fast_convert(dv, s, out, P.flag, P.root, ff, C::MPB, tb);
+        done = fast_convert<true>(dv, s, out, P.flag, P.root, ff, C::MPB, tb);
     } else {
         SrcT<glb_u64> s = global_src(P, i);
-        done = fast_convert(dv, s, out, P.flag, P.root, ff, C::MPB, tb);
+        done = fast_convert<true>(dv, s, out, P.flag, P.root, ff, C::MPB, tb);
     }
     if (done) {
         P.ret[i] = 0;
