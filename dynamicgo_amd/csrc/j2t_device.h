@@ -128,14 +128,15 @@ struct Workspace {
  * the 8-aligned word at or below the message start, `off0` the start's byte
  * offset from it. Reads at i >= n yield 0. Whole aligned words are read, so
  * up to 7 bytes before/after the message must be readable (arena padding). */
-template <class W>
+template <class W, class I = int64_t>
 struct SrcT {
+    typedef I idx;   /* position type: int32_t when the whole source is an LDS window */
     const W *w8;
-    int64_t off0;
-    int64_t n;
-    int64_t tag;
+    I off0;
+    I n;
+    I tag;
     uint64_t word;
-    DGI void init(const W *words, int64_t off, int64_t len)
+    DGI void init(const W *words, I off, I len)
     {
         w8 = words;
         off0 = off;
@@ -143,7 +144,7 @@ struct SrcT {
         tag = -1;
         word = 0;
     }
-    DGI uint64_t wordk(int64_t k)
+    DGI uint64_t wordk(I k)
     {
         if (k != tag) {
             tag = k;
@@ -151,17 +152,17 @@ struct SrcT {
         }
         return word;
     }
-    DGI uint8_t raw(int64_t i)
+    DGI uint8_t raw(I i)
     {
-        int64_t b = off0 + i;
+        I b = off0 + i;
         return (uint8_t)(wordk(b >> 3) >> ((b & 7) << 3));
     }
-    DGI uint8_t at(int64_t i) { return (uint64_t)i < (uint64_t)n ? raw(i) : 0; }
+    DGI uint8_t at(I i) { return (std::make_unsigned_t<I>)i < (std::make_unsigned_t<I>)n ? raw(i) : 0; }
     /* 8 bytes at [i, i+8) (caller guarantees i + 8 <= n), first byte lowest */
-    DGI uint64_t get8(int64_t i)
+    DGI uint64_t get8(I i)
     {
-        int64_t b = off0 + i;
-        int64_t k = b >> 3;
+        I b = off0 + i;
+        I k = b >> 3;
         uint32_t sh = (uint32_t)(b & 7) << 3;
         uint64_t lo = wordk(k);
         if (sh == 0) return lo;
@@ -169,7 +170,7 @@ struct SrcT {
         return (lo >> sh) | (hi << (64 - sh));
     }
     /* sub-view [s0, s0+len) of this message (same memory) */
-    DGI SrcT sub(int64_t s0, int64_t len) const
+    DGI SrcT sub(I s0, I len) const
     {
         SrcT r;
         r.init(w8, off0 + s0, len);
@@ -354,25 +355,27 @@ DGI int64_t advance_dword(S &s, int64_t &p, int64_t dec, int64_t ret, uint32_t v
  * esc = whether a backslash occurs inside the string. 8 bytes per step: the
  * window word is tested for '"' and '\\' with exact SWAR byte compares. */
 template <class S>
-DGI int64_t advance_string(S &s, int64_t p, bool &esc)
+DGI int64_t advance_string(S &s, int64_t p0, bool &esc)
 {
+    typedef typename S::idx I;
     esc = false;
+    const I p = (I)p0;
     if (s.n == p) return -(int64_t)E_EOF;
-    int64_t i = p;
+    I i = p;
     while (i < s.n) {
-        int64_t b = s.off0 + i;
-        int64_t k = b >> 3;
+        I b = s.off0 + i;
+        I k = b >> 3;
         uint64_t w = s.wordk(k);
         uint64_t m = zbytes(w ^ 0x2222222222222222ull) | zbytes(w ^ 0x5C5C5C5C5C5C5C5Cull);
         m &= ~0ull << ((b & 7) << 3);
-        int64_t lim = s.n - (k * 8 - s.off0); /* bytes of this word inside the message */
+        I lim = s.n - (k * 8 - s.off0); /* bytes of this word inside the message */
         if (lim < 8) m &= (1ull << (lim << 3)) - 1;
         if (m == 0) {
             i = (k + 1) * 8 - s.off0;
             continue;
         }
         int j = __builtin_ctzll(m) >> 3;
-        int64_t pos = k * 8 + j - s.off0;
+        I pos = k * 8 + j - s.off0;
         if ((uint8_t)(w >> (j << 3)) == '"') return pos + 1;
         esc = true;
         if (pos + 1 >= s.n) return -(int64_t)E_EOF;

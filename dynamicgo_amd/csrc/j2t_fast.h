@@ -29,6 +29,10 @@
 
 namespace dg {
 
+/* positions inside one message: the source's index type (32-bit for an
+ * LDS-staged source, 64-bit for a global one) */
+#define SI typename S::idx
+
 constexpr uint32_t FK_STRUCT = 1, FK_MAP = 2, FK_LIST = 3;
 constexpr uint32_t FAST_LDS_DEPTH = 8; /* parent frames per lane in LDS */
 
@@ -56,13 +60,13 @@ struct FastTabs {
 /* leading ASCII digits among the 8 bytes at src[i..] (bytes at >= n excluded);
  * x = the bytes XOR '0' (digit values in the digit bytes) */
 template <class S>
-DGI uint32_t digits8(S &src, int64_t i, uint64_t &x)
+DGI uint32_t digits8(S &src, SI i, uint64_t &x)
 {
     const uint64_t H = 0x8080808080808080ull;
     uint64_t w = src.get8(i);
     x = w ^ 0x3030303030303030ull;
     uint64_t nd = (((x & 0x7F7F7F7F7F7F7F7Full) + 0x7676767676767676ull) | x) & H;
-    int64_t lim = src.n - i;
+    SI lim = src.n - i;
     if (lim < 8) nd |= lim <= 0 ? H : (H & (~0ull << (lim << 3)));
     return nd ? (uint32_t)__builtin_ctzll(nd) >> 3 : 8u;
 }
@@ -115,9 +119,9 @@ DGI bool atof_exact_l(uint64_t man, int exp, int sgn, double &val, const FastTab
 /* vnumber (native/scanning.c:958-1083) on the success paths; false = the
  * reference would error or need atof_native -> bail. */
 template <class S>
-DGI bool fast_vnumber(S &src, int64_t &p, const FastTabs &tb, int64_t &iv, double &dv, bool &isint)
+DGI bool fast_vnumber(S &src, SI &p, const FastTabs &tb, int64_t &iv, double &dv, bool &isint)
 {
-    int64_t i = p;
+    SI i = p;
     uint8_t c = src.at(i);
     int sgn = 1;
     if (c == '-') {
@@ -229,16 +233,16 @@ DGI bool emit_number(O &out, uint8_t tt, bool isint, int64_t iv, double dv)
 
 /* copy src[s0, s0+n) to the output, 8 bytes per step */
 template <class S, class O>
-DGI void fast_copy(S &src, int64_t s0, int64_t n, O &out)
+DGI void fast_copy(S &src, SI s0, SI n, O &out)
 {
-    int64_t i = 0;
+    SI i = 0;
     for (; i + 8 <= n; i += 8) out.wle(src.get8(s0 + i), 8);
     if (i < n) out.wle(src.get8(s0 + i), (uint32_t)(n - i));
 }
 
 /* 4 hex digits at src[i..i+4) */
 template <class S>
-DGI bool hex4w(S &src, int64_t i, uint32_t &v)
+DGI bool hex4w(S &src, SI i, uint32_t &v)
 {
     uint32_t w = (uint32_t)src.get8(i);
     uint32_t r = 0;
@@ -255,12 +259,12 @@ DGI bool hex4w(S &src, int64_t i, uint32_t &v)
 /* unquote (native/parsing.c:702-945, flags 0) of src[s0, s0+nb) appended to
  * out: runs between backslashes are copied as words. false = error. */
 template <class S, class O>
-DGI bool fast_unquote(S &src, int64_t s0, int64_t nb, O &out)
+DGI bool fast_unquote(S &src, SI s0, SI nb, O &out)
 {
-    int64_t i = s0, end = s0 + nb;
+    SI i = s0, end = s0 + nb;
     while (i < end) {
         uint64_t w = src.get8(i);
-        int64_t rem = end - i;
+        SI rem = end - i;
         uint64_t m = zbytes(w ^ 0x5C5C5C5C5C5C5C5Cull);
         if (rem < 8) m &= (1ull << (rem << 3)) - 1;
         if (m == 0) {
@@ -318,14 +322,14 @@ DGI bool fast_unquote(S &src, int64_t s0, int64_t nb, O &out)
 
 /* j2t_string (native/thrift.c:367-399); p is just past the opening quote */
 template <class S>
-DGI bool fast_string(S &src, int64_t &p, Out &out)
+DGI bool fast_string(S &src, SI &p, Out &out)
 {
-    int64_t s0 = p;
+    SI s0 = p;
     bool esc;
-    int64_t e = advance_string(src, s0, esc);
+    SI e = advance_string(src, s0, esc);
     if (e < 0) return false;
     p = e;
-    int64_t nb = e - 1 - s0;
+    SI nb = e - 1 - s0;
     if (!esc) {
         out.w32((uint32_t)nb);
         fast_copy(src, s0, nb, out);
@@ -365,16 +369,17 @@ DGI bool b64_8(uint64_t w, uint64_t &o)
 
 /* j2t_binary (native/thrift.c:401-420) */
 template <class S>
-DGI bool fast_binary(S &src, int64_t &p, Out &out)
+DGI bool fast_binary(S &src, SI &p, Out &out)
 {
-    int64_t s0 = p;
+    SI s0 = p;
     bool esc;
-    int64_t e = advance_string(src, s0, esc);
+    SI e = advance_string(src, s0, esc);
     if (e < 0 || esc) return false; /* '\\' is outside the alphabet: decode error */
     p = e;
-    int64_t nb = e - 1 - s0;
+    SI nb = e - 1 - s0;
     uint64_t lp = out.alloc(4);
-    int64_t ip = 0, op = 0;
+    SI ip = 0;
+    int64_t op = 0;
     while (ip + 8 <= nb) {
         uint64_t o;
         if (!b64_8(src.get8(s0 + ip), o)) break;
@@ -392,7 +397,7 @@ DGI bool fast_binary(S &src, int64_t &p, Out &out)
 
 /* key bytes src[k0, k0+kn) == the zero-padded 8-aligned pool key at pk */
 template <class S, int AS>
-DGI bool key_eq(S &src, int64_t k0, uint32_t kn, const __attribute__((address_space(AS))) uint64_t *pk)
+DGI bool key_eq(S &src, SI k0, uint32_t kn, const __attribute__((address_space(AS))) uint64_t *pk)
 {
     for (uint32_t j = 0; j < kn; j += 8) {
         uint64_t a = src.get8(k0 + j);
@@ -416,7 +421,7 @@ DGI bool fast_convert(const DV &D, S &src, Out &out, uint64_t flag, uint32_t roo
 {
     /* empty body and unquoted STRING roots are the prelude's business (convert_one) */
     if (src.n == 0 || ldrec(&D.T[root]).ttype == DG_T_STRING) return false;
-    int64_t p = 0;
+    SI p = 0;
     uint32_t sp = 0;                  /* open containers */
     uint32_t ca = 0, ck = 0, cb = 0;  /* innermost: a, kind, hint/count */
     uint64_t cu = 0;                  /* innermost: reqs or size position */
@@ -604,9 +609,9 @@ DGI bool fast_convert(const DV &D, S &src, Out &out, uint64_t flag, uint32_t roo
             /* a key */
             if (c != '"') return false;
             {
-                int64_t k0 = p;
+                SI k0 = p;
                 bool esc;
-                int64_t e = advance_string(src, k0, esc);
+                SI e = advance_string(src, k0, esc);
                 if (e < 0 || esc) return false;
                 p = e;
                 uint32_t kn = (uint32_t)(e - 1 - k0);
@@ -625,7 +630,8 @@ DGI bool fast_convert(const DV &D, S &src, Out &out, uint64_t flag, uint32_t roo
                     } else {
                         if constexpr (LEAN) return false;
                         S ks = src.sub(k0, kn);
-                        int64_t q = 0, iv;
+                        SI q = 0;
+                        int64_t iv;
                         double dv;
                         bool isint;
                         if (!fast_vnumber(ks, q, tb, iv, dv, isint)) return false;
@@ -735,5 +741,6 @@ DGI bool fast_convert(const DV &D, S &src, Out &out, uint64_t flag, uint32_t roo
 #undef FAST_PUSH
 #undef FAST_POP
 }
+#undef SI
 
 }  // namespace dg

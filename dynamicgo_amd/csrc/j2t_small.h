@@ -89,8 +89,8 @@ __global__ __launch_bounds__(64 * SM_WAVES) __attribute__((amdgpu_waves_per_eu(D
     LFFrame *ff = (LFFrame *)(void *)&lframes[j];
     bool done;
     if (staged) {
-        SrcT<lds_u64> s;
-        s.init((lds_u64 *)(void *)stage, (int64_t)(a - base), (int64_t)(b - a));
+        SrcT<lds_u64, int32_t> s; /* the stage is < 2 GiB: 32-bit positions */
+        s.init((lds_u64 *)(void *)stage, (int32_t)(a - base), (int32_t)(b - a));
         done = fast_convert<true>(dv, s, out, P.flag, P.root, ff, C::MPB, tb);
     } else {
         SrcT<glb_u64> s = global_src(P, i);

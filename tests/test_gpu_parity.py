@@ -257,3 +257,38 @@ def test_pack_device_matches_slots():
     for i in (0, 1, 2, n - 3, n - 2, n - 1):
         er, eo = chk.j2t(fl, msgs[i], 1)
         assert int(d_ret[i]) == er and got[doff[i]:doff[i + 1]].tobytes() == eo
+
+
+def _lean_decline_msgs(rng):
+    """Small messages (<= 512 B) the small kernel's lean fast path declines on
+    purpose: unknown fields with nested values, numeric map keys, unset fields
+    under the default/require/optional write flags."""
+    simple, nest = [], []
+    for _ in range(300):
+        o = W.simple_obj(rng)
+        k = rng.randint(0, 3)
+        if k == 0:  # unknown field holding a nested value, somewhere in the object
+            o = o[:-1] + ',"Unknown%d":{"a":[1,"x",{"b":null}],"c":-1.5e3}}' % rng.randint(0, 9)
+        elif k == 1:  # drop fields so the write flags have unset fields to fill
+            o = '{"I32Field":%d,"StringField":"s"}' % rng.randint(-9, 9)
+        elif k == 2:
+            o = '{"Unknown":[[],{}],' + o[1:]
+        simple.append(o.encode())
+        m = ",".join('"%d":"v%d"' % (rng.randint(-2**63, 2**63 - 1), i) for i in range(rng.randint(1, 4)))
+        nest.append(('{"I64":%d,"MapI64String":{%s},"MapI32I64":{"%d":7}}'
+                     % (rng.randint(-99, 99), m, rng.randint(-2**31, 2**31 - 1))).encode())
+    return simple, nest
+
+
+@pytest.mark.parametrize("flags", [1, 1 | 2, 1 | 32, 1 | 128, 1 | 2 | 32 | 128, 0])
+def test_small_kernel_declines_vs_oracle(flags):
+    """The small kernel leaves unknown-field skips, numeric map keys and
+    default writes to the list pass (full fast path, then the exact machine):
+    the hybrid route must still be bit-exact with the oracle on them."""
+    simple, nest = _lean_decline_msgs(random.Random(7 + flags))
+    chk = _checker()
+    for fl, msgs in ((T.flatten(W.simple_desc()), simple), (T.flatten(W.nesting_desc()), nest)):
+        assert max(len(m) for m in msgs) <= 512
+        outs, rets = _raw_batch(fl, msgs, flags)
+        for m, o, r in zip(msgs, outs, rets):
+            assert (int(r), o) == chk.j2t(fl, m, flags), m[:200]
