@@ -13,7 +13,7 @@ while [ $# -gt 0 ] && [ "$1" != "--" ]; do PASSES+=("$1"); shift; done
 i=0
 for C in "${PASSES[@]}"; do
   i=$((i+1))
-  cd /tmp && timeout -k 10 300 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $OUT/pmc$i -o run -- python3 $ROOT/bench.py --no-cpu-baseline "$@" > $OUT/pmc$i.log 2>&1 || { echo "pmc pass $i failed rc=$?"; tail -20 $OUT/pmc$i.log; exit 1; }
+  cd /tmp && timeout -s KILL 90 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $OUT/pmc$i -o run -- python3 $ROOT/bench.py --no-cpu-baseline "$@" > $OUT/pmc$i.log 2>&1 || { echo "pmc pass $i failed rc=$?"; tail -20 $OUT/pmc$i.log; exit 1; }
 done
 for f in $(find $OUT -name "*counter_collection.csv"); do echo "== $f"; python3 - "$f" <<'PY'
 import csv, sys, collections
