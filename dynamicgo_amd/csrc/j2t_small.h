@@ -71,12 +71,37 @@ __global__ __launch_bounds__(64 * SM_WAVES) __attribute__((amdgpu_waves_per_eu(D
     }
     if (tid < 23) s_p10d[tid] = P10[tid];
     __syncthreads();
-    if (lane >= (uint32_t)MPW) return;
     const uint32_t j = wave * MPW + lane; /* message slot within the block */
     const uint64_t i = b0 + j;
-    if (i >= b1) return;
-    const uint64_t a = P.in_off[i], b = P.in_off[i + 1];
-    if (P.big_list && b - a > P.big_max) {
+    const bool mine = lane < (uint32_t)MPW && i < b1;
+    uint64_t a = 0, b = 0;
+    if (mine) {
+        a = P.in_off[i];
+        b = P.in_off[i + 1];
+    }
+    const bool big = mine && P.big_list && b - a > P.big_max;
+    /* The block's span did not fit the stage (a mixed batch: large messages
+     * sit between the small ones). Stage per WAVE instead: each lane copies
+     * the aligned words of its own small message to a packed position in
+     * the wave's quarter of the stage (wave prefix sum of word counts). A
+     * lane only ever reads back what it wrote itself, so no barrier. */
+    constexpr uint32_t WSTAGE = C::STAGE / 8 / SM_WAVES; /* words per wave */
+    bool wst = false;
+    uint32_t wbase = 0;
+    if (!staged) {
+        uint64_t wc64 = mine && !big ? ((b + 7) >> 3) - (a >> 3) + 1 : 0; /* +1: the window may read one word past */
+        const uint32_t wc = wc64 > WSTAGE ? WSTAGE + 1 : (uint32_t)wc64;
+        const uint32_t incl = wave_incl_sum(wc, lane);
+        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        if (tot <= WSTAGE) {
+            wst = true;
+            wbase = wave * WSTAGE + incl - wc;
+            const glb_u64 *g = (const glb_u64 *)(const void *)P.json + (a >> 3); /* arena: 16 readable bytes past the end */
+            for (uint32_t k = 0; k < wc; k++) stage[wbase + k] = g[k];
+        }
+    }
+    if (!mine) return;
+    if (big) {
         uint32_t q = __hip_atomic_fetch_add(P.big_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         P.big_list[q] = (uint32_t)i;
         return;
@@ -88,9 +113,10 @@ __global__ __launch_bounds__(64 * SM_WAVES) __attribute__((amdgpu_waves_per_eu(D
     FastTabs tb{(const __attribute__((address_space(3))) uint64_t *)(void *)s_p10u, (lds_f64 *)(void *)s_p10d};
     LFFrame *ff = (LFFrame *)(void *)&lframes[j];
     bool done;
-    if (staged) {
+    if (staged || wst) {
         SrcT<lds_u64, int32_t> s; /* the stage is < 2 GiB: 32-bit positions */
-        s.init((lds_u64 *)(void *)stage, (int32_t)(a - base), (int32_t)(b - a));
+        if (staged) s.init((lds_u64 *)(void *)stage, (int32_t)(a - base), (int32_t)(b - a));
+        else s.init((lds_u64 *)(void *)stage + wbase, (int32_t)(a & 7), (int32_t)(b - a));
         done = fast_convert<true>(dv, s, out, P.flag, P.root, ff, C::MPB, tb);
     } else {
         SrcT<glb_u64> s = global_src(P, i);

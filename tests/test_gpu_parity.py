@@ -292,3 +292,25 @@ def test_small_kernel_declines_vs_oracle(flags):
         outs, rets = _raw_batch(fl, msgs, flags)
         for m, o, r in zip(msgs, outs, rets):
             assert (int(r), o) == chk.j2t(fl, m, flags), m[:200]
+
+
+def test_small_kernel_wave_staging_vs_oracle():
+    """Blocks whose JSON span does not fit the stage (large messages between
+    small ones) stage per wave; waves whose small messages still do not fit
+    read global memory. Both must be bit-exact with the oracle."""
+    rng = random.Random(11)
+    fl = T.flatten(W.simple_desc())
+    msgs = []
+    for blk in range(12):
+        for k in range(256):
+            r = rng.random()
+            if blk % 3 == 0 and r < 0.05:  # large: the wave kernel's
+                msgs.append(('{"StringField":"%s","I32Field":%d}' % ("x" * rng.randint(600, 3000), k)).encode())
+            elif blk % 3 == 1 and r < 0.5:  # 400-512 B: the wave's quarter overflows -> global source
+                msgs.append(('{"StringField":"%s","ByteField":1}' % ("y" * rng.randint(380, 480))).encode())
+            else:
+                msgs.append(W.simple_obj(rng).encode())
+    chk = _checker()
+    outs, rets = _raw_batch(fl, msgs, 1)
+    for m, o, r in zip(msgs, outs, rets):
+        assert (int(r), o) == chk.j2t(fl, m, 1), m[:120]
