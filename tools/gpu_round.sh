@@ -24,3 +24,6 @@ for CFG in c3 c4 c5; do
   timeout -k 10 400 python bench.py --config $CFG --no-cpu-baseline --steps 10 > $OUT/$CFG.json 2> $OUT/$CFG.err || { tail -5 $OUT/$CFG.err; exit 1; }
 done
 head -c 2000 $OUT/c2.txt; echo; for CFG in c3 c4 c5; do head -c 600 $OUT/$CFG.json; echo; done
+step rocprof-c5
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/c5prof -o run -- python3 $ROOT/bench.py --config c5 --no-cpu-baseline --no-e2e --steps 10 > $OUT/c5prof.json 2> $OUT/c5prof.err || { echo "rocprof c5 failed"; exit 1; }
+find $OUT/c5prof -name "*kernel_stats.csv" -exec head -5 {} \;
