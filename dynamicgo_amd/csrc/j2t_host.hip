@@ -323,7 +323,9 @@ static int launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *jso
         P3.list = c->d_bail_list;
         P3.list_count = c->d_bail_count;
         P3.reset2 = c->d_bail_count + 1; /* P3.fast stays set: the small kernel's declines try the full fast path */
-        lane_launch(dim3((uint32_t)std::min<uint64_t>(blocks, 16)), P3);
+        const char *lb_env = getenv("DG_LIST_BLOCKS"); /* list-pass grid (default 16) */
+        const uint64_t lb = lb_env ? std::max<uint64_t>(1, strtoull(lb_env, nullptr, 10)) : 16;
+        lane_launch(dim3((uint32_t)std::min<uint64_t>(blocks, lb)), P3);
     } else if (!wave) {
         lane_launch(dim3((uint32_t)blocks), P);
     } else {
