@@ -2,21 +2,32 @@
 """bench.py — conv/j2t device-resident throughput on MI355X.
 
 A "step" = one pass of the hot path (JSON -> Thrift binary, BinaryConv.Do per
-message) over one batch that is already resident in HBM. At N GPUs each rank
-converts its own batch of the configured workload (weak scaling; messages are
-independent, no data-path collective); the flattened descriptor is broadcast
-once from rank 0 over RCCL.
+message) over one batch that is already resident in HBM.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5|c1]
-    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c2x|c2s|c3|c4|c5|c1]
 
-Prints ONE JSON line (rank 0). `value` = total JSON bytes converted by all
-ranks / max-over-ranks wall time of the K timed steps.
+Multi-GPU: with --gpus N > 1 and no WORLD_SIZE in the environment this
+process launches N ranks itself (one process per GPU, RANK/LOCAL_RANK/
+WORLD_SIZE/MASTER_ADDR=127.0.0.1/MASTER_PORT set, before anything touches
+the GPU) and exits with their status; under torchrun it is one of the ranks.
+Messages are independent, so no data-path collective exists: the flattened
+descriptor is broadcast once from rank 0 (RCCL over xGMI) and every rank
+converts its own shard.
+  * c2/c2x/c2s/c3/c4/c1 — weak scaling: every rank converts a batch of the
+    config's size (rank r draws with seed + 1000 r), global batch = N x size.
+  * c5 — strong scaling: ONE 1 048 576-message mixed batch (seed 45), split
+    into N byte-balanced contiguous shards (dist.shard_ranges), rank r
+    converts shard r.
+Prints ONE JSON line (rank 0). `value` = JSON bytes converted by all ranks /
+max-over-ranks wall time of the K timed steps (barrier + synchronize on both
+sides).
 """
 import argparse
 import json
 import os
 import random
+import socket
+import subprocess
 import sys
 import time
 
@@ -24,76 +35,149 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
-import torch  # noqa: E402  (first: one HIP runtime per process, see dynamicgo_amd/_lib.py)
-
-from dynamicgo_amd import _lib, workloads as W  # noqa: E402
-from dynamicgo_amd.thrift import flatten  # noqa: E402
 
 METRIC = "conv/j2t GB/s JSON in + msgs/s, 64K-batch device-resident, 1→8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PER_MSG_META = 28      # in_off 8 + out_off 8 + out_len 4 + ret 8 bytes
+CPU_SHARE = 16         # host CPUs the GPU box grants per GPU
 
 CONFIGS = {
-    "c2": ("C2: 65536 flat baseline.Simple messages <=256 B, seed 42", 65536),
-    "c3": ("C3: 65536 nested NestingI64 messages (list<string> + map<i64,Simple>), seed 43", 65536),
-    "c4": ("C4: 4096 large messages (48 KiB base64 binary + 1024 doubles), seed 44", 4096),
-    "c1": ("C1: the reference's Simple payload x 65536 (236 B each)", 65536),
-    "c5": ("C5: mixed 90% flat / 9.5% nested / 0.5% large, 131072 per GPU (1M over 8), seed 45", 131072),
+    "c2": ("C2: 65536 flat baseline.Simple messages <=256 B, seed 42", 65536, "weak"),
+    "c2x": ("C2 with the reference benchmark's options (WriteDefaultField + EnableValueMapping, flags 0x7; "
+            "testdata/test/baseline_j2t_test.go:721-737): 65536 flat Simple messages, seed 42", 65536, "weak"),
+    "c2s": ("C2 divergence stress: 65536 flat Simple messages with the keys of every message in a random "
+            "order, seed 42", 65536, "weak"),
+    "c3": ("C3: 65536 nested NestingI64 messages (list<string> + map<i64,Simple>), seed 43", 65536, "weak"),
+    "c4": ("C4: 4096 large messages (48 KiB base64 binary + 1024 doubles), seed 44", 4096, "weak"),
+    "c1": ("C1: the reference's Simple payload (236 B) x 65536", 65536, "weak"),
+    "c5": ("C5: ONE 1048576-message mixed batch (90% flat / 9.5% nested / 0.5% large), seed 45, "
+           "byte-balanced shards over the ranks", 1 << 20, "strong"),
 }
+FLAGS = {"c2x": 0x7}  # default: conv.Options{} -> F_ALLOW_UNKNOWN (conv/j2t/conv.go:102-104)
 
 
-def make_batch(cfg: str, rank: int):
-    if cfg == "c2":
-        return W.simple_desc(), W.gen_flat_batch(random.Random(42 + 1000 * rank), CONFIGS[cfg][1])
-    if cfg == "c3":
-        return W.nesting_i64_desc(), W.gen_nested_batch(random.Random(43 + 1000 * rank), CONFIGS[cfg][1])
-    if cfg == "c4":
-        return W.large_desc(), W.gen_large_batch(random.Random(44 + 1000 * rank), CONFIGS[cfg][1])
-    if cfg == "c1":
-        return W.simple_desc(), [W.c1_simple_json()] * CONFIGS[cfg][1]
+# ---------------------------------------------------------------- launching
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv, python=sys.executable, script=None) -> int:
+    """One child process per GPU running this script with the same args, the
+    torch.distributed env set; returns the worst exit status. The parent
+    never touches the GPU (children are started, not exec'd)."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([python, script or os.path.abspath(__file__), *argv], env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
+# ---------------------------------------------------------------- workloads
+def rank_workload(cfg: str, rank: int, world: int, workers: int = 1, c5_n: int = None, c5_scale: float = 1.0):
+    """This rank's (TypeDescriptor, arena, offsets, meta). Weak configs: a
+    batch of the config's size per rank; c5: shard `rank` of the one global
+    batch (byte-balanced contiguous ranges, dist.shard_ranges)."""
+    from dynamicgo_amd import workloads as W
+    from dynamicgo_amd.dist import shard_ranges
+    size = CONFIGS[cfg][1]
     if cfg == "c5":
-        return W.mixed_desc(), W.gen_mixed_batch(random.Random(45 + 1000 * rank), CONFIGS[cfg][1])
-    raise ValueError(cfg)
+        n = c5_n or size
+        a, off = W.gen_mixed_arena(n, 45, workers=workers, large_scale=c5_scale)
+        lo, hi = shard_ranges(off, world)[rank]
+        sa, so = W.arena_slice(a, off, lo, hi)
+        return W.mixed_desc(), sa, so, {"global_batch": n, "global_json_bytes": int(off[-1]), "shard": [lo, hi]}
+    rng = random.Random({"c2": 42, "c2x": 42, "c2s": 42, "c3": 43, "c4": 44, "c1": 0}[cfg] + 1000 * rank)
+    if cfg in ("c2", "c2x"):
+        td, msgs = W.simple_desc(), W.gen_flat_batch(rng, size)
+    elif cfg == "c2s":
+        td, msgs = W.simple_desc(), W.gen_flat_batch_shuffled(rng, size)
+    elif cfg == "c3":
+        td, msgs = W.nesting_i64_desc(), W.gen_nested_batch(rng, size)
+    elif cfg == "c4":
+        td, msgs = W.large_desc(), W.gen_large_batch(rng, size)
+    else:
+        td, msgs = W.simple_desc(), [W.c1_simple_json()] * size
+    a, off = W.arena(msgs)
+    return td, a, off, {"global_batch": size * world, "global_json_bytes": None, "shard": None}
 
 
-def cpu_baseline(flat, arena, off, flags, budget_s: float = 12.0):
-    """The reference's own native/*.c (oracle/_ref) on this host's cores."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle  # reported baseline only
-    ref = oracle.RefOracle()
-    kind = "reference"
-    if ref is None:
-        ref, kind = oracle.PortOracle(), "port"
-    cores = 1 if kind == "port" else max(1, min(16, (os.cpu_count() or 1)))
-    nbytes = int(off[-1] - off[0])
-    reps, t_best = 0, None
-    t_end = time.perf_counter() + budget_s
-    while time.perf_counter() < t_end or reps < 2:
-        t0 = time.perf_counter()
-        ref.j2t_arena(flat, arena, off, flags, nthreads=cores, decode=False)
-        dt = time.perf_counter() - t0
-        t_best = dt if t_best is None else min(t_best, dt)
-        reps += 1
-    model = "unknown"
+def share_descriptor(flat, rank: int, dev, backend: str):
+    """Rank 0's flattened descriptor on every rank, as a uint8 tensor on `dev`
+    (RCCL broadcast straight into device memory; gloo via host memory)."""
+    import torch
+    from dynamicgo_amd import dist as D
+    where = dev if backend == "nccl" else torch.device("cpu")
+    t = D.broadcast_blob(flat.blob if rank == 0 else None, where)
+    return t.to(dev) if t.device != dev else t
+
+
+# ---------------------------------------------------------------- CPU baseline
+def cpu_model() -> str:
     try:
         with open("/proc/cpuinfo") as fh:
             for line in fh:
                 if line.startswith("model name"):
-                    model = line.split(":", 1)[1].strip()
-                    break
+                    return line.split(":", 1)[1].strip()
     except OSError:
         pass
-    return {"value": round(nbytes / t_best / 1e9, 4), "unit": "GB/s", "cores": cores, "kind": kind,
-            "sample": f"the full batch ({len(off) - 1} msgs, {nbytes} B) x {reps} reps, best of reps, "
-                      f"{cores} threads of '{model}' (nproc={os.cpu_count()})"}
+    return "unknown"
 
 
-def e2e_host_path(L, ctx, dh, root, flags, arena, off, dev, chunks: int = 8, reps: int = 5):
-    """End-to-end from host memory (HTTP bodies in) to host memory (Thrift out):
-    pinned H2D of each chunk's JSON + offsets, conversion, device-side packing
-    of the outputs (dg_pack_device), D2H of the packed bytes + out_len + ret.
-    Chunks alternate between two streams so copies overlap conversion.
-    Returns GB/s of JSON in (best of reps) and the serial breakdown."""
+def cpu_baseline(flat, arena, off, flags, budget_s: float = 8.0):
+    """The reference's own native/*.c (oracle/_ref, clang -O3 like the
+    reference's build) on this host: one pinned thread per physical core of
+    this process's CPU share (<= CPU_SHARE), byte-balanced shards, outputs
+    preallocated and first touched by an untimed pass, best of reps; plus the
+    same on one core over a bounded prefix."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # reported baseline only
+    ref = oracle.RefOracle()
+    if ref is None:
+        return None
+    phys, logical = oracle.physical_cpus()
+    cores = max(1, min(CPU_SHARE, len(phys)))
+    n = len(off) - 1
+    nbytes = int(off[-1] - off[0])
+
+    def timed(a, o, cpus):
+        t1 = ref.j2t_timed(flat, a, o, flags, cpus, 1)
+        reps = int(max(3, min(200, budget_s / 2 / max(t1, 1e-6))))
+        return ref.j2t_timed(flat, a, o, flags, cpus, reps), reps
+
+    t_all, reps_all = timed(arena, off, phys[:cores])
+    # one core: a prefix of at most ~64 MB / 65536 messages
+    k = int(min(n, 65536, max(1, np.searchsorted(off, off[0] + 64 * 1024 * 1024))))
+    a1, o1 = arena[:int(off[k]) + 64], off[:k + 1]
+    t_one, reps_one = timed(a1, o1, phys[:1])
+    one_bytes = int(o1[-1] - o1[0])
+    return {"value": round(nbytes / t_all / 1e9, 4), "unit": "GB/s", "cores": cores, "kind": "reference",
+            "msgs_per_s": round(n / t_all),
+            "one_core_gbs": round(one_bytes / t_one / 1e9, 4), "one_core_ns_per_msg": round(t_one / k * 1e9, 1),
+            "per_core_gbs": round(nbytes / t_all / 1e9 / cores, 4),
+            "sample": f"all-core: the rank's whole batch ({n} msgs, {nbytes} B), best of {reps_all} passes, "
+                      f"{cores} threads pinned to distinct physical cores of '{cpu_model()}' "
+                      f"(affinity: {logical} logical CPUs = {len(phys)} physical cores; the box grants "
+                      f"{CPU_SHARE} CPUs per GPU); one-core: first {k} msgs ({one_bytes} B), best of {reps_one}; "
+                      f"reference native.c built by oracle/Makefile (clang -O3 -mavx2)"}
+
+
+# ---------------------------------------------------------------- end to end
+def e2e_host_path(L, ctx, dh, root, flags, arena, off, dev, flat, chunks: int = 4, reps: int = 5):
+    """End-to-end from host memory (HTTP bodies in) to host memory (Thrift
+    out): per chunk, pinned H2D of JSON + offsets, conversion,
+    dg_pack_device_scan (prefix sum of out_len + packing in one launch), D2H
+    of the packed bytes + out_len + ret. Chunks alternate over 2 streams of
+    the same context (per-stream scratch) so copies overlap conversion.
+    Every chunk's packed output is checked against the oracle once, outside
+    the timed loop. Returns GB/s of JSON in (best of reps) and the link rates."""
+    import torch
+    from dynamicgo_amd import _lib
     n = len(off) - 1
     bounds = np.linspace(0, n, chunks + 1).astype(np.int64)
     C = []
@@ -106,7 +190,7 @@ def e2e_host_path(L, ctx, dh, root, flags, arena, off, dev, chunks: int = 8, rep
         np.cumsum((lens * 4 + 64 + 7) & ~7, out=slots[1:])
         h_json = torch.from_numpy(np.concatenate([arena[lo:hi], np.zeros(64, np.uint8)])).pin_memory()
         h_in = torch.from_numpy(o).pin_memory()
-        C.append(dict(n=b - a, h_json=h_json, h_in=h_in,
+        C.append(dict(n=b - a, a=a, b=b, h_json=h_json, h_in=h_in, max_len=int(lens.max()) if b > a else 0,
                       d_json=torch.empty_like(h_json, device=dev), d_in=torch.empty_like(h_in, device=dev),
                       d_out=torch.empty(int(slots[-1]) + 64, dtype=torch.uint8, device=dev),
                       d_oo=torch.from_numpy(slots).to(dev), d_ol=torch.zeros(b - a, dtype=torch.int32, device=dev),
@@ -114,7 +198,8 @@ def e2e_host_path(L, ctx, dh, root, flags, arena, off, dev, chunks: int = 8, rep
                       d_doff=torch.zeros(b - a + 1, dtype=torch.int64, device=dev),
                       d_pack=torch.empty(int(slots[-1]) + 64, dtype=torch.uint8, device=dev),
                       h_ol=torch.empty(b - a, dtype=torch.int32).pin_memory(),
-                      h_ret=torch.empty(b - a, dtype=torch.int64).pin_memory()))
+                      h_ret=torch.empty(b - a, dtype=torch.int64).pin_memory(),
+                      h_doff=torch.empty(b - a + 1, dtype=torch.int64).pin_memory()))
     streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
 
     def run(sizes):
@@ -123,21 +208,24 @@ def e2e_host_path(L, ctx, dh, root, flags, arena, off, dev, chunks: int = 8, rep
             with torch.cuda.stream(st):
                 c["d_json"].copy_(c["h_json"], non_blocking=True)
                 c["d_in"].copy_(c["h_in"], non_blocking=True)
-                _lib.check(L.dg_j2t_batch_device(ctx.h, dh, root, c["d_json"].data_ptr(), c["d_in"].data_ptr(), c["n"],
-                                                 flags, c["d_out"].data_ptr(), c["d_oo"].data_ptr(), c["d_ol"].data_ptr(),
-                                                 c["d_ret"].data_ptr(), None, st.cuda_stream))
-                torch.cumsum(c["d_ol"], 0, dtype=torch.int64, out=c["d_doff"][1:])
-                _lib.check(L.dg_pack_device(ctx.h, c["d_out"].data_ptr(), c["d_oo"].data_ptr(), c["d_ol"].data_ptr(),
-                                            c["n"], c["d_pack"].data_ptr(), c["d_doff"].data_ptr(), st.cuda_stream))
+                _lib.check(L.dg_j2t_batch_device_ml(ctx.h, dh, root, c["d_json"].data_ptr(), c["d_in"].data_ptr(),
+                                                    c["n"], flags, c["d_out"].data_ptr(), c["d_oo"].data_ptr(),
+                                                    c["d_ol"].data_ptr(), c["d_ret"].data_ptr(), None,
+                                                    st.cuda_stream, c["max_len"]))
+                _lib.check(L.dg_pack_device_scan(ctx.h, c["d_out"].data_ptr(), c["d_oo"].data_ptr(),
+                                                 c["d_ol"].data_ptr(), c["n"], c["d_pack"].data_ptr(),
+                                                 c["d_doff"].data_ptr(), st.cuda_stream))
                 c["h_ol"].copy_(c["d_ol"], non_blocking=True)
                 c["h_ret"].copy_(c["d_ret"], non_blocking=True)
                 if sizes is not None:
                     c["h_pack"][:sizes[k]].copy_(c["d_pack"][:sizes[k]], non_blocking=True)
+                else:
+                    c["h_doff"].copy_(c["d_doff"], non_blocking=True)
         for st in streams:
             st.synchronize()
 
-    run(None)  # warm-up: learn each chunk's packed size (deterministic)
-    sizes = [int(c["h_ol"].to(torch.int64).sum()) for c in C]
+    run(None)  # learn each chunk's packed size (deterministic)
+    sizes = [int(c["h_doff"][-1]) for c in C]
     for c, sz in zip(C, sizes):
         c["h_pack"] = torch.empty(max(sz, 1), dtype=torch.uint8).pin_memory()
     best = None
@@ -147,60 +235,99 @@ def e2e_host_path(L, ctx, dh, root, flags, arena, off, dev, chunks: int = 8, rep
         run(sizes)
         dt = time.perf_counter() - t0
         best = dt if best is None else min(best, dt)
-    # what came back is what the kernel wrote: packed bytes == the slots' used prefixes
-    c = C[0]
-    slots_h, oo_h, ol_h = c["d_out"].cpu().numpy(), c["d_oo"].cpu().numpy(), c["h_ol"].numpy()
-    want = b"".join(slots_h[int(oo_h[i]):int(oo_h[i]) + int(ol_h[i])].tobytes() for i in range(c["n"]))
-    if c["h_pack"][:sizes[0]].numpy().tobytes() != want[:sizes[0]]:
-        raise RuntimeError("e2e: packed output differs from the device slots")
+    # what came back to the host is the reference's output, message by message
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # checker only, outside the timed loop
+    chk = oracle.RefOracle() or oracle.PortOracle()
+    er, eo = chk.j2t_arena(flat, arena, off, flags, nthreads=min(CPU_SHARE, os.cpu_count() or 1))
+    bad = 0
+    for k, c in enumerate(C):
+        pk, doff, rets = c["h_pack"].numpy(), c["h_doff"].numpy(), c["h_ret"].numpy()
+        for i in range(c["n"]):
+            g = c["a"] + i
+            if int(rets[i]) != int(er[g]) or pk[doff[i]:doff[i + 1]].tobytes() != eo[g]:
+                bad += 1
+    if bad:
+        raise RuntimeError(f"e2e: {bad} messages differ from the oracle")
     json_bytes = int(off[-1] - off[0])
+    thrift = sum(sizes)
+    # the copies alone, same sizes, same chunking (what the link sustains here)
+    h_all = torch.from_numpy(np.ascontiguousarray(arena[:json_bytes])).pin_memory()
+    d_all = torch.empty_like(h_all, device=dev)
+    h_back = torch.empty(max(thrift, 1), dtype=torch.uint8).pin_memory()
+    d_back = torch.empty(max(thrift, 1), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    d_all.copy_(h_all, non_blocking=True)
+    torch.cuda.synchronize()
+    t_h2d = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    h_back.copy_(d_back, non_blocking=True)
+    torch.cuda.synchronize()
+    t_d2h = time.perf_counter() - t0
     return {"value": round(json_bytes / best / 1e9, 3), "unit": "GB/s", "ms": round(best * 1e3, 3),
-            "thrift_bytes": sum(sizes), "chunks": chunks, "streams": 2,
-            "method": "pinned H2D (JSON+offsets) -> convert -> dg_pack_device -> D2H (packed Thrift + out_len + ret), "
-                      "chunks alternating over 2 streams, wall clock, best of %d" % reps}
+            "thrift_bytes": thrift, "chunks": chunks, "streams": 2, "checked_vs_oracle": n,
+            "h2d_gbs_alone": round(json_bytes / t_h2d / 1e9, 2), "d2h_gbs_alone": round(thrift / t_d2h / 1e9, 2),
+            "method": "pinned H2D (JSON+offsets) -> convert -> dg_pack_device_scan -> D2H (packed Thrift + "
+                      "out_len + ret), chunks alternating over 2 streams of one context, wall clock, best of %d"
+                      % reps}
 
 
-def main():
+# ---------------------------------------------------------------- main
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory end-to-end measurement")
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus, argv))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+
+    # the batch is built on the CPU before anything touches the GPU (fork pool)
+    cpus = max(1, min(CPU_SHARE // max(1, world) or 1, len(os.sched_getaffinity(0))))
+    td, arena, off, meta = rank_workload(args.config, rank, world, workers=max(cpus, 2))
+
+    import torch
+    ndev = torch.cuda.device_count()
+    if ndev == 0:
+        raise SystemExit("bench.py needs an MI355X (no HIP device visible)")
+    dev = torch.device("cuda", local % ndev)
+    torch.cuda.set_device(dev)
+    backend = os.environ.get("DG_DIST_BACKEND", "nccl" if ndev >= world else "gloo")
     dist = world > 1
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
     if dist:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.distributed.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        kw = {"device_id": dev} if backend == "nccl" else {}
+        torch.distributed.init_process_group(backend, rank=rank, world_size=world, **kw)
 
-    from dynamicgo_amd import conv
-    td, msgs = make_batch(args.config, rank)
+    from dynamicgo_amd import _lib, conv
+    from dynamicgo_amd.thrift import flatten
+    import ctypes as C
     flat = flatten(td)
-    flags = 1  # conv.Options{} -> F_ALLOW_UNKNOWN (conv/j2t/conv.go:102-104)
-
-    # descriptor: built on rank 0, broadcast over RCCL, created from device memory
+    flags = FLAGS.get(args.config, 1)
     L = _lib.lib()
-    ctx = conv.Context(local)
-    if dist:
-        from dynamicgo_amd import dist as D
-        import ctypes as C
-        blob = D.broadcast_blob(flat.blob if rank == 0 else None, dev)  # RCCL over xGMI
+    ctx = conv.Context(dev.index)
+    if dist:  # descriptor: built on rank 0, broadcast, created from device memory
+        blob = share_descriptor(flat, rank, dev, backend)
         h = C.c_void_p()
         _lib.check(L.dg_desc_create_device(ctx.h, blob.data_ptr(), blob.numel(), C.byref(h)))
         ctx._descs[flat.blob] = h
     dh = ctx.desc(flat)
 
-    arena, off = W.arena(msgs)
-    n = len(msgs)
+    n = len(off) - 1
     lens = np.diff(off).astype(np.int64)
-    max_len = int(lens.max())  # known to the host that built the arena (dg_j2t_batch_device_ml)
+    max_len = int(lens.max()) if n else 0  # known to the host that built the arena (dg_j2t_batch_device_ml)
     slots = np.zeros(n + 1, dtype=np.int64)
     np.cumsum((lens * 4 + 64 + 7) & ~7, out=slots[1:])  # dg_slot_bound: 8-aligned slots
     d_json = torch.from_numpy(arena).to(dev)
@@ -210,21 +337,19 @@ def main():
     d_ol = torch.zeros(n, dtype=torch.int32, device=dev)
     d_ret = torch.zeros(n, dtype=torch.int64, device=dev)
     d_pend = torch.zeros(4, dtype=torch.int32, device=dev)
-    # a real (non-null) stream: the kernels and the timing events share it
-    stream = torch.cuda.Stream(dev)
+    stream = torch.cuda.Stream(dev)  # the kernels and the timing events share it
     torch.cuda.set_stream(stream)
 
     def step():
         _lib.check(L.dg_j2t_batch_device_ml(ctx.h, dh, flat.root_type, d_json.data_ptr(), d_in.data_ptr(), n, flags,
-                                         d_out.data_ptr(), d_oo.data_ptr(), d_ol.data_ptr(), d_ret.data_ptr(),
-                                         d_pend.data_ptr(), stream.cuda_stream, max_len))
+                                            d_out.data_ptr(), d_oo.data_ptr(), d_ol.data_ptr(), d_ret.data_ptr(),
+                                            d_pend.data_ptr(), stream.cuda_stream, max_len))
 
     ctx.stats(reset=True)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     bails, deeps = ctx.stats(reset=True)
-    # correctness of what we time: every message converted, none left pending
     rets = d_ret.cpu().numpy()
     ok = int((rets == 0).sum())
     if int(d_pend.sum().item()) != 0 or ok != n:
@@ -233,7 +358,7 @@ def main():
     thrift_bytes = int(d_ol.to(torch.int64).sum().item())
     alg_bytes = json_bytes + thrift_bytes + PER_MSG_META * n
 
-    # timed region
+    # timed region: barrier + synchronize on both sides, max over ranks
     if dist:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -249,22 +374,39 @@ def main():
         torch.distributed.barrier()
     wall = time.perf_counter() - t0
     gpu_ms = ev0.elapsed_time(ev1) / args.steps  # HIP events on the launch stream
-    t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    stats = torch.tensor([wall, float(json_bytes), float(n), gpu_ms], dtype=torch.float64,
+                         device=dev if backend == "nccl" else "cpu")
     if dist:
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-    wall_max = float(t.item())
-
-    total_json = json_bytes * world
+        gathered = [torch.zeros_like(stats) for _ in range(world)]
+        torch.distributed.all_gather(gathered, stats)
+        per_rank = [g.cpu().tolist() for g in gathered]
+    else:
+        per_rank = [stats.cpu().tolist()]
+    wall_max = max(p[0] for p in per_rank)
+    total_json = sum(p[1] for p in per_rank)
+    total_msgs = sum(p[2] for p in per_rank)
     value = total_json / wall_max * args.steps / 1e9
-    msgs_per_s = n * world * args.steps / wall_max
     achieved = alg_bytes / (gpu_ms / 1e3) / 1e9
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(flat, arena, off, flags)
     e2e = None
-    if rank == 0 and not args.no_e2e:
-        e2e = e2e_host_path(L, ctx, dh, flat.root_type, flags, arena, off, dev)
+    if rank == 0 and world == 1 and not args.no_e2e and args.config in ("c2", "c3"):
+        e2e = e2e_host_path(L, ctx, dh, flat.root_type, flags, arena, off, dev, flat)
+    c1 = None
+    if rank == 0 and args.config == "c1":  # BinaryConv.Do latency: one message, host in -> host out
+        cv = conv.BinaryConv(conv.Options(), ctx=ctx)
+        m = bytes(arena[:int(off[1])])
+        for _ in range(20):
+            cv.do(flat, m)
+        t = []
+        for _ in range(200):
+            t0 = time.perf_counter()
+            cv.do(flat, m)
+            t.append(time.perf_counter() - t0)
+        c1 = {"do_latency_us_median": round(float(np.median(t)) * 1e6, 1),
+              "note": "one message through dg_j2t_do (H2D, kernels, D2H, synchronous) from Python"}
 
     traffic = None
     tp = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
@@ -273,23 +415,32 @@ def main():
             traffic = json.load(fh).get("hbm_bytes_per_launch")
 
     if rank == 0:
+        scaling = CONFIGS[args.config][2]
         line = {
             "metric": METRIC, "value": round(value, 3), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(wall_max / args.steps * 1e3, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-            "config": {"workload": CONFIGS[args.config][0], "global_batch": n * world, "msgs_per_rank": n,
-                       "avg_json_bytes": round(json_bytes / n, 1), "msgs_per_s": round(msgs_per_s),
-                       "thrift_bytes_per_rank": thrift_bytes, "flags": flags,
-                       "parallelism": f"dp{world} (independent shards, descriptor RCCL-broadcast)",
-                       "ok_msgs_per_rank": ok,
+            "scaling": scaling, "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "config": {"workload": CONFIGS[args.config][0], "global_batch": meta["global_batch"],
+                       "msgs_per_rank": n, "avg_json_bytes": round(json_bytes / max(n, 1), 1),
+                       "msgs_per_s": round(total_msgs * args.steps / wall_max),
+                       "thrift_bytes_rank0": thrift_bytes, "flags": flags,
+                       "parallelism": f"dp{world} ({'byte-balanced shards of one batch' if scaling == 'strong' else 'one batch per rank'}, "
+                                      f"descriptor broadcast over {backend if dist else '-'}), no data-path collective",
+                       "ok_msgs_rank0": ok,
                        "exact_path_msgs_per_step": bails / max(1, args.warmup),
-                       "deep_msgs_per_step": deeps / max(1, args.warmup)},
+                       "deep_msgs_per_step": deeps / max(1, args.warmup),
+                       "per_rank_gbs": [round(p[1] / p[0] * args.steps / 1e9, 3) for p in per_rank],
+                       "per_rank_kernel_ms": [round(p[3], 5) for p in per_rank]},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                         "traffic_source": f"profiles/traffic_{args.config}.json (PMC, committed)" if traffic else None,
                          "kernel_ms": round(gpu_ms, 5), "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
-            "e2e_host": e2e,
         }
+        if e2e is not None:
+            line["e2e_host"] = e2e
+        if c1 is not None:
+            line["c1"] = c1
         print(json.dumps(line), flush=True)
     if dist:
         torch.distributed.destroy_process_group()

@@ -12,11 +12,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DG_LIB_PATH") or os.path.join(HERE, "libdgj2t.so")
 
 # symbols include/dgj2t.h declares (checked by tests/test_abi.py)
-EXPORTS = ["dg_last_error", "dg_ctx_create", "dg_ctx_destroy", "dg_ctx_stream", "dg_ctx_stats", "dg_ctx_counters",
+EXPORTS = ["dg_last_error", "dg_build_info", "dg_ctx_create", "dg_ctx_destroy", "dg_ctx_stream", "dg_ctx_stats", "dg_ctx_counters",
            "dg_desc_create",
            "dg_desc_create_device", "dg_desc_destroy", "dg_desc_root", "dg_j2t_batch_device",
            "dg_j2t_batch_device_ml",
-           "dg_slot_bound", "dg_j2t_batch_host", "dg_j2t_do", "dg_pack_device", "dg_bench_device"]
+           "dg_slot_bound", "dg_j2t_batch_host", "dg_j2t_do", "dg_pack_device", "dg_pack_device_scan", "dg_bench_device"]
 
 _lib = None
 
@@ -44,6 +44,7 @@ def lib() -> C.CDLL:
     P64 = C.POINTER(C.c_uint64)
     sig = {
         "dg_last_error": (C.c_char_p, []),
+        "dg_build_info": (C.c_char_p, []),
         "dg_ctx_create": (i32, [i32, C.POINTER(vp)]),
         "dg_ctx_destroy": (None, [vp]),
         "dg_ctx_stream": (vp, [vp]),
@@ -59,14 +60,38 @@ def lib() -> C.CDLL:
         "dg_j2t_batch_host": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, u64, vp, vp, P64]),
         "dg_j2t_do": (i32, [vp, vp, u32, C.c_char_p, sz, u64, vp, sz, C.POINTER(sz), P64]),
         "dg_pack_device": (i32, [vp, vp, vp, vp, u64, vp, vp, vp]),
+        "dg_pack_device_scan": (i32, [vp, vp, vp, vp, u64, vp, vp, vp]),
         "dg_bench_device": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, vp, vp, vp, i32, C.POINTER(C.c_float)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
+    _check_provenance(L)
     _lib = L
     return L
+
+
+BUILD_INFO = None
+
+
+def _check_provenance(L):
+    """The loaded library must be built from the sources next to it (the
+    hash build.py compiles in); a stale or foreign binary fails loudly."""
+    global BUILD_INFO
+    BUILD_INFO = L.dg_build_info().decode()
+    got = BUILD_INFO.split(":", 1)[1].split()[0] if ":" in BUILD_INFO else "?"
+    try:
+        from .build import source_hash
+        want = source_hash()
+    except OSError:  # sources not shipped: nothing to compare against
+        want = got
+    if got != want and not os.environ.get("DG_ALLOW_STALE"):
+        raise DGError(f"{LIB_PATH} was built from other sources ({got}, sources here: {want}); "
+                      "rebuild with python -m dynamicgo_amd.build")
+    if os.environ.get("DG_LOG_LIB"):
+        import sys
+        print(f"[dynamicgo_amd] loaded {LIB_PATH} ({BUILD_INFO})", file=sys.stderr, flush=True)
 
 
 def check(rc: int):

@@ -7,6 +7,7 @@
 
 Usage: python -m dynamicgo_amd.build [--no-oracle]
 """
+import hashlib
 import os
 import subprocess
 import sys
@@ -26,28 +27,99 @@ UNITS = ("j2t_kern_wave.hip", "j2t_kern_small.hip", "j2t_kern_lds.hip", "j2t_ker
 HEADERS = ("j2t_small.h", "j2t_wave.h", "j2t_machine.h", "j2t_device.h", "j2t_fast.h", "dg_tables.h")
 
 
+def source_hash(extra_flags=()) -> str:
+    """sha256 over every source the library is built from, the compiler
+    flags and the target arch: the library's identity."""
+    h = hashlib.sha256()
+    for f in sorted(UNITS + HEADERS):
+        with open(os.path.join(CSRC, f), "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read())
+    for f in ("dgj2t.h", "dgj2t_desc.h"):
+        with open(os.path.join(ROOT, "include", f), "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read())
+    h.update(repr((ARCH, COMMON_FLAGS, tuple(extra_flags))).encode())
+    return h.hexdigest()[:16]
+
+
+COMMON_FLAGS = ("-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wno-unused-result")
+MARK = b"dgj2t-build:"
+
+
+def _deps(unit: str):
+    """unit + the csrc/include headers it includes, transitively."""
+    import re
+    seen, todo = [], [unit]
+    while todo:
+        f = todo.pop()
+        if f in seen:
+            continue
+        seen.append(f)
+        p = os.path.join(CSRC, f) if os.path.exists(os.path.join(CSRC, f)) else os.path.join(ROOT, "include", f)
+        with open(p) as fh:
+            for inc in re.findall(r'^\s*#\s*include\s+"([^"]+)"', fh.read(), re.M):
+                todo.append(os.path.basename(inc))
+    return sorted(seen)
+
+
+def unit_hash(unit: str, extra_flags=()) -> str:
+    h = hashlib.sha256()
+    for f in _deps(unit):
+        p = os.path.join(CSRC, f) if os.path.exists(os.path.join(CSRC, f)) else os.path.join(ROOT, "include", f)
+        with open(p, "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read())
+    h.update(repr((ARCH, COMMON_FLAGS, tuple(extra_flags))).encode())
+    return h.hexdigest()[:16]
+
+
+def embedded_hash(path: str):
+    """The source hash compiled into a built library (dg_build_info), read
+    from the file without loading it."""
+    try:
+        with open(path, "rb") as fh:
+            data = fh.read()
+    except OSError:
+        return None
+    k = data.find(MARK)
+    if k < 0:
+        return None
+    return data[k + len(MARK):k + len(MARK) + 16].decode("ascii", "replace")
+
+
 def build_hip(force=False, extra_flags=(), out=None):
-    """Compile the translation units in parallel (one hipcc each), then link."""
+    """Compile the translation units in parallel (one hipcc each), then link.
+    Skipped only when the existing library carries the hash of exactly these
+    sources + flags (compiled in as dg_build_info); a library built from
+    anything else is rebuilt."""
     out = out or os.path.join(ROOT, "dynamicgo_amd", "libdgj2t.so")
-    srcs = [os.path.join(CSRC, f) for f in UNITS + HEADERS]
-    srcs += [os.path.join(ROOT, "include", f) for f in ("dgj2t.h", "dgj2t_desc.h")]
-    if not force and os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(s) for s in srcs):
+    sh = source_hash(extra_flags)
+    if not force and embedded_hash(out) == sh:
+        print(f"libdgj2t.so up to date (sources {sh})", flush=True)
         return out
-    objdir = os.path.join(ROOT, "build", "obj" + ("_" + str(abs(hash(tuple(extra_flags)))) if extra_flags else ""))
+    objdir = os.path.join(ROOT, "build", "obj")
     os.makedirs(objdir, exist_ok=True)
-    common = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
-              "-Wno-unused-result", *extra_flags]
+    common = [HIPCC, f"--offload-arch={ARCH}", *COMMON_FLAGS, *extra_flags]
     procs, objs = [], []
     for u in UNITS:
-        o = os.path.join(objdir, u.replace(".hip", ".o"))
-        cmd = common + ["-c", "-o", o, os.path.join(CSRC, u)]
-        print("+", " ".join(cmd), flush=True)
-        procs.append((u, subprocess.Popen(cmd)))
+        # objects are cached by the hash of what they are built from; the
+        # host unit also carries the library hash (dg_build_info)
+        uh = unit_hash(u, extra_flags) + (sh if u == "j2t_host.hip" else "")
+        o = os.path.join(objdir, u.replace(".hip", "") + "_" + uh + ".o")
         objs.append(o)
-    failed = [u for u, p in procs if p.wait() != 0]
+        if os.path.exists(o) and not force:
+            continue
+        cmd = common + ([f'-DDG_SRC_HASH="{sh}"'] if u == "j2t_host.hip" else [])
+        cmd = cmd + ["-c", "-o", o + ".tmp", os.path.join(CSRC, u)]
+        print("+", " ".join(cmd), flush=True)
+        procs.append((u, o, subprocess.Popen(cmd)))
+    failed = [u for u, o, p in procs if p.wait() != 0]
     if failed:
         raise RuntimeError(f"hipcc failed on {failed}")
-    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out, *objs])
+    for u, o, p in procs:
+        os.replace(o + ".tmp", o)
+    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out + ".tmp", *objs])
+    os.replace(out + ".tmp", out)
+    if embedded_hash(out) != sh:
+        raise RuntimeError("built library does not carry its source hash")
     return out
 
 

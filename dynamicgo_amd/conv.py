@@ -207,10 +207,14 @@ class BinaryConv:
     def _flat(self, desc) -> FlatDescriptor:
         if isinstance(desc, FlatDescriptor):
             return desc
-        f = self._flat_cache.get(id(desc))
-        if f is None:
-            f = flatten(desc)
-            self._flat_cache[id(desc)] = f
+        # keyed by id() but holding the descriptor itself: a live entry pins
+        # its object, so the id cannot be reused by another descriptor (the
+        # reference caches by *TypeDescriptor pointer the same way)
+        hit = self._flat_cache.get(id(desc))
+        if hit is not None and hit[0] is desc:
+            return hit[1]
+        f = flatten(desc)
+        self._flat_cache[id(desc)] = (desc, f)
         return f
 
     def _check_opts(self):
@@ -265,13 +269,18 @@ class BinaryConv:
 
         json: uint8[>= in_off[-1] + 16]; in_off/out_off: int64[n+1];
         out: uint8 arena; out_len: int32[n]; ret: int64[n]. Asynchronous on
-        `stream` (a torch.cuda.Stream) or the context's stream.
+        `stream` (a torch.cuda.Stream), by default torch's current stream of
+        the tensors' device, so the launch is ordered after whatever torch
+        enqueued to fill the inputs and before whatever reads the outputs.
         """
         self._check_opts()
         flat = self._flat(desc)
         ctx = self._ctx()
         n = in_off.numel() - 1
-        s = stream.cuda_stream if stream is not None else None
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream(json.device)
+        s = stream.cuda_stream
         _lib.check(_lib.lib().dg_j2t_batch_device(
             ctx.h, ctx.desc(flat), flat.root_type, json.data_ptr(), in_off.data_ptr(), n,
             to_flags(self.opts), out.data_ptr(), out_off.data_ptr(), out_len.data_ptr(), ret.data_ptr(),

@@ -35,23 +35,43 @@ static int set_err(int code, const char *fmt, ...)
         if (e_ != hipSuccess) return set_err(DG_E_HIP, "%s: %s", #x, hipGetErrorString(e_));  \
     } while (0)
 
-struct dg_ctx {
-    int device;
-    hipStream_t stream;
+/* Device scratch of one launch pipeline: the bail/big lists, their
+ * self-resetting counters, the wave queue and the workspaces. Launches on the
+ * SAME stream reuse it in stream order. Each stream a caller passes gets its
+ * own scratch (up to DG_MAX_SCRATCH per context), so concurrent streams never
+ * share lists or counters; past that cap a scratch is shared and the next
+ * launch on another stream waits for its previous launch (hipStreamWaitEvent
+ * on `done`), which keeps the ordering rule true in every case. */
+constexpr int DG_MAX_SCRATCH = 8;
+struct Scratch {
+    hipStream_t owner = nullptr;   /* the stream it was created for */
+    hipStream_t last = nullptr;    /* stream of the last launch that used it */
+    bool used = false;
+    hipEvent_t done = nullptr;     /* recorded after every launch that used it */
     uint8_t *ws_fast = nullptr;
     uint64_t ws_fast_lanes = 0;
-    uint32_t *d_deep_count = nullptr;
     uint64_t *d_deep_list = nullptr;
-    uint8_t *ws_deep = nullptr;
-    uint32_t *d_pending = nullptr;
-    unsigned long long *d_stats = nullptr; /* {bails, deeps} since the last dg_ctx_stats reset */
-    uint32_t *d_bail_count = nullptr;      /* [0] wave kernel bails, [1] large messages, [2] wave queue (self-reset) */
+    /* [0] bails, [1] large messages, [2] wave queue, [3] -, [4] deep count,
+     * [5] blocks done (deep pass): self-reset by the list-mode launch;
+     * [6] arrivals, [7] departures of dg_pack_device_scan: self-reset */
+    uint32_t *d_counts = nullptr;
     uint32_t *d_bail_list = nullptr;
     uint64_t bail_cap = 0;
     uint32_t *d_big_list = nullptr;
     uint64_t big_cap = 0;
-    int n_cu = 0;
     uint8_t *ws_wave = nullptr;
+    uint8_t *ws_deep = nullptr;
+    uint64_t *d_sums = nullptr;    /* dg_pack_device_scan: per-block byte totals (n_cu) */
+};
+
+struct dg_ctx {
+    int device;
+    hipStream_t stream;
+    int n_cu = 0;
+    uint32_t *d_pending = nullptr;
+    unsigned long long *d_stats = nullptr; /* {bails, deeps} since the last dg_ctx_stats reset */
+    std::vector<Scratch *> scratch;
+    uint32_t rr = 0; /* round-robin pick once DG_MAX_SCRATCH scratches exist */
     std::mutex mu;
     /* staging for the host API */
     uint8_t *d_json = nullptr; uint64_t d_json_cap = 0;
@@ -85,9 +105,83 @@ static int grow(T *&p, uint64_t &cap, uint64_t want)
     return DG_OK;
 }
 
+static void scratch_free(Scratch *x)
+{
+    if (!x) return;
+    if (x->used) (void)hipEventSynchronize(x->done);
+    (void)hipFree(x->ws_fast);
+    (void)hipFree(x->d_deep_list);
+    (void)hipFree(x->d_counts);
+    (void)hipFree(x->d_bail_list);
+    (void)hipFree(x->d_big_list);
+    (void)hipFree(x->ws_wave);
+    (void)hipFree(x->ws_deep);
+    (void)hipFree(x->d_sums);
+    if (x->done) (void)hipEventDestroy(x->done);
+    delete x;
+}
+
+static int scratch_new(dg_ctx *c, hipStream_t owner, Scratch **out)
+{
+    Scratch *x = new Scratch();
+    x->owner = owner;
+    hipError_t e = hipEventCreateWithFlags(&x->done, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipMalloc(&x->d_counts, 32);
+    if (e == hipSuccess) e = hipMemset(x->d_counts, 0, 32);
+    if (e == hipSuccess) e = hipMalloc(&x->ws_deep, DEEP_WS_STRIDE * DEEP_THREADS);
+    if (e == hipSuccess) e = hipMalloc(&x->ws_wave, (size_t)c->n_cu * WV_BLOCKS_PER_CU * WV_WAVES * DCAP);
+    if (e == hipSuccess) e = hipMalloc(&x->d_sums, (size_t)c->n_cu * 8);
+    if (e != hipSuccess) {
+        scratch_free(x);
+        return set_err(DG_E_HIP, "scratch allocation: %s", hipGetErrorString(e));
+    }
+    *out = x;
+    return DG_OK;
+}
+
+/* The scratch for a launch on stream s (ctx mutex held); orders s after the
+ * scratch's previous launch when that ran on another stream. */
+static int scratch_for(dg_ctx *c, hipStream_t s, Scratch **out)
+{
+    Scratch *x = nullptr;
+    for (Scratch *y : c->scratch)
+        if (y->owner == s) x = y;
+    if (!x) {
+        if ((int)c->scratch.size() < DG_MAX_SCRATCH) {
+            int rc = scratch_new(c, s, &x);
+            if (rc) return rc;
+            c->scratch.push_back(x);
+        } else {
+            x = c->scratch[c->rr++ % c->scratch.size()];
+        }
+    }
+    if (x->used && x->last != s) HIPCHK(hipStreamWaitEvent(s, x->done, 0));
+    *out = x;
+    return DG_OK;
+}
+
+/* grow a scratch buffer: the old one may still be read by the scratch's
+ * previous launch, so wait for it before freeing */
+template <class T>
+static int grow_x(Scratch *x, T *&p, uint64_t &cap, uint64_t want)
+{
+    if (cap >= want) return DG_OK;
+    if (x->used) HIPCHK(hipEventSynchronize(x->done));
+    return grow(p, cap, want);
+}
+
+#ifndef DG_SRC_HASH
+#define DG_SRC_HASH "unknown"
+#endif
+/* provenance: the source hash dynamicgo_amd/build.py compiled this library
+ * from (checked by _lib.lib() against the sources next to it) */
+static const char g_build_info[] = "dgj2t-build:" DG_SRC_HASH " arch:gfx950";
+
 extern "C" {
 
 const char *dg_last_error(void) { return g_err; }
+
+const char *dg_build_info(void) { return g_build_info; }
 
 int dg_ctx_create(int device, dg_ctx **out)
 {
@@ -99,16 +193,10 @@ int dg_ctx_create(int device, dg_ctx **out)
     dg_ctx *c = new dg_ctx();
     c->device = device;
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    HIPCHK(hipMalloc(&c->ws_deep, DEEP_WS_STRIDE * DEEP_THREADS));
     HIPCHK(hipMalloc(&c->d_pending, 16));
-    HIPCHK(hipMalloc(&c->d_deep_count, 16));
-    HIPCHK(hipMemset(c->d_deep_count, 0, 16)); /* {deep_count, done}: self-reset by each launch */
     HIPCHK(hipMalloc(&c->d_stats, 16 * 8));
     HIPCHK(hipMemset(c->d_stats, 0, 16 * 8));
-    HIPCHK(hipMalloc(&c->d_bail_count, 16));
-    HIPCHK(hipMemset(c->d_bail_count, 0, 16));
     HIPCHK(hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device));
-    HIPCHK(hipMalloc(&c->ws_wave, (size_t)c->n_cu * WV_BLOCKS_PER_CU * WV_WAVES * DCAP));
     *out = c;
     return DG_OK;
 }
@@ -118,16 +206,10 @@ void dg_ctx_destroy(dg_ctx *c)
     if (!c) return;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
-    (void)hipFree(c->ws_fast);
-    (void)hipFree(c->ws_deep);
+    for (Scratch *x : c->scratch) scratch_free(x);
+    c->scratch.clear();
     (void)hipFree(c->d_pending);
-    (void)hipFree(c->d_deep_count);
     (void)hipFree(c->d_stats);
-    (void)hipFree(c->d_bail_count);
-    (void)hipFree(c->d_bail_list);
-    (void)hipFree(c->d_big_list);
-    (void)hipFree(c->ws_wave);
-    (void)hipFree(c->d_deep_list);
     (void)hipFree(c->d_json);
     (void)hipFree(c->d_in_off);
     (void)hipFree(c->d_out);
@@ -214,27 +296,27 @@ int dg_ctx_counters(dg_ctx *c, uint64_t *out, int n, int reset)
 
 uint64_t dg_slot_bound(uint64_t len) { return (4 * len + 64 + 7) & ~7ull; }
 
-static int ensure_fast_ws(dg_ctx *c, uint64_t lanes)
+static int ensure_fast_ws(Scratch *x, uint64_t lanes)
 {
-    if (c->ws_fast_lanes >= lanes) return DG_OK;
-    (void)hipFree(c->ws_fast);
-    (void)hipFree(c->d_deep_list);
-    c->ws_fast = nullptr;
-    c->d_deep_list = nullptr;
+    if (x->ws_fast_lanes >= lanes) return DG_OK;
+    if (x->used) HIPCHK(hipEventSynchronize(x->done));
+    (void)hipFree(x->ws_fast);
+    (void)hipFree(x->d_deep_list);
+    x->ws_fast = nullptr;
+    x->d_deep_list = nullptr;
+    x->ws_fast_lanes = 0;
     uint64_t want = std::max<uint64_t>(lanes, 1 << 16);
-    HIPCHK(hipMalloc(&c->ws_fast, want * FAST_WS_STRIDE));
-    HIPCHK(hipMalloc(&c->d_deep_list, want * 8));
-    c->ws_fast_lanes = want;
+    HIPCHK(hipMalloc(&x->ws_fast, want * FAST_WS_STRIDE));
+    HIPCHK(hipMalloc(&x->d_deep_list, want * 8));
+    x->ws_fast_lanes = want;
     return DG_OK;
 }
 
-static int launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *json, const uint64_t *in_off,
-                  uint64_t n, uint64_t flags, uint8_t *out, const uint64_t *out_off, uint32_t *out_len,
-                  uint64_t *ret, uint32_t *pending, hipStream_t s, uint64_t max_len = 0)
+static int enqueue(dg_ctx *c, Scratch *x, const dg_desc *d, uint32_t root, const uint8_t *json,
+                   const uint64_t *in_off, uint64_t n, uint64_t flags, uint8_t *out, const uint64_t *out_off,
+                   uint32_t *out_len, uint64_t *ret, uint32_t *pending, hipStream_t s, uint64_t max_len)
 {
-    if (n == 0) return DG_OK;
-    if (root >= d->hdr.n_types) return set_err(DG_E_INVALID, "root type %u out of range", root);
-    int rc = ensure_fast_ws(c, n);
+    int rc = ensure_fast_ws(x, n);
     if (rc) return rc;
     const bool no_wave = (flags & DG_F_NO_WAVE_PATH) != 0;
     flags &= ~DG_F_NO_WAVE_PATH;
@@ -255,9 +337,9 @@ static int launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *jso
     P.out_len = out_len;
     P.ret = ret;
     P.pending = pending;
-    P.deep_count = c->d_deep_count;
-    P.deep_list = c->d_deep_list;
-    P.ws = c->ws_fast;
+    P.deep_count = x->d_counts + 4;
+    P.deep_list = x->d_deep_list;
+    P.ws = x->ws_fast;
     P.ws_stride = FAST_WS_STRIDE;
     P.keycap = WS_KEYCAP;
     P.reqcap = WS_REQCAP;
@@ -265,11 +347,11 @@ static int launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *jso
     P.stats = c->d_stats;
     uint64_t blocks = (n + LANE_BLOCK - 1) / LANE_BLOCK;
     DeepParams DP;
-    DP.ws = c->ws_deep;
+    DP.ws = x->ws_deep;
     DP.ws_stride = DEEP_WS_STRIDE;
     DP.keycap = DEEP_KEYCAP;
     DP.reqcap = DEEP_REQCAP;
-    DP.done = c->d_deep_count + 1;
+    DP.done = x->d_counts + 5;
     DP.blob = d->d_blob;
     DP.hdr = d->hdr;
     const char *wm = getenv("DG_WAVE_MIN"); /* messages longer than this go to the wave kernel */
@@ -288,20 +370,20 @@ static int launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *jso
          *    messages longer than big_max -> big list (when the batch has any)
          * 2. wave kernel over the big list
          * 3. lane kernel in list mode: the exact machine on the bail list */
-        if ((rc = grow(c->d_bail_list, c->bail_cap, n))) return rc;
-        if ((rc = grow(c->d_big_list, c->big_cap, n))) return rc;
+        if ((rc = grow_x(x, x->d_bail_list, x->bail_cap, n))) return rc;
+        if ((rc = grow_x(x, x->d_big_list, x->big_cap, n))) return rc;
         const bool need_wave = max_len == 0 || max_len > big_max;
         Params P1 = P;
         if (need_wave) {
-            P1.big_list = c->d_big_list;
-            P1.big_count = c->d_bail_count + 1;
+            P1.big_list = x->d_big_list;
+            P1.big_count = x->d_counts + 1;
             P1.big_max = big_max;
         }
         SmallParams S;
         S.blob = d->d_blob;
         S.hdr = d->hdr;
-        S.bail_count = c->d_bail_count;
-        S.bail_list = c->d_bail_list;
+        S.bail_count = x->d_counts;
+        S.bail_list = x->d_bail_list;
         const uint64_t mpb = (uint64_t)SM_WAVES * (uint64_t)(mpw == 64 ? 64 : mpw == 16 ? 16 : 32);
         launch_small_kernel(mpw, dim3((uint32_t)((n + mpb - 1) / mpb)), s, P1, S);
         HIPCHK(hipGetLastError());
@@ -309,20 +391,20 @@ static int launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *jso
             WaveParams W;
             W.blob = d->d_blob;
             W.hdr = d->hdr;
-            W.bail_count = c->d_bail_count;
-            W.bail_list = c->d_bail_list;
-            W.list = c->d_big_list;
-            W.list_count = c->d_bail_count + 1;
-            W.ws = c->ws_wave;
-            W.queue = c->d_bail_count + 2;
+            W.bail_count = x->d_counts;
+            W.bail_list = x->d_bail_list;
+            W.list = x->d_big_list;
+            W.list_count = x->d_counts + 1;
+            W.ws = x->ws_wave;
+            W.queue = x->d_counts + 2;
             uint64_t wblocks = std::min<uint64_t>((n + WV_WAVES - 1) / WV_WAVES, (uint64_t)c->n_cu * WV_BLOCKS_PER_CU);
             launch_wave_kernel(dim3((uint32_t)wblocks), s, P, W);
             HIPCHK(hipGetLastError());
         }
         Params P3 = P;
-        P3.list = c->d_bail_list;
-        P3.list_count = c->d_bail_count;
-        P3.reset2 = c->d_bail_count + 1; /* P3.fast stays set: the small kernel's declines try the full fast path */
+        P3.list = x->d_bail_list;
+        P3.list_count = x->d_counts;
+        P3.reset2 = x->d_counts + 1; /* P3.fast stays set: the small kernel's declines try the full fast path */
         const char *lb_env = getenv("DG_LIST_BLOCKS"); /* list-pass grid (default 16) */
         const uint64_t lb = lb_env ? std::max<uint64_t>(1, strtoull(lb_env, nullptr, 10)) : 16;
         lane_launch(dim3((uint32_t)std::min<uint64_t>(blocks, lb)), P3);
@@ -333,35 +415,56 @@ static int launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *jso
          *    messages longer than big_max are listed for the wave kernel
          * 2. wave kernel: the listed ones, one wavefront per message
          * 3. lane kernel in list mode: the wave kernel's bails, exact machine */
-        if ((rc = grow(c->d_bail_list, c->bail_cap, n))) return rc;
-        if ((rc = grow(c->d_big_list, c->big_cap, n))) return rc;
+        if ((rc = grow_x(x, x->d_bail_list, x->bail_cap, n))) return rc;
+        if ((rc = grow_x(x, x->d_big_list, x->big_cap, n))) return rc;
         Params P1 = P;
-        P1.big_list = c->d_big_list;
-        P1.big_count = c->d_bail_count + 1;
+        P1.big_list = x->d_big_list;
+        P1.big_count = x->d_counts + 1;
         P1.big_max = big_max;
         lane_launch(dim3((uint32_t)blocks), P1);
         HIPCHK(hipGetLastError());
         WaveParams W;
         W.blob = d->d_blob;
         W.hdr = d->hdr;
-        W.bail_count = c->d_bail_count;
-        W.bail_list = c->d_bail_list;
-        W.list = c->d_big_list;
-        W.list_count = c->d_bail_count + 1;
-        W.ws = c->ws_wave;
-        W.queue = c->d_bail_count + 2;
+        W.bail_count = x->d_counts;
+        W.bail_list = x->d_bail_list;
+        W.list = x->d_big_list;
+        W.list_count = x->d_counts + 1;
+        W.ws = x->ws_wave;
+        W.queue = x->d_counts + 2;
         uint64_t wblocks = std::min<uint64_t>((n + WV_WAVES - 1) / WV_WAVES, (uint64_t)c->n_cu * WV_BLOCKS_PER_CU);
         launch_wave_kernel(dim3((uint32_t)wblocks), s, P, W);
         HIPCHK(hipGetLastError());
         Params P3 = P;
-        P3.list = c->d_bail_list;
-        P3.list_count = c->d_bail_count;
-        P3.reset2 = c->d_bail_count + 1;
+        P3.list = x->d_bail_list;
+        P3.list_count = x->d_counts;
+        P3.reset2 = x->d_counts + 1;
         P3.fast = 0;
         lane_launch(dim3((uint32_t)std::min<uint64_t>(blocks, 32)), P3);
     }
     HIPCHK(hipGetLastError());
     return DG_OK;
+}
+
+/* One batch on stream s: the scratch for s, the kernels, then the scratch's
+ * `done` event. If an enqueue fails half way, the counters the list-mode
+ * launch would have reset are cleared on the stream, so the next launch on
+ * this scratch starts clean. */
+static int launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *json, const uint64_t *in_off,
+                  uint64_t n, uint64_t flags, uint8_t *out, const uint64_t *out_off, uint32_t *out_len,
+                  uint64_t *ret, uint32_t *pending, hipStream_t s, uint64_t max_len = 0)
+{
+    if (n == 0) return DG_OK;
+    if (root >= d->hdr.n_types) return set_err(DG_E_INVALID, "root type %u out of range", root);
+    Scratch *x;
+    int rc = scratch_for(c, s, &x);
+    if (rc) return rc;
+    rc = enqueue(c, x, d, root, json, in_off, n, flags, out, out_off, out_len, ret, pending, s, max_len);
+    if (rc) (void)hipMemsetAsync(x->d_counts, 0, 32, s);
+    HIPCHK(hipEventRecord(x->done, s));
+    x->used = true;
+    x->last = s;
+    return rc;
 }
 
 int dg_j2t_batch_device(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *d_json, const uint64_t *d_in_off,
@@ -426,7 +529,7 @@ int dg_j2t_batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
     std::vector<std::vector<uint8_t>> redo_out(redo.size());
     for (size_t k = 0; k < redo.size(); k++) {
         uint64_t i = redo[k];
-        uint64_t need = ret[i] >> 40;
+        uint64_t need = olen[i]; /* DG_ST_OUT_OVERFLOW: out_len carries the bytes needed */
         uint64_t one_in[2] = {0, ioff[i + 1] - ioff[i]};
         uint64_t one_out[2] = {0, need + 64};
         uint8_t *d1;
@@ -445,6 +548,8 @@ int dg_j2t_batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
         HIPCHK(hipMemcpyAsync(&ret[i], d_r, 8, hipMemcpyDeviceToHost, s));
         HIPCHK(hipMemcpyAsync(&l1, d_ol, 4, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
+        if ((uint8_t)ret[i] == DG_ST_OUT_OVERFLOW)
+            return set_err(DG_E_NOMEM, "message %llu overflowed its exact-size slot", (unsigned long long)i);
         olen[i] = l1;
         redo_out[k].resize(l1);
         if (l1) HIPCHK(hipMemcpy(redo_out[k].data(), d1, l1, hipMemcpyDeviceToHost));
@@ -468,14 +573,10 @@ int dg_j2t_batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
     HIPCHK(hipMemcpy(stage.data(), c->d_out, soff[n], hipMemcpyDeviceToHost));
     size_t rk = 0;
     for (uint64_t i = 0; i < n; i++) {
+        while (rk < redo.size() && redo[rk] < i) rk++; /* redo is ascending */
         if (!olen[i]) continue;
-        if (rk < redo.size() && redo[rk] == i) {
-            memcpy(out + out_off[i], redo_out[rk].data(), olen[i]);
-            rk++;
-        } else {
-            memcpy(out + out_off[i], stage.data() + soff[i], olen[i]);
-        }
-        while (rk < redo.size() && redo[rk] < i) rk++;
+        if (rk < redo.size() && redo[rk] == i) memcpy(out + out_off[i], redo_out[rk].data(), olen[i]);
+        else memcpy(out + out_off[i], stage.data() + soff[i], olen[i]);
     }
     return DG_OK;
 }
@@ -502,6 +603,34 @@ int dg_pack_device(dg_ctx *c, const uint8_t *d_out, const uint64_t *d_out_off, c
     uint64_t blocks = std::min<uint64_t>((n + 3) / 4, (uint64_t)c->n_cu * 8);
     launch_pack_kernel(dim3((uint32_t)blocks), s, d_out, d_out_off, d_out_len, n, d_dst, d_dst_off);
     HIPCHK(hipGetLastError());
+    return DG_OK;
+}
+
+int dg_pack_device_scan(dg_ctx *c, const uint8_t *d_out, const uint64_t *d_out_off, const uint32_t *d_out_len,
+                        uint64_t n, uint8_t *d_dst, uint64_t *d_dst_off, void *stream)
+{
+    if (!c || !d_dst_off || (n && (!d_out || !d_out_off || !d_out_len || !d_dst))) return set_err(DG_E_INVALID, "bad args");
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    if (n == 0) {
+        HIPCHK(hipMemsetAsync(d_dst_off, 0, 8, s));
+        return DG_OK;
+    }
+    Scratch *x;
+    int rc = scratch_for(c, s, &x);
+    if (rc) return rc;
+    /* every block must be resident at once (they wait for each other): at
+     * most one block per CU */
+    const uint64_t G = std::min<uint64_t>((n + 255) / 256, (uint64_t)c->n_cu);
+    launch_pack_scan_kernel(dim3((uint32_t)G), s, d_out, d_out_off, d_out_len, n, d_dst, d_dst_off, x->d_sums,
+                            x->d_counts + 6);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) (void)hipMemsetAsync(x->d_counts + 6, 0, 8, s);
+    HIPCHK(hipEventRecord(x->done, s));
+    x->used = true;
+    x->last = s;
+    if (e != hipSuccess) return set_err(DG_E_HIP, "pack scan launch: %s", hipGetErrorString(e));
     return DG_OK;
 }
 

@@ -773,7 +773,13 @@ DGI uint64_t convert_one(const Params &P, const DV &dv, uint64_t i, const S &src
 #endif
     }
     if (r == 0) m.out.finish();
-    if (r == 0 && m.out.len > m.out.cap) r = pack(DG_ST_OUT_OVERFLOW, m.out.len, 0);
+    if (r == 0 && m.out.len > m.out.cap) {
+        /* the bytes needed travel in out_len (32 bits); the 24-bit value field
+         * of the status word only carries them saturated */
+        const uint64_t need = m.out.len;
+        olen = need > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)need;
+        return pack(DG_ST_OUT_OVERFLOW, need > 0xFFFFFFull ? 0xFFFFFFull : need, 0);
+    }
     olen = r == 0 ? (uint32_t)m.out.len : 0;
     return r;
 }

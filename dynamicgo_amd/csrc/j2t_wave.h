@@ -1121,6 +1121,89 @@ __global__ __launch_bounds__(256) void dg_pack_kernel(const uint8_t *out, const 
     }
 }
 
+/* Prefix sum of out_len + packing in ONE launch (the e2e path's D2H staging).
+ * A grid of G <= #CU blocks (all co-resident): block b owns messages
+ * [b*per, (b+1)*per); it publishes its byte total, waits until every block
+ * has (agent-scope release/acquire on sync[0]), adds the totals of the blocks
+ * before it, then scans its range tile by tile (256 messages per tile),
+ * writes dst_off[i] and copies message i's bytes with one wavefront.
+ * dst_off[n] = the grand total. The last block to leave resets sync[]. */
+DGI uint64_t block_sum_u64(uint64_t v, uint64_t *red)
+{
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int d = 32; d; d >>= 1) v += __shfl_xor(v, d);
+    if (lane == 0) red[w] = v;
+    __syncthreads();
+    v = red[0] + red[1] + red[2] + red[3];
+    __syncthreads();
+    return v;
+}
+
+template <int V>
+__global__ __launch_bounds__(256) void dg_pack_scan_kernel(const uint8_t *out, const uint64_t *out_off,
+                                                           const uint32_t *out_len, uint64_t n, uint8_t *dst,
+                                                           uint64_t *dst_off, uint64_t *sums, uint32_t *sync)
+{
+    __shared__ uint64_t red[4];
+    __shared__ uint64_t s_pos[256];
+    __shared__ uint32_t s_len[256];
+    const uint32_t G = gridDim.x, b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint64_t per = (n + G - 1) / G;
+    const uint64_t lo = (uint64_t)b * per < n ? (uint64_t)b * per : n;
+    const uint64_t hi = lo + per < n ? lo + per : n;
+    uint64_t s = 0;
+    for (uint64_t i = lo + tid; i < hi; i += 256) s += out_len[i];
+    s = block_sum_u64(s, red);
+    if (tid == 0) {
+        __hip_atomic_store(&sums[b], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(&sync[0], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        while (__hip_atomic_load(&sync[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < G)
+            __builtin_amdgcn_s_sleep(4);
+    }
+    __syncthreads();
+    uint64_t base = 0;
+    for (uint32_t k = tid; k < b; k += 256) base += __hip_atomic_load(&sums[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    base = block_sum_u64(base, red);
+    for (uint64_t t0 = lo; t0 < hi; t0 += 256) {
+        const uint64_t i = t0 + tid;
+        const uint32_t len = i < hi ? out_len[i] : 0u;
+        /* block exclusive scan of len */
+        uint32_t incl = wave_incl_sum(len, lane);
+        if (lane == 63) red[w] = incl;
+        __syncthreads();
+        uint64_t wpre = 0;
+        for (uint32_t k = 0; k < w; k++) wpre += red[k];
+        const uint64_t tile = red[0] + red[1] + red[2] + red[3];
+        const uint64_t pos = base + wpre + incl - len;
+        if (i < hi) dst_off[i] = pos;
+        s_pos[tid] = pos;
+        s_len[tid] = len;
+        __syncthreads();
+        const uint32_t nt = hi - t0 < 256 ? (uint32_t)(hi - t0) : 256u;
+        for (uint32_t k = w; k < nt; k += 4) {
+            const uint32_t nb = s_len[k];
+            if (!nb) continue;
+            SrcT<const uint64_t> src;
+            src.init((const uint64_t *)(const void *)(out + out_off[t0 + k]), 0, nb);
+            coop_copy(src, 0, nb, (gu8 *)(void *)(dst + s_pos[k]), lane);
+        }
+        base += tile;
+        __syncthreads();
+    }
+    if (tid == 0) {
+        if (b == G - 1) dst_off[n] = base; /* the last range ends at the grand total */
+        const uint32_t prev = __hip_atomic_fetch_add(&sync[1], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == G - 1) { /* every block is past its wait: reset for the next launch */
+            __hip_atomic_store(&sync[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&sync[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+void launch_pack_scan_kernel(dim3 grid, hipStream_t s, const uint8_t *out, const uint64_t *out_off,
+                             const uint32_t *out_len, uint64_t n, uint8_t *dst, uint64_t *dst_off, uint64_t *sums,
+                             uint32_t *sync);
 void launch_wave_kernel(dim3 grid, hipStream_t s, const Params &P, const WaveParams &W);
 void launch_pack_kernel(dim3 grid, hipStream_t s, const uint8_t *out, const uint64_t *out_off, const uint32_t *out_len,
                         uint64_t n, uint8_t *dst, const uint64_t *dst_off);

@@ -231,3 +231,69 @@ def arena(msgs: List[bytes], pad: int = 64):
     np.cumsum(lens, out=off[1:])
     a = np.frombuffer(b"".join(msgs) + b"\0" * pad, dtype=np.uint8).copy()
     return a, off
+
+
+# ---- C5 as ONE global batch: chunk-seeded so that it can be
+# generated in parallel and identically on every rank ----
+C5_MESSAGES = 1 << 20
+C5_CHUNK = 16384
+
+
+def _mixed_chunk(args):
+    seed, c, n, large_scale = args
+    msgs = gen_mixed_batch(random.Random(seed * 1_000_003 + c), n, large_scale)
+    return b"".join(msgs), np.fromiter((len(m) for m in msgs), dtype=np.uint64, count=len(msgs))
+
+
+def gen_mixed_arena(n: int = C5_MESSAGES, seed: int = 45, workers: int = 1, large_scale: float = 1.0,
+                    chunk: int = C5_CHUNK, pad: int = 64):
+    """C5: n mixed messages as (arena, offsets[n+1]). Message block c (chunk
+    messages each) draws from Random(seed * 1000003 + c), so the batch is the
+    same whatever the worker count; workers > 1 uses a fork pool (call before
+    anything initialises the GPU)."""
+    jobs = [(seed, c, min(chunk, n - c * chunk), large_scale) for c in range((n + chunk - 1) // chunk)]
+    if workers > 1 and len(jobs) > 1:
+        import multiprocessing as mp
+        with mp.get_context("fork").Pool(min(workers, len(jobs))) as pool:
+            parts = pool.map(_mixed_chunk, jobs)
+    else:
+        parts = [_mixed_chunk(j) for j in jobs]
+    lens = np.concatenate([p[1] for p in parts]) if parts else np.zeros(0, dtype=np.uint64)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    np.cumsum(lens, out=off[1:])
+    a = np.empty(int(off[-1]) + pad, dtype=np.uint8)
+    pos = 0
+    for blob, _ in parts:
+        a[pos:pos + len(blob)] = np.frombuffer(blob, dtype=np.uint8)
+        pos += len(blob)
+    a[pos:] = 0
+    return a, off
+
+
+def arena_slice(a: np.ndarray, off: np.ndarray, lo: int, hi: int, pad: int = 64):
+    """Messages [lo, hi) of an arena as their own (arena, offsets) pair."""
+    s, e = int(off[lo]), int(off[hi])
+    sub = np.zeros(e - s + pad, dtype=np.uint8)
+    sub[:e - s] = a[s:e]
+    return sub, (off[lo:hi + 1] - off[lo]).astype(np.uint64)
+
+
+def simple_obj_shuffled(rng: random.Random) -> str:
+    """simple_obj with the six keys in a random order (C2's divergence
+    stress, SURVEY.md §8(d): lanes of a wave no longer meet the same key)."""
+    parts = ['"ByteField":%d' % rng.randint(-128, 127), '"I64Field":%d' % rng.randint(-2**63, 2**63 - 1),
+             '"DoubleField":%s' % _rdouble(rng), '"I32Field":%d' % rng.randint(-2**31, 2**31 - 1),
+             '"StringField":%s' % _rstring(rng),
+             '"BinaryField":"%s"' % base64.b64encode(rng.randbytes(rng.randint(0, 60))).decode()]
+    rng.shuffle(parts)
+    return "{" + ",".join(parts) + "}"
+
+
+def gen_flat_batch_shuffled(rng: random.Random, n: int, max_len: int = 256) -> List[bytes]:
+    """C2 divergence stress: flat Simple messages with shuffled key order."""
+    out = []
+    while len(out) < n:
+        m = simple_obj_shuffled(rng).encode()
+        if len(m) <= max_len:
+            out.append(m)
+    return out

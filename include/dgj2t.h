@@ -58,7 +58,7 @@ extern "C" {
 /* library-internal per-message statuses (code byte values the reference never
  * produces). The host entry points resolve them before returning; the device
  * entry point leaves them for the caller and counts them in *d_pending. */
-#define DG_ST_OUT_OVERFLOW 0xF0u /* slot too small; value bits = bytes needed */
+#define DG_ST_OUT_OVERFLOW 0xF0u /* slot too small; out_len = bytes needed (value bits: same, saturated at 2^24-1) */
 #define DG_ST_DEEP 0xF1u         /* (internal) nesting beyond the fast kernel's stack */
 
 /* API error codes */
@@ -73,6 +73,10 @@ typedef struct dg_desc dg_desc;
 
 /* Per-thread description of the last failure. */
 const char *dg_last_error(void);
+
+/* "dgj2t-build:<source sha256/16> arch:gfx950": what this library was built
+ * from (dynamicgo_amd/build.py); no reference counterpart. */
+const char *dg_build_info(void);
 
 /* A context owns one HIP device, a stream and device workspaces. */
 int dg_ctx_create(int device, dg_ctx **out);
@@ -106,11 +110,15 @@ uint32_t dg_desc_root(const dg_desc *desc);
  *   d_in_off    n+1 u64 offsets into d_json; message i = [in_off[i], in_off[i+1])
  *   d_out       output arena; message i may use [out_off[i], out_off[i+1])
  *   d_out_off   n+1 u64 slot bounds (e.g. prefix sum of dg_slot_bound(len))
- *   d_out_len   n u32: Thrift bytes written for message i (0 on error)
+ *   d_out_len   n u32: Thrift bytes written for message i (0 on error; for
+ *               DG_ST_OUT_OVERFLOW: the bytes the message needs)
  *   d_ret       n u64: packed reference status (0 = ok), or DG_ST_OUT_OVERFLOW
  *   d_pending   optional u32 counter (device), incremented once per message
  *               left with DG_ST_OUT_OVERFLOW; may be NULL
- * Enqueued on ctx's stream (or `stream` if non-NULL); asynchronous.
+ * Enqueued on ctx's stream (or `stream` if non-NULL); asynchronous. Launches
+ * on different streams of one context may run concurrently: each stream gets
+ * its own device scratch (lists, counters, workspaces), up to 8 streams per
+ * context; beyond that a shared scratch orders the launches with events.
  * Equivalent, per message, to BinaryConv.Do(ctx, desc, jbytes)
  * (conv/j2t/conv.go:53-77) with the given flags.
  */
@@ -147,9 +155,6 @@ int dg_j2t_batch_host(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, cons
 int dg_j2t_do(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, const uint8_t *json, size_t len,
               uint64_t flags, uint8_t *out, size_t out_cap, size_t *out_len, uint64_t *ret);
 
-/* Timing helper for benchmarks: launch the device batch `iters` times on the
- * context stream bracketed by HIP events; returns total milliseconds of GPU
- * time in *ms (events are recorded on the stream the kernels run on). */
 /* Pack the converted messages for the device->host copy: message i's
  * d_out_len[i] bytes move from its slot (d_out + d_out_off[i]) to
  * d_dst + d_dst_off[i], where d_dst_off is the exclusive prefix sum of
@@ -159,6 +164,16 @@ int dg_j2t_do(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, const uint8_
 int dg_pack_device(dg_ctx *ctx, const uint8_t *d_out, const uint64_t *d_out_off, const uint32_t *d_out_len, uint64_t n,
                    uint8_t *d_dst, const uint64_t *d_dst_off, void *stream);
 
+/* dg_pack_device with the prefix sum folded in (one launch): computes
+ * d_dst_off[0..n] = exclusive prefix sum of d_out_len (d_dst_off[n] = total
+ * bytes) and packs message i's bytes at d_dst + d_dst_off[i]. Stream-ordered
+ * after the conversion that wrote d_out_len. */
+int dg_pack_device_scan(dg_ctx *ctx, const uint8_t *d_out, const uint64_t *d_out_off, const uint32_t *d_out_len,
+                        uint64_t n, uint8_t *d_dst, uint64_t *d_dst_off, void *stream);
+
+/* Timing helper for benchmarks: launch the device batch `iters` times on the
+ * context stream bracketed by HIP events; returns total milliseconds of GPU
+ * time in *ms (events are recorded on the stream the kernels run on). */
 int dg_bench_device(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, const uint8_t *d_json,
                     const uint64_t *d_in_off, uint64_t n, uint64_t flags, uint8_t *d_out,
                     const uint64_t *d_out_off, uint32_t *d_out_len, uint64_t *d_ret, int iters,

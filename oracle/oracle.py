@@ -69,8 +69,12 @@ class _Base:
         ret = getattr(self.lib, self.p + "j2t")(d, root, json, len(json), flags, out, cap, C.byref(ol))
         if ret != 0:
             return int(ret), b""
-        if ol.value > cap:
-            raise RuntimeError("oracle output exceeded harness capacity")
+        if ol.value > cap:  # the harness reports the full length: once more with room
+            cap = ol.value + 64
+            out = C.create_string_buffer(cap)
+            ret = getattr(self.lib, self.p + "j2t")(d, root, json, len(json), flags, out, cap, C.byref(ol))
+            if ret != 0 or ol.value > cap:
+                raise RuntimeError("oracle output exceeded harness capacity")
         return 0, out.raw[:ol.value]
 
     def j2t_batch(self, flat, msgs: Sequence[bytes], flags: int, nthreads: int = 1,
@@ -104,6 +108,58 @@ class _Base:
                 o = int(out_off[i])
                 outs.append(out[o:o + int(out_len[i])].tobytes())
         return rets, outs
+
+
+    def j2t_timed(self, flat, arena: np.ndarray, in_off: np.ndarray, flags: int, cpus: Sequence[int],
+                  reps: int, root: Optional[int] = None) -> float:
+        """bench.py cpu_baseline: best-of-`reps` seconds for the whole arena,
+        len(cpus) threads each pinned to one of `cpus` (byte-balanced shards,
+        outputs preallocated here and first touched by an untimed pass).
+        Reference harness only (oracle/_ref: dgref_j2t_timed)."""
+        f = getattr(self.lib, self.p + "j2t_timed", None)
+        if f is None:
+            raise NotImplementedError("timed driver exists only in the reference harness")
+        f.restype = C.c_int
+        f.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p,
+                      C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_int), C.c_int,
+                      C.POINTER(C.c_double)]
+        n = len(in_off) - 1
+        in_off = np.ascontiguousarray(in_off, dtype=np.uint64)
+        lens = np.diff(in_off)
+        out_off = np.zeros(n + 1, dtype=np.uint64)
+        np.cumsum(lens * 4 + 64, out=out_off[1:])
+        out = np.empty(int(out_off[-1]) + 64, dtype=np.uint8)
+        out_len = np.zeros(n, dtype=np.uint32)
+        rets = np.zeros(n, dtype=np.uint64)
+        cpu_arr = (C.c_int * len(cpus))(*cpus)
+        best = C.c_double(-1.0)
+        root = flat.root_type if root is None else root
+        rc = f(self._desc(flat.blob), root, arena.ctypes.data, in_off.ctypes.data, n, flags, out.ctypes.data,
+               out_off.ctypes.data, out_len.ctypes.data, rets.ctypes.data, len(cpus), cpu_arr, reps, C.byref(best))
+        if rc != 0:
+            raise RuntimeError("dgref_j2t_timed failed")
+        return float(best.value)
+
+
+def physical_cpus() -> Tuple[List[int], int]:
+    """CPUs this process may run on, one per physical core (lowest SMT
+    sibling), and how many logical CPUs the affinity mask allows."""
+    allowed = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count() or 1))
+    seen, pick = set(), []
+    for c in allowed:
+        try:
+            base = "/sys/devices/system/cpu/cpu%d/topology/" % c
+            with open(base + "physical_package_id") as fh:
+                pkg = fh.read().strip()
+            with open(base + "core_id") as fh:
+                core = fh.read().strip()
+            key = (pkg, core)
+        except OSError:
+            key = ("?", c)
+        if key not in seen:
+            seen.add(key)
+            pick.append(c)
+    return pick, len(allowed)
 
 
 def pack_arena(msgs: Sequence[bytes]) -> Tuple[np.ndarray, np.ndarray]:

@@ -22,9 +22,12 @@
  * reference's reads of src[len] (e.g. check_leading_zero, native/scanning.c:
  * 781-786) are deterministic; the GPU path defines src[len] == 0 the same way.
  */
+#define _GNU_SOURCE 1 /* pthread_setaffinity_np, for the timed CPU baseline */
 #include "native.c"
 
 #include <pthread.h>
+#include <sched.h>
+#include <time.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -420,5 +423,96 @@ int dgref_j2t_batch(void *desc, uint32_t root, const uint8_t *json, const uint64
         pthread_join(th[t], NULL);
     free(jobs);
     free(th);
+    return 0;
+}
+
+/* ---- timed driver for bench.py's cpu_baseline (reported baseline only) ----
+ * nthreads threads, each pinned to cpus[t] (when given) and owning one
+ * contiguous byte-balanced shard, run one untimed warm-up pass (first touch
+ * of the caller's preallocated outputs) and then `reps` passes; between
+ * passes all threads meet at a barrier, so a pass's time is the slowest
+ * shard's. Returns the best pass in seconds through *best_s. */
+typedef struct {
+    Job job;
+    int cpu, tid, reps;
+    pthread_barrier_t *bar;
+    double *best;
+} TJob;
+
+static double now_s(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+static void *run_timed(void *arg)
+{
+    TJob *t = (TJob *)arg;
+    if (t->cpu >= 0) {
+        cpu_set_t cs;
+        CPU_ZERO(&cs);
+        CPU_SET(t->cpu, &cs);
+        pthread_setaffinity_np(pthread_self(), sizeof cs, &cs);
+    }
+    Job *j = &t->job;
+    RefCtx *c = ctx_new();
+    double t0 = 0;
+    for (int r = -1; r < t->reps; r++) {
+        pthread_barrier_wait(t->bar);
+        if (t->tid == 0)
+            t0 = now_s();
+        for (uint64_t i = j->lo; i < j->hi; i++) {
+            size_t ol = 0;
+            uint64_t cap = j->out_off[i + 1] - j->out_off[i];
+            j->ret[i] = ref_do(c, j->d, j->root, j->json + j->in_off[i], j->in_off[i + 1] - j->in_off[i],
+                               j->flags, j->out + j->out_off[i], cap, &ol);
+            j->out_len[i] = (uint32_t)ol;
+        }
+        pthread_barrier_wait(t->bar);
+        if (t->tid == 0 && r >= 0) {
+            double dt = now_s() - t0;
+            if (*t->best < 0 || dt < *t->best)
+                *t->best = dt;
+        }
+    }
+    ctx_free(c);
+    return NULL;
+}
+
+int dgref_j2t_timed(void *desc, uint32_t root, const uint8_t *json, const uint64_t *in_off, uint64_t n,
+                    uint64_t flags, uint8_t *out, const uint64_t *out_off, uint32_t *out_len, uint64_t *ret,
+                    int nthreads, const int *cpus, int reps, double *best_s)
+{
+    if (nthreads < 1 || reps < 1 || !best_s)
+        return -1;
+    TJob *tj = (TJob *)calloc(nthreads, sizeof(TJob));
+    pthread_t *th = (pthread_t *)calloc(nthreads, sizeof(pthread_t));
+    pthread_barrier_t bar;
+    pthread_barrier_init(&bar, NULL, (unsigned)nthreads);
+    double best = -1;
+    uint64_t total = in_off[n] - in_off[0];
+    uint64_t lo = 0;
+    for (int t = 0; t < nthreads; t++) {
+        uint64_t target = in_off[0] + total * (uint64_t)(t + 1) / nthreads;
+        uint64_t hi = lo;
+        while (hi < n && (t == nthreads - 1 || in_off[hi] < target))
+            hi++;
+        tj[t].job = (Job){(RefDesc *)desc, root, json, in_off, lo, hi, flags, out, out_off, out_len, ret};
+        tj[t].cpu = cpus ? cpus[t] : -1;
+        tj[t].tid = t;
+        tj[t].reps = reps;
+        tj[t].bar = &bar;
+        tj[t].best = &best;
+        lo = hi;
+    }
+    for (int t = 0; t < nthreads; t++)
+        pthread_create(&th[t], NULL, run_timed, &tj[t]);
+    for (int t = 0; t < nthreads; t++)
+        pthread_join(th[t], NULL);
+    pthread_barrier_destroy(&bar);
+    free(tj);
+    free(th);
+    *best_s = best;
     return 0;
 }

@@ -1,9 +1,13 @@
-"""The N>1 path on CPU (gloo, world_size 2): descriptor broadcast and
-byte-balanced sharding give each rank exactly its messages, and the per-rank
-results concatenate to the single-rank result."""
+"""The N>1 path on CPU (gloo, world_size 2), driven through bench.py's own
+rank code: rank_workload (C5 as ONE batch, byte-balanced shard per rank),
+share_descriptor (the broadcast), and spawn_ranks (bench.py --gpus N
+launching its ranks). Each rank's shard converted by the oracle concatenates
+to the whole batch's result."""
 import os
 import random
 import socket
+import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -13,6 +17,12 @@ import torch.multiprocessing as mp
 
 import oracle
 from dynamicgo_amd import dist as D, thrift as T, workloads as W
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+C5_N, C5_SCALE = 3000, 0.05
 
 
 def test_shard_ranges_cover_and_balance():
@@ -28,6 +38,19 @@ def test_shard_ranges_cover_and_balance():
     assert D.shard_ranges(np.array([0], dtype=np.uint64), 4) == [(0, 0)] * 4
 
 
+def test_c5_generation_is_worker_independent_and_shards_partition():
+    a1, o1 = W.gen_mixed_arena(C5_N, 45, workers=1, large_scale=C5_SCALE, chunk=512)
+    a2, o2 = W.gen_mixed_arena(C5_N, 45, workers=3, large_scale=C5_SCALE, chunk=512)
+    assert (o1 == o2).all() and (a1 == a2).all()
+    for world in (1, 2, 4, 8):
+        parts = [bench.rank_workload("c5", r, world, c5_n=C5_N, c5_scale=C5_SCALE) for r in range(world)]
+        assert all(p[3]["global_batch"] == C5_N for p in parts)
+        got = b"".join(bytes(p[1][:int(p[2][-1])]) for p in parts)
+        a, o = W.gen_mixed_arena(C5_N, 45, large_scale=C5_SCALE)
+        assert got == bytes(a[:int(o[-1])])
+        assert sum(len(p[2]) - 1 for p in parts) == C5_N
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -39,23 +62,22 @@ def _worker(rank, world, port, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        fl = T.flatten(W.simple_desc())
-        blob = D.broadcast_blob(fl.blob if rank == 0 else None, torch.device("cpu"))
+        td, a, off, meta = bench.rank_workload("c5", rank, world, c5_n=C5_N, c5_scale=C5_SCALE)
+        fl = T.flatten(td)
+        blob = bench.share_descriptor(fl if rank == 0 else T.FlatDescriptor(b"", fl.root_type, fl.types), rank,
+                                      torch.device("cpu"), "gloo")
         got = bytes(blob.numpy().tobytes())
-        msgs = W.gen_flat_batch(random.Random(42), 600)
-        a, off = W.arena(msgs)
-        lo, hi = D.shard_ranges(off, world)[rank]
         chk = oracle.PortOracle()
-        mine = [chk.j2t(T.FlatDescriptor(got, fl.root_type, fl.types), m, 1) for m in msgs[lo:hi]]
+        rets, outs = chk.j2t_arena(T.FlatDescriptor(got, fl.root_type, fl.types), a, off, 1)
         allr = [None] * world
-        dist.all_gather_object(allr, (lo, hi, mine))
+        dist.all_gather_object(allr, (meta["shard"], [int(r) for r in rets], outs))
         if rank == 0:
             q.put((got == fl.blob, allr))
     finally:
         dist.destroy_process_group()
 
 
-def test_gloo_world2_broadcast_and_shards():
+def test_gloo_world2_bench_rank_path():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -69,12 +91,23 @@ def test_gloo_world2_broadcast_and_shards():
             p.join(timeout=60)
     assert all(p.exitcode == 0 for p in procs)
     assert same_blob
-    msgs = W.gen_flat_batch(random.Random(42), 600)
-    fl = T.flatten(W.simple_desc())
-    chk = oracle.PortOracle()
-    whole = [chk.j2t(fl, m, 1) for m in msgs]
-    cat = []
-    for lo, hi, res in sorted(parts, key=lambda x: x[0]):
-        cat.extend(res)
-    assert parts[0][1] == parts[1][0]
-    assert cat == whole
+    td, a, off, _ = bench.rank_workload("c5", 0, 1, c5_n=C5_N, c5_scale=C5_SCALE)
+    fl = T.flatten(td)
+    rets, outs = oracle.PortOracle().j2t_arena(fl, a, off, 1)
+    parts = sorted(parts, key=lambda x: x[0][0])
+    assert parts[0][0][1] == parts[1][0][0] and parts[0][0][0] == 0 and parts[1][0][1] == C5_N
+    assert sum((p[1] for p in parts), []) == [int(r) for r in rets]
+    assert sum((p[2] for p in parts), []) == outs
+
+
+def test_spawn_ranks_sets_the_rank_env(tmp_path):
+    """bench.py --gpus N (no WORLD_SIZE) starts N children with the
+    torch.distributed env; here the child is a probe script, not the GPU run."""
+    probe = tmp_path / "probe.py"
+    probe.write_text("import os, sys\n"
+                     "open(os.path.join(sys.argv[1], 'r' + os.environ['RANK']), 'w').write("
+                     "' '.join(os.environ[k] for k in ('RANK', 'LOCAL_RANK', 'WORLD_SIZE', 'MASTER_ADDR')))\n")
+    rc = bench.spawn_ranks(3, [str(tmp_path)], script=str(probe))
+    assert rc == 0
+    for r in range(3):
+        assert (tmp_path / f"r{r}").read_text() == f"{r} {r} 3 127.0.0.1"
