@@ -98,13 +98,22 @@ def unpack_ret(ret: int) -> Tuple[int, int, int]:
     return ret & 0xFF, (ret >> 8) & 0xFFFFFFFF, ret >> 40
 
 
+# meta.ErrorCode behaviours explainNativeError files each native code under
+# (conv/j2t/impl_amd64.go:261-298, meta/error.go)
+_BEHAVIOR = {2: "ErrRead", 6: "ErrConvert", 11: "ErrUnsupportedType", 20: "ErrUnsupportedType",
+             9: "ErrDismatchType", 10: "ErrMissRequiredField", 12: "ErrUnknownField", 7: "ErrStackOverflow",
+             14: "ErrRead"}
+
+
 class J2TError(Exception):
-    """A conversion error, carrying the reference's packed status word."""
+    """A conversion error, carrying the reference's packed status word and the
+    meta behaviour explainNativeError assigns it (default ErrConvert)."""
 
     def __init__(self, ret: int, msg: str):
         super().__init__(msg)
         self.ret = ret
         self.code, self.pos, self.value = unpack_ret(ret)
+        self.behavior = _BEHAVIOR.get(self.code, "ErrConvert")
 
 
 def _locate(src: bytes, ip: int) -> str:

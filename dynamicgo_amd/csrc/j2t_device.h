@@ -206,24 +206,31 @@ struct Out {
         wbuf = 0;
         wide = ((uintptr_t)base & 7) == 0;
     }
+    /* the byte-wise edge cases (unaligned slot, last partial word of the
+     * slot) are out of line: every write site inlines only the word store */
+    static __device__ __noinline__ void store_bytes(gu8 *b, uint64_t a, uint64_t cap, uint64_t v)
+    {
+        for (int k = 0; k < 8; k++)
+            if (a + k < cap) b[a + k] = (uint8_t)(v >> (8 * k));
+    }
+    static __device__ __noinline__ uint64_t load_bytes(const gu8 *b, uint64_t a, uint64_t cap)
+    {
+        uint64_t v = 0;
+        for (int k = 0; k < 8; k++)
+            if (a + k < cap) v |= (uint64_t)b[a + k] << (8 * k);
+        return v;
+    }
     DGI void store_word(uint64_t wi, uint64_t v)
     {
         uint64_t a = wi << 3;
-        if (wide && a + 8 <= cap) {
-            *(gu64 *)(b + a) = v;
-        } else {
-            for (int k = 0; k < 8; k++)
-                if (a + k < cap) b[a + k] = (uint8_t)(v >> (8 * k));
-        }
+        if (wide && a + 8 <= cap) *(gu64 *)(b + a) = v;
+        else if (a < cap) store_bytes(b, a, cap, v);
     }
     DGI uint64_t load_word(uint64_t wi) const
     {
         uint64_t a = wi << 3;
         if (wide && a + 8 <= cap) return *(const gu64 *)(b + a);
-        uint64_t v = 0;
-        for (int k = 0; k < 8; k++)
-            if (a + k < cap) v |= (uint64_t)b[a + k] << (8 * k);
-        return v;
+        return a < cap ? load_bytes(b, a, cap) : 0;
     }
     /* append n (1..8) bytes given little-endian in v (first byte lowest) */
     DGI void wle(uint64_t v, uint32_t n)

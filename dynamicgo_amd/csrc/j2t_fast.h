@@ -377,7 +377,17 @@ DGI bool fast_binary(S &src, SI &p, Out &out)
     if (e < 0 || esc) return false; /* '\\' is outside the alphabet: decode error */
     p = e;
     SI nb = e - 1 - s0;
-    uint64_t lp = out.alloc(4);
+    /* a canonical padded body decodes to nb/4*3 - pad bytes: write that length
+     * up front (no back-patch); any other shape (\r \n, bad padding) is
+     * decoded behind a reserved length as before */
+    int64_t want = -1;
+    if ((nb & 3) == 0) {
+        const uint8_t c2 = nb ? src.raw(s0 + nb - 2) : 0, c3 = nb ? src.raw(s0 + nb - 1) : 0;
+        want = (int64_t)(nb / 4 * 3) - (c3 == '=' ? (c2 == '=' ? 2 : 1) : 0);
+    }
+    uint64_t lp = 0;
+    if (want >= 0) out.w32((uint32_t)want);
+    else lp = out.alloc(4);
     SI ip = 0;
     int64_t op = 0;
     while (ip + 8 <= nb) {
@@ -391,6 +401,7 @@ DGI bool fast_binary(S &src, SI &p, Out &out)
         op = b64decode_from(out, src, s0, nb, ip, op);
         if (op < 0) return false;
     }
+    if (want >= 0) return op == want;
     out.put32(lp, (uint32_t)op);
     return true;
 }
@@ -429,6 +440,7 @@ DGI bool fast_convert(const DV &D, S &src, Out &out, uint64_t flag, uint32_t roo
     uint64_t unwind = 0;
     uint32_t lastf = 0;
     uint32_t td = root;
+    bool vmv = false;                 /* the value is an api.js_conv field's (VM_JSCONV) */
     uint8_t c;
 
 #define FAST_PUSH(na, nk, nu)                                             \
@@ -466,6 +478,62 @@ DGI bool fast_convert(const DV &D, S &src, Out &out, uint64_t flag, uint32_t roo
         }
         const dg_type t = ldrec(&D.T[td]);
         bool opened = false; /* a container was opened: look for its first key/element */
+        if (vmv) {
+            /* j2t_field_vm VM_JSCONV (native/thrift.c:514-634): the field
+             * header is already written; a quoted or bare number into an
+             * int/double/string field, "" -> default or empty */
+            vmv = false;
+            const bool quoted = c == '"';
+            bool number = true;
+            if (quoted) {
+                if (t.ttype == DG_T_STRING) {
+                    if (!fast_string(src, p, out)) return false;
+                    number = false;
+                } else if (src.at(p) == '"') {
+                    if constexpr (LEAN) return false; /* tb_write_default_or_empty: the list pass */
+                    const dg_field f = ldrec(&D.F[lastf]);
+                    if (f.dflt_len != DG_NONE) {
+                        for (uint32_t j = 0; j < f.dflt_len; j++) out.w8(D.P[f.dflt_off + j]);
+                    } else {
+                        switch (t.ttype) { /* tb_write_empty native/thrift.c:171-203 */
+                        case DG_T_BOOL:
+                        case DG_T_BYTE: out.w8(0); break;
+                        case DG_T_I16: out.w16(0); break;
+                        case DG_T_I32: out.w32(0); break;
+                        case DG_T_I64:
+                        case DG_T_DOUBLE: out.w64(0); break;
+                        default: return false;
+                        }
+                    }
+                    p += 1;
+                    number = false;
+                }
+            } else {
+                if (c != '-' && (uint8_t)(c - '0') > 9) return false; /* ERR_INVAL */
+                p -= 1;
+            }
+            if (number) {
+                const SI s0 = p;
+                int64_t iv;
+                double dv;
+                bool isint;
+                if (!fast_vnumber(src, p, tb, iv, dv, isint)) return false;
+                if (t.ttype == DG_T_STRING) {
+                    out.w32((uint32_t)(p - s0));
+                    fast_copy(src, s0, p - s0, out);
+                } else if (t.ttype == DG_T_I16) { /* the reference's missing break: i16 then i8 */
+                    emit_number(out, DG_T_I16, isint, iv, dv);
+                    emit_number(out, DG_T_BYTE, isint, iv, dv);
+                } else if (t.ttype == DG_T_BOOL || !emit_number(out, t.ttype, isint, iv, dv)) {
+                    return false; /* ERR_UNSUPPORT_THRIFT_TYPE */
+                }
+                if (quoted) {
+                    if (src.at(p) != '"') return false;
+                    p += 1;
+                }
+            }
+            goto after_value;
+        }
         switch (c) {
         case '"':
             if (t.ttype != DG_T_STRING) return false;
@@ -526,6 +594,7 @@ DGI bool fast_convert(const DV &D, S &src, Out &out, uint64_t flag, uint32_t roo
             return false;
         }
 
+        after_value:
         /* ------------- after a value / an opening bracket ------------- */
         bool first = opened;
         for (;;) {
@@ -679,11 +748,20 @@ DGI bool fast_convert(const DV &D, S &src, Out &out, uint64_t flag, uint32_t roo
                     p = sr.p;
                     continue; /* back to "after a value" */
                 }
-                if ((flag & DG_F_ENABLE_VM) && f.vm != DG_VM_NONE) return false;
                 uint32_t k = (uint32_t)fi - sd.field_begin;
-                unwind = out.len;
-                lastf = (uint32_t)fi;
                 const dg_type ft = ldrec(&D.T[f.type]);
+                if ((flag & DG_F_ENABLE_VM) && f.vm != DG_VM_NONE) {
+                    /* value mapping (native/thrift.c:739-757): the header is
+                     * written here by j2t_field_vm's tb_write_field_begin, and
+                     * unwindPos/lastField are NOT updated (a null value is an
+                     * error there anyway); only inline js_conv is handled */
+                    if (f.vm != DG_VM_JSCONV) return false; /* ERR_VM_END / ERR_UNSUPPORT_VM_TYPE */
+                    vmv = true;
+                    lastf = (uint32_t)fi; /* read back only for the "" default (same field) */
+                } else {
+                    unwind = out.len;
+                    lastf = (uint32_t)fi;
+                }
                 out.wle((uint32_t)ft.ttype | ((uint32_t)__builtin_bswap16(f.id) << 8), 3);
                 cu &= ~(1ull << k);
                 cb = k + 1;

@@ -384,7 +384,7 @@ static int enqueue(dg_ctx *c, Scratch *x, const dg_desc *d, uint32_t root, const
         S.hdr = d->hdr;
         S.bail_count = x->d_counts;
         S.bail_list = x->d_bail_list;
-        const uint64_t mpb = (uint64_t)SM_WAVES * (uint64_t)(mpw == 64 ? 64 : mpw == 16 ? 16 : 32);
+        const uint64_t mpb = (uint64_t)SM_WAVES * (uint64_t)(mpw >= 64 ? 64 : mpw == 16 ? 16 : 32);
         launch_small_kernel(mpw, dim3((uint32_t)((n + mpb - 1) / mpb)), s, P1, S);
         HIPCHK(hipGetLastError());
         if (need_wave) {

@@ -884,14 +884,27 @@ __global__ __launch_bounds__(LANE_BLOCK) __attribute__((amdgpu_waves_per_eu(1, 1
     if (P.list) {
         /* list mode: the messages the wave kernel bailed on, on the exact
          * machine only, grid-strided over the device-side count */
+        if (threadIdx.x == 0) {
+            s_cnt = __hip_atomic_load(P.list_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (blockIdx.x == 0 && s_cnt) atomicAdd(&P.stats[0], (unsigned long long)s_cnt);
+        }
+        __syncthreads();
+        if (s_cnt == 0) {
+            /* nothing declined (the common case): no descriptor copy, no deep
+             * pass, no fences; every block saw the same zero count (nothing
+             * writes it during this launch), block 0 resets the counters the
+             * earlier launches of the pipeline left (list count is 0, the deep
+             * count and `done` are only ever raised by list work) */
+            if (blockIdx.x == 0 && threadIdx.x == 0 && P.reset2) {
+                __hip_atomic_store(P.reset2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(P.reset2 + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            return;
+        }
         if constexpr (LDS_DESC) {
             const uint4 *g = (const uint4 *)DP.blob;
             uint4 *l = (uint4 *)ldesc;
             for (uint32_t k = threadIdx.x; k < (DP.hdr.total_len + 15) / 16; k += LANE_BLOCK) l[k] = g[k];
-        }
-        if (threadIdx.x == 0) {
-            s_cnt = __hip_atomic_load(P.list_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (blockIdx.x == 0 && s_cnt) atomicAdd(&P.stats[0], (unsigned long long)s_cnt);
         }
         if (P.fast) {
             if (threadIdx.x < 20) {

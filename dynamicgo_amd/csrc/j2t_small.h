@@ -37,7 +37,7 @@ struct SmallParams {
 #ifndef DG_SMALL_WPE
 #define DG_SMALL_WPE 2 /* waves per SIMD the register budget is cut for */
 #endif
-template <int MPW>
+template <int MPW, bool LEAN = true>
 __global__ __launch_bounds__(64 * SM_WAVES) __attribute__((amdgpu_waves_per_eu(DG_SMALL_WPE))) void j2t_small_kernel(
     Params P, SmallParams S)
 {
@@ -117,10 +117,10 @@ __global__ __launch_bounds__(64 * SM_WAVES) __attribute__((amdgpu_waves_per_eu(D
         SrcT<lds_u64, int32_t> s; /* the stage is < 2 GiB: 32-bit positions */
         if (staged) s.init((lds_u64 *)(void *)stage, (int32_t)(a - base), (int32_t)(b - a));
         else s.init((lds_u64 *)(void *)stage + wbase, (int32_t)(a & 7), (int32_t)(b - a));
-        done = fast_convert<true>(dv, s, out, P.flag, P.root, ff, C::MPB, tb);
+        done = fast_convert<LEAN>(dv, s, out, P.flag, P.root, ff, C::MPB, tb);
     } else {
         SrcT<glb_u64> s = global_src(P, i);
-        done = fast_convert<true>(dv, s, out, P.flag, P.root, ff, C::MPB, tb);
+        done = fast_convert<LEAN>(dv, s, out, P.flag, P.root, ff, C::MPB, tb);
     }
     if (done) {
         P.ret[i] = 0;

@@ -119,6 +119,20 @@ def main():
     for name in ("D1", "D2", "D3", "simple", "nesting", "example3", "null", "nesting2"):
         for _ in range(250):
             add(name, rng.choice(FLAGS), fuzz.gen_message(rng, descs[name]))
+    # F_ENABLE_HM (0x8) and F_ENABLE_HM|F_TRACE_BACK (0x108): structs with
+    # HTTP-mapped fields return ERR_HM at entry (native/thrift.c:1119-1123),
+    # unset tracked fields ERR_HM_END at '}' (native/thrift.c:898-903,
+    # 952-957), mapped keys are skipped (native/thrift.c:725); the callbacks
+    # themselves are the Go host's (out of scope), the codes are the parity bar
+    hm_rng = random.Random(20261016)
+    HM_FLAGS = [0x8, 0x9, 0x108, 0x109, 0x10b, 0x12b, 0x18f]
+    for name in ("simple", "nesting", "nesting2", "example3", "null", "D1", "D2"):
+        for _ in range(60):
+            add(name, hm_rng.choice(HM_FLAGS), fuzz.gen_message(hm_rng, descs[name]))
+    for fl in HM_FLAGS:
+        add("nesting", fl, nesting_payload())
+        add("simple", fl, W.c1_simple_json())
+        add("example3", fl, ex3)
     with open(os.path.join(HERE, "j2t_golden.jsonl"), "w") as fh:
         for r in rows:
             fh.write(json.dumps(r) + "\n")

@@ -314,3 +314,52 @@ def test_small_kernel_wave_staging_vs_oracle():
     outs, rets = _raw_batch(fl, msgs, 1)
     for m, o, r in zip(msgs, outs, rets):
         assert (int(r), o) == chk.j2t(fl, m, 1), m[:120]
+
+
+@pytest.mark.parametrize("cfg", ["c2x", "c2s"])
+def test_reference_options_and_shuffled_keys_vs_oracle(cfg):
+    """c2x: the reference benchmark's options (WriteDefaultField +
+    EnableValueMapping, flags 0x7, testdata/test/baseline_j2t_test.go:721-737)
+    on the C2 batch, where I64Field carries api.js_conv: every message must
+    stay on the fast path (inline js_conv, native/thrift.c:514-634).
+    c2s: C2 with shuffled key order (the divergence stress). Both at full
+    size, byte-exact vs the oracle, zero messages on the exact machine."""
+    if cfg == "c2x":
+        msgs, flags = W.gen_flat_batch(random.Random(42), 65536), 0x7
+    else:
+        msgs, flags = W.gen_flat_batch_shuffled(random.Random(42), 65536), 0x1
+    fl = T.flatten(W.simple_desc())
+    ctx = conv.default_context()
+    ctx.stats(reset=True)
+    outs, rets = _raw_batch(fl, msgs, flags)
+    bails, deeps = ctx.stats(reset=True)
+    a, off = W.arena(msgs)
+    er, eo = _checker().j2t_arena(fl, a, off, flags, nthreads=8)
+    assert (np.asarray(rets) == er).all()
+    assert outs == eo
+    assert (bails, deeps) == (0, 0)
+
+
+def test_jsconv_value_forms_vs_oracle():
+    """api.js_conv under F_ENABLE_VM on every Thrift type the inline mapping
+    supports: quoted and bare numbers, "" (default / empty), strings,
+    quoted garbage, the i16 fall-through, and non-js_conv neighbours."""
+    rng = random.Random(101)
+    F = T.FieldDescriptor
+    fields = [F(1, "I8", T.builtin("byte"), vm=T.VM_JSCONV), F(2, "I16", T.builtin("i16"), vm=T.VM_JSCONV),
+              F(3, "I32", T.builtin("i32"), vm=T.VM_JSCONV), F(4, "I64", T.builtin("i64"), vm=T.VM_JSCONV),
+              F(5, "D", T.builtin("double"), vm=T.VM_JSCONV), F(6, "S", T.builtin("string"), vm=T.VM_JSCONV),
+              F(7, "B", T.builtin("bool"), vm=T.VM_JSCONV), F(8, "P", T.builtin("i64")),
+              F(9, "Q", T.builtin("i32"), vm=T.VM_JSCONV, default_value=b"\x00\x00\x00\x07")]
+    fl = T.flatten(T.struct_type("VM", fields))
+    vals = ['"12"', "12", '"-7"', "-7", '""', '"1.5e3"', "1.5e3", '"x"', '"12x"', "null", "true", '"abc"',
+            "300", '"70000"', "9223372036854775807", '"9223372036854775808"', "-0", '"-"', "1e400"]
+    msgs = []
+    for _ in range(3000):
+        ks = rng.sample(["I8", "I16", "I32", "I64", "D", "S", "B", "P", "Q"], rng.randint(1, 5))
+        msgs.append(("{" + ",".join('"%s":%s' % (k, rng.choice(vals)) for k in ks) + "}").encode())
+    chk = _checker()
+    for flags in (0x5, 0x7, 0x1, 0x27):
+        outs, rets = _raw_batch(fl, msgs, flags)
+        for m, o, r in zip(msgs, outs, rets):
+            assert (int(r), o) == chk.j2t(fl, m, flags), (hex(flags), m)
