@@ -16,7 +16,8 @@ EXPORTS = ["dg_last_error", "dg_build_info", "dg_ctx_create", "dg_ctx_destroy", 
            "dg_desc_create",
            "dg_desc_create_device", "dg_desc_destroy", "dg_desc_root", "dg_j2t_batch_device",
            "dg_j2t_batch_device_ml",
-           "dg_slot_bound", "dg_j2t_batch_host", "dg_j2t_do", "dg_pack_device", "dg_pack_device_scan", "dg_bench_device"]
+           "dg_slot_bound", "dg_j2t_batch_host", "dg_j2t_do", "dg_pack_device", "dg_pack_device_scan", "dg_pack_device_framed", "dg_agg_create", "dg_agg_do", "dg_agg_stats",
+           "dg_agg_destroy", "dg_bench_device"]
 
 _lib = None
 
@@ -61,6 +62,11 @@ def lib() -> C.CDLL:
         "dg_j2t_do": (i32, [vp, vp, u32, C.c_char_p, sz, u64, vp, sz, C.POINTER(sz), P64]),
         "dg_pack_device": (i32, [vp, vp, vp, vp, u64, vp, vp, vp]),
         "dg_pack_device_scan": (i32, [vp, vp, vp, vp, u64, vp, vp, vp]),
+        "dg_pack_device_framed": (i32, [vp, vp, vp, vp, vp, u64, C.c_char_p, u32, C.c_char_p, u32, vp, vp, vp]),
+        "dg_agg_create": (i32, [vp, vp, u32, u64, u32, u32, C.POINTER(vp)]),
+        "dg_agg_do": (i32, [vp, C.c_char_p, sz, vp, sz, C.POINTER(sz), P64]),
+        "dg_agg_stats": (i32, [vp, P64, P64]),
+        "dg_agg_destroy": (None, [vp]),
         "dg_bench_device": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, vp, vp, vp, i32, C.POINTER(C.c_float)]),
     }
     for name, (res, args) in sig.items():

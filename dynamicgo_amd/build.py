@@ -23,7 +23,8 @@ def _run(cmd, cwd=None):
     subprocess.run(cmd, cwd=cwd, check=True)
 
 
-UNITS = ("j2t_kern_wave.hip", "j2t_kern_small.hip", "j2t_kern_lds.hip", "j2t_kern_glb.hip", "j2t_host.hip")
+UNITS = ("j2t_kern_wave.hip", "j2t_kern_small.hip", "j2t_kern_lds.hip", "j2t_kern_glb.hip", "j2t_host.hip",
+         "j2t_agg.hip")
 HEADERS = ("j2t_small.h", "j2t_wave.h", "j2t_machine.h", "j2t_device.h", "j2t_fast.h", "dg_tables.h")
 
 
@@ -34,7 +35,7 @@ def source_hash(extra_flags=()) -> str:
     for f in sorted(UNITS + HEADERS):
         with open(os.path.join(CSRC, f), "rb") as fh:
             h.update(f.encode() + b"\0" + fh.read())
-    for f in ("dgj2t.h", "dgj2t_desc.h"):
+    for f in ("dgj2t.h", "dgj2t_defs.h", "dgj2t_desc.h"):
         with open(os.path.join(ROOT, "include", f), "rb") as fh:
             h.update(f.encode() + b"\0" + fh.read())
     h.update(repr((ARCH, COMMON_FLAGS, tuple(extra_flags))).encode())

@@ -227,9 +227,11 @@ class BinaryConv:
         return f
 
     def _check_opts(self):
-        if self.opts.EnableHttpMapping:
-            # conv/j2t/conv.go:57-68: HTTP mapping needs a request and Go callbacks
-            raise J2TError(0, "EnableHttpMapping needs host callbacks (out of scope on the GPU path)")
+        """EnableHttpMapping is accepted: the GPU returns the reference's
+        callback codes (ERR_HM at a struct with HTTP-mapped fields,
+        native/thrift.c:1119-1123; ERR_HM_END, native/thrift.c:898-903), which
+        the Go host serves from the request (conv/j2t/impl_amd64.go:174-198);
+        structs without mapped fields convert as usual."""
 
     def do(self, desc, jbytes: bytes) -> Optional[bytes]:
         """Do: returns Thrift bytes (None for an empty result) or raises J2TError."""
@@ -299,3 +301,158 @@ class BinaryConv:
 def new_binary_conv(opts: Optional[Options] = None) -> BinaryConv:
     """j2t.NewBinaryConv (conv/j2t/conv.go:36)."""
     return BinaryConv(opts)
+
+
+class Aggregator:
+    """BinaryConv.Do for many concurrent callers (dg_agg): each call blocks its
+    thread; a flusher converts whatever is queued as one device batch as soon
+    as max_batch messages wait or the oldest has waited max_wait_us. The
+    shape a cgo shim gives the reference's goroutine-parallel Do
+    (conv/j2t/conv_timing_test.go:76-99)."""
+
+    def __init__(self, desc, opts: Optional[Options] = None, max_batch: int = 4096, max_wait_us: int = 200,
+                 ctx: Optional[Context] = None):
+        self.conv = BinaryConv(opts, ctx=ctx)
+        self.flat = self.conv._flat(desc)
+        c = self.conv._ctx()
+        h = C.c_void_p()
+        _lib.check(_lib.lib().dg_agg_create(c.h, c.desc(self.flat), self.flat.root_type, to_flags(self.conv.opts),
+                                            max_batch, max_wait_us, C.byref(h)))
+        self.h = h
+
+    def do(self, jbytes: bytes) -> Optional[bytes]:
+        """BinaryConv.Do through the aggregator (thread-safe; ctypes drops the
+        GIL for the blocking call)."""
+        L = _lib.lib()
+        cap = 4 * len(jbytes) + 64
+        for _ in range(2):
+            out = C.create_string_buffer(max(cap, 1))
+            ol, ret = C.c_size_t(0), C.c_uint64(0)
+            rc = L.dg_agg_do(self.h, jbytes, len(jbytes), out, cap, C.byref(ol), C.byref(ret))
+            if rc == -3 and ol.value > cap:  # DG_E_NOMEM: retry with the size it needs
+                cap = ol.value
+                continue
+            _lib.check(rc)
+            if ret.value != 0:
+                raise J2TError(int(ret.value), explain_native_error(int(ret.value), jbytes))
+            return out.raw[:ol.value] or None
+        raise J2TError(0, "aggregator: output did not fit")
+
+    def stats(self) -> Tuple[int, int]:
+        """(batches flushed, messages converted)."""
+        b, m = C.c_uint64(0), C.c_uint64(0)
+        _lib.check(_lib.lib().dg_agg_stats(self.h, C.byref(b), C.byref(m)))
+        return int(b.value), int(m.value)
+
+    def close(self):
+        if self.h:
+            _lib.lib().dg_agg_destroy(self.h)
+            self.h = None
+
+
+# ---- HTTPConv (conv/j2t/http_conv.go) ----
+ENCODING_THRIFT_BINARY = 0  # meta.EncodingThriftBinary
+MSG_CALL = 1                # thrift.CALL (thrift/binary.go:55)
+VERSION_1 = 0x80010000      # thrift/descriptor.go:30
+
+
+def get_binary_message_header_and_footer(method: str, msg_type: int, struct_id: int,
+                                         seq_id: int = 0) -> Tuple[bytes, bytes]:
+    """thrift.GetBinaryMessageHeaderAndFooter (thrift/binary.go:137-175):
+    WriteMessageBegin (i32 VERSION_1|type, string name, i32 seq) +
+    WriteStructBegin (nothing) + WriteFieldBegin(STRUCT, id); the footer is
+    WriteFieldEnd (nothing) + WriteStructEnd (STOP) + WriteMessageEnd (nothing)."""
+    import struct as _s
+    name = method.encode()
+    hdr = (_s.pack(">I", (VERSION_1 | msg_type) & 0xFFFFFFFF) + _s.pack(">I", len(name)) + name +
+           _s.pack(">i", seq_id) + bytes([12]) + _s.pack(">h", struct_id))
+    return hdr, b"\x00"
+
+
+class HTTPConv:
+    """j2t.HTTPConv (conv/j2t/http_conv.go:28-114): the request body converted
+    with EnableHttpMapping and wrapped in the Thrift message header/footer of
+    the method's first request field. ``do_batch`` frames on the GPU
+    (dg_pack_device_framed)."""
+
+    def __init__(self, proto: int, fn_desc, ctx: Optional[Context] = None):
+        if proto != ENCODING_THRIFT_BINARY:
+            raise ValueError("now only support binary protocol")
+        first = fn_desc.request().struct.fields[0]
+        if first.type.type != 12:
+            raise ValueError("first request field doesn't have struct kind")
+        self.proto = proto
+        self.st = first.type
+        self.top, self.bottom = get_binary_message_header_and_footer(fn_desc.name, MSG_CALL, first.id, 0)
+        self.ctx = ctx
+
+    def _conv(self, opts: Optional[Options]) -> BinaryConv:
+        o = Options(**vars(opts)) if opts is not None else Options()
+        o.EnableHttpMapping = True  # conv/j2t/http_conv.go:73
+        return BinaryConv(o, ctx=self.ctx)
+
+    def do(self, req, opts: Optional[Options] = None) -> bytes:
+        """HTTPConv.Do: header + body + footer, or J2TError."""
+        body = self._conv(opts).do(self.st, req.get_body()) or b""
+        return self.top + body + self.bottom
+
+    def do_into(self, req, buf: bytearray, opts: Optional[Options] = None):
+        """HTTPConv.DoInto: appends header + body + footer to buf."""
+        out = self.do(req, opts)
+        buf.extend(out)
+
+    def do_batch(self, reqs: Sequence, opts: Optional[Options] = None):
+        """Many requests: converted and framed on the GPU. Returns (framed
+        message per request (b"" where it failed), packed status words)."""
+        import torch
+        cv = self._conv(opts)
+        ctx = cv._ctx()
+        flat = cv._flat(self.st)
+        bodies = [r.get_body() for r in reqs]
+        n = len(bodies)
+        lens = np.fromiter((len(b) for b in bodies), dtype=np.int64, count=n)
+        in_off = np.zeros(n + 1, dtype=np.int64)
+        np.cumsum(lens, out=in_off[1:])
+        slots = np.zeros(n + 1, dtype=np.int64)
+        np.cumsum((lens * 4 + 64 + 7) & ~7, out=slots[1:])
+        dev = torch.device("cuda", ctx.device)
+        st = torch.cuda.current_stream(dev)
+        d_json = torch.from_numpy(np.frombuffer(b"".join(bodies) + b"\0" * 64, dtype=np.uint8).copy()).to(dev)
+        d_in = torch.from_numpy(in_off).to(dev)
+        d_oo = torch.from_numpy(slots).to(dev)
+        d_out = torch.empty(int(slots[-1]) + 64, dtype=torch.uint8, device=dev)
+        d_ol = torch.zeros(n, dtype=torch.int32, device=dev)
+        d_ret = torch.zeros(n, dtype=torch.int64, device=dev)
+        fx = len(self.top) + len(self.bottom)
+        d_dst = torch.empty(int(slots[-1]) + fx * n + 64, dtype=torch.uint8, device=dev)
+        d_doff = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        L = _lib.lib()
+        _lib.check(L.dg_j2t_batch_device(ctx.h, ctx.desc(flat), flat.root_type, d_json.data_ptr(), d_in.data_ptr(), n,
+                                         to_flags(cv.opts), d_out.data_ptr(), d_oo.data_ptr(), d_ol.data_ptr(),
+                                         d_ret.data_ptr(), None, st.cuda_stream))
+        _lib.check(L.dg_pack_device_framed(ctx.h, d_out.data_ptr(), d_oo.data_ptr(), d_ol.data_ptr(), d_ret.data_ptr(),
+                                           n, self.top, len(self.top), self.bottom, len(self.bottom), d_dst.data_ptr(),
+                                           d_doff.data_ptr(), st.cuda_stream))
+        doff = d_doff.cpu().numpy()
+        packed = d_dst[:int(doff[-1])].cpu().numpy().tobytes()
+        rets = d_ret.cpu().numpy().astype(np.uint64)
+        pending = [i for i in range(n) if (int(rets[i]) & 0xFF) == DG_ST_OUT_OVERFLOW]
+        outs = [packed[int(doff[i]):int(doff[i + 1])] for i in range(n)]
+        for i in pending:  # slot overflow: the exact-size host rerun
+            try:
+                outs[i] = self.do(reqs[i], opts)
+                rets[i] = 0
+            except J2TError as e:
+                outs[i], rets[i] = b"", e.ret
+        return outs, rets
+
+
+class HTTPRequest:
+    """Minimal http.RequestGetter (http/http.go:63-84): what HTTPConv reads
+    from the request on the GPU path is its body."""
+
+    def __init__(self, body: bytes):
+        self.body = body
+
+    def get_body(self) -> bytes:
+        return self.body

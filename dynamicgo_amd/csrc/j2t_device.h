@@ -25,7 +25,7 @@
 
 #include <type_traits>
 
-#include "../../include/dgj2t.h"
+#include "../../include/dgj2t_defs.h"
 #include "../../include/dgj2t_desc.h"
 #include "dg_tables.h"
 
@@ -179,11 +179,24 @@ struct SrcT {
 };
 
 /* exact per-byte zero flags (0x80 in each zero byte, no false positives) */
+/* SWAR on gfx950: the VALU is 32 bits wide and takes 32-bit literal
+ * constants inline, while a 64-bit constant needs an SGPR pair (and under the
+ * kernels' SGPR pressure, spill lanes: v_readlane/v_writelane churn in the
+ * inner loops). So the byte-parallel helpers work on 32-bit halves with
+ * replicated-byte literals; no carry ever crosses a byte, let alone a half. */
+DGI uint32_t zb32(uint32_t v) { return ~(((v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | v | 0x7F7F7F7Fu); }
 DGI uint64_t zbytes(uint64_t v)
 {
-    const uint64_t M = 0x7F7F7F7F7F7F7F7Full;
-    return ~(((v & M) + M) | v | M);
+    return (uint64_t)zb32((uint32_t)v) | ((uint64_t)zb32((uint32_t)(v >> 32)) << 32);
 }
+/* 0x80 in each byte of w equal to c */
+DGI uint64_t eqbytes(uint64_t w, uint8_t c)
+{
+    const uint32_t cc = (uint32_t)c * 0x01010101u;
+    return (uint64_t)zb32((uint32_t)w ^ cc) | ((uint64_t)zb32((uint32_t)(w >> 32) ^ cc) << 32);
+}
+/* 0xFF in every byte whose top bit is set in m (m: 0x80 flags only) */
+DGI uint32_t ff32(uint32_t m) { return (m << 1) - (m >> 7); }
 
 /* Thrift output with a hard slot bound and 8-byte write combining.
  * Bytes are assembled in `wbuf` (the word holding position len) and stored
@@ -373,7 +386,7 @@ DGI int64_t advance_string(S &s, int64_t p0, bool &esc)
         I b = s.off0 + i;
         I k = b >> 3;
         uint64_t w = s.wordk(k);
-        uint64_t m = zbytes(w ^ 0x2222222222222222ull) | zbytes(w ^ 0x5C5C5C5C5C5C5C5Cull);
+        uint64_t m = eqbytes(w, '"') | eqbytes(w, '\\');
         m &= ~0ull << ((b & 7) << 3);
         I lim = s.n - (k * 8 - s.off0); /* bytes of this word inside the message */
         if (lim < 8) m &= (1ull << (lim << 3)) - 1;

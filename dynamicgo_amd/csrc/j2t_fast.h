@@ -29,6 +29,30 @@
 
 namespace dg {
 
+/* -DDG_FPROF: wave-time breakdown of the fast path by region (cycles per
+ * wave, s_memtime, summed in LDS by the first active lane of each mark) */
+#ifdef DG_FPROF
+DGI unsigned long long *fprof_slots()
+{
+    __shared__ unsigned long long s_fp[16][17]; /* [wave][0..15 regions, 16 = last mark] */
+    return &s_fp[0][0];
+}
+DGI void fprof_mark(int k)
+{
+    const uint64_t now = __builtin_amdgcn_s_memtime();
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t ex = __builtin_amdgcn_read_exec();
+    if (lane == (uint32_t)__builtin_ctzll(ex)) {
+        unsigned long long *f = fprof_slots() + w * 17;
+        f[k] += now - f[16];
+        f[16] = now;
+    }
+}
+#define FP_MARK(k) fprof_mark(k)
+#else
+#define FP_MARK(k)
+#endif
+
 /* positions inside one message: the source's index type (32-bit for an
  * LDS-staged source, 64-bit for a global one) */
 #define SI typename S::idx
@@ -46,8 +70,13 @@ typedef __attribute__((address_space(3))) FFrame LFFrame;
 typedef const __attribute__((address_space(3))) double lds_f64;
 
 /* flags the fast path handles itself; any other flag bit -> bail at entry */
+/* F_ENABLE_HM is in: its only effects are on structs with HTTP-mapped fields
+ * (ERR_HM at entry native/thrift.c:1119-1123, mapped keys skipped
+ * native/thrift.c:725), which the fast paths decline; ERR_HM_END needs
+ * F_TRACE_BACK, which stays out */
 constexpr uint64_t FAST_FLAGS = DG_F_ALLOW_UNKNOWN | DG_F_WRITE_DEFAULT | DG_F_ENABLE_VM | DG_F_ENABLE_I2S |
-                                DG_F_WRITE_REQUIRE | DG_F_NO_BASE64 | DG_F_WRITE_OPTIONAL | DG_F_NO_WRITE_BASE;
+                                DG_F_WRITE_REQUIRE | DG_F_NO_BASE64 | DG_F_WRITE_OPTIONAL | DG_F_NO_WRITE_BASE |
+                                DG_F_ENABLE_HM;
 
 /* small power tables, copied to LDS by the kernel prologue */
 struct FastTabs {
@@ -62,22 +91,43 @@ struct FastTabs {
 template <class S>
 DGI uint32_t digits8(S &src, SI i, uint64_t &x)
 {
-    const uint64_t H = 0x8080808080808080ull;
     uint64_t w = src.get8(i);
-    x = w ^ 0x3030303030303030ull;
-    uint64_t nd = (((x & 0x7F7F7F7F7F7F7F7Full) + 0x7676767676767676ull) | x) & H;
+    const uint32_t xl = (uint32_t)w ^ 0x30303030u, xh = (uint32_t)(w >> 32) ^ 0x30303030u;
+    x = (uint64_t)xl | ((uint64_t)xh << 32);
+    /* a byte is a digit iff (b ^ '0') < 10: adding 0x76 sets its top bit otherwise */
+    uint32_t ndl = (((xl & 0x7F7F7F7Fu) + 0x76767676u) | xl) & 0x80808080u;
+    uint32_t ndh = (((xh & 0x7F7F7F7Fu) + 0x76767676u) | xh) & 0x80808080u;
     SI lim = src.n - i;
-    if (lim < 8) nd |= lim <= 0 ? H : (H & (~0ull << (lim << 3)));
-    return nd ? (uint32_t)__builtin_ctzll(nd) >> 3 : 8u;
+    if (lim < 8) {
+        if (lim <= 4) {
+            ndh = 0x80808080u;
+            if (lim < 4) ndl |= lim <= 0 ? 0x80808080u : (0x80808080u & (~0u << (lim << 3)));
+        } else {
+            ndh |= 0x80808080u & (~0u << ((lim - 4) << 3));
+        }
+    }
+    if (ndl) return (uint32_t)__builtin_ctz(ndl) >> 3;
+    return ndh ? 4u + ((uint32_t)__builtin_ctz(ndh) >> 3) : 8u;
 }
 
+/* value of the first k (0..4) digits of a 32-bit group (bytes XOR '0', first
+ * digit lowest): shifts and 24-bit multiplies only */
+DGI uint32_t swar_val4(uint32_t x, uint32_t k)
+{
+    uint32_t y = k >= 4 ? x : (k == 0 ? 0u : x << ((4 - k) << 3));
+    y &= 0x0F0F0F0Fu;
+    y = (((y << 3) + (y << 1)) + (y >> 8)) & 0x00FF00FFu; /* d0*10+d1 | d2*10+d3 << 16 */
+    return __umul24(y & 0xFFu, 100u) + (y >> 16);
+}
 /* value of the first t (1..8) digits of x */
 DGI uint64_t swar_val(uint64_t x, uint32_t t)
 {
-    uint64_t y = t >= 8 ? x : x << ((8 - t) << 3);
-    y = ((y & 0x0F0F0F0F0F0F0F0Full) * 2561) >> 8;
-    y = ((y & 0x00FF00FF00FF00FFull) * 6553601) >> 16;
-    return ((y & 0x0000FFFF0000FFFFull) * 42949672960001ull) >> 32;
+    const uint32_t t1 = t < 4 ? t : 4u, t2 = t - t1;
+    const uint32_t v1 = swar_val4((uint32_t)x, t1);
+    if (!t2) return v1;
+    const uint32_t v2 = swar_val4((uint32_t)(x >> 32), t2);
+    const uint32_t p = t2 == 1 ? 10u : t2 == 2 ? 100u : t2 == 3 ? 1000u : 10000u;
+    return (uint64_t)v1 * p + v2; /* < 10^8 */
 }
 
 /* man = man * 10^t + (first t digits), t = min(k, 19 - nd) (the reference's
@@ -265,7 +315,7 @@ DGI bool fast_unquote(S &src, SI s0, SI nb, O &out)
     while (i < end) {
         uint64_t w = src.get8(i);
         SI rem = end - i;
-        uint64_t m = zbytes(w ^ 0x5C5C5C5C5C5C5C5Cull);
+        uint64_t m = eqbytes(w, '\\');
         if (rem < 8) m &= (1ull << (rem << 3)) - 1;
         if (m == 0) {
             uint32_t k = rem < 8 ? (uint32_t)rem : 8u;
@@ -344,27 +394,35 @@ DGI bool fast_string(S &src, SI &p, Out &out)
 
 /* 8 base64 characters -> 6 bytes (little-endian in *o); false if any is not
  * in the standard alphabet */
-DGI bool b64_8(uint64_t w, uint64_t &o)
+/* 4 base64 characters (little-endian in w) -> 3 bytes in output order in the
+ * low 24 bits of o; false if any is not in the standard alphabet */
+DGI bool b64_4(uint32_t w, uint32_t &o)
 {
-    const uint64_t H = 0x8080808080808080ull, L = 0x0101010101010101ull, M7 = 0x7F7F7F7F7F7F7F7Full;
+    const uint32_t H = 0x80808080u;
     if (w & H) return false;
-#define DG_GE(lo) ((w + (uint64_t)(0x80 - (lo)) * L) & H)
-    uint64_t up = DG_GE('A') & ~DG_GE('Z' + 1);
-    uint64_t lw = DG_GE('a') & ~DG_GE('z' + 1);
-    uint64_t dg = DG_GE('0') & ~DG_GE('9' + 1);
+#define DG_GE(lo) ((w + (uint32_t)(0x80 - (lo)) * 0x01010101u) & H)
+    const uint32_t up = DG_GE('A') & ~DG_GE('Z' + 1);
+    const uint32_t lw = DG_GE('a') & ~DG_GE('z' + 1);
+    const uint32_t dg = DG_GE('0') & ~DG_GE('9' + 1);
 #undef DG_GE
-    uint64_t pl = zbytes(w ^ 0x2B2B2B2B2B2B2B2Bull);
-    uint64_t sl = zbytes(w ^ 0x2F2F2F2F2F2F2F2Full);
+    const uint32_t pl = zb32(w ^ 0x2B2B2B2Bu), sl = zb32(w ^ 0x2F2F2F2Fu);
     if ((up | lw | dg | pl | sl) != H) return false;
     /* per-byte offsets: 'A'->0 (-65), 'a'->26 (-71), '0'->52 (+4), '+'->62 (+19), '/'->63 (+16) */
-    uint64_t off = (((up >> 7) * 0xFF) & (0xBFull * L)) | (((lw >> 7) * 0xFF) & (0xB9ull * L)) |
-                   (((dg >> 7) * 0xFF) & (0x04ull * L)) | (((pl >> 7) * 0xFF) & (0x13ull * L)) |
-                   (((sl >> 7) * 0xFF) & (0x10ull * L));
-    uint64_t v = ((w & M7) + (off & M7)) ^ ((w ^ off) & H); /* bytewise add mod 256 */
-    uint64_t a = ((v & 0x003F003F003F003Full) << 6) | ((v >> 8) & 0x003F003F003F003Full);
-    uint64_t b = ((a & 0x00000FFF00000FFFull) << 12) | ((a >> 16) & 0x00000FFF00000FFFull);
-    o = (uint64_t)(__builtin_bswap32((uint32_t)b) >> 8) | ((uint64_t)(__builtin_bswap32((uint32_t)(b >> 32)) >> 8) << 24);
+    const uint32_t off = (ff32(up) & 0xBFBFBFBFu) | (ff32(lw) & 0xB9B9B9B9u) | (ff32(dg) & 0x04040404u) |
+                         (ff32(pl) & 0x13131313u) | (ff32(sl) & 0x10101010u);
+    const uint32_t v = ((w & 0x7F7F7F7Fu) + (off & 0x7F7F7F7Fu)) ^ ((w ^ off) & H); /* bytewise add mod 256 */
+    const uint32_t t = ((v & 0x3Fu) << 18) | (((v >> 8) & 0x3Fu) << 12) | (((v >> 16) & 0x3Fu) << 6) | (v >> 24);
+    o = (t >> 16) | (t & 0xFF00u) | ((t & 0xFFu) << 16);
     return true;
+}
+/* 8 base64 characters -> 6 bytes (little-endian in *o); false if any is not
+ * in the standard alphabet */
+DGI bool b64_8(uint64_t w, uint64_t &o)
+{
+    uint32_t lo, hi;
+    const bool a = b64_4((uint32_t)w, lo), b = b64_4((uint32_t)(w >> 32), hi);
+    o = (uint64_t)lo | ((uint64_t)hi << 24);
+    return a && b;
 }
 
 /* j2t_binary (native/thrift.c:401-420) */
@@ -471,6 +529,7 @@ DGI bool fast_convert(const DV &D, S &src, Out &out, uint64_t flag, uint32_t roo
 
     for (;;) {
         /* ---------------- a value of type td ---------------- */
+        FP_MARK(0);
         c = src.at(p++);
         while (c <= ' ') {
             if (!isspace_(c)) return false;
@@ -478,6 +537,7 @@ DGI bool fast_convert(const DV &D, S &src, Out &out, uint64_t flag, uint32_t roo
         }
         const dg_type t = ldrec(&D.T[td]);
         bool opened = false; /* a container was opened: look for its first key/element */
+        FP_MARK(1);
         if (vmv) {
             /* j2t_field_vm VM_JSCONV (native/thrift.c:514-634): the field
              * header is already written; a quoted or bare number into an
@@ -539,8 +599,10 @@ DGI bool fast_convert(const DV &D, S &src, Out &out, uint64_t flag, uint32_t roo
             if (t.ttype != DG_T_STRING) return false;
             if ((flag & DG_F_NO_BASE64) == 0 && (t.flags & DG_TF_BINARY)) {
                 if (!fast_binary(src, p, out)) return false;
+                FP_MARK(2);
             } else {
                 if (!fast_string(src, p, out)) return false;
+                FP_MARK(3);
             }
             break;
         case '0': case '1': case '2': case '3': case '4':
@@ -550,7 +612,9 @@ DGI bool fast_convert(const DV &D, S &src, Out &out, uint64_t flag, uint32_t roo
             double dv;
             bool isint;
             if (!fast_vnumber(src, p, tb, iv, dv, isint)) return false;
+            FP_MARK(4);
             if (!emit_number(out, t.ttype, isint, iv, dv)) return false;
+            FP_MARK(5);
             break;
         }
         case 't':
@@ -580,6 +644,7 @@ DGI bool fast_convert(const DV &D, S &src, Out &out, uint64_t flag, uint32_t roo
             if (t.ttype == DG_T_STRUCT) {
                 const dg_struct sd = ldrec(&D.S[t.st]);
                 if (sd.req_words != 1) return false;
+                if ((flag & DG_F_ENABLE_HM) && (sd.flags & DG_SF_HTTP_MAPPING)) return false; /* ERR_HM callback */
                 FAST_PUSH(t.st, FK_STRUCT, D.R[sd.req_begin]);
             } else if (t.ttype == DG_T_MAP) {
                 out.wle(ldrec(&D.T[t.key]).ttype | ((uint32_t)ldrec(&D.T[t.elem]).ttype << 8), 2);
@@ -596,6 +661,7 @@ DGI bool fast_convert(const DV &D, S &src, Out &out, uint64_t flag, uint32_t roo
 
         after_value:
         /* ------------- after a value / an opening bracket ------------- */
+        FP_MARK(6);
         bool first = opened;
         for (;;) {
             if (sp == 0) {
@@ -676,20 +742,43 @@ DGI bool fast_convert(const DV &D, S &src, Out &out, uint64_t flag, uint32_t roo
                 }
             }
             /* a key */
+            FP_MARK(7);
             if (c != '"') return false;
             {
                 SI k0 = p;
-                bool esc;
-                SI e = advance_string(src, k0, esc);
-                if (e < 0 || esc) return false;
-                p = e;
-                uint32_t kn = (uint32_t)(e - 1 - k0);
+                uint32_t kn;
+                int32_t fi = -1;
+                dg_field f;
+                /* the predicted field (the one after the previous): its plain
+                 * alias followed by the closing quote IS the key advance_string
+                 * would find, so one compare replaces the scan and the lookup */
+                if (ck == FK_STRUCT) {
+                    const dg_struct sdp = ldrec(&D.S[ca]);
+                    if (cb < sdp.n_fields) {
+                        f = ldrec(&D.F[sdp.field_begin + cb]);
+                        kn = f.key_len;
+                        if ((f.flags & (DG_FF_ALIAS_SELF | DG_FF_KEY_PLAIN)) == (DG_FF_ALIAS_SELF | DG_FF_KEY_PLAIN) &&
+                            k0 + (SI)kn < src.n && key_eq(src, k0, kn, (decltype(&D.R[0]))(&D.P[f.key_off])) &&
+                            src.raw(k0 + (SI)kn) == '"') {
+                            fi = (int32_t)(sdp.field_begin + cb);
+                            p = k0 + (SI)kn + 1;
+                        }
+                    }
+                }
+                if (fi < 0) {
+                    bool esc;
+                    SI e = advance_string(src, k0, esc);
+                    if (e < 0 || esc) return false;
+                    p = e;
+                    kn = (uint32_t)(e - 1 - k0);
+                }
                 c = src.at(p++);
                 while (c <= ' ') {
                     if (!isspace_(c)) return false;
                     c = src.at(p++);
                 }
                 if (c != ':') return false;
+                FP_MARK(8);
                 if (ck == FK_MAP) { /* j2t_map_key native/thrift.c:422-447 */
                     unwind = out.len;
                     const uint8_t kt = ldrec(&D.T[(uint32_t)(cu >> 32)]).ttype;
@@ -711,9 +800,7 @@ DGI bool fast_convert(const DV &D, S &src, Out &out, uint64_t flag, uint32_t roo
                 }
                 /* struct field: predicted, then hashed (j2t_key native/thrift.c:668-763) */
                 const dg_struct sd = ldrec(&D.S[ca]);
-                int32_t fi = -1;
-                dg_field f;
-                if (cb < sd.n_fields) {
+                if (fi < 0 && cb < sd.n_fields) {
                     f = ldrec(&D.F[sd.field_begin + cb]);
                     if ((f.flags & DG_FF_ALIAS_SELF) && f.key_len == kn &&
                         key_eq(src, k0, kn, (decltype(&D.R[0]))(&D.P[f.key_off])))
@@ -721,7 +808,13 @@ DGI bool fast_convert(const DV &D, S &src, Out &out, uint64_t flag, uint32_t roo
                 }
                 if (fi < 0) {
                     uint32_t h = DG_NAME_HASH_SEED;
-                    for (uint32_t j = 0; j < kn; j++) h = DG_NAME_HASH_STEP(h, src.raw(k0 + j));
+                    for (uint32_t j = 0; j < kn; j += 8) { /* a word per 8 key bytes (16 readable bytes past the end) */
+                        const uint64_t w = src.get8(k0 + (SI)j);
+                        const uint32_t r = kn - j < 8 ? kn - j : 8u;
+#pragma unroll
+                        for (uint32_t b = 0; b < 8; b++)
+                            if (b < r) h = DG_NAME_HASH_STEP(h, (uint8_t)(w >> (8 * b)));
+                    }
                     for (uint32_t s = h & sd.name_mask;; s = (s + 1) & sd.name_mask) {
                         const dg_name nm = ldrec(&D.N[sd.name_begin + s]);
                         if (nm.field == DG_NONE) break;
@@ -766,9 +859,11 @@ DGI bool fast_convert(const DV &D, S &src, Out &out, uint64_t flag, uint32_t roo
                 cu &= ~(1ull << k);
                 cb = k + 1;
                 td = f.type;
+                FP_MARK(9);
                 break;
             }
         close_struct: { /* j2t_write_unset_fields native/thrift.c:258-310, then STOP */
+            FP_MARK(10);
             const dg_struct sd = ldrec(&D.S[ca]);
             uint64_t bits = cu;
             bool wr = flag & DG_F_WRITE_REQUIRE, wd = flag & DG_F_WRITE_DEFAULT, wo = flag & DG_F_WRITE_OPTIONAL;
@@ -812,6 +907,7 @@ DGI bool fast_convert(const DV &D, S &src, Out &out, uint64_t flag, uint32_t roo
             }
             out.w8(0);
             FAST_POP();
+            FP_MARK(11);
             continue;
         }
         }

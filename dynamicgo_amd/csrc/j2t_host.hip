@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "j2t_small.h"
+#include "../../include/dgj2t.h"
 
 /* ========================================================================== */
 /* host side: C ABI                                                            */
@@ -62,7 +63,10 @@ struct Scratch {
     uint8_t *ws_wave = nullptr;
     uint8_t *ws_deep = nullptr;
     uint64_t *d_sums = nullptr;    /* dg_pack_device_scan: per-block byte totals (n_cu) */
+    uint8_t *d_frame = nullptr;    /* dg_pack_device_framed: header + footer bytes */
+    std::vector<uint8_t> frame;    /* what d_frame holds */
 };
+constexpr uint32_t FRAME_CAP = 4096;
 
 struct dg_ctx {
     int device;
@@ -117,6 +121,7 @@ static void scratch_free(Scratch *x)
     (void)hipFree(x->ws_wave);
     (void)hipFree(x->ws_deep);
     (void)hipFree(x->d_sums);
+    (void)hipFree(x->d_frame);
     if (x->done) (void)hipEventDestroy(x->done);
     delete x;
 }
@@ -131,6 +136,7 @@ static int scratch_new(dg_ctx *c, hipStream_t owner, Scratch **out)
     if (e == hipSuccess) e = hipMalloc(&x->ws_deep, DEEP_WS_STRIDE * DEEP_THREADS);
     if (e == hipSuccess) e = hipMalloc(&x->ws_wave, (size_t)c->n_cu * WV_BLOCKS_PER_CU * WV_WAVES * DCAP);
     if (e == hipSuccess) e = hipMalloc(&x->d_sums, (size_t)c->n_cu * 8);
+    if (e == hipSuccess) e = hipMalloc(&x->d_frame, FRAME_CAP);
     if (e != hipSuccess) {
         scratch_free(x);
         return set_err(DG_E_HIP, "scratch allocation: %s", hipGetErrorString(e));
@@ -192,7 +198,10 @@ int dg_ctx_create(int device, dg_ctx **out)
     HIPCHK(hipSetDevice(device));
     dg_ctx *c = new dg_ctx();
     c->device = device;
-    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    /* a blocking stream: ordered with the legacy default stream (handle 0), so
+     * a caller passing stream NULL (torch's default stream) sees the results
+     * in order */
+    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamDefault));
     HIPCHK(hipMalloc(&c->d_pending, 16));
     HIPCHK(hipMalloc(&c->d_stats, 16 * 8));
     HIPCHK(hipMemset(c->d_stats, 0, 16 * 8));
@@ -606,10 +615,10 @@ int dg_pack_device(dg_ctx *c, const uint8_t *d_out, const uint64_t *d_out_off, c
     return DG_OK;
 }
 
-int dg_pack_device_scan(dg_ctx *c, const uint8_t *d_out, const uint64_t *d_out_off, const uint32_t *d_out_len,
-                        uint64_t n, uint8_t *d_dst, uint64_t *d_dst_off, void *stream)
+static int pack_scan(dg_ctx *c, const uint8_t *d_out, const uint64_t *d_out_off, const uint32_t *d_out_len,
+                     const uint64_t *d_ret, uint64_t n, const uint8_t *hdr, uint32_t hdr_len, const uint8_t *ftr,
+                     uint32_t ftr_len, uint8_t *d_dst, uint64_t *d_dst_off, void *stream)
 {
-    if (!c || !d_dst_off || (n && (!d_out || !d_out_off || !d_out_len || !d_dst))) return set_err(DG_E_INVALID, "bad args");
     std::lock_guard<std::mutex> g(c->mu);
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
@@ -620,11 +629,31 @@ int dg_pack_device_scan(dg_ctx *c, const uint8_t *d_out, const uint64_t *d_out_o
     Scratch *x;
     int rc = scratch_for(c, s, &x);
     if (rc) return rc;
+    MsgFrame fr{};
+    if (hdr) {
+        /* header at 0, footer 8-aligned after it; both followed by >= 16 readable bytes */
+        const uint32_t fo = (hdr_len + 7) & ~7u;
+        std::vector<uint8_t> tmp(fo + ftr_len + 16, 0);
+        memcpy(tmp.data(), hdr, hdr_len);
+        if (ftr_len) memcpy(tmp.data() + fo, ftr, ftr_len);
+        if (tmp != x->frame) {
+            /* a new header/footer (a new method): wait until the scratch's
+             * last launch is done reading the old one, then upload */
+            if (x->used) HIPCHK(hipEventSynchronize(x->done));
+            HIPCHK(hipMemcpy(x->d_frame, tmp.data(), tmp.size(), hipMemcpyHostToDevice));
+            x->frame = tmp;
+        }
+        fr.hdr = x->d_frame;
+        fr.hdr_len = hdr_len;
+        fr.ftr = x->d_frame + fo;
+        fr.ftr_len = ftr_len;
+        fr.ret = d_ret;
+    }
     /* every block must be resident at once (they wait for each other): at
      * most one block per CU */
     const uint64_t G = std::min<uint64_t>((n + 255) / 256, (uint64_t)c->n_cu);
     launch_pack_scan_kernel(dim3((uint32_t)G), s, d_out, d_out_off, d_out_len, n, d_dst, d_dst_off, x->d_sums,
-                            x->d_counts + 6);
+                            x->d_counts + 6, fr);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) (void)hipMemsetAsync(x->d_counts + 6, 0, 8, s);
     HIPCHK(hipEventRecord(x->done, s));
@@ -632,6 +661,23 @@ int dg_pack_device_scan(dg_ctx *c, const uint8_t *d_out, const uint64_t *d_out_o
     x->last = s;
     if (e != hipSuccess) return set_err(DG_E_HIP, "pack scan launch: %s", hipGetErrorString(e));
     return DG_OK;
+}
+
+int dg_pack_device_scan(dg_ctx *c, const uint8_t *d_out, const uint64_t *d_out_off, const uint32_t *d_out_len,
+                        uint64_t n, uint8_t *d_dst, uint64_t *d_dst_off, void *stream)
+{
+    if (!c || !d_dst_off || (n && (!d_out || !d_out_off || !d_out_len || !d_dst))) return set_err(DG_E_INVALID, "bad args");
+    return pack_scan(c, d_out, d_out_off, d_out_len, nullptr, n, nullptr, 0, nullptr, 0, d_dst, d_dst_off, stream);
+}
+
+int dg_pack_device_framed(dg_ctx *c, const uint8_t *d_out, const uint64_t *d_out_off, const uint32_t *d_out_len,
+                          const uint64_t *d_ret, uint64_t n, const uint8_t *hdr, uint32_t hdr_len, const uint8_t *ftr,
+                          uint32_t ftr_len, uint8_t *d_dst, uint64_t *d_dst_off, void *stream)
+{
+    if (!c || !d_dst_off || !hdr || (ftr_len && !ftr) || ((hdr_len + 7) & ~7u) + ftr_len + 16 > FRAME_CAP ||
+        (n && (!d_out || !d_out_off || !d_out_len || !d_ret || !d_dst)))
+        return set_err(DG_E_INVALID, "bad args");
+    return pack_scan(c, d_out, d_out_off, d_out_len, d_ret, n, hdr, hdr_len, ftr, ftr_len, d_dst, d_dst_off, stream);
 }
 
 int dg_bench_device(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *d_json, const uint64_t *d_in_off,

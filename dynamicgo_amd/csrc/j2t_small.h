@@ -70,6 +70,10 @@ __global__ __launch_bounds__(64 * SM_WAVES) __attribute__((amdgpu_waves_per_eu(D
         s_p10u[tid] = v;
     }
     if (tid < 23) s_p10d[tid] = P10[tid];
+#ifdef DG_FPROF
+    if (lane < 17) fprof_slots()[wave * 17 + lane] = lane == 16 ? __builtin_amdgcn_s_memtime() : 0;
+    FP_MARK(12);
+#endif
     __syncthreads();
     const uint32_t j = wave * MPW + lane; /* message slot within the block */
     const uint64_t i = b0 + j;
@@ -129,6 +133,10 @@ __global__ __launch_bounds__(64 * SM_WAVES) __attribute__((amdgpu_waves_per_eu(D
         uint32_t q = atomicAdd(S.bail_count, 1u);
         S.bail_list[q] = (uint32_t)i;
     }
+#ifdef DG_FPROF
+    FP_MARK(13);
+    if (lane < 14) atomicAdd(&P.stats[2 + lane], fprof_slots()[wave * 17 + lane]);
+#endif
 }
 
 void launch_small_kernel(int mpw, dim3 grid, hipStream_t s, const Params &P, const SmallParams &S);

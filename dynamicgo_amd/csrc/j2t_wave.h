@@ -256,7 +256,7 @@ template <class S>
 DGI bool has_bslash(S &src, int64_t s0, int64_t n)
 {
     for (int64_t i = 0; i < n; i += 8) {
-        uint64_t m = zbytes(src.get8(s0 + i) ^ 0x5C5C5C5C5C5C5C5Cull);
+        uint64_t m = eqbytes(src.get8(s0 + i), 0x5C);
         int64_t rem = n - i;
         if (rem < 8) m &= (1ull << (rem << 3)) - 1;
         if (m) return true;
@@ -713,7 +713,9 @@ DGI bool wave_run(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L
                             if (kind == K_LBRACE) {
                                 if (ct.ttype == DG_T_STRUCT) {
                                     c.flags |= CF_STRUCT;
-                                    if (ldrec(&D.S[ct.st]).req_words != 1) bad = true;
+                                    const dg_struct csd = ldrec(&D.S[ct.st]);
+                                    if (csd.req_words != 1) bad = true;
+                                    if ((flag & DG_F_ENABLE_HM) && (csd.flags & DG_SF_HTTP_MAPPING)) bad = true;
                                 } else if (ct.ttype == DG_T_MAP) {
                                     c.flags |= CF_MAP;
                                 } else {
@@ -1140,10 +1142,21 @@ DGI uint64_t block_sum_u64(uint64_t v, uint64_t *red)
     return v;
 }
 
+/* Framing (HTTPConv.Do, conv/j2t/http_conv.go:68-94): with fr.hdr set, a
+ * message that converted (ret 0) is packed as hdr + body + ftr, one that
+ * failed as nothing. */
+struct MsgFrame {
+    const uint8_t *hdr; /* device; 16 readable bytes past the end */
+    uint32_t hdr_len;
+    const uint8_t *ftr;
+    uint32_t ftr_len;
+    const uint64_t *ret;
+};
+
 template <int V>
 __global__ __launch_bounds__(256) void dg_pack_scan_kernel(const uint8_t *out, const uint64_t *out_off,
                                                            const uint32_t *out_len, uint64_t n, uint8_t *dst,
-                                                           uint64_t *dst_off, uint64_t *sums, uint32_t *sync)
+                                                           uint64_t *dst_off, uint64_t *sums, uint32_t *sync, MsgFrame fr)
 {
     __shared__ uint64_t red[4];
     __shared__ uint64_t s_pos[256];
@@ -1152,8 +1165,13 @@ __global__ __launch_bounds__(256) void dg_pack_scan_kernel(const uint8_t *out, c
     const uint64_t per = (n + G - 1) / G;
     const uint64_t lo = (uint64_t)b * per < n ? (uint64_t)b * per : n;
     const uint64_t hi = lo + per < n ? lo + per : n;
+    const uint32_t fx = fr.hdr ? fr.hdr_len + fr.ftr_len : 0u;
+    auto msg_len = [&](uint64_t i) -> uint32_t {
+        if (!fr.hdr) return out_len[i];
+        return fr.ret[i] == 0 ? out_len[i] + fx : 0u;
+    };
     uint64_t s = 0;
-    for (uint64_t i = lo + tid; i < hi; i += 256) s += out_len[i];
+    for (uint64_t i = lo + tid; i < hi; i += 256) s += msg_len(i);
     s = block_sum_u64(s, red);
     if (tid == 0) {
         __hip_atomic_store(&sums[b], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1167,7 +1185,7 @@ __global__ __launch_bounds__(256) void dg_pack_scan_kernel(const uint8_t *out, c
     base = block_sum_u64(base, red);
     for (uint64_t t0 = lo; t0 < hi; t0 += 256) {
         const uint64_t i = t0 + tid;
-        const uint32_t len = i < hi ? out_len[i] : 0u;
+        const uint32_t len = i < hi ? msg_len(i) : 0u;
         /* block exclusive scan of len */
         uint32_t incl = wave_incl_sum(len, lane);
         if (lane == 63) red[w] = incl;
@@ -1182,11 +1200,24 @@ __global__ __launch_bounds__(256) void dg_pack_scan_kernel(const uint8_t *out, c
         __syncthreads();
         const uint32_t nt = hi - t0 < 256 ? (uint32_t)(hi - t0) : 256u;
         for (uint32_t k = w; k < nt; k += 4) {
-            const uint32_t nb = s_len[k];
+            uint32_t nb = s_len[k];
             if (!nb) continue;
+            gu8 *d = (gu8 *)(void *)(dst + s_pos[k]);
+            if (fr.hdr) { /* header, body, footer: byte-exact edges, in program order */
+                SrcT<const uint64_t> h;
+                h.init((const uint64_t *)(const void *)fr.hdr, 0, fr.hdr_len);
+                coop_copy(h, 0, fr.hdr_len, d, lane);
+                d += fr.hdr_len;
+                nb -= fx;
+            }
             SrcT<const uint64_t> src;
             src.init((const uint64_t *)(const void *)(out + out_off[t0 + k]), 0, nb);
-            coop_copy(src, 0, nb, (gu8 *)(void *)(dst + s_pos[k]), lane);
+            coop_copy(src, 0, nb, d, lane);
+            if (fr.hdr && fr.ftr_len) {
+                SrcT<const uint64_t> f;
+                f.init((const uint64_t *)(const void *)fr.ftr, 0, fr.ftr_len);
+                coop_copy(f, 0, fr.ftr_len, d + nb, lane);
+            }
         }
         base += tile;
         __syncthreads();
@@ -1203,7 +1234,7 @@ __global__ __launch_bounds__(256) void dg_pack_scan_kernel(const uint8_t *out, c
 
 void launch_pack_scan_kernel(dim3 grid, hipStream_t s, const uint8_t *out, const uint64_t *out_off,
                              const uint32_t *out_len, uint64_t n, uint8_t *dst, uint64_t *dst_off, uint64_t *sums,
-                             uint32_t *sync);
+                             uint32_t *sync, const MsgFrame &fr);
 void launch_wave_kernel(dim3 grid, hipStream_t s, const Params &P, const WaveParams &W);
 void launch_pack_kernel(dim3 grid, hipStream_t s, const uint8_t *out, const uint64_t *out_off, const uint32_t *out_len,
                         uint64_t n, uint8_t *dst, const uint64_t *dst_off);

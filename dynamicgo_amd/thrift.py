@@ -287,6 +287,8 @@ def flatten(root: TypeDescriptor) -> FlatDescriptor:
             fl = (1 if f.is_request_base else 0) | (2 if f.http_mappings else 0)
             if sd.names.get(f.alias) is f:
                 fl |= 4  # DG_FF_ALIAS_SELF
+            if b'"' not in f.alias.encode() and b"\\" not in f.alias.encode():
+                fl |= 8  # DG_FF_KEY_PLAIN
             if f.default_value is not None:
                 doff, dlen = pool_put(bytes(f.default_value)), len(f.default_value)
             else:

@@ -40,36 +40,11 @@
 extern "C" {
 #endif
 
-/* j2t flag bits (reference native/thrift.h:23-32) */
-#define DG_F_ALLOW_UNKNOWN (1ull << 0)
-#define DG_F_WRITE_DEFAULT (1ull << 1)
-#define DG_F_ENABLE_VM (1ull << 2)
-#define DG_F_ENABLE_HM (1ull << 3)
-#define DG_F_ENABLE_I2S (1ull << 4)
-#define DG_F_WRITE_REQUIRE (1ull << 5)
-#define DG_F_NO_BASE64 (1ull << 6)
-#define DG_F_WRITE_OPTIONAL (1ull << 7)
-#define DG_F_TRACE_BACK (1ull << 8)
-#define DG_F_NO_WRITE_BASE (1ull << 9)
-#define DG_F_VALIDATE_UTF8 (1ull << 16) /* extension: reject invalid UTF-8 in strings */
-#define DG_F_NO_FAST_PATH (1ull << 17)  /* extension: run every message on the exact machine (testing) */
-#define DG_F_NO_WAVE_PATH (1ull << 18)  /* extension: skip the wave-per-message kernel, lane kernel only (testing) */
-
-/* library-internal per-message statuses (code byte values the reference never
- * produces). The host entry points resolve them before returning; the device
- * entry point leaves them for the caller and counts them in *d_pending. */
-#define DG_ST_OUT_OVERFLOW 0xF0u /* slot too small; out_len = bytes needed (value bits: same, saturated at 2^24-1) */
-#define DG_ST_DEEP 0xF1u         /* (internal) nesting beyond the fast kernel's stack */
-
-/* API error codes */
-#define DG_OK 0
-#define DG_E_INVALID (-1)
-#define DG_E_HIP (-2)
-#define DG_E_NOMEM (-3)
-#define DG_E_DESC (-4)
+#include "dgj2t_defs.h"
 
 typedef struct dg_ctx dg_ctx;
 typedef struct dg_desc dg_desc;
+typedef struct dg_agg dg_agg;
 
 /* Per-thread description of the last failure. */
 const char *dg_last_error(void);
@@ -115,7 +90,9 @@ uint32_t dg_desc_root(const dg_desc *desc);
  *   d_ret       n u64: packed reference status (0 = ok), or DG_ST_OUT_OVERFLOW
  *   d_pending   optional u32 counter (device), incremented once per message
  *               left with DG_ST_OUT_OVERFLOW; may be NULL
- * Enqueued on ctx's stream (or `stream` if non-NULL); asynchronous. Launches
+ * Enqueued on ctx's stream (or `stream` if non-NULL); asynchronous. ctx's
+ * stream is a blocking stream, so it is ordered with the legacy default
+ * stream (handle 0) both ways. Launches
  * on different streams of one context may run concurrently: each stream gets
  * its own device scratch (lists, counters, workspaces), up to 8 streams per
  * context; beyond that a shared scratch orders the launches with events.
@@ -170,6 +147,35 @@ int dg_pack_device(dg_ctx *ctx, const uint8_t *d_out, const uint64_t *d_out_off,
  * after the conversion that wrote d_out_len. */
 int dg_pack_device_scan(dg_ctx *ctx, const uint8_t *d_out, const uint64_t *d_out_off, const uint32_t *d_out_len,
                         uint64_t n, uint8_t *d_dst, uint64_t *d_dst_off, void *stream);
+
+/* HTTPConv framing (conv/j2t/http_conv.go:68-114) fused into the packing:
+ * every message that converted (d_ret[i] == 0) is packed as
+ * hdr + body + ftr, every failed one as nothing; d_dst_off as in
+ * dg_pack_device_scan. hdr/ftr are host bytes (the message header and footer
+ * of thrift.GetBinaryMessageHeaderAndFooter, thrift/binary.go:137-175),
+ * copied by the call; (hdr_len rounded up to 8) + ftr_len must be <= 4080. */
+int dg_pack_device_framed(dg_ctx *ctx, const uint8_t *d_out, const uint64_t *d_out_off, const uint32_t *d_out_len,
+                          const uint64_t *d_ret, uint64_t n, const uint8_t *hdr, uint32_t hdr_len, const uint8_t *ftr,
+                          uint32_t ftr_len, uint8_t *d_dst, uint64_t *d_dst_off, void *stream);
+
+/*
+ * Batching aggregator: concurrent single-message calls coalesced into device
+ * batches (the reference's callers run BinaryConv.Do from many goroutines,
+ * conv/j2t/conv_timing_test.go:76-99). dg_agg_do blocks the calling thread
+ * until its message is converted, with the semantics of dg_j2t_do
+ * (BinaryConv.Do, conv/j2t/conv.go:53-77); a flusher thread converts up to
+ * max_batch queued messages at once, as soon as max_batch are waiting or the
+ * oldest has waited max_wait_us. If out_cap is too small the call returns
+ * DG_E_NOMEM with *out_len = the bytes needed. Thread-safe.
+ */
+int dg_agg_create(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, uint64_t flags, uint32_t max_batch,
+                  uint32_t max_wait_us, dg_agg **out);
+int dg_agg_do(dg_agg *agg, const uint8_t *json, size_t len, uint8_t *out, size_t out_cap, size_t *out_len,
+              uint64_t *ret);
+/* batches flushed and messages converted so far */
+int dg_agg_stats(dg_agg *agg, uint64_t *batches, uint64_t *msgs);
+/* converts what is still queued, then stops the flusher */
+void dg_agg_destroy(dg_agg *agg);
 
 /* Timing helper for benchmarks: launch the device batch `iters` times on the
  * context stream bracketed by HIP events; returns total milliseconds of GPU

@@ -67,6 +67,8 @@
 #define DG_FF_HTTP_MAPPING 2u /* len(FieldDescriptor.httpMappings) != 0 */
 #define DG_FF_ALIAS_SELF 4u   /* the field's alias key resolves to this field in the name map
                                  (lets the fast path confirm a predicted key by one compare) */
+#define DG_FF_KEY_PLAIN 8u    /* the alias has no '"' and no '\\' byte: a JSON key equal to it
+                                 ends right after it (no escape can start inside it) */
 
 /* dg_field.vm (reference native/thrift.h:64-67) */
 #define DG_VM_NONE 0

@@ -1,0 +1,63 @@
+"""HTTPConv (conv/j2t/http_conv.go:28-114) on the GPU: the message header and
+footer (thrift.GetBinaryMessageHeaderAndFooter, thrift/binary.go:137-175)
+around the body converted with EnableHttpMapping, framed by
+dg_pack_device_framed. Bodies are checked against the oracle with the same
+flags; structs with HTTP-mapped fields return the reference's ERR_HM code
+(the Go host's callback, out of scope)."""
+import os
+import random
+
+import pytest
+
+import oracle
+from dynamicgo_amd import conv, thrift as T, workloads as W
+
+pytestmark = pytest.mark.gpu
+IDL = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "idl")
+
+
+def fn(method):
+    return T.new_descriptor_from_path(os.path.join(IDL, "baseline.thrift")).functions()[method]
+
+
+def test_header_footer_known_answer():
+    hdr, ftr = conv.get_binary_message_header_and_footer("SimpleMethod", conv.MSG_CALL, 1, 0)
+    assert hdr.hex() == "80010001" + "0000000c" + b"SimpleMethod".hex() + "00000000" + "0c0001"
+    assert ftr == b"\x00"
+
+
+def test_httpconv_do_vs_oracle():
+    hc = conv.HTTPConv(conv.ENCODING_THRIFT_BINARY, fn("SimpleMethod"))
+    chk = oracle.RefOracle() or oracle.PortOracle()
+    fl = T.flatten(hc.st)
+    flags = conv.to_flags(conv.Options(EnableHttpMapping=True))
+    for body in [W.c1_simple_json(), b"{}", b"", b'{"I32Field":7}']:
+        out = hc.do(conv.HTTPRequest(body))
+        er, eo = chk.j2t(fl, body, flags)
+        assert er == 0
+        assert out == hc.top + eo + hc.bottom
+        buf = bytearray(b"xy")
+        hc.do_into(conv.HTTPRequest(body), buf)
+        assert bytes(buf) == b"xy" + out
+
+
+def test_httpconv_batch_framed_on_gpu():
+    rng = random.Random(5)
+    chk = oracle.RefOracle() or oracle.PortOracle()
+    for method in ("SimpleMethod", "NestingMethod"):
+        hc = conv.HTTPConv(conv.ENCODING_THRIFT_BINARY, fn(method))
+        fl = T.flatten(hc.st)
+        if method == "SimpleMethod":
+            bodies = W.gen_flat_batch(rng, 3000) + [b"{]", b"", b"{}", b'{"I32Field":tru}']
+        else:  # Nesting has api.header / api.query fields: ERR_HM at its entry
+            bodies = W.gen_nested_batch(rng, 300) + [b"{}", b"[]"]
+        reqs = [conv.HTTPRequest(b) for b in bodies]
+        for opts in (conv.Options(), conv.Options(WriteDefaultField=True)):
+            outs, rets = hc.do_batch(reqs, opts)
+            flags = conv.to_flags(opts) | conv.F_HTTP_MAPPING
+            for b, o, r in zip(bodies, outs, rets):
+                er, eo = chk.j2t(fl, b, flags)
+                assert int(r) == er, (method, b[:80])
+                assert o == (hc.top + eo + hc.bottom if er == 0 else b""), (method, b[:80])
+            if method == "NestingMethod":
+                assert all((int(r) & 0xFF) in (19, 9) for r in rets[:300]), "expected ERR_HM on mapped structs"
