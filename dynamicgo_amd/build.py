@@ -24,8 +24,9 @@ def _run(cmd, cwd=None):
 
 
 UNITS = ("j2t_kern_wave.hip", "j2t_kern_small.hip", "j2t_kern_lds.hip", "j2t_kern_glb.hip", "j2t_host.hip",
-         "j2t_agg.hip")
-HEADERS = ("j2t_small.h", "j2t_wave.h", "j2t_machine.h", "j2t_device.h", "j2t_fast.h", "dg_tables.h")
+         "j2t_agg.hip", "t2j_kern.hip", "t2j_host.hip")
+HEADERS = ("j2t_small.h", "j2t_wave.h", "j2t_machine.h", "j2t_device.h", "j2t_fast.h", "dg_tables.h", "host_internal.h",
+           "t2j_device.h", "t2j_tables.h")
 
 
 def source_hash(extra_flags=()) -> str:
@@ -86,13 +87,14 @@ def embedded_hash(path: str):
     return data[k + len(MARK):k + len(MARK) + 16].decode("ascii", "replace")
 
 
-def build_hip(force=False, extra_flags=(), out=None):
+def build_hip(force=False, extra_flags=(), out=None, unit_flags=None):
     """Compile the translation units in parallel (one hipcc each), then link.
     Skipped only when the existing library carries the hash of exactly these
     sources + flags (compiled in as dg_build_info); a library built from
     anything else is rebuilt."""
     out = out or os.path.join(ROOT, "dynamicgo_amd", "libdgj2t.so")
-    sh = source_hash(extra_flags)
+    unit_flags = unit_flags or {}
+    sh = source_hash(tuple(extra_flags) + tuple(sorted((u, tuple(f)) for u, f in unit_flags.items())))
     if not force and embedded_hash(out) == sh:
         print(f"libdgj2t.so up to date (sources {sh})", flush=True)
         return out
@@ -103,12 +105,13 @@ def build_hip(force=False, extra_flags=(), out=None):
     for u in UNITS:
         # objects are cached by the hash of what they are built from; the
         # host unit also carries the library hash (dg_build_info)
-        uh = unit_hash(u, extra_flags) + (sh if u == "j2t_host.hip" else "")
+        uf = tuple(extra_flags) + tuple(unit_flags.get(u, ()))
+        uh = unit_hash(u, uf) + (sh if u == "j2t_host.hip" else "")
         o = os.path.join(objdir, u.replace(".hip", "") + "_" + uh + ".o")
         objs.append(o)
         if os.path.exists(o) and not force:
             continue
-        cmd = common + ([f'-DDG_SRC_HASH="{sh}"'] if u == "j2t_host.hip" else [])
+        cmd = common + list(unit_flags.get(u, ())) + ([f'-DDG_SRC_HASH="{sh}"'] if u == "j2t_host.hip" else [])
         cmd = cmd + ["-c", "-o", o + ".tmp", os.path.join(CSRC, u)]
         print("+", " ".join(cmd), flush=True)
         procs.append((u, o, subprocess.Popen(cmd)))

@@ -65,6 +65,12 @@ class Options:
     DisallowUnknownField: bool = False
     ReadHttpValueFallback: bool = False
     ValidateUTF8: bool = False  # extension (north_star: "UTF-8 validation"), default off
+    # fields only the reverse path (t2j, dynamicgo_amd.t2j) reads
+    Int642String: bool = False
+    ByteAsUint8: bool = False
+    EncodeNullJSONForInfOrNan: bool = False
+    ConvertException: bool = False
+    WriteHttpValueFallback: bool = False
 
 
 def to_flags(o: Options) -> int:
@@ -159,6 +165,17 @@ class Context:
         self.h = h
         self.device = device
         self._descs = {}
+        self._t2j = set()
+
+    def desc_t2j(self, flat: FlatDescriptor):
+        """desc() with the t2j side table attached (dg_desc_attach_t2j)."""
+        d = self.desc(flat)
+        if flat.blob not in self._t2j:
+            from .thrift import flatten_t2j
+            side = flatten_t2j(flat)
+            _lib.check(_lib.lib().dg_desc_attach_t2j(d, side, len(side)))
+            self._t2j.add(flat.blob)
+        return d
 
     def desc(self, flat: FlatDescriptor):
         """Device-resident copy of a flattened descriptor (cached by content)."""
@@ -182,6 +199,7 @@ class Context:
         for d in self._descs.values():
             L.dg_desc_destroy(d)
         self._descs.clear()
+        self._t2j.clear()
         if self.h:
             L.dg_ctx_destroy(self.h)
             self.h = None

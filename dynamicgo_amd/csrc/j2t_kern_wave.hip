@@ -4,7 +4,7 @@
 namespace dg {
 void launch_wave_kernel(dim3 grid, hipStream_t s, const Params &P, const WaveParams &W)
 {
-    hipLaunchKernelGGL(j2t_wave_kernel<0>, grid, dim3(64 * WV_WAVES), 0, s, P, W);
+    hipLaunchKernelGGL(j2t_wave_kernel<0>, grid, dim3(64 * WV_WAVES), (W.hdr.total_len + 15) & ~15u, s, P, W);
 }
 void launch_pack_kernel(dim3 grid, hipStream_t s, const uint8_t *out, const uint64_t *out_off, const uint32_t *out_len,
                         uint64_t n, uint8_t *dst, const uint64_t *dst_off)

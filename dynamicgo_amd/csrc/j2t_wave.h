@@ -46,20 +46,37 @@
 
 namespace dg {
 
+/* Occupancy (measured, C3 65536 x 2.2 KB): 2 waves/SIMD (ring 512, 4 KiB
+ * staging, 191 VGPRs) 4.18 ms; 3 waves (168 VGPRs) 3.34 ms; 4 waves (ring
+ * 256, 2 KiB staging, 128 VGPRs + 24 spilled, 4 blocks/CU) 2.88 ms. The
+ * kernel is latency-bound (dependent ballot/LDS chains), so waves per SIMD
+ * beat per-wave efficiency. */
+#ifndef DG_WV_RING
+#define DG_WV_RING 256
+#endif
+#ifndef DG_WV_MSG
+#define DG_WV_MSG 2048
+#endif
+#ifndef DG_WV_BPC
+#define DG_WV_BPC 4
+#endif
+#ifndef DG_WV_WPE
+#define DG_WV_WPE 4
+#endif
 constexpr uint32_t WV_WAVES = 4;               /* waves (= messages in flight) per block */
-constexpr uint32_t WV_RING = 512;              /* token ring per wave */
+constexpr uint32_t WV_RING = DG_WV_RING;       /* token ring per wave (a scan step that would overrun it bails) */
 constexpr uint32_t WV_RMASK = WV_RING - 1;
 constexpr uint32_t WV_CHUNK = 256;             /* bytes classified per scan step: 64 lanes x 4 */
 constexpr uint32_t WV_MAXD = 16;               /* container levels handled on the wave path */
 constexpr uint32_t WV_LA = 2;                  /* token lookahead kept unconsumed while scanning */
 constexpr uint32_t WV_NOEND = 0xFFFFFFFFu;     /* string not closed (yet) */
 constexpr uint32_t WV_POSMASK = (1u << 29) - 1;
-constexpr uint32_t WV_MSG = 4096;              /* messages up to this (minus 16) are staged in LDS */
-constexpr uint32_t WV_DESC = 16384;            /* the wave path needs the descriptor in LDS */
+constexpr uint32_t WV_MSG = DG_WV_MSG;         /* messages up to this (minus 16) are staged in LDS */
+constexpr uint32_t WV_DESC = 16384;            /* the wave path needs the descriptor in LDS (dynamic, sized to it) */
 constexpr uint32_t WV_LONG = 192;              /* strings longer than this are copied/decoded by the whole wave */
-constexpr uint32_t WV_BLOCKS_PER_CU = 2;       /* persistent grid: 2 blocks x 4 waves per CU */
-constexpr uint32_t WV_MIN_DEFAULT = 512; 
-constexpr uint32_t WV_REQMASKS = 64;           /* per-struct REQUIRED-field masks kept in LDS */      /* messages longer than this go to the wave kernel (DG_WAVE_MIN) */
+constexpr uint32_t WV_BLOCKS_PER_CU = DG_WV_BPC; /* persistent grid: blocks of 4 waves per CU */
+constexpr uint32_t WV_MIN_DEFAULT = 512;       /* messages longer than this go to the wave kernel (DG_WAVE_MIN) */
+constexpr uint32_t WV_REQMASKS = 64;           /* per-struct REQUIRED-field masks kept in LDS */
 
 /* token kinds (3 bits, stored above the 29-bit position) */
 enum : uint32_t {
@@ -565,6 +582,10 @@ DGI bool wave_run(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L
                 if (lane == 0) L.tend[(ss.produced - 1) & WV_RMASK] = (uint32_t)len;
             }
         }
+        /* the live window is [consumed - 2, produced): a token-dense chunk
+         * that overran it (fewer than 2 bytes per token) goes to the exact
+         * machine */
+        if (ss.produced - consumed + 2 > WV_RING) return false;
         WP(0);
         uint32_t avail = ss.produced - consumed;
         if (scanned < nchunks) avail -= WV_LA;
@@ -1028,11 +1049,12 @@ DGI bool wave_convert(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, L
  * staged in the wave's LDS buffer. Bailed messages are listed for the exact
  * machine (j2t_lane_kernel in list mode). */
 template <int V> /* instantiated in j2t_kern_wave.hip only */
-__global__ __launch_bounds__(64 * WV_WAVES) void j2t_wave_kernel(Params P, WaveParams W)
+__global__ __launch_bounds__(64 * WV_WAVES) __attribute__((amdgpu_waves_per_eu(DG_WV_WPE))) void j2t_wave_kernel(
+    Params P, WaveParams W)
 {
     __shared__ __attribute__((aligned(16))) WaveLds wl[WV_WAVES];
     __shared__ __attribute__((aligned(16))) uint64_t s_msg[WV_WAVES][WV_MSG / 8];
-    __shared__ __attribute__((aligned(16))) uint64_t s_desc[WV_DESC / 8];
+    extern __shared__ __attribute__((aligned(16))) uint64_t s_desc[]; /* the blob, rounded to 16 B (launch size) */
     __shared__ uint8_t s_cls[256];
     __shared__ uint64_t s_reqmask[WV_REQMASKS];
     __shared__ uint64_t s_p10u[20];
@@ -1235,7 +1257,7 @@ __global__ __launch_bounds__(256) void dg_pack_scan_kernel(const uint8_t *out, c
 void launch_pack_scan_kernel(dim3 grid, hipStream_t s, const uint8_t *out, const uint64_t *out_off,
                              const uint32_t *out_len, uint64_t n, uint8_t *dst, uint64_t *dst_off, uint64_t *sums,
                              uint32_t *sync, const MsgFrame &fr);
-void launch_wave_kernel(dim3 grid, hipStream_t s, const Params &P, const WaveParams &W);
+void launch_wave_kernel(dim3 grid, hipStream_t s, const Params &P, const WaveParams &W); /* LDS: + the blob */
 void launch_pack_kernel(dim3 grid, hipStream_t s, const uint8_t *out, const uint64_t *out_off, const uint32_t *out_len,
                         uint64_t n, uint8_t *dst, const uint64_t *dst_off);
 

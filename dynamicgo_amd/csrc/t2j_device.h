@@ -1,0 +1,815 @@
+/*
+ * t2j_device.h — the reverse path, Thrift binary -> JSON (conv/t2j), on the
+ * GPU: one lane per message.
+ *
+ * Thrift binary is length-prefixed, so a message is walked front to back
+ * with no scanning: every lane runs the reference's doRecurse
+ * (conv/t2j/impl.go:189-393) iteratively over a small frame stack in LDS
+ * (messages nested deeper than T2J_LDS_DEPTH are reported DG_ST_DEEP and
+ * rerun by the same code with the frames in device memory). The JSON bytes
+ * are the reference's, byte for byte:
+ *   numbers   i64toa (native/fastint.c:212-231) and f64toa, the Schubfach
+ *             shortest round-trip formatter (native/fastfloat.c:288-404,
+ *             R. Giulietti, "The Schubfach way to render doubles", 2022);
+ *   strings   quote with flags 0 (native/parsing.c:28-63, 487): '"' and '\\'
+ *             backslashed, \t \n \r short, other bytes < 0x20 as \u00xx;
+ *   binary    standard padded base64 (base64x.StdEncoding);
+ *   keys      pre-encoded on the host (the t2j side table,
+ *             include/dgj2t_desc.h dg_t2j_*);
+ *   unsets    thrift/utils.go:149-176 HandleRequires + writeDefaultOrEmpty
+ *             (conv/t2j/impl.go:440-468);
+ *   js_conv   thrift/annotation/value_mapping.go:143-214 (numbers quoted).
+ * Errors are status words (include/dgj2t_defs.h DG_T2J_E_*), code | pos << 8
+ * | value << 40, pos = the Thrift read offset where the reference's read
+ * failed.
+ */
+#pragma once
+#include "j2t_device.h"
+#include "t2j_tables.h"
+
+namespace dg {
+
+constexpr uint32_t T2J_LDS_DEPTH = 12;   /* frames per lane in LDS */
+constexpr uint32_t T2J_DEEP_DEPTH = 4096; /* frames per lane in the deep rerun */
+constexpr uint32_t T2J_BLOCK = 256;
+constexpr int T2J_SKIP_DEPTH = 1023;     /* MaxSkipDepth, thrift/binary_skip.go:24 */
+
+enum : uint32_t { RD_EOF = 1, RD_BAD_TYPE = 2, RD_BAD_SIZE = 3, RD_DEPTH = 4 };
+enum : uint32_t { TF_STRUCT = 1, TF_LIST = 2, TF_MAP = 3, TF_SKIP_STRUCT = 4, TF_SKIP_LIST = 5, TF_SKIP_MAP = 6 };
+
+/* one open container (24 B) */
+struct T2JFrame {
+    uint32_t kind; /* TF_* */
+    uint32_t td;   /* type index; skip frames: element wire type(s) */
+    uint32_t n;    /* elements (list/map) */
+    uint32_t i;    /* elements done; struct: fields written (comma) */
+    uint64_t u;    /* struct: requires bits by field index; skip frames: maxDepth */
+};
+
+struct T2JSide {
+    const __attribute__((address_space(1))) dg_t2j_field *X;
+    const __attribute__((address_space(1))) uint8_t *P;
+};
+
+DGI uint64_t t2j_err(uint32_t code, uint64_t pos, uint64_t val) { return (val << 40) | (pos << 8) | code; }
+
+/* ---------------- encoders ---------------- */
+
+/* 4 decimal digits of y < 10000 as ASCII, first digit lowest */
+DGI uint32_t dig4(uint32_t y)
+{
+    const uint32_t hi = y / 100, lo = y - hi * 100;
+    const uint32_t a = hi / 10, b = hi - a * 10, c = lo / 10, d = lo - c * 10;
+    return 0x30303030u | a | (b << 8) | (c << 16) | (d << 24);
+}
+/* 8 decimal digits of x < 10^8 with leading zeros, first digit lowest */
+DGI uint64_t dig8(uint32_t x)
+{
+    const uint32_t a = x / 10000, b = x - a * 10000;
+    return (uint64_t)dig4(a) | ((uint64_t)dig4(b) << 32);
+}
+DGI uint32_t ndigits32(uint32_t x)
+{
+    uint32_t n = 1;
+    for (uint32_t p = 10; n < 10 && x >= p; p *= 10) n++;
+    return n;
+}
+/* x < 10^8 without leading zeros */
+DGI void emit_small(Out &o, uint32_t x)
+{
+    const uint32_t nd = ndigits32(x);
+    o.wle(dig8(x) >> ((8 - nd) << 3), nd);
+}
+/* u64toa (native/fastint.c:221-231): decimal, no leading zeros */
+DGI void emit_u64(Out &o, uint64_t v)
+{
+    if (v < 100000000ull) {
+        emit_small(o, (uint32_t)v);
+        return;
+    }
+    const uint64_t q = v / 100000000ull;
+    const uint32_t r = (uint32_t)(v - q * 100000000ull);
+    if (q < 100000000ull) {
+        emit_small(o, (uint32_t)q);
+    } else {
+        const uint64_t q2 = q / 100000000ull;
+        emit_small(o, (uint32_t)q2);
+        o.wle(dig8((uint32_t)(q - q2 * 100000000ull)), 8);
+    }
+    o.wle(dig8(r), 8);
+}
+/* i64toa (native/fastint.c:212-219) */
+DGI void emit_i64(Out &o, int64_t v)
+{
+    if (v >= 0) {
+        emit_u64(o, (uint64_t)v);
+    } else {
+        o.w8('-');
+        emit_u64(o, 0ull - (uint64_t)v);
+    }
+}
+
+/* decimal digits of v (1..17; the reference's misnamed ctz10) */
+DGI uint32_t ndigits64(uint64_t v)
+{
+    uint32_t n = 1;
+    for (uint64_t p = 10; n < 20 && v >= p; p *= 10) n++;
+    return n;
+}
+
+/* Schubfach: the shortest decimal sig * 10^exp in the rounding interval of
+ * c * 2^q (native/fastfloat.c:288-347) */
+DGI uint64_t round_odd(uint64_t ghi, uint64_t glo, uint64_t cp)
+{
+    const uint64_t x_hi = __umul64hi(cp, glo);
+    const uint64_t y_lo0 = cp * ghi;
+    const uint64_t y_lo = y_lo0 + x_hi;
+    const uint64_t y_hi = __umul64hi(cp, ghi) + (y_lo < y_lo0 ? 1ull : 0ull);
+    return y_hi | (y_lo > 1 ? 1ull : 0ull);
+}
+DGI void f64_to_dec(uint64_t rsig, int32_t rexp, uint64_t c, int32_t q, uint64_t &sig, int32_t &dexp)
+{
+    const bool even = !(c & 1);
+    const bool irregular = rsig == 0 && rexp > 1;
+    const uint64_t cbl = 4 * c - 2 + (irregular ? 1 : 0), cb = 4 * c, cbr = 4 * c + 2;
+    const int32_t k = (q * 1262611 - (irregular ? 524031 : 0)) >> 22;
+    const int32_t h = q + (((-k) * 1741647) >> 19) + 1;
+    const uint64_t ghi = DG_POW10_CEIL[-k + 292][0], glo = DG_POW10_CEIL[-k + 292][1];
+    const uint64_t vbl = round_odd(ghi, glo, cbl << h);
+    const uint64_t vb = round_odd(ghi, glo, cb << h);
+    const uint64_t vbr = round_odd(ghi, glo, cbr << h);
+    const uint64_t lower = vbl + (even ? 0 : 1), upper = vbr - (even ? 0 : 1);
+    const uint64_t s = vb / 4;
+    if (s >= 10) {
+        const uint64_t sp = s / 10;
+        const bool up_in = lower <= 40 * sp, wp_in = 40 * sp + 40 <= upper;
+        if (up_in != wp_in) {
+            sig = sp + (wp_in ? 1 : 0);
+            dexp = k + 1;
+            return;
+        }
+    }
+    const bool u_in = lower <= 4 * s, w_in = 4 * s + 4 <= upper;
+    if (u_in != w_in) {
+        sig = s + (w_in ? 1 : 0);
+        dexp = k;
+        return;
+    }
+    const uint64_t mid = 4 * s + 2;
+    const bool up = vb > mid || (vb == mid && (s & 1) != 0);
+    sig = s + (up ? 1 : 0);
+    dexp = k;
+}
+
+/* the digits of sig (cnt of them, <= 17) into d[0..cnt) */
+DGI void sig_digits(uint64_t sig, uint32_t cnt, uint8_t *d)
+{
+    for (int32_t i = (int32_t)cnt - 1; i >= 0; i--) {
+        const uint64_t q = sig / 10;
+        d[i] = (uint8_t)('0' + (sig - q * 10));
+        sig = q;
+    }
+}
+
+/* f64toa (native/fastfloat.c:349-404) for a finite double: the shortest
+ * round-trip digits, written as an integer, a decimal, or d.ddde[+-]x when
+ * the decimal exponent is < -6 or > 20 (write_dec :241-259) */
+DGI void emit_f64(Out &o, double fp)
+{
+    const uint64_t raw = (uint64_t)__double_as_longlong(fp);
+    const bool neg = (raw >> 63) != 0;
+    const uint64_t rsig = raw & 0x000FFFFFFFFFFFFFull;
+    const int32_t rexp = (int32_t)((raw >> 52) & 0x7FF);
+    if (neg) o.w8('-');
+    if ((raw << 1) == 0) {
+        o.w8('0');
+        return;
+    }
+    uint64_t c;
+    int32_t q;
+    if (rexp != 0) {
+        c = rsig | 0x0010000000000000ull;
+        q = rexp - 1075;
+        if (q <= 0 && q >= -52 && (c & ((1ull << -q) - 1)) == 0) { /* an integer */
+            emit_u64(o, c >> -q);
+            return;
+        }
+    } else {
+        c = rsig;
+        q = -1074;
+    }
+    uint64_t sig;
+    int32_t exp;
+    f64_to_dec(rsig, rexp, c, q, sig, exp);
+    const uint32_t cnt = ndigits64(sig);
+    const int32_t dot = (int32_t)cnt + exp;
+    const int32_t sci = dot - 1;
+    uint8_t d[20];
+    sig_digits(sig, cnt, d);
+    uint32_t nd = cnt; /* digits without trailing zeros */
+    if (sci < -6 || sci > 20) { /* format_exponent :168-203 */
+        while (nd > 1 && d[nd - 1] == '0') nd--;
+        o.w8(d[0]);
+        if (nd > 1) {
+            o.w8('.');
+            for (uint32_t i = 1; i < nd; i++) o.w8(d[i]);
+        }
+        o.w8('e');
+        int32_t e = exp + (int32_t)cnt - 1;
+        if (e < 0) {
+            o.w8('-');
+            e = -e;
+        } else {
+            o.w8('+');
+        }
+        emit_small(o, (uint32_t)e);
+        return;
+    }
+    if (dot < (int32_t)cnt) { /* format_decimal :205-239 */
+        while (nd > 1 && d[nd - 1] == '0') nd--;
+        if (dot <= 0) {
+            o.w8('0');
+            o.w8('.');
+            for (int32_t i = 0; i < -dot; i++) o.w8('0');
+            for (uint32_t i = 0; i < nd; i++) o.w8(d[i]);
+            return;
+        }
+        if ((int32_t)nd > dot) {
+            for (int32_t i = 0; i < dot; i++) o.w8(d[i]);
+            o.w8('.');
+            for (uint32_t i = (uint32_t)dot; i < nd; i++) o.w8(d[i]);
+        } else {
+            for (uint32_t i = 0; i < nd; i++) o.w8(d[i]);
+            for (int32_t i = (int32_t)nd; i < dot; i++) o.w8('0');
+        }
+        return;
+    }
+    for (uint32_t i = 0; i < cnt; i++) o.w8(d[i]); /* integer digits, then zeros up to the point */
+    for (int32_t i = (int32_t)cnt; i < dot; i++) o.w8('0');
+}
+
+/* quote (native/parsing.c:487, flags 0) of src[s0, s0+n): 8 bytes per step
+ * when none of them needs an escape */
+template <class S>
+DGI void emit_quoted(Out &o, S &src, int64_t s0, int64_t n)
+{
+    int64_t i = 0;
+    while (i < n) {
+        const uint64_t w = src.get8(s0 + i);
+        const int64_t rem = n - i;
+        const uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
+        /* bytes < 0x20 (top bit clear, + 0x60 does not reach 0x80), '"', '\\' */
+        const uint32_t cl = ~((lo & 0x7F7F7F7Fu) + 0x60606060u) & ~lo & 0x80808080u;
+        const uint32_t ch = ~((hi & 0x7F7F7F7Fu) + 0x60606060u) & ~hi & 0x80808080u;
+        uint64_t m = ((uint64_t)cl | ((uint64_t)ch << 32)) | eqbytes(w, '"') | eqbytes(w, '\\');
+        if (rem < 8) m &= (1ull << (rem << 3)) - 1;
+        if (m == 0) {
+            const uint32_t k = rem < 8 ? (uint32_t)rem : 8u;
+            o.wle(w, k);
+            i += k;
+            continue;
+        }
+        const uint32_t j = (uint32_t)__builtin_ctzll(m) >> 3;
+        if (j) o.wle(w, j);
+        const uint8_t c = (uint8_t)(w >> (j << 3));
+        if (c == '"') o.wle('\\' | ('"' << 8), 2);
+        else if (c == '\\') o.wle('\\' | ('\\' << 8), 2);
+        else if (c == '\t') o.wle('\\' | ('t' << 8), 2);
+        else if (c == '\n') o.wle('\\' | ('n' << 8), 2);
+        else if (c == '\r') o.wle('\\' | ('r' << 8), 2);
+        else {
+            const uint32_t h1 = c >> 4, h2 = c & 15;
+            const uint64_t x1 = h1 < 10 ? '0' + h1 : 'a' + h1 - 10, x2 = h2 < 10 ? '0' + h2 : 'a' + h2 - 10;
+            o.wle('\\' | ('u' << 8) | ('0' << 16) | ('0' << 24) | (x1 << 32) | (x2 << 40), 6);
+        }
+        i += j + 1;
+    }
+}
+
+DGI uint64_t b64c(uint32_t v) /* one standard-alphabet character */
+{
+    return v < 26 ? 'A' + v : v < 52 ? 'a' + v - 26 : v < 62 ? '0' + v - 52 : v == 62 ? '+' : '/';
+}
+/* standard padded base64 of src[s0, s0+n) (base64x.StdEncoding; the
+ * reference's b64encode, native/base64.c:173, mode 0) */
+template <class S>
+DGI void emit_base64(Out &o, S &src, int64_t s0, int64_t n)
+{
+    int64_t i = 0;
+    for (; i + 3 <= n; i += 3) {
+        const uint64_t w = src.get8(s0 + i);
+        const uint32_t t = ((uint32_t)(w & 0xFF) << 16) | ((uint32_t)((w >> 8) & 0xFF) << 8) | (uint32_t)((w >> 16) & 0xFF);
+        o.wle(b64c(t >> 18) | (b64c((t >> 12) & 63) << 8) | (b64c((t >> 6) & 63) << 16) | (b64c(t & 63) << 24), 4);
+    }
+    if (i < n) {
+        const uint64_t w = src.get8(s0 + i);
+        const uint32_t b0 = (uint32_t)(w & 0xFF), b1 = n - i > 1 ? (uint32_t)((w >> 8) & 0xFF) : 0u;
+        const uint32_t t = (b0 << 16) | (b1 << 8);
+        const uint64_t c2 = n - i > 1 ? b64c((t >> 6) & 63) : '=';
+        o.wle(b64c(t >> 18) | (b64c((t >> 12) & 63) << 8) | (c2 << 16) | ((uint64_t)'=' << 24), 4);
+    }
+}
+
+/* ---------------- the walk ---------------- */
+
+template <class S>
+struct T2JRd {
+    S src;
+    int64_t p;
+    DGI bool need(int64_t k) const { return p + k <= (int64_t)src.n; }
+    DGI uint8_t u8() { return src.raw(p++); }
+    DGI uint64_t be(uint32_t k) /* k <= 8 bytes, big-endian */
+    {
+        const uint64_t w = src.get8(p);
+        p += k;
+        return __builtin_bswap64(w) >> ((8 - k) << 3);
+    }
+};
+
+DGI bool ttype_valid(uint8_t t) /* thrift/descriptor.go:60-67 */
+{
+    return t <= 17 && ((0x3FDDFu >> t) & 1); /* 0 1 2 3 4 6 8 10 11 12 13 14 15 16 17 */
+}
+DGI uint32_t fixed_size(uint8_t t) /* typeSize, thrift/binary_skip.go:26-41 */
+{
+    switch (t) {
+    case 2: case 3: return 1;
+    case 6: return 2;
+    case 8: return 4;
+    case 4: case 10: return 8;
+    }
+    return 0;
+}
+
+template <class DV>
+DGI int32_t t2j_field(const DV &D, const dg_struct &sd, uint32_t hint, uint16_t id)
+{
+    if (hint < sd.n_fields && ldrec(&D.F[sd.field_begin + hint]).id == id) return (int32_t)(sd.field_begin + hint);
+    uint32_t lo = 0, hi = sd.n_fields; /* fields are sorted by id */
+    while (lo < hi) {
+        const uint32_t m = (lo + hi) >> 1;
+        const uint16_t fid = ldrec(&D.F[sd.field_begin + m]).id;
+        if (fid == id) return (int32_t)(sd.field_begin + m);
+        if (fid < id) lo = m + 1;
+        else hi = m;
+    }
+    return -1;
+}
+
+/* side-table bytes [off, off+len) (8-aligned, 16 readable past the end) */
+DGI void emit_side(Out &o, const T2JSide &X, uint32_t off, uint32_t len)
+{
+    const __attribute__((address_space(1))) uint64_t *w = (const __attribute__((address_space(1))) uint64_t *)(X.P + off);
+    uint32_t i = 0;
+    for (; i + 8 <= len; i += 8) o.wle(w[i >> 3], 8);
+    if (i < len) o.wle(w[i >> 3], len - i);
+}
+
+/* one message. FP: frame storage (LDS or device workspace), `cap` frames. */
+template <class S, class FP, class DV>
+DGI uint64_t t2j_convert(const DV &D, const T2JSide &X, S src, uint32_t root, uint64_t opts, Out &o, FP fr,
+                         uint32_t fstride, uint32_t cap)
+{
+    T2JRd<S> r{src, 0};
+    uint32_t sp = 0;
+    auto F = [&](uint32_t k) -> auto & { return fr[k * fstride]; };
+
+    /* the value of type td at the reader: scalars written, containers opened
+     * (their header read and checked, the frame pushed) */
+    auto value = [&](uint32_t td) -> uint64_t {
+        const dg_type t = ldrec(&D.T[td]);
+        switch (t.ttype) {
+        case DG_T_BOOL:
+            if (!r.need(1)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+            if (r.u8() == 1) o.wle('t' | ('r' << 8) | ('u' << 16) | ('e' << 24), 4);
+            else o.wle('f' | ('a' << 8) | ('l' << 16) | ('s' << 24) | (0x65ull << 32), 5);
+            return 0;
+        case DG_T_BYTE: {
+            if (!r.need(1)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+            const uint8_t v = r.u8();
+            emit_i64(o, (opts & DG_T2J_BYTE_AS_UINT8) ? (int64_t)v : (int64_t)(int8_t)v);
+            return 0;
+        }
+        case DG_T_I16:
+            if (!r.need(2)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+            emit_i64(o, (int16_t)r.be(2));
+            return 0;
+        case DG_T_I32:
+            if (!r.need(4)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+            emit_i64(o, (int32_t)r.be(4));
+            return 0;
+        case DG_T_I64: {
+            if (!r.need(8)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+            const int64_t v = (int64_t)r.be(8);
+            if (opts & DG_T2J_INT64_AS_STRING) {
+                o.w8('"');
+                emit_i64(o, v);
+                o.w8('"');
+            } else {
+                emit_i64(o, v);
+            }
+            return 0;
+        }
+        case DG_T_DOUBLE: {
+            if (!r.need(8)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+            const uint64_t u = r.be(8);
+            if (((u >> 52) & 0x7FF) == 0x7FF) {
+                if (!(opts & DG_T2J_NULL_FOR_NAN_INF)) return t2j_err(DG_T2J_E_NAN_INF, r.p, 0);
+                o.wle('n' | ('u' << 8) | ('l' << 16) | ('l' << 24), 4);
+                return 0;
+            }
+            emit_f64(o, __longlong_as_double((long long)u));
+            return 0;
+        }
+        case DG_T_STRING: {
+            if (!r.need(4)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+            const int32_t sz = (int32_t)r.be(4);
+            if (sz < 0 || !r.need(sz)) return t2j_err(DG_T2J_E_READ, r.p, RD_BAD_SIZE);
+            const int64_t s0 = r.p;
+            r.p += sz;
+            o.w8('"');
+            if ((t.flags & DG_TF_BINARY) && !(opts & DG_T2J_NO_BASE64)) emit_base64(o, r.src, s0, sz); /* EncodeBaniry */
+            else emit_quoted(o, r.src, s0, sz);
+            o.w8('"');
+            return 0;
+        }
+        case DG_T_STRUCT: {
+            if (sp >= cap) return pack0(DG_ST_DEEP, 0);
+            const dg_struct sd = ldrec(&D.S[t.st]);
+            if (sd.req_words != 1) return t2j_err(DG_T2J_E_NEEDS_HOST, r.p, 0); /* > 64 fields */
+            auto &f = F(sp++);
+            f.kind = TF_STRUCT;
+            f.td = td;
+            f.n = 0; /* predicted next field index */
+            f.i = 0;
+            f.u = D.R[sd.req_begin];
+            o.w8('{');
+            return 0;
+        }
+        case DG_T_LIST:
+        case DG_T_SET: {
+            if (!r.need(1)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+            const uint8_t et = r.u8();
+            if (!ttype_valid(et)) return t2j_err(DG_T2J_E_READ, r.p, RD_BAD_TYPE);
+            if (!r.need(4)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+            const int32_t n = (int32_t)r.be(4);
+            if (n < 0) return t2j_err(DG_T2J_E_READ, r.p, RD_BAD_SIZE);
+            const uint8_t want = ldrec(&D.T[t.elem]).ttype;
+            if (et != want) return t2j_err(DG_T2J_E_DISMATCH_TYPE, r.p, ((uint32_t)want << 8) | et);
+            if (sp >= cap) return pack0(DG_ST_DEEP, 0);
+            auto &f = F(sp++);
+            f.kind = TF_LIST;
+            f.td = td;
+            f.n = (uint32_t)n;
+            f.i = 0;
+            o.w8('[');
+            return 0;
+        }
+        case DG_T_MAP: {
+            if (!r.need(1)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+            const uint8_t kt = r.u8();
+            if (!ttype_valid(kt)) return t2j_err(DG_T2J_E_READ, r.p, RD_BAD_TYPE);
+            if (!r.need(1)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+            const uint8_t vt = r.u8();
+            if (!ttype_valid(vt)) return t2j_err(DG_T2J_E_READ, r.p, RD_BAD_TYPE);
+            if (!r.need(4)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+            const int32_t n = (int32_t)r.be(4);
+            if (n < 0) return t2j_err(DG_T2J_E_READ, r.p, RD_BAD_SIZE);
+            const uint8_t wk = ldrec(&D.T[t.key]).ttype, wv = ldrec(&D.T[t.elem]).ttype;
+            if (kt != wk) return t2j_err(DG_T2J_E_DISMATCH_TYPE, r.p, ((uint32_t)wk << 8) | kt);
+            if (vt != wv) return t2j_err(DG_T2J_E_DISMATCH_TYPE, r.p, ((uint32_t)wv << 8) | vt);
+            if (sp >= cap) return pack0(DG_ST_DEEP, 0);
+            auto &f = F(sp++);
+            f.kind = TF_MAP;
+            f.td = td;
+            f.n = (uint32_t)n;
+            f.i = 0;
+            o.w8('{');
+            return 0;
+        }
+        }
+        return t2j_err(DG_T2J_E_UNSUPPORTED, r.p, t.ttype);
+    };
+
+    /* one element inside a skipped container, or skipType
+     * (thrift/binary_skip.go:109-210) of wire type t with budget `depth`:
+     * fixed sizes are skipn'd before any depth check, list/map strings are
+     * skipstr'd directly (str_direct), everything else is skipType(t, depth):
+     * containers continue as a skip frame */
+    auto skip = [&](uint8_t t, uint32_t depth, bool str_direct) -> uint64_t {
+        const uint32_t fs = fixed_size(t);
+        if (fs) {
+            if (!r.need(fs)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+            r.p += fs;
+            return 0;
+        }
+        if (!(str_direct && t == DG_T_STRING) && (int32_t)depth <= 0) return t2j_err(DG_T2J_E_READ, r.p, RD_DEPTH);
+        if (t == DG_T_STRING) { /* skipstr (:80-95): the size as uint32 in a 64-bit int */
+            if (!r.need(4)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+            const uint64_t sz = (uint32_t)__builtin_bswap32((uint32_t)r.src.get8(r.p));
+            if (r.p + 4 + (int64_t)sz > (int64_t)r.src.n) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+            r.p += 4 + (int64_t)sz;
+            return 0;
+        }
+        if (t == DG_T_STRUCT) {
+            if (sp >= cap) return pack0(DG_ST_DEEP, 0);
+            auto &f = F(sp++);
+            f.kind = TF_SKIP_STRUCT;
+            f.u = depth;
+            return 0;
+        }
+        if (t == DG_T_MAP) {
+            if (!r.need(6)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+            const uint8_t kt = r.u8(), vt = r.u8();
+            const int32_t sz = (int32_t)r.be(4);
+            if (sz < 0) return t2j_err(DG_T2J_E_READ, r.p, RD_BAD_SIZE);
+            const uint32_t ks = fixed_size(kt), vs = fixed_size(vt);
+            if (ks && vs) {
+                const int64_t k = (int64_t)sz * (int64_t)(ks + vs);
+                if (!r.need(k)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+                r.p += k;
+                return 0;
+            }
+            if (sp >= cap) return pack0(DG_ST_DEEP, 0);
+            auto &f = F(sp++);
+            f.kind = TF_SKIP_MAP;
+            f.td = kt | ((uint32_t)vt << 8);
+            f.n = (uint32_t)sz * 2; /* keys and values alternate */
+            f.i = 0;
+            f.u = depth;
+            return 0;
+        }
+        if (t == DG_T_LIST || t == DG_T_SET) {
+            if (!r.need(5)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+            const uint8_t vt = r.u8();
+            const int32_t sz = (int32_t)r.be(4);
+            if (sz < 0) return t2j_err(DG_T2J_E_READ, r.p, RD_BAD_SIZE);
+            const uint32_t vs = fixed_size(vt);
+            if (vs) {
+                const int64_t k = (int64_t)sz * (int64_t)vs;
+                if (!r.need(k)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+                r.p += k;
+                return 0;
+            }
+            if (sp >= cap) return pack0(DG_ST_DEEP, 0);
+            auto &f = F(sp++);
+            f.kind = TF_SKIP_LIST;
+            f.td = vt;
+            f.n = (uint32_t)sz;
+            f.i = 0;
+            f.u = depth;
+            return 0;
+        }
+        return t2j_err(DG_T2J_E_READ, r.p, RD_BAD_SIZE); /* default: errInvalidDataSize */
+    };
+
+    uint64_t e = value(root);
+    if (e) return e;
+    while (sp) {
+        auto &f = F(sp - 1);
+        switch (f.kind) {
+        case TF_STRUCT: {
+            const dg_type st = ldrec(&D.T[f.td]);
+            const dg_struct sd = ldrec(&D.S[st.st]);
+            if (!r.need(1)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+            const uint8_t t = r.u8();
+            if (!ttype_valid(t)) return t2j_err(DG_T2J_E_READ, r.p, RD_BAD_TYPE);
+            if (t == 0) {
+                /* handleUnsets -> HandleRequires (thrift/utils.go:149-176), ascending id */
+                uint64_t bits = f.u;
+                while (bits) {
+                    const uint32_t k = (uint32_t)__builtin_ctzll(bits);
+                    bits &= bits - 1;
+                    const dg_field fd = ldrec(&D.F[sd.field_begin + k]);
+                    if (fd.required == DG_REQ_REQUIRED && !(opts & DG_T2J_WRITE_REQUIRE))
+                        return t2j_err(DG_T2J_E_MISS_REQUIRED, r.p, fd.id);
+                    if ((fd.required == DG_REQ_DEFAULT && !(opts & DG_T2J_WRITE_DEFAULT)) ||
+                        (fd.required == DG_REQ_OPTIONAL && !(opts & DG_T2J_WRITE_OPTIONAL) && fd.dflt_len == DG_NONE))
+                        continue;
+                    if (fd.dflt_len != DG_NONE) return t2j_err(DG_T2J_E_NEEDS_HOST, r.p, fd.id); /* JSONValue() */
+                    if (f.i) o.w8(',');
+                    f.i = 1;
+                    const dg_t2j_field xf = ldrec(&X.X[sd.field_begin + k]);
+                    emit_side(o, X, xf.name_off, xf.name_len); /* "name": */
+                    switch (ldrec(&D.T[fd.type]).ttype) { /* writeDefaultOrEmpty conv/t2j/impl.go:440-468 */
+                    case DG_T_BOOL: o.wle('f' | ('a' << 8) | ('l' << 16) | ('s' << 24) | (0x65ull << 32), 5); break;
+                    case DG_T_BYTE: case DG_T_I16: case DG_T_I32: case DG_T_I64: case DG_T_DOUBLE: o.w8('0'); break;
+                    case DG_T_STRING: o.wle('"' | ('"' << 8), 2); break;
+                    case DG_T_LIST: case DG_T_SET: o.wle('[' | (']' << 8), 2); break;
+                    case DG_T_MAP: case DG_T_STRUCT: o.wle('{' | ('}' << 8), 2); break;
+                    default: return t2j_err(DG_T2J_E_UNSUPPORTED, r.p, ldrec(&D.T[fd.type]).ttype);
+                    }
+                }
+                o.w8('}');
+                sp--;
+                continue;
+            }
+            if (!r.need(2)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+            const uint16_t id = (uint16_t)r.be(2);
+            const int32_t fi = t2j_field(D, sd, f.n, id);
+            if (fi < 0) {
+                if (opts & DG_T2J_DISALLOW_UNKNOWN) return t2j_err(DG_T2J_E_UNKNOWN_FIELD, r.p, id);
+                if ((e = skip(t, T2J_SKIP_DEPTH, false))) return e;
+                continue;
+            }
+            const uint32_t k = (uint32_t)fi - sd.field_begin;
+            f.u &= ~(1ull << k);
+            f.n = k + 1;
+            if (f.i) o.w8(',');
+            f.i = 1;
+            const dg_t2j_field xf = ldrec(&X.X[fi]);
+            emit_side(o, X, xf.key_off, xf.key_len); /* "alias": */
+            const dg_field fd = ldrec(&D.F[fi]);
+            if ((opts & DG_T2J_ENABLE_VM) && fd.vm != DG_VM_NONE) {
+                /* apiJSConv.Read (thrift/annotation/value_mapping.go:143-214) */
+                if (fd.vm != DG_VM_JSCONV) return t2j_err(DG_T2J_E_NEEDS_HOST, r.p, fd.vm);
+                const uint8_t ft = ldrec(&D.T[fd.type]).ttype;
+                uint8_t et = ft;
+                int32_t cnt = 1;
+                if (ft == DG_T_LIST) {
+                    o.w8('[');
+                    if (!r.need(1)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+                    et = r.u8();
+                    if (!ttype_valid(et)) return t2j_err(DG_T2J_E_READ, r.p, RD_BAD_TYPE);
+                    if (!r.need(4)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+                    cnt = (int32_t)r.be(4);
+                    if (cnt < 0) return t2j_err(DG_T2J_E_READ, r.p, RD_BAD_SIZE);
+                }
+                for (int32_t j = 0; j < cnt; j++) { /* appendInt */
+                    o.w8('"');
+                    switch (et) {
+                    case DG_T_BYTE:
+                        if (!r.need(1)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+                        emit_i64(o, (int64_t)r.u8()); /* ReadByte: 0..255 */
+                        break;
+                    case DG_T_I16:
+                        if (!r.need(2)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+                        emit_i64(o, (int16_t)r.be(2));
+                        break;
+                    case DG_T_I32:
+                        if (!r.need(4)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+                        emit_i64(o, (int32_t)r.be(4));
+                        break;
+                    case DG_T_I64:
+                        if (!r.need(8)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+                        emit_i64(o, (int64_t)r.be(8));
+                        break;
+                    case DG_T_DOUBLE: {
+                        if (!r.need(8)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+                        const uint64_t u = r.be(8);
+                        if (((u >> 52) & 0x7FF) != 0x7FF) emit_f64(o, __longlong_as_double((long long)u)); /* f64toa: nothing for inf/nan */
+                        break;
+                    }
+                    case DG_T_STRING: {
+                        if (!r.need(4)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+                        const int32_t sz = (int32_t)r.be(4);
+                        if (sz < 0 || !r.need(sz)) return t2j_err(DG_T2J_E_READ, r.p, RD_BAD_SIZE);
+                        for (int32_t b = 0; b < sz; b++) o.w8(r.src.raw(r.p + b)); /* raw, not escaped */
+                        r.p += sz;
+                        break;
+                    }
+                    default:
+                        return t2j_err(DG_T2J_E_UNSUPPORTED, r.p, et);
+                    }
+                    o.w8('"');
+                    if (ft == DG_T_LIST && j != cnt - 1) o.w8(',');
+                }
+                if (ft == DG_T_LIST) o.w8(']');
+                continue;
+            }
+            if ((e = value(fd.type))) return e;
+            continue;
+        }
+        case TF_LIST: {
+            if (f.i == f.n) {
+                o.w8(']');
+                sp--;
+                continue;
+            }
+            if (f.i) o.w8(',');
+            f.i++;
+            if ((e = value(ldrec(&D.T[f.td]).elem))) return e;
+            continue;
+        }
+        case TF_MAP: {
+            if (f.i == f.n) {
+                o.w8('}');
+                sp--;
+                continue;
+            }
+            if (f.i) o.w8(',');
+            f.i++;
+            const dg_type mt = ldrec(&D.T[f.td]);
+            const uint8_t kt = ldrec(&D.T[mt.key]).ttype;
+            o.w8('"'); /* buildinTypeToKey (conv/t2j/impl.go:470-530) */
+            switch (kt) {
+            case DG_T_BYTE: {
+                if (!r.need(1)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+                const uint8_t v = r.u8();
+                emit_i64(o, (opts & DG_T2J_BYTE_AS_UINT8) ? (int64_t)v : (int64_t)(int8_t)v);
+                break;
+            }
+            case DG_T_I16:
+                if (!r.need(2)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+                emit_i64(o, (int16_t)r.be(2));
+                break;
+            case DG_T_I32:
+                if (!r.need(4)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+                emit_i64(o, (int32_t)r.be(4));
+                break;
+            case DG_T_I64:
+                if (!r.need(8)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+                emit_i64(o, (int64_t)r.be(8));
+                break;
+            case DG_T_STRING: {
+                if (!r.need(4)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+                const int32_t sz = (int32_t)r.be(4);
+                if (sz < 0 || !r.need(sz)) return t2j_err(DG_T2J_E_READ, r.p, RD_BAD_SIZE);
+                emit_quoted(o, r.src, r.p, sz); /* json.NoQuote */
+                r.p += sz;
+                break;
+            }
+            default:
+                return t2j_err(DG_T2J_E_UNSUPPORTED, r.p, kt);
+            }
+            o.wle('"' | (':' << 8), 2);
+            if ((e = value(mt.elem))) return e;
+            continue;
+        }
+        case TF_SKIP_STRUCT: {
+            const uint32_t depth = (uint32_t)f.u;
+            if (!r.need(1)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+            const uint8_t tp = r.u8();
+            if (tp == 0) {
+                sp--;
+                continue;
+            }
+            if (!r.need(2)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+            r.p += 2;
+            if ((e = skip(tp, depth - 1, false))) return e;
+            continue;
+        }
+        case TF_SKIP_LIST:
+        case TF_SKIP_MAP: {
+            if (f.i == f.n) {
+                sp--;
+                continue;
+            }
+            const uint8_t et = f.kind == TF_SKIP_LIST ? (uint8_t)f.td : (uint8_t)(f.i & 1 ? f.td >> 8 : f.td);
+            f.i++;
+            if ((e = skip(et, (uint32_t)f.u - 1, true))) return e;
+            continue;
+        }
+        }
+    }
+    return 0;
+}
+
+struct T2JParams {
+    uint32_t root;
+    uint64_t opts;
+    const uint8_t *src;       /* Thrift arena */
+    const uint64_t *in_off;   /* n + 1 */
+    uint64_t n;
+    uint8_t *out;             /* JSON slots */
+    const uint64_t *out_off;
+    uint32_t *out_len;        /* JSON bytes; DG_ST_OUT_OVERFLOW: bytes needed */
+    uint64_t *ret;
+    const uint8_t *blob;      /* descriptor (device) */
+    dg_desc_hdr hdr;
+    const uint8_t *side;      /* t2j side table (device) */
+    uint32_t *deep_list;      /* messages nested beyond the LDS frames */
+    uint32_t *deep_count;     /* their number (reset by the host after the deep pass) */
+    uint8_t *ws;              /* deep pass: T2J_DEEP_DEPTH frames per lane */
+};
+
+DGI T2JSide t2j_side(const uint8_t *side)
+{
+    const dg_t2j_hdr xh = *(const dg_t2j_hdr *)side;
+    return T2JSide{(const __attribute__((address_space(1))) dg_t2j_field *)(const void *)(side + xh.off_fields),
+                   (const __attribute__((address_space(1))) uint8_t *)(const void *)(side + xh.off_pool)};
+}
+
+/* finish one message: overflow check, status and length */
+DGI void t2j_store(const T2JParams &P, uint64_t i, uint64_t r, Out &o)
+{
+    uint32_t olen = 0;
+    if (r == 0) {
+        o.finish();
+        if (o.len > o.cap) {
+            const uint64_t need = o.len;
+            olen = need > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)need;
+            r = pack(DG_ST_OUT_OVERFLOW, need > 0xFFFFFFull ? 0xFFFFFFull : need, 0);
+        } else {
+            olen = (uint32_t)o.len;
+        }
+    }
+    P.ret[i] = r;
+    P.out_len[i] = olen;
+}
+
+constexpr uint32_t T2J_DEEP_BLOCKS = 4; /* 1024 lanes x 96 KiB of frames */
+
+void launch_t2j_kernels(uint64_t n, hipStream_t s, const T2JParams &P);
+
+}  // namespace dg

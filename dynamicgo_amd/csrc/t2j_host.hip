@@ -1,0 +1,184 @@
+/*
+ * t2j_host.hip — the C ABI of the reverse path, Thrift binary -> JSON
+ * (include/dgj2t.h dg_desc_attach_t2j / dg_t2j_*; the reference's
+ * t2j.BinaryConv.Do / DoInto, conv/t2j/conv.go:50-95). Kernels: t2j_device.h.
+ */
+#include <string.h>
+
+#include "host_internal.h"
+#include "t2j_device.h"
+
+using namespace dg;
+
+static const uint64_t T2J_DEEP_WS = (uint64_t)T2J_DEEP_BLOCKS * T2J_BLOCK * T2J_DEEP_DEPTH * sizeof(T2JFrame);
+
+/* one batch on stream s: the LDS-frame pass, the deep pass over what it
+ * queued, then the queue counter reset; the scratch's `done` event after */
+static int t2j_launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *src, const uint64_t *in_off,
+                      uint64_t n, uint64_t opts, uint8_t *out, const uint64_t *out_off, uint32_t *out_len,
+                      uint64_t *ret, hipStream_t s)
+{
+    if (n == 0) return DG_OK;
+    if (!d->d_side) return set_err(DG_E_DESC, "descriptor has no t2j side table (dg_desc_attach_t2j)");
+    if (root >= d->hdr.n_types) return set_err(DG_E_INVALID, "root type %u out of range", root);
+    if (n > 0xFFFFFFFFull) return set_err(DG_E_INVALID, "batch of %llu messages", (unsigned long long)n);
+    Scratch *x;
+    int rc = scratch_for(c, s, &x);
+    if (rc) return rc;
+    if ((rc = grow_x(x, x->t2j_list, x->t2j_list_cap, n))) return rc;
+    if (!x->ws_t2j) HIPCHK(hipMalloc(&x->ws_t2j, T2J_DEEP_WS));
+    T2JParams P;
+    memset(&P, 0, sizeof P);
+    P.root = root;
+    P.opts = opts;
+    P.src = src;
+    P.in_off = in_off;
+    P.n = n;
+    P.out = out;
+    P.out_off = out_off;
+    P.out_len = out_len;
+    P.ret = ret;
+    P.blob = d->d_blob;
+    P.hdr = d->hdr;
+    P.side = d->d_side;
+    P.deep_list = x->t2j_list;
+    P.deep_count = x->d_counts + 3;
+    P.ws = x->ws_t2j;
+    launch_t2j_kernels(n, s, P);
+    hipError_t e = hipGetLastError();
+    (void)hipMemsetAsync(x->d_counts + 3, 0, 4, s);
+    HIPCHK(hipEventRecord(x->done, s));
+    x->used = true;
+    x->last = s;
+    if (e != hipSuccess) return set_err(DG_E_HIP, "t2j launch: %s", hipGetErrorString(e));
+    return DG_OK;
+}
+
+extern "C" {
+
+int dg_desc_attach_t2j(dg_desc *d, const void *side, size_t len)
+{
+    if (!d || !side || len < sizeof(dg_t2j_hdr)) return set_err(DG_E_INVALID, "bad args");
+    dg_t2j_hdr h;
+    memcpy(&h, side, sizeof h);
+    if (h.magic != DG_T2J_MAGIC || h.version != 1 || h.total_len > len || h.n_fields != d->hdr.n_fields ||
+        (uint64_t)h.off_fields + (uint64_t)h.n_fields * sizeof(dg_t2j_field) > len ||
+        (uint64_t)h.off_pool + h.pool_len > len || (h.off_pool & 7))
+        return set_err(DG_E_DESC, "bad t2j side table");
+    /* every key range inside the pool (the kernel reads them unchecked) */
+    const dg_t2j_field *f = (const dg_t2j_field *)((const uint8_t *)side + h.off_fields);
+    for (uint32_t k = 0; k < h.n_fields; k++)
+        if ((uint64_t)f[k].key_off + f[k].key_len > h.pool_len || (uint64_t)f[k].name_off + f[k].name_len > h.pool_len ||
+            (f[k].key_off & 7) || (f[k].name_off & 7))
+            return set_err(DG_E_DESC, "t2j side table: field %u key out of range", k);
+    std::lock_guard<std::mutex> g(d->ctx->mu);
+    HIPCHK(hipSetDevice(d->ctx->device));
+    uint8_t *p;
+    HIPCHK(hipMalloc(&p, len + 16)); /* the kernel reads whole words past a key's end */
+    HIPCHK(hipMemcpy(p, side, len, hipMemcpyHostToDevice));
+    HIPCHK(hipMemset(p + len, 0, 16));
+    if (d->d_side) {
+        HIPCHK(hipDeviceSynchronize()); /* launches in flight may read the old table */
+        (void)hipFree(d->d_side);
+    }
+    d->d_side = p;
+    d->side_len = len;
+    return DG_OK;
+}
+
+uint64_t dg_t2j_slot_bound(uint64_t len) { return (3 * len + 64 + 7) & ~7ull; }
+
+int dg_t2j_batch_device(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *d_thrift, const uint64_t *d_in_off,
+                        uint64_t n, uint64_t opts, uint8_t *d_out, const uint64_t *d_out_off, uint32_t *d_out_len,
+                        uint64_t *d_ret, void *stream)
+{
+    if (!c || !d) return set_err(DG_E_INVALID, "null ctx/desc");
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    return t2j_launch(c, d, root, d_thrift, d_in_off, n, opts, d_out, d_out_off, d_out_len, d_ret, s);
+}
+
+int dg_t2j_batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *thrift, const uint64_t *in_off,
+                      uint64_t n, uint64_t opts, uint8_t *out, uint64_t out_cap, uint64_t *out_off, uint64_t *ret,
+                      uint64_t *out_need)
+{
+    if (!c || !d || (!thrift && n) || !in_off || !out_off || (!ret && n)) return set_err(DG_E_INVALID, "bad args");
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    const uint64_t base = in_off[0];
+    std::vector<uint64_t> ioff(n + 1), soff(n + 1);
+    std::vector<uint32_t> olen(n);
+    std::vector<uint8_t> stage;
+    hipStream_t s = c->stream;
+    int rc;
+    /* pass 0: every message in a dg_t2j_slot_bound slot; pass 1: the
+     * overflowed ones again, each in a slot of exactly the size it reported */
+    std::vector<uint64_t> todo(n);
+    for (uint64_t i = 0; i < n; i++) todo[i] = i;
+    std::vector<uint64_t> slot_of(n, 0); /* stage offset of message i's final bytes */
+    for (int pass = 0; pass < 2 && !todo.empty(); pass++) {
+        const uint64_t m = todo.size();
+        std::vector<uint64_t> io(m + 1), so(m + 1);
+        io[0] = so[0] = 0;
+        for (uint64_t k = 0; k < m; k++) {
+            const uint64_t i = todo[k], len = in_off[i + 1] - in_off[i];
+            io[k + 1] = io[k] + len;
+            so[k + 1] = so[k] + (pass == 0 ? dg_t2j_slot_bound(len) : ((uint64_t)olen[i] + 64 + 7) & ~7ull);
+        }
+        if ((rc = grow(c->d_json, c->d_json_cap, io[m] + 64))) return rc;
+        if ((rc = grow(c->d_in_off, c->d_in_cap, m + 1))) return rc;
+        if ((rc = grow(c->d_out, c->d_out_cap, so[m] + 64))) return rc;
+        if ((rc = grow(c->d_out_off, c->d_oo_cap, m + 1))) return rc;
+        if ((rc = grow(c->d_out_len, c->d_ol_cap, m + 1))) return rc;
+        if ((rc = grow(c->d_ret, c->d_ret_cap, m + 1))) return rc;
+        if (pass == 0) {
+            HIPCHK(hipMemcpyAsync(c->d_json, thrift + base, io[m], hipMemcpyHostToDevice, s));
+        } else {
+            for (uint64_t k = 0; k < m; k++)
+                HIPCHK(hipMemcpyAsync(c->d_json + io[k], thrift + in_off[todo[k]], io[k + 1] - io[k],
+                                      hipMemcpyHostToDevice, s));
+        }
+        HIPCHK(hipMemsetAsync(c->d_json + io[m], 0, 64, s));
+        HIPCHK(hipMemcpyAsync(c->d_in_off, io.data(), (m + 1) * 8, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(c->d_out_off, so.data(), (m + 1) * 8, hipMemcpyHostToDevice, s));
+        if ((rc = t2j_launch(c, d, root, c->d_json, c->d_in_off, m, opts, c->d_out, c->d_out_off, c->d_out_len,
+                             c->d_ret, s)))
+            return rc;
+        std::vector<uint64_t> r(m);
+        std::vector<uint32_t> l(m);
+        HIPCHK(hipMemcpyAsync(r.data(), c->d_ret, m * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(l.data(), c->d_out_len, m * 4, hipMemcpyDeviceToHost, s));
+        const uint64_t off0 = stage.size();
+        stage.resize(off0 + so[m]);
+        HIPCHK(hipMemcpyAsync(stage.data() + off0, c->d_out, so[m], hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        std::vector<uint64_t> next;
+        for (uint64_t k = 0; k < m; k++) {
+            const uint64_t i = todo[k];
+            ret[i] = r[k];
+            olen[i] = l[k];
+            slot_of[i] = off0 + so[k];
+            if ((uint8_t)r[k] == DG_ST_OUT_OVERFLOW) {
+                if (pass == 1)
+                    return set_err(DG_E_NOMEM, "message %llu overflowed its exact-size slot", (unsigned long long)i);
+                next.push_back(i);
+            }
+        }
+        todo.swap(next);
+    }
+    uint64_t total = 0;
+    out_off[0] = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        if (ret[i] != 0) olen[i] = 0;
+        total += olen[i];
+        out_off[i + 1] = total;
+    }
+    if (out_need) *out_need = total;
+    if (total > out_cap || (!out && total)) return set_err(DG_E_NOMEM, "output needs %llu bytes", (unsigned long long)total);
+    for (uint64_t i = 0; i < n; i++)
+        if (olen[i]) memcpy(out + out_off[i], stage.data() + slot_of[i], olen[i]);
+    return DG_OK;
+}
+
+}  // extern "C"

@@ -274,6 +274,7 @@ def flatten(root: TypeDescriptor) -> FlatDescriptor:
             sindex[id(t.struct)] if t.struct is not None else DG_NONE))
 
     field_rows, name_rows, req_words, struct_rows = [], [], [], []
+    field_objs: List[FieldDescriptor] = []  # blob order (t2j side table)
     for sd in structs:
         fields = sorted(sd.fields, key=lambda f: f.id)
         # a field id may be Set twice in the IDL (ids.Set overwrites); keep last
@@ -284,6 +285,7 @@ def flatten(root: TypeDescriptor) -> FlatDescriptor:
         fbegin = len(field_rows)
         findex = {id(f): fbegin + i for i, f in enumerate(fields)}
         for f in fields:
+            field_objs.append(f)
             fl = (1 if f.is_request_base else 0) | (2 if f.http_mappings else 0)
             if sd.names.get(f.alias) is f:
                 fl |= 4  # DG_FF_ALIAS_SELF
@@ -342,7 +344,60 @@ def flatten(root: TypeDescriptor) -> FlatDescriptor:
                    len(field_rows), offs[2], len(name_rows), offs[3],
                    len(req_words), offs[4], len(pool), offs[5])
     body[:64] = hdr
-    return FlatDescriptor(bytes(body), root_idx, types)
+    fd = FlatDescriptor(bytes(body), root_idx, types)
+    fd.fields = field_objs
+    return fd
+
+
+def json_quote(b: bytes) -> bytes:
+    r"""The reference's native quote() with flags 0 (native/parsing.c:28-63,
+    _SingleQuoteTab): '"' and '\\' backslashed, \t \n \r short, every other
+    byte < 0x20 as \u00xx; no HTML escaping, no UTF-8 check."""
+    out = bytearray()
+    for c in b:
+        if c == 0x22:
+            out += b'\\"'
+        elif c == 0x5C:
+            out += b"\\\\"
+        elif c == 0x09:
+            out += b"\\t"
+        elif c == 0x0A:
+            out += b"\\n"
+        elif c == 0x0D:
+            out += b"\\r"
+        elif c < 0x20:
+            out += b"\\u%04x" % c
+        else:
+            out.append(c)
+    return bytes(out)
+
+
+DG_T2J_MAGIC = 0x32544744
+
+
+def flatten_t2j(fd: FlatDescriptor) -> bytes:
+    """The t2j side table of a flattened descriptor (include/dgj2t_desc.h
+    dg_t2j_*): per field, json.EncodeString(alias) + ':' and
+    EncodeString(name) + ':' (conv/t2j/impl.go:150-152, 431-433), and the raw
+    alias / name bytes."""
+    pool = bytearray()
+
+    def put(b: bytes):
+        off = len(pool)
+        pool.extend(b)
+        while len(pool) % 8:
+            pool.append(0)
+        return off, len(b)
+
+    rows = []
+    for f in fd.fields:
+        a, n = f.alias.encode(), f.name.encode()
+        rows.append(_st.pack("<8I", *put(b'"' + json_quote(a) + b'":'), *put(b'"' + json_quote(n) + b'":'),
+                             *put(a), *put(n)))
+    off_fields = 32
+    off_pool = off_fields + 32 * len(rows)
+    body = _st.pack("<8I", DG_T2J_MAGIC, 1, off_pool + len(pool) + 16, len(rows), off_fields, len(pool), off_pool, 0)
+    return body + b"".join(rows) + bytes(pool) + bytes(16)
 
 
 # ============================================================================

@@ -177,6 +177,36 @@ int dg_agg_stats(dg_agg *agg, uint64_t *batches, uint64_t *msgs);
 /* converts what is still queued, then stops the flusher */
 void dg_agg_destroy(dg_agg *agg);
 
+/*
+ * t2j: Thrift binary -> JSON (the reverse path, conv/t2j). Replaces
+ * BinaryConv.Do / DoInto (conv/t2j/conv.go:50-95 over impl.go:74-468) for
+ * the options in dgj2t_defs.h DG_T2J_* (the Go-side ones -- HTTP mapping,
+ * ConvertException, EnableThriftBase -- stay on the Go host).
+ *
+ * dg_desc_attach_t2j uploads the descriptor's t2j side table (the JSON key
+ * text per field, include/dgj2t_desc.h dg_t2j_*) once; the t2j entry points
+ * need it. Status words: 0, DG_T2J_E_* | pos << 8 | value << 40 (pos = the
+ * Thrift read offset), or DG_ST_OUT_OVERFLOW with *out_len = bytes needed
+ * (device entry point only; the host entry point reruns those itself).
+ * Nesting deeper than the fast kernel's LDS frames is rerun on device with
+ * 4096 frames per message; deeper still is DG_T2J_E_DEPTH.
+ */
+int dg_desc_attach_t2j(dg_desc *desc, const void *side, size_t len);
+/* the slot size the host entry point gives a message of len Thrift bytes
+ * (a guess: JSON has no fixed bound over Thrift; larger outputs overflow and
+ * are rerun with their exact size) */
+uint64_t dg_t2j_slot_bound(uint64_t len);
+/* device buffers, stream-ordered, async; arena readable 16 bytes past the
+ * last message; d_out_off 8-aligned slots */
+int dg_t2j_batch_device(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, const uint8_t *d_thrift,
+                        const uint64_t *d_in_off, uint64_t n, uint64_t opts, uint8_t *d_out,
+                        const uint64_t *d_out_off, uint32_t *d_out_len, uint64_t *d_ret, void *stream);
+/* host buffers, synchronous: JSON packed back to back into out (out_off[n+1]);
+ * DG_E_NOMEM with *out_need when out_cap is too small */
+int dg_t2j_batch_host(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, const uint8_t *thrift,
+                      const uint64_t *in_off, uint64_t n, uint64_t opts, uint8_t *out, uint64_t out_cap,
+                      uint64_t *out_off, uint64_t *ret, uint64_t *out_need);
+
 /* Timing helper for benchmarks: launch the device batch `iters` times on the
  * context stream bracketed by HIP events; returns total milliseconds of GPU
  * time in *ms (events are recorded on the stream the kernels run on). */

@@ -34,4 +34,29 @@
 #define DG_E_NOMEM (-3)
 #define DG_E_DESC (-4)
 
+/* t2j (Thrift binary -> JSON, conv/t2j) option bits: the conv.Options fields
+ * conv/t2j/impl.go reads (conv/api.go:52-121) */
+#define DG_T2J_BYTE_AS_UINT8 (1ull << 0)     /* ByteAsUint8 */
+#define DG_T2J_INT64_AS_STRING (1ull << 1)   /* Int642String */
+#define DG_T2J_NULL_FOR_NAN_INF (1ull << 2)  /* EncodeNullJSONForInfOrNan */
+#define DG_T2J_NO_BASE64 (1ull << 3)         /* NoBase64Binary */
+#define DG_T2J_DISALLOW_UNKNOWN (1ull << 4)  /* DisallowUnknownField */
+#define DG_T2J_WRITE_DEFAULT (1ull << 5)     /* WriteDefaultField */
+#define DG_T2J_WRITE_REQUIRE (1ull << 6)     /* WriteRequireField */
+#define DG_T2J_WRITE_OPTIONAL (1ull << 7)    /* WriteOptionalField */
+#define DG_T2J_ENABLE_VM (1ull << 8)         /* EnableValueMapping (api.js_conv) */
+
+/* t2j per-message status codes (bits 0-7 of the status word; pos = Thrift
+ * read offset, value as noted). The reference returns Go errors whose
+ * meta.ErrorCode behaviour is given. */
+#define DG_T2J_E_READ 1           /* ErrRead: truncated input, invalid type / size, skip depth; value = reason */
+#define DG_T2J_E_UNKNOWN_FIELD 2  /* ErrUnknownField: value = field id */
+#define DG_T2J_E_DISMATCH_TYPE 3  /* ErrDismatchType: value = expected << 8 | got */
+#define DG_T2J_E_UNSUPPORTED 4    /* ErrUnsupportedType: value = type */
+#define DG_T2J_E_NAN_INF 5        /* ErrWrite: "encounter Nan or Inf double" */
+#define DG_T2J_E_MISS_REQUIRED 6  /* ErrMissRequiredField: value = field id */
+#define DG_T2J_E_NEEDS_HOST 7     /* a Go-side feature: IDL default JSON values, HTTP mapping, non-inline value mapping,
+                                     structs of more than 64 fields */
+#define DG_T2J_E_DEPTH 8          /* nesting beyond 4096 containers (the GPU's frame budget; Go recurses further) */
+
 #endif /* DGJ2T_DEFS_H */

@@ -130,6 +130,29 @@ typedef struct dg_name {
     uint32_t field;       /* global field index, DG_NONE = empty slot */
 } dg_name;
 
+/* t2j side table (dg_desc_attach_t2j): per field of the descriptor blob,
+ * the JSON text t2j writes for its key, pre-encoded on the host
+ * (json.EncodeString(alias) + ':' for fields, EncodeString(name) + ':' for
+ * the unset fields handleUnsets writes, conv/t2j/impl.go:150-152,431-433),
+ * and the raw alias / name bytes. */
+#define DG_T2J_MAGIC 0x32544744u /* "DGT2" */
+typedef struct dg_t2j_hdr {
+    uint32_t magic;
+    uint32_t version;   /* 1 */
+    uint32_t total_len;
+    uint32_t n_fields;  /* == the descriptor's n_fields */
+    uint32_t off_fields;
+    uint32_t pool_len, off_pool;
+    uint32_t _pad;
+} dg_t2j_hdr; /* 32 B */
+
+typedef struct dg_t2j_field {
+    uint32_t key_off, key_len;       /* "alias": (quoted, colon) */
+    uint32_t name_off, name_len;     /* "name": */
+    uint32_t alias_off, alias_len;   /* raw alias bytes */
+    uint32_t rname_off, rname_len;   /* raw name bytes */
+} dg_t2j_field;
+
 /* Key hash used by the name tables: h = (h * 33) ^ byte, seed 5381. */
 #define DG_NAME_HASH_SEED 5381u
 #define DG_NAME_HASH_STEP(h, b) ((((h) << 5) + (h)) ^ (uint32_t)(uint8_t)(b))

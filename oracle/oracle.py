@@ -141,6 +141,36 @@ class _Base:
         return float(best.value)
 
 
+class RefT2J:
+    """t2j checker: the C restatement of conv/t2j over the reference's own
+    native encoders (oracle/ref_harness.c dgref_t2j)."""
+
+    def __init__(self, lib: C.CDLL):
+        self.f = lib.dgref_t2j
+        self.f.restype = C.c_uint64
+        self.f.argtypes = [C.c_char_p, C.c_char_p, C.c_uint32, C.c_char_p, C.c_size_t, C.c_uint64,
+                           C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]
+
+    def t2j(self, flat, side: bytes, thrift: bytes, opts: int, root: Optional[int] = None) -> Tuple[int, bytes]:
+        root = flat.root_type if root is None else root
+        cap = 8 * len(thrift) + 4096
+        for _ in range(2):
+            out = C.create_string_buffer(cap)
+            ol = C.c_size_t(0)
+            ret = int(self.f(flat.blob, side, root, thrift, len(thrift), opts, out, cap, C.byref(ol)))
+            if ret != 0:
+                return ret, b""
+            if ol.value <= cap:
+                return 0, out.raw[:ol.value]
+            cap = ol.value + 64
+        raise RuntimeError("t2j oracle output did not fit")
+
+
+def RefT2JOracle() -> Optional[RefT2J]:
+    p = ref_lib_path()
+    return RefT2J(C.CDLL(p)) if p else None
+
+
 def physical_cpus() -> Tuple[List[int], int]:
     """CPUs this process may run on, one per physical core (lowest SMT
     sibling), and how many logical CPUs the affinity mask allows."""

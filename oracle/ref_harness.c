@@ -32,6 +32,7 @@
 #include <string.h>
 
 #include "../include/dgj2t_desc.h"
+#include "../include/dgj2t_defs.h"
 
 typedef struct {
     tTypeDesc *types;
@@ -515,4 +516,504 @@ int dgref_j2t_timed(void *desc, uint32_t root, const uint8_t *json, const uint64
     free(th);
     *best_s = best;
     return 0;
+}
+
+/* ====================================================================== */
+/* t2j (Thrift binary -> JSON): a C restatement of the reference's Go t2j  */
+/* (conv/t2j/impl.go:74-607, thrift/binary.go read functions,              */
+/* thrift/binary_skip.go:105-210 skipType, thrift/utils.go:149-176         */
+/* HandleRequires, thrift/annotation/value_mapping.go:143-214 js_conv Read)*/
+/* over the reference's OWN native encoders compiled above: quote()        */
+/* (native/parsing.c:487), i64toa (native/fastint.c:212), f64toa           */
+/* (native/fastfloat.c:349) and b64encode (native/base64.c:173). The Go    */
+/* control flow is restated (no Go toolchain here); the byte encoders are  */
+/* the reference's.                                                        */
+/* ====================================================================== */
+typedef struct {
+    const uint8_t *b;
+    size_t n, p;
+} TRd;
+typedef struct {
+    char *b;
+    size_t len, cap;
+} JBuf;
+typedef struct {
+    const uint8_t *blob;
+    const dg_desc_hdr *h;
+    const dg_type *T;
+    const dg_struct *S;
+    const dg_field *F;
+    const uint64_t *R;
+    const dg_t2j_field *X;
+    const char *XP; /* side-table pool */
+    uint64_t opts;
+} T2J;
+
+#define T2J_ERR(code, pos, val) ((uint64_t)(code) | ((uint64_t)(pos) << 8) | ((uint64_t)(val) << 40))
+enum { RD_EOF = 1, RD_BAD_TYPE = 2, RD_BAD_SIZE = 3, RD_DEPTH = 4 };
+
+static void jb_put(JBuf *o, const void *s, size_t k)
+{
+    if (o->len + k + 64 > o->cap) {
+        size_t nc = (o->cap + k + 64) * 2;
+        char *nb = (char *)malloc(nc);
+        memcpy(nb, o->b, o->len);
+        free(o->b);
+        o->b = nb;
+        o->cap = nc;
+    }
+    memcpy(o->b + o->len, s, k);
+    o->len += k;
+}
+static void jb_c(JBuf *o, char c) { jb_put(o, &c, 1); }
+static void jb_i64(JBuf *o, int64_t v)
+{
+    char t[32];
+    int k = i64toa(t, v); /* native/fastint.c:212 */
+    jb_put(o, t, (size_t)k);
+}
+static void jb_f64(JBuf *o, double v)
+{
+    char t[40];
+    int k = f64toa(t, v); /* native/fastfloat.c:349 (0 for inf/nan: nothing, like the Go wrapper) */
+    jb_put(o, t, (size_t)k);
+}
+static void jb_quote(JBuf *o, const uint8_t *s, size_t n) /* json.NoQuote: native quote, flags 0 */
+{
+    if (!n)
+        return;
+    ssize_t dn = (ssize_t)(n * 6 + 8);
+    char *t = (char *)malloc((size_t)dn);
+    quote((const char *)s, (ssize_t)n, t, &dn, 0);
+    jb_put(o, t, (size_t)dn);
+    free(t);
+}
+static void jb_string(JBuf *o, const uint8_t *s, size_t n) /* json.EncodeString */
+{
+    jb_c(o, '"');
+    jb_quote(o, s, n);
+    jb_c(o, '"');
+}
+
+static int rd_need(TRd *r, size_t k) { return r->p + k <= r->n; }
+static uint64_t rd_be(TRd *r, int k)
+{
+    uint64_t v = 0;
+    for (int i = 0; i < k; i++)
+        v = (v << 8) | r->b[r->p + i];
+    r->p += (size_t)k;
+    return v;
+}
+static int ttype_valid(uint8_t t) /* thrift/descriptor.go:60-67 */
+{
+    switch (t) {
+    case 0: case 1: case 2: case 3: case 4: case 6: case 8: case 10: case 11: case 12: case 13: case 14: case 15:
+    case 16: case 17:
+        return 1;
+    }
+    return 0;
+}
+static int fixed_size(uint8_t t) /* typeSize, thrift/binary_skip.go:26-41 */
+{
+    switch (t) {
+    case 2: case 3: return 1;
+    case 6: return 2;
+    case 8: return 4;
+    case 10: case 4: return 8;
+    }
+    return 0;
+}
+
+/* skipstr (thrift/binary_skip.go:80-95): the size is read as uint32 into a
+ * 64-bit int; nothing is consumed on failure */
+static int t2j_skipstr(TRd *r)
+{
+    if (!rd_need(r, 4)) return RD_EOF;
+    uint64_t sz = ((uint64_t)r->b[r->p] << 24) | ((uint64_t)r->b[r->p + 1] << 16) | ((uint64_t)r->b[r->p + 2] << 8) |
+                  r->b[r->p + 3];
+    if (r->p + 4 + sz > r->n) return RD_EOF;
+    r->p += 4 + sz;
+    return 0;
+}
+
+/* skipType (thrift/binary_skip.go:109-210): 0 or an RD_* reason */
+static int t2j_skip(TRd *r, uint8_t t, int depth)
+{
+    if (depth <= 0)
+        return RD_DEPTH;
+    int fs = fixed_size(t);
+    if (fs > 0) {
+        if (!rd_need(r, (size_t)fs)) return RD_EOF;
+        r->p += (size_t)fs;
+        return 0;
+    }
+    switch (t) {
+    case 11:
+        return t2j_skipstr(r);
+    case 12:
+        for (;;) {
+            if (!rd_need(r, 1)) return RD_EOF;
+            uint8_t tp = r->b[r->p++];
+            if (tp == 0) break;
+            if (!rd_need(r, 2)) return RD_EOF;
+            r->p += 2;
+            int e = fixed_size(tp) > 0 ? (rd_need(r, (size_t)fixed_size(tp)) ? (r->p += (size_t)fixed_size(tp), 0) : RD_EOF)
+                                       : t2j_skip(r, tp, depth - 1);
+            if (e) return e;
+        }
+        return 0;
+    case 13: {
+        if (!rd_need(r, 6)) return RD_EOF;
+        uint8_t kt = r->b[r->p], vt = r->b[r->p + 1];
+        r->p += 2;
+        int32_t sz = (int32_t)rd_be(r, 4);
+        if (sz < 0) return RD_BAD_SIZE;
+        int ks = fixed_size(kt), vs = fixed_size(vt);
+        if (ks > 0 && vs > 0) {
+            uint64_t k = (uint64_t)sz * (uint64_t)(ks + vs);
+            if (!rd_need(r, k)) return RD_EOF;
+            r->p += k;
+            return 0;
+        }
+        for (int32_t i = 0; i < sz; i++) {
+            int e;
+            if (ks > 0) e = rd_need(r, (size_t)ks) ? (r->p += (size_t)ks, 0) : RD_EOF;
+            else e = kt == 11 ? t2j_skipstr(r) : t2j_skip(r, kt, depth - 1);
+            if (e) return e;
+            if (vs > 0) e = rd_need(r, (size_t)vs) ? (r->p += (size_t)vs, 0) : RD_EOF;
+            else e = vt == 11 ? t2j_skipstr(r) : t2j_skip(r, vt, depth - 1);
+            if (e) return e;
+        }
+        return 0;
+    }
+    case 14: case 15: {
+        if (!rd_need(r, 5)) return RD_EOF;
+        uint8_t vt = r->b[r->p++];
+        int32_t sz = (int32_t)rd_be(r, 4);
+        if (sz < 0) return RD_BAD_SIZE;
+        int vs = fixed_size(vt);
+        if (vs > 0) {
+            uint64_t k = (uint64_t)sz * (uint64_t)vs;
+            if (!rd_need(r, k)) return RD_EOF;
+            r->p += k;
+            return 0;
+        }
+        for (int32_t i = 0; i < sz; i++) {
+            int e = vt == 11 ? t2j_skipstr(r) : t2j_skip(r, vt, depth - 1);
+            if (e) return e;
+        }
+        return 0;
+    }
+    }
+    return RD_BAD_SIZE; /* default: errInvalidDataSize */
+}
+
+static int32_t t2j_field_by_id(const T2J *c, const dg_struct *sd, uint16_t id)
+{
+    for (uint32_t k = 0; k < sd->n_fields; k++)
+        if (c->F[sd->field_begin + k].id == id)
+            return (int32_t)(sd->field_begin + k);
+    return -1;
+}
+
+static uint64_t t2j_value(const T2J *c, uint32_t td, TRd *r, JBuf *o);
+
+/* writeDefaultOrEmpty (conv/t2j/impl.go:440-468) */
+static uint64_t t2j_default_or_empty(const T2J *c, const dg_field *f, size_t pos, JBuf *o)
+{
+    if (f->dflt_len != DG_NONE)
+        return T2J_ERR(DG_T2J_E_NEEDS_HOST, pos, f->id); /* DefaultValue().JSONValue(): Go-side */
+    switch (c->T[f->type].ttype) {
+    case 2: jb_put(o, "false", 5); return 0;
+    case 3: case 6: case 8: case 10: jb_i64(o, 0); return 0;
+    case 4: jb_f64(o, 0.0); return 0;
+    case 11: jb_put(o, "\"\"", 2); return 0;
+    case 14: case 15: jb_put(o, "[]", 2); return 0;
+    case 13: jb_put(o, "{}", 2); return 0;
+    case 12: jb_put(o, "{}", 2); return 0;
+    }
+    return T2J_ERR(DG_T2J_E_UNSUPPORTED, pos, c->T[f->type].ttype);
+}
+
+/* js_conv Read (thrift/annotation/value_mapping.go:143-214): appendInt */
+static uint64_t t2j_append_int(const T2J *c, uint8_t t, TRd *r, JBuf *o)
+{
+    jb_c(o, '"');
+    switch (t) {
+    case 3: if (!rd_need(r, 1)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_EOF); jb_i64(o, (int64_t)(uint8_t)rd_be(r, 1)); break;
+    case 6: if (!rd_need(r, 2)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_EOF); jb_i64(o, (int16_t)rd_be(r, 2)); break;
+    case 8: if (!rd_need(r, 4)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_EOF); jb_i64(o, (int32_t)rd_be(r, 4)); break;
+    case 10: if (!rd_need(r, 8)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_EOF); jb_i64(o, (int64_t)rd_be(r, 8)); break;
+    case 4: {
+        if (!rd_need(r, 8)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_EOF);
+        uint64_t u = rd_be(r, 8);
+        double d;
+        memcpy(&d, &u, 8);
+        jb_f64(o, d);
+        break;
+    }
+    case 11: {
+        if (!rd_need(r, 4)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_EOF);
+        int32_t sz = (int32_t)rd_be(r, 4);
+        if (sz < 0 || !rd_need(r, (size_t)sz)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_BAD_SIZE);
+        jb_put(o, r->b + r->p, (size_t)sz); /* raw, not escaped */
+        r->p += (size_t)sz;
+        break;
+    }
+    default:
+        return T2J_ERR(DG_T2J_E_UNSUPPORTED, r->p, t);
+    }
+    jb_c(o, '"');
+    return 0;
+}
+
+static uint64_t t2j_vm(const T2J *c, const dg_field *f, TRd *r, JBuf *o)
+{
+    if (f->vm != DG_VM_JSCONV)
+        return T2J_ERR(DG_T2J_E_NEEDS_HOST, r->p, f->vm);
+    if (c->T[f->type].ttype == 15) { /* LIST: ReadListBegin, elements by the wire type */
+        jb_c(o, '[');
+        if (!rd_need(r, 1)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_EOF); /* ReadListBegin */
+        uint8_t et = r->b[r->p++];
+        if (!ttype_valid(et)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_BAD_TYPE);
+        if (!rd_need(r, 4)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_EOF);
+        int32_t n = (int32_t)rd_be(r, 4);
+        if (n < 0) return T2J_ERR(DG_T2J_E_READ, r->p, RD_BAD_SIZE);
+        for (int32_t i = 0; i < n; i++) {
+            uint64_t e = t2j_append_int(c, et, r, o);
+            if (e) return e;
+            if (i != n - 1) jb_c(o, ',');
+        }
+        jb_c(o, ']');
+        return 0;
+    }
+    return t2j_append_int(c, c->T[f->type].ttype, r, o);
+}
+
+/* a STRUCT value (conv/t2j/impl.go:265-339; the top level :89-187 is the same
+ * without HTTP mapping / exceptions / ThriftBase, which the GPU path leaves
+ * to the Go host) */
+static uint64_t t2j_struct(const T2J *c, uint32_t td, TRd *r, JBuf *o)
+{
+    const dg_struct *sd = &c->S[c->T[td].st];
+    jb_c(o, '{');
+    uint64_t req[64];
+    uint32_t nw = sd->req_words < 64 ? sd->req_words : 64;
+    for (uint32_t w = 0; w < nw; w++)
+        req[w] = c->R[sd->req_begin + w];
+    int comma = 0;
+    for (;;) {
+        if (!rd_need(r, 1)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_EOF);
+        uint8_t t = r->b[r->p++];
+        if (!ttype_valid(t)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_BAD_TYPE);
+        if (t == 0) break;
+        if (!rd_need(r, 2)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_EOF);
+        uint16_t id = (uint16_t)rd_be(r, 2);
+        int32_t fi = t2j_field_by_id(c, sd, id);
+        if (fi < 0) {
+            if (c->opts & DG_T2J_DISALLOW_UNKNOWN) return T2J_ERR(DG_T2J_E_UNKNOWN_FIELD, r->p, id);
+            int e = t2j_skip(r, t, 1023);
+            if (e) return T2J_ERR(DG_T2J_E_READ, r->p, e);
+            continue;
+        }
+        const dg_field *f = &c->F[fi];
+        uint32_t k = (uint32_t)fi - sd->field_begin;
+        req[k / 64] &= ~(1ull << (k % 64)); /* r.Set(id, Optional) */
+        if (comma) jb_c(o, ',');
+        else comma = 1;
+        const dg_t2j_field *x = &c->X[fi];
+        jb_string(o, (const uint8_t *)c->XP + x->alias_off, x->alias_len);
+        jb_c(o, ':');
+        uint64_t e;
+        if ((c->opts & DG_T2J_ENABLE_VM) && f->vm != DG_VM_NONE) e = t2j_vm(c, f, r, o);
+        else e = t2j_value(c, f->type, r, o);
+        if (e) return e;
+    }
+    /* handleUnsets -> HandleRequires (thrift/utils.go:149-176), ascending id */
+    for (uint32_t k = 0; k < sd->n_fields; k++) {
+        if (!((req[k / 64] >> (k % 64)) & 1)) continue;
+        const dg_field *f = &c->F[sd->field_begin + k];
+        if (f->required == DG_REQ_REQUIRED && !(c->opts & DG_T2J_WRITE_REQUIRE))
+            return T2J_ERR(DG_T2J_E_MISS_REQUIRED, r->p, f->id);
+        if ((f->required == DG_REQ_DEFAULT && !(c->opts & DG_T2J_WRITE_DEFAULT)) ||
+            (f->required == DG_REQ_OPTIONAL && !(c->opts & DG_T2J_WRITE_OPTIONAL) && f->dflt_len == DG_NONE))
+            continue;
+        if (f->flags & DG_FF_HTTP_MAPPING) { /* resp == nil below the top level; the top level is Go-side */ }
+        if (comma) jb_c(o, ','); /* EncodeArrayComma */
+        else comma = 1;
+        const dg_t2j_field *x = &c->X[sd->field_begin + k];
+        jb_string(o, (const uint8_t *)c->XP + x->rname_off, x->rname_len); /* field.Name() */
+        jb_c(o, ':');
+        uint64_t e = t2j_default_or_empty(c, f, r->p, o);
+        if (e) return e;
+    }
+    jb_c(o, '}');
+    return 0;
+}
+
+/* doRecurse (conv/t2j/impl.go:189-393) */
+static uint64_t t2j_value(const T2J *c, uint32_t td, TRd *r, JBuf *o)
+{
+    const dg_type *t = &c->T[td];
+    switch (t->ttype) {
+    case 2: {
+        if (!rd_need(r, 1)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_EOF);
+        if (r->b[r->p++] == 1) jb_put(o, "true", 4);
+        else jb_put(o, "false", 5);
+        return 0;
+    }
+    case 3: {
+        if (!rd_need(r, 1)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_EOF);
+        uint8_t v = r->b[r->p++];
+        jb_i64(o, (c->opts & DG_T2J_BYTE_AS_UINT8) ? (int64_t)v : (int64_t)(int8_t)v);
+        return 0;
+    }
+    case 6:
+        if (!rd_need(r, 2)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_EOF);
+        jb_i64(o, (int16_t)rd_be(r, 2));
+        return 0;
+    case 8:
+        if (!rd_need(r, 4)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_EOF);
+        jb_i64(o, (int32_t)rd_be(r, 4));
+        return 0;
+    case 10:
+        if (!rd_need(r, 8)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_EOF);
+        if (c->opts & DG_T2J_INT64_AS_STRING) {
+            jb_c(o, '"');
+            jb_i64(o, (int64_t)rd_be(r, 8));
+            jb_c(o, '"');
+        } else {
+            jb_i64(o, (int64_t)rd_be(r, 8));
+        }
+        return 0;
+    case 4: {
+        if (!rd_need(r, 8)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_EOF);
+        uint64_t u = rd_be(r, 8);
+        if (((u >> 52) & 0x7FF) == 0x7FF) { /* NaN or Inf */
+            if (!(c->opts & DG_T2J_NULL_FOR_NAN_INF)) return T2J_ERR(DG_T2J_E_NAN_INF, r->p, 0);
+            jb_put(o, "null", 4);
+            return 0;
+        }
+        double d;
+        memcpy(&d, &u, 8);
+        jb_f64(o, d);
+        return 0;
+    }
+    case 11: {
+        if (!rd_need(r, 4)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_EOF);
+        int32_t sz = (int32_t)rd_be(r, 4);
+        if (sz < 0 || !rd_need(r, (size_t)sz)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_BAD_SIZE);
+        const uint8_t *s = r->b + r->p;
+        r->p += (size_t)sz;
+        if ((t->flags & DG_TF_BINARY) && !(c->opts & DG_T2J_NO_BASE64)) { /* EncodeBaniry */
+            jb_c(o, '"');
+            if (sz) {
+                size_t cap = ((size_t)sz + 2) / 3 * 4 + 8;
+                char *tmp = (char *)malloc(cap);
+                GoSlice out = {tmp, 0, (ssize_t)cap};
+                GoSlice src = {(char *)s, sz, sz};
+                b64encode(&out, &src, 0); /* std alphabet, padded (base64x.StdEncoding) */
+                jb_put(o, tmp, ((size_t)sz + 2) / 3 * 4);
+                free(tmp);
+            }
+            jb_c(o, '"');
+        } else {
+            jb_string(o, s, (size_t)sz);
+        }
+        return 0;
+    }
+    case 12:
+        return t2j_struct(c, td, r, o);
+    case 13: {
+        if (!rd_need(r, 1)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_EOF);
+        uint8_t kt = r->b[r->p++];
+        if (!ttype_valid(kt)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_BAD_TYPE);
+        if (!rd_need(r, 1)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_EOF);
+        uint8_t vt = r->b[r->p++];
+        if (!ttype_valid(vt)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_BAD_TYPE);
+        if (!rd_need(r, 4)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_EOF);
+        int32_t n = (int32_t)rd_be(r, 4);
+        if (n < 0) return T2J_ERR(DG_T2J_E_READ, r->p, RD_BAD_SIZE);
+        const dg_type *K = &c->T[t->key], *V = &c->T[t->elem];
+        if (kt != K->ttype) return T2J_ERR(DG_T2J_E_DISMATCH_TYPE, r->p, ((uint32_t)K->ttype << 8) | kt);
+        if (vt != V->ttype) return T2J_ERR(DG_T2J_E_DISMATCH_TYPE, r->p, ((uint32_t)V->ttype << 8) | vt);
+        jb_c(o, '{');
+        for (int32_t i = 0; i < n; i++) {
+            if (i) jb_c(o, ',');
+            jb_c(o, '"'); /* buildinTypeToKey (conv/t2j/impl.go:470-530) */
+            switch (K->ttype) {
+            case 3: {
+                if (!rd_need(r, 1)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_EOF);
+                uint8_t v = r->b[r->p++];
+                jb_i64(o, (c->opts & DG_T2J_BYTE_AS_UINT8) ? (int64_t)v : (int64_t)(int8_t)v);
+                break;
+            }
+            case 6: if (!rd_need(r, 2)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_EOF); jb_i64(o, (int16_t)rd_be(r, 2)); break;
+            case 8: if (!rd_need(r, 4)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_EOF); jb_i64(o, (int32_t)rd_be(r, 4)); break;
+            case 10: if (!rd_need(r, 8)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_EOF); jb_i64(o, (int64_t)rd_be(r, 8)); break;
+            case 11: {
+                if (!rd_need(r, 4)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_EOF);
+                int32_t sz = (int32_t)rd_be(r, 4);
+                if (sz < 0 || !rd_need(r, (size_t)sz)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_BAD_SIZE);
+                jb_quote(o, r->b + r->p, (size_t)sz);
+                r->p += (size_t)sz;
+                break;
+            }
+            default:
+                return T2J_ERR(DG_T2J_E_UNSUPPORTED, r->p, K->ttype); /* wrapped as ErrConvert by the caller */
+            }
+            jb_c(o, '"');
+            jb_c(o, ':');
+            uint64_t e = t2j_value(c, t->elem, r, o);
+            if (e) return e;
+        }
+        jb_c(o, '}');
+        return 0;
+    }
+    case 14: case 15: {
+        if (!rd_need(r, 1)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_EOF);
+        uint8_t et = r->b[r->p++];
+        if (!ttype_valid(et)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_BAD_TYPE);
+        if (!rd_need(r, 4)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_EOF);
+        int32_t n = (int32_t)rd_be(r, 4);
+        if (n < 0) return T2J_ERR(DG_T2J_E_READ, r->p, RD_BAD_SIZE);
+        const dg_type *E = &c->T[t->elem];
+        if (et != E->ttype) return T2J_ERR(DG_T2J_E_DISMATCH_TYPE, r->p, ((uint32_t)E->ttype << 8) | et);
+        jb_c(o, '[');
+        for (int32_t i = 0; i < n; i++) {
+            if (i) jb_c(o, ',');
+            uint64_t e = t2j_value(c, t->elem, r, o);
+            if (e) return e;
+        }
+        jb_c(o, ']');
+        return 0;
+    }
+    }
+    return T2J_ERR(DG_T2J_E_UNSUPPORTED, r->p, t->ttype);
+}
+
+/* BinaryConv.Do (conv/t2j/conv.go:43-66 + impl.go:74-91): one message.
+ * Returns the status word; *out_len = JSON bytes (written if <= cap). */
+uint64_t dgref_t2j(const uint8_t *blob, const uint8_t *side, uint32_t root, const uint8_t *thrift, size_t n,
+                   uint64_t opts, uint8_t *out, size_t cap, size_t *out_len)
+{
+    T2J c;
+    c.blob = blob;
+    c.h = (const dg_desc_hdr *)blob;
+    c.T = (const dg_type *)(blob + c.h->off_types);
+    c.S = (const dg_struct *)(blob + c.h->off_structs);
+    c.F = (const dg_field *)(blob + c.h->off_fields);
+    c.R = (const uint64_t *)(blob + c.h->off_reqwords);
+    const dg_t2j_hdr *xh = (const dg_t2j_hdr *)side;
+    c.X = (const dg_t2j_field *)(side + xh->off_fields);
+    c.XP = (const char *)(side + xh->off_pool);
+    c.opts = opts;
+    TRd r = {thrift, n, 0};
+    JBuf o = {(char *)malloc(256), 0, 256};
+    uint64_t e = t2j_value(&c, root, &r, &o);
+    *out_len = e ? 0 : o.len;
+    if (!e && o.len <= cap)
+        memcpy(out, o.b, o.len);
+    free(o.b);
+    return e;
 }

@@ -1,0 +1,260 @@
+"""GPU parity of the reverse path (Thrift binary -> JSON, conv/t2j): the HIP
+kernels through the C ABI against the t2j checker (oracle/ref_harness.c
+dgref_t2j: the reference's control flow over the reference's own native
+quote / i64toa / f64toa / b64encode), byte for byte and status word for
+status word; plus the reference's own known answers (conv/t2j/conv_test.go
+TestInt2String)."""
+import ctypes as C
+import math
+import random
+import struct
+
+import numpy as np
+import pytest
+
+import oracle
+import t2jgen
+from dynamicgo_amd import _lib, conv, t2j, thrift as T, workloads as W
+
+pytestmark = pytest.mark.gpu
+
+B8, I64S, NULLNAN, NOB64, DISALLOW, WDEF, WREQ, WOPT, VM = (1 << k for k in range(9))
+OPTS = [0, B8 | I64S, NULLNAN, NOB64, DISALLOW, WDEF | WREQ | WOPT, VM, B8 | I64S | NULLNAN | NOB64 | WDEF | WOPT | VM]
+
+
+@pytest.fixture(scope="module")
+def chk():
+    o = oracle.RefT2JOracle()
+    if o is None:
+        pytest.skip("oracle/_ref not built")
+    return o
+
+
+def gpu_t2j(flat, msgs, opts, root=None):
+    """dg_t2j_batch_host over the messages -> (outs, rets)."""
+    ctx = conv.default_context()
+    n = len(msgs)
+    a, off = W.arena(msgs)
+    cap = int(off[-1]) * 8 + 64 * n + 65536
+    out = np.zeros(cap, dtype=np.uint8)
+    oo = np.zeros(n + 1, dtype=np.uint64)
+    rets = np.zeros(max(n, 1), dtype=np.uint64)
+    need = C.c_uint64(0)
+    _lib.check(_lib.lib().dg_t2j_batch_host(ctx.h, ctx.desc_t2j(flat), flat.root_type if root is None else root,
+                                            a.ctypes.data, off.ctypes.data, n, opts, out.ctypes.data, cap,
+                                            oo.ctypes.data, rets.ctypes.data, C.byref(need)))
+    return [out[int(oo[i]):int(oo[i + 1])].tobytes() for i in range(n)], rets[:n]
+
+
+def compare(chk, flat, msgs, opts, root=None):
+    side = T.flatten_t2j(flat)
+    outs, rets = gpu_t2j(flat, msgs, opts, root)
+    bad = []
+    for i, m in enumerate(msgs):
+        er, eo = chk.t2j(flat, side, m, opts, root)
+        if int(rets[i]) != er or outs[i] != eo:
+            bad.append((i, hex(int(rets[i])), hex(er), outs[i][:80], eo[:80], m[:40].hex()))
+    return bad
+
+
+def test_int2string_known_answers():
+    """conv/t2j/conv_test.go:332-386 through the Python mirror."""
+    from schemas import idl_desc
+    from test_t2j_oracle import int2float_thrift
+    td = idl_desc("example3.thrift", "Int2FloatMethod")
+    src = int2float_thrift()
+    cv = t2j.BinaryConv(conv.Options(EnableValueMapping=True))
+    assert cv.do(td, src) == '{"Int32":"1","Float64":"3.14","中文":"hello","Int64":2,"Subfix":0.92653}'.encode()
+    cv = t2j.BinaryConv(conv.Options())
+    assert cv.do(td, src) == '{"Int32":1,"Float64":3.14,"中文":"hello","Int64":2,"Subfix":0.92653}'.encode()
+    cv = t2j.BinaryConv(conv.Options(Int642String=True))
+    assert cv.do(td, src) == '{"Int32":1,"Float64":3.14,"中文":"hello","Int64":"2","Subfix":0.92653}'.encode()
+    with pytest.raises(t2j.T2JError) as ei:
+        t2j.BinaryConv(conv.Options()).do(td, int2float_thrift(math.nan))
+    assert ei.value.behavior == "ErrWrite"
+    cv = t2j.BinaryConv(conv.Options(EncodeNullJSONForInfOrNan=True))
+    assert cv.do(td, int2float_thrift(math.inf)) == \
+        '{"Int32":1,"Float64":3.14,"中文":"hello","Int64":2,"Subfix":null}'.encode()
+
+
+@pytest.mark.parametrize("opts", OPTS)
+def test_random_parity(chk, opts):
+    td = t2jgen.all_types_desc()
+    fl = T.flatten(td)
+    rng = random.Random(1000 + opts)
+    msgs = [t2jgen.gen_thrift(rng, td) for _ in range(1500)]
+    msgs += [t2jgen.mutate(rng, t2jgen.gen_thrift(rng, td)) for _ in range(700)]
+    bad = compare(chk, fl, msgs, opts)
+    assert not bad, bad[:5]
+
+
+def test_numbers_and_strings_exhaustive(chk):
+    """Many doubles (every f64toa format branch), integers and strings."""
+    td = T.struct_type("N", [T.FieldDescriptor(1, "d", T.list_of(T.builtin("double")), T.OPTIONAL),
+                             T.FieldDescriptor(2, "i", T.list_of(T.builtin("i64")), T.OPTIONAL),
+                             T.FieldDescriptor(3, "s", T.list_of(T.builtin("string")), T.OPTIONAL),
+                             T.FieldDescriptor(4, "b", T.list_of(T.builtin("binary")), T.OPTIONAL)])
+    fl = T.flatten(td)
+    rng = random.Random(5)
+    msgs = []
+    for _ in range(400):
+        ds = [t2jgen.rdouble(rng) for _ in range(40)]
+        ds += [float(10 ** k) for k in range(-8, 23)] + [1.5 * 10 ** k for k in range(-8, 23)]
+        iv = [t2jgen.rint(rng, 64) for _ in range(20)] + [-(1 << 63), (1 << 63) - 1, 10 ** 8, 10 ** 16 - 1]
+        ss = [t2jgen.rbytes(rng, 40) for _ in range(10)] + [bytes(range(256)), b""]
+        bs = [bytes(rng.randrange(256) for _ in range(rng.randrange(20))) for _ in range(10)]
+        m = b"\x0f\x00\x01\x04" + struct.pack(">i", len(ds)) + b"".join(struct.pack(">d", d) for d in ds)
+        m += b"\x0f\x00\x02\x0a" + struct.pack(">i", len(iv)) + b"".join(struct.pack(">q", v) for v in iv)
+        m += b"\x0f\x00\x03\x0b" + struct.pack(">i", len(ss)) + b"".join(struct.pack(">i", len(s)) + s for s in ss)
+        m += b"\x0f\x00\x04\x0b" + struct.pack(">i", len(bs)) + b"".join(struct.pack(">i", len(s)) + s for s in bs)
+        msgs.append(m + b"\x00")
+    for opts in (0, NOB64):
+        bad = compare(chk, fl, msgs, opts)
+        assert not bad, bad[:3]
+
+
+@pytest.mark.parametrize("depth", [1, 11, 12, 13, 40, 1000, 4095])
+def test_deep_chain(chk, depth):
+    """Nesting beyond the LDS frames reruns on the deep pass, same bytes."""
+    fl = T.flatten(t2jgen.chain_desc())
+    msgs = [t2jgen.chain_thrift(depth), t2jgen.chain_thrift(2)] * 3
+    assert not compare(chk, fl, msgs, 0)
+
+
+def test_deeper_than_frames():
+    """Past 4096 containers the GPU reports DG_T2J_E_DEPTH (Go recurses on)."""
+    fl = T.flatten(t2jgen.chain_desc())
+    outs, rets = gpu_t2j(fl, [t2jgen.chain_thrift(5000), t2jgen.chain_thrift(3)], 0)
+    assert int(rets[0]) & 0xFF == 8 and outs[0] == b""
+    assert int(rets[1]) == 0 and outs[1] == b'{"next":{"next":{"v":7}}}'
+
+
+@pytest.mark.parametrize("levels", [5, 20, 1021, 1022, 1023, 1100])
+def test_skip_depth_limit(chk, levels):
+    """An unknown field of nested lists: skipType's MaxSkipDepth (1023,
+    thrift/binary_skip.go:24) holds on the GPU too."""
+    td = T.struct_type("S", [T.FieldDescriptor(1, "a", T.builtin("i32"), T.OPTIONAL)])
+    fl = T.flatten(td)
+    body = b"\x0f" + struct.pack(">i", 1)
+    inner = b"\x08" + struct.pack(">i", 1) + struct.pack(">i", 9)
+    v = body * (levels - 1) + inner
+    m = b"\x0f\x00\x63" + v + b"\x08\x00\x01" + struct.pack(">i", 3) + b"\x00"
+    # unknown struct-of-structs as well
+    s = b"\x0c\x00\x64" + b"\x0c\x00\x01" * (levels - 1) + b"\x00" * levels + b"\x00"
+    assert not compare(chk, fl, [m, s, m[:len(m) // 2]], 0)
+
+
+def test_wide_struct_needs_host():
+    fl = T.flatten(t2jgen.wide_desc(70))
+    m = b"\x08\x00\x05" + struct.pack(">i", 1) + b"\x00"
+    outs, rets = gpu_t2j(fl, [m], 0)
+    assert int(rets[0]) & 0xFF == 7
+
+
+def test_defaults_need_host(chk):
+    """An unset field with an IDL default is written from DefaultValue().
+    JSONValue() on the Go side: the GPU returns NEEDS_HOST exactly where the
+    checker does."""
+    td = t2jgen.all_types_desc(with_default=True)
+    fl = T.flatten(td)
+    rng = random.Random(9)
+    msgs = [t2jgen.gen_thrift(rng, td) for _ in range(200)]
+    for opts in (0, WOPT, WDEF | WREQ | WOPT):
+        assert not compare(chk, fl, msgs, opts)
+
+
+def test_scalar_and_container_roots(chk):
+    """Non-struct root descriptors (doRecurse on the root type directly)."""
+    rng = random.Random(3)
+    cases = [(T.builtin("i64"), [struct.pack(">q", -5), b"\x01"]),
+             (T.builtin("string"), [struct.pack(">i", 3) + b'a"b', struct.pack(">i", 9) + b"ab"]),
+             (T.builtin("double"), [struct.pack(">d", 0.1), struct.pack(">d", math.nan)]),
+             (T.list_of(T.builtin("i32")), [b"\x08" + struct.pack(">i", 2) + struct.pack(">ii", 1, -2),
+                                             b"\x0b" + struct.pack(">i", 0)]),
+             (T.map_of(T.builtin("string"), T.builtin("i32")),
+              [b"\x0b\x08" + struct.pack(">i", 1) + struct.pack(">i", 1) + b"k" + struct.pack(">i", 4)]),
+             (T.map_of(T.builtin("bool"), T.builtin("i32")), [b"\x02\x08" + struct.pack(">i", 1) + b"\x01" +
+                                                                struct.pack(">i", 4)])]
+    for td, msgs in cases:
+        fl = T.flatten(td)
+        msgs = msgs + [t2jgen.mutate(rng, m) for m in msgs] + [b""]
+        assert not compare(chk, fl, msgs, 0)
+
+
+def test_empty_and_truncated(chk):
+    td = t2jgen.all_types_desc()
+    fl = T.flatten(td)
+    rng = random.Random(11)
+    m = t2jgen.gen_thrift(rng, td)
+    msgs = [b"", b"\x00"] + [m[:k] for k in range(0, len(m), max(1, len(m) // 60))]
+    assert not compare(chk, fl, msgs, 0)
+
+
+def test_overflow_rerun(chk):
+    """JSON much larger than dg_t2j_slot_bound (control bytes -> \\u00xx):
+    the host entry point reruns those messages with exact slots."""
+    td = T.struct_type("S", [T.FieldDescriptor(1, "s", T.builtin("string"), T.OPTIONAL)])
+    fl = T.flatten(td)
+    msgs = []
+    for k in (0, 1, 7, 100, 5000):
+        s = b"\x01" * k
+        msgs.append(b"\x0b\x00\x01" + struct.pack(">i", k) + s + b"\x00")
+    assert not compare(chk, fl, msgs, 0)
+
+
+def test_roundtrip_c2(chk):
+    """C2's JSON through the GPU j2t, then the Thrift bytes back through the
+    GPU t2j: identical to the checker, and JSON-equivalent to the input
+    (t2j(j2t(x)) keeps every value)."""
+    import json
+    rng = random.Random(21)
+    td = W.simple_desc()
+    fl = T.flatten(td)
+    js = W.gen_flat_batch(rng, 500)
+    cv = conv.BinaryConv(conv.Options())
+    thr, rets = cv.do_batch(td, js)
+    assert not any(int(r) for r in rets)
+    bad = compare(chk, fl, thr, 0)
+    assert not bad, bad[:3]
+    outs, _ = gpu_t2j(fl, thr, 0)
+    for a, b in zip(js, outs):
+        ja, jb = json.loads(a), json.loads(b)
+        assert set(ja) <= set(jb)
+
+
+def test_device_entry_point(chk):
+    """dg_t2j_batch_device over torch tensors on the current stream:
+    overflowing slots report DG_ST_OUT_OVERFLOW with the bytes needed."""
+    import torch
+    td = t2jgen.all_types_desc()
+    fl = T.flatten(td)
+    side = T.flatten_t2j(fl)
+    rng = random.Random(13)
+    msgs = [t2jgen.gen_thrift(rng, td) for _ in range(3000)]
+    a, off = W.arena(msgs)
+    n = len(msgs)
+    lens = np.diff(off).astype(np.int64)
+    slots = ((lens * 2 + 16 + 7) // 8) * 8  # small on purpose: some overflow
+    oo = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(slots, out=oo[1:])
+    dev = torch.device("cuda:0")
+    d_src = torch.from_numpy(a).to(dev)
+    d_in = torch.from_numpy(off.astype(np.int64)).to(dev)
+    d_oo = torch.from_numpy(oo).to(dev)
+    d_out = torch.zeros(int(oo[-1]) + 64, dtype=torch.uint8, device=dev)
+    d_ol = torch.zeros(n, dtype=torch.int32, device=dev)
+    d_ret = torch.zeros(n, dtype=torch.int64, device=dev)
+    t2j.BinaryConv(conv.Options()).do_device(td, d_src, d_in, d_out, d_oo, d_ol, d_ret)
+    torch.cuda.synchronize()
+    out, ol, ret = d_out.cpu().numpy(), d_ol.cpu().numpy(), d_ret.cpu().numpy().view(np.uint64)
+    over = 0
+    for i, m in enumerate(msgs):
+        er, eo = chk.t2j(fl, side, m, 0)
+        if int(ret[i]) & 0xFF == 0xF0:
+            over += 1
+            assert er == 0 and int(ol[i]) == len(eo)
+            continue
+        assert int(ret[i]) == er
+        if er == 0:
+            assert out[int(oo[i]):int(oo[i]) + int(ol[i])].tobytes() == eo
+    assert over > 0

@@ -1,0 +1,14 @@
+"""Build experiment variants of the library (wave-kernel occupancy knobs):
+python tools/build_variants.py NAME=-DFLAG=..,-DFLAG=.. ...  -> dynamicgo_amd/libdgj2t_NAME.so"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from dynamicgo_amd import build as b  # noqa: E402
+
+for spec in sys.argv[1:]:
+    name, flags = spec.split("=", 1)
+    fl = tuple(flags.split(","))
+    out = os.path.join(b.ROOT, "dynamicgo_amd", f"libdgj2t_{name}.so")
+    b.build_hip(out=out, unit_flags={"j2t_kern_wave.hip": fl, "j2t_host.hip": fl})
+    print("built", out, flush=True)
