@@ -4,7 +4,7 @@
 A "step" = one pass of the hot path (JSON -> Thrift binary, BinaryConv.Do per
 message) over one batch that is already resident in HBM.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c2x|c2s|c3|c4|c5|c1]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c2x|c2s|c3|c4|c5|c1|t2j-c2|t2j-c3]
 
 Multi-GPU: with --gpus N > 1 and no WORLD_SIZE in the environment this
 process launches N ranks itself (one process per GPU, RANK/LOCAL_RANK/
@@ -52,7 +52,12 @@ CONFIGS = {
     "c1": ("C1: the reference's Simple payload (236 B) x 65536", 65536, "weak"),
     "c5": ("C5: ONE 1048576-message mixed batch (90% flat / 9.5% nested / 0.5% large), seed 45, "
            "byte-balanced shards over the ranks", 1 << 20, "strong"),
+    # the reverse path (conv/t2j): the Thrift bytes of a j2t
+    # config (converted on the GPU at setup, packed in HBM) back to JSON
+    "t2j-c2": ("t2j over C2: the Thrift of 65536 flat Simple messages (seed 42) -> JSON", 65536, "weak"),
+    "t2j-c3": ("t2j over C3: the Thrift of 65536 nested NestingI64 messages (seed 43) -> JSON", 65536, "weak"),
 }
+T2J_METRIC = "conv/t2j GB/s Thrift in + msgs/s, 64K-batch device-resident"
 FLAGS = {"c2x": 0x7}  # default: conv.Options{} -> F_ALLOW_UNKNOWN (conv/j2t/conv.go:102-104)
 
 
@@ -92,6 +97,8 @@ def rank_workload(cfg: str, rank: int, world: int, workers: int = 1, c5_n: int =
         lo, hi = shard_ranges(off, world)[rank]
         sa, so = W.arena_slice(a, off, lo, hi)
         return W.mixed_desc(), sa, so, {"global_batch": n, "global_json_bytes": int(off[-1]), "shard": [lo, hi]}
+    if cfg.startswith("t2j-"):
+        cfg = cfg[4:]
     rng = random.Random({"c2": 42, "c2x": 42, "c2s": 42, "c3": 43, "c4": 44, "c1": 0}[cfg] + 1000 * rank)
     if cfg in ("c2", "c2x"):
         td, msgs = W.simple_desc(), W.gen_flat_batch(rng, size)
@@ -273,6 +280,163 @@ def e2e_host_path(L, ctx, dh, root, flags, arena, off, dev, flat, chunks: int = 
                       % reps}
 
 
+# ---------------------------------------------------------------- t2j
+def cpu_baseline_t2j(flat, side, arena, off, opts, budget_s: float = 8.0):
+    """The t2j checker (oracle/ref_harness.c dgref_t2j: conv/t2j's control
+    flow restated in C over the reference's own native encoders) on this
+    host, pinned like cpu_baseline: a port, not the Go reference itself."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # reported baseline only
+    ref = oracle.RefT2JOracle()
+    if ref is None:
+        return None
+    phys, logical = oracle.physical_cpus()
+    cores = max(1, min(CPU_SHARE, len(phys)))
+    n = len(off) - 1
+    nbytes = int(off[-1] - off[0])
+    t1 = ref.t2j_timed(flat, side, arena, off, opts, phys[:cores], 1)
+    reps = int(max(3, min(200, budget_s / 2 / max(t1, 1e-6))))
+    t_all = ref.t2j_timed(flat, side, arena, off, opts, phys[:cores], reps)
+    t_one = ref.t2j_timed(flat, side, arena, off, opts, phys[:1], 3)
+    return {"value": round(nbytes / t_all / 1e9, 4), "unit": "GB/s", "cores": cores, "kind": "port",
+            "msgs_per_s": round(n / t_all), "one_core_gbs": round(nbytes / t_one / 1e9, 4),
+            "sample": f"the rank's whole Thrift batch ({n} msgs, {nbytes} B), best of {reps} passes, {cores} threads "
+                      f"pinned to distinct physical cores of '{cpu_model()}' ({logical} logical CPUs allowed); "
+                      f"one-core: same batch, best of 3; oracle/ref_harness.c dgref_t2j_timed (conv/t2j restated "
+                      f"in C over the reference's native quote/i64toa/f64toa/b64encode, clang -O3)"}
+
+
+def bench_t2j(args, rank, world, dev, dist, backend, td, arena, off, meta):
+    """t2j configs: the j2t config's batch is converted to Thrift once on the
+    GPU (setup, untimed) and packed back to back in HBM; a step converts that
+    whole Thrift batch to JSON (dg_t2j_batch_device)."""
+    import torch
+    import ctypes as C
+    from dynamicgo_amd import _lib, conv
+    from dynamicgo_amd.thrift import flatten, flatten_t2j
+    flat = flatten(td)
+    side = flatten_t2j(flat)
+    L = _lib.lib()
+    ctx = conv.Context(dev.index)
+    dh = ctx.desc_t2j(flat)
+    n = len(off) - 1
+    lens = np.diff(off).astype(np.int64)
+    slots = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum((lens * 4 + 64 + 7) & ~7, out=slots[1:])
+    d_json = torch.from_numpy(arena).to(dev)
+    d_in = torch.from_numpy(off.astype(np.int64)).to(dev)
+    d_j2t = torch.empty(int(slots[-1]) + 64, dtype=torch.uint8, device=dev)
+    d_oo = torch.from_numpy(slots).to(dev)
+    d_ol = torch.zeros(n, dtype=torch.int32, device=dev)
+    d_ret = torch.zeros(n, dtype=torch.int64, device=dev)
+    d_thrift = torch.zeros(int(slots[-1]) + 64, dtype=torch.uint8, device=dev)
+    d_toff = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    _lib.check(L.dg_j2t_batch_device(ctx.h, dh, flat.root_type, d_json.data_ptr(), d_in.data_ptr(), n, 1,
+                                     d_j2t.data_ptr(), d_oo.data_ptr(), d_ol.data_ptr(), d_ret.data_ptr(), None,
+                                     stream.cuda_stream))
+    _lib.check(L.dg_pack_device_scan(ctx.h, d_j2t.data_ptr(), d_oo.data_ptr(), d_ol.data_ptr(), n,
+                                     d_thrift.data_ptr(), d_toff.data_ptr(), stream.cuda_stream))
+    torch.cuda.synchronize()
+    if int((d_ret != 0).sum().item()):
+        raise RuntimeError("t2j bench: the j2t setup pass failed on some messages")
+    toff = d_toff.cpu().numpy().astype(np.uint64)
+    thrift_bytes = int(toff[-1])
+    h_thrift = d_thrift[:thrift_bytes + 64].cpu().numpy()
+    tl = np.diff(toff).astype(np.int64)
+    jslots = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum((tl * 3 + 64 + 7) & ~7, out=jslots[1:])  # dg_t2j_slot_bound
+    del d_j2t, d_json
+    d_out = torch.empty(int(jslots[-1]) + 64, dtype=torch.uint8, device=dev)
+    d_jo = torch.from_numpy(jslots).to(dev)
+    d_jl = torch.zeros(n, dtype=torch.int32, device=dev)
+    d_jr = torch.zeros(n, dtype=torch.int64, device=dev)
+    opts = 0
+
+    def step():
+        _lib.check(L.dg_t2j_batch_device(ctx.h, dh, flat.root_type, d_thrift.data_ptr(), d_toff.data_ptr(), n, opts,
+                                         d_out.data_ptr(), d_jo.data_ptr(), d_jl.data_ptr(), d_jr.data_ptr(),
+                                         stream.cuda_stream))
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    rets = d_jr.cpu().numpy()
+    ok = int((rets == 0).sum())
+    if ok != n:
+        print(f"[rank {rank}] WARNING: {n - ok} t2j messages not ok", file=sys.stderr)
+    json_out = int(d_jl.to(torch.int64).sum().item())
+    # parity spot check (outside the timed region): the first 2048 messages
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # checker only
+    chk = oracle.RefT2JOracle()
+    checked = 0
+    if chk is not None and rank == 0:
+        out_h, jl_h = d_out.cpu().numpy(), d_jl.cpu().numpy()
+        for i in range(min(n, 2048)):
+            m = h_thrift[int(toff[i]):int(toff[i + 1])].tobytes()
+            er, eo = chk.t2j(flat, side, m, opts)
+            got = out_h[int(jslots[i]):int(jslots[i]) + int(jl_h[i])].tobytes()
+            if er != int(rets[i]) or eo != got:
+                raise RuntimeError(f"t2j bench: message {i} differs from the checker")
+            checked += 1
+    alg_bytes = thrift_bytes + json_out + PER_MSG_META * n
+    if dist:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if dist:
+        torch.distributed.barrier()
+    wall = time.perf_counter() - t0
+    gpu_ms = ev0.elapsed_time(ev1) / args.steps
+    stats = torch.tensor([wall, float(thrift_bytes), float(n), gpu_ms], dtype=torch.float64,
+                         device=dev if backend == "nccl" else "cpu")
+    if dist:
+        gathered = [torch.zeros_like(stats) for _ in range(world)]
+        torch.distributed.all_gather(gathered, stats)
+        per_rank = [g.cpu().tolist() for g in gathered]
+    else:
+        per_rank = [stats.cpu().tolist()]
+    wall_max = max(p[0] for p in per_rank)
+    value = sum(p[1] for p in per_rank) / wall_max * args.steps / 1e9
+    achieved = alg_bytes / (gpu_ms / 1e3) / 1e9
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline_t2j(flat, side, h_thrift, toff, opts)
+    traffic = None
+    tp = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
+    if os.path.exists(tp):
+        with open(tp) as fh:
+            traffic = json.load(fh).get("hbm_bytes_per_launch")
+    if rank == 0:
+        line = {
+            "metric": T2J_METRIC, "value": round(value, 3), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(wall_max / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "config": {"workload": CONFIGS[args.config][0], "global_batch": meta["global_batch"], "msgs_per_rank": n,
+                       "avg_thrift_bytes": round(thrift_bytes / max(n, 1), 1), "json_bytes_rank0": json_out,
+                       "msgs_per_s": round(sum(p[2] for p in per_rank) * args.steps / wall_max), "opts": opts,
+                       "ok_msgs_rank0": ok, "checked_vs_oracle": checked,
+                       "parallelism": f"dp{world} (one batch per rank), no data-path collective",
+                       "per_rank_kernel_ms": [round(p[3], 5) for p in per_rank]},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                         "kernel_ms": round(gpu_ms, 5), "alg_bytes_per_launch": alg_bytes},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist:
+        torch.distributed.destroy_process_group()
+    ctx.close()
+
+
 # ---------------------------------------------------------------- main
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
@@ -310,6 +474,9 @@ def main(argv=None):
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         kw = {"device_id": dev} if backend == "nccl" else {}
         torch.distributed.init_process_group(backend, rank=rank, world_size=world, **kw)
+
+    if args.config.startswith("t2j-"):
+        return bench_t2j(args, rank, world, dev, dist, backend, td, arena, off, meta)
 
     from dynamicgo_amd import _lib, conv
     from dynamicgo_amd.thrift import flatten

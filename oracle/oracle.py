@@ -146,6 +146,7 @@ class RefT2J:
     native encoders (oracle/ref_harness.c dgref_t2j)."""
 
     def __init__(self, lib: C.CDLL):
+        self.lib = lib
         self.f = lib.dgref_t2j
         self.f.restype = C.c_uint64
         self.f.argtypes = [C.c_char_p, C.c_char_p, C.c_uint32, C.c_char_p, C.c_size_t, C.c_uint64,
@@ -164,6 +165,33 @@ class RefT2J:
                 return 0, out.raw[:ol.value]
             cap = ol.value + 64
         raise RuntimeError("t2j oracle output did not fit")
+
+
+    def t2j_timed(self, flat, side: bytes, arena: np.ndarray, in_off: np.ndarray, opts: int, cpus: Sequence[int],
+                  reps: int, root: Optional[int] = None) -> float:
+        """bench.py t2j cpu_baseline: best-of-`reps` seconds for the whole
+        arena, len(cpus) threads pinned one per cpu (dgref_t2j_timed)."""
+        f = self.lib.dgref_t2j_timed
+        f.restype = C.c_int
+        f.argtypes = [C.c_char_p, C.c_char_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64,
+                      C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_int), C.c_int,
+                      C.POINTER(C.c_double)]
+        n = len(in_off) - 1
+        in_off = np.ascontiguousarray(in_off, dtype=np.uint64)
+        lens = np.diff(in_off)
+        out_off = np.zeros(n + 1, dtype=np.uint64)
+        np.cumsum(lens * 8 + 256, out=out_off[1:])
+        out = np.empty(int(out_off[-1]) + 64, dtype=np.uint8)
+        out_len = np.zeros(n, dtype=np.uint32)
+        rets = np.zeros(n, dtype=np.uint64)
+        cpu_arr = (C.c_int * len(cpus))(*cpus)
+        best = C.c_double(-1.0)
+        root = flat.root_type if root is None else root
+        rc = f(flat.blob, side, root, arena.ctypes.data, in_off.ctypes.data, n, opts, out.ctypes.data,
+               out_off.ctypes.data, out_len.ctypes.data, rets.ctypes.data, len(cpus), cpu_arr, reps, C.byref(best))
+        if rc != 0:
+            raise RuntimeError("dgref_t2j_timed failed")
+        return float(best.value)
 
 
 def RefT2JOracle() -> Optional[RefT2J]:

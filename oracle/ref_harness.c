@@ -552,7 +552,7 @@ typedef struct {
 #define T2J_ERR(code, pos, val) ((uint64_t)(code) | ((uint64_t)(pos) << 8) | ((uint64_t)(val) << 40))
 enum { RD_EOF = 1, RD_BAD_TYPE = 2, RD_BAD_SIZE = 3, RD_DEPTH = 4 };
 
-static void jb_put(JBuf *o, const void *s, size_t k)
+static void jb_reserve(JBuf *o, size_t k)
 {
     if (o->len + k + 64 > o->cap) {
         size_t nc = (o->cap + k + 64) * 2;
@@ -562,31 +562,32 @@ static void jb_put(JBuf *o, const void *s, size_t k)
         o->b = nb;
         o->cap = nc;
     }
+}
+static void jb_put(JBuf *o, const void *s, size_t k)
+{
+    jb_reserve(o, k);
     memcpy(o->b + o->len, s, k);
     o->len += k;
 }
 static void jb_c(JBuf *o, char c) { jb_put(o, &c, 1); }
 static void jb_i64(JBuf *o, int64_t v)
 {
-    char t[32];
-    int k = i64toa(t, v); /* native/fastint.c:212 */
-    jb_put(o, t, (size_t)k);
+    jb_reserve(o, 32);
+    o->len += (size_t)i64toa(o->b + o->len, v); /* native/fastint.c:212 */
 }
 static void jb_f64(JBuf *o, double v)
 {
-    char t[40];
-    int k = f64toa(t, v); /* native/fastfloat.c:349 (0 for inf/nan: nothing, like the Go wrapper) */
-    jb_put(o, t, (size_t)k);
+    jb_reserve(o, 40);
+    o->len += (size_t)f64toa(o->b + o->len, v); /* native/fastfloat.c:349 (0 for inf/nan: nothing, like the Go wrapper) */
 }
 static void jb_quote(JBuf *o, const uint8_t *s, size_t n) /* json.NoQuote: native quote, flags 0 */
 {
     if (!n)
         return;
     ssize_t dn = (ssize_t)(n * 6 + 8);
-    char *t = (char *)malloc((size_t)dn);
-    quote((const char *)s, (ssize_t)n, t, &dn, 0);
-    jb_put(o, t, (size_t)dn);
-    free(t);
+    jb_reserve(o, (size_t)dn);
+    quote((const char *)s, (ssize_t)n, o->b + o->len, &dn, 0);
+    o->len += (size_t)dn;
 }
 static void jb_string(JBuf *o, const uint8_t *s, size_t n) /* json.EncodeString */
 {
@@ -909,12 +910,11 @@ static uint64_t t2j_value(const T2J *c, uint32_t td, TRd *r, JBuf *o)
             jb_c(o, '"');
             if (sz) {
                 size_t cap = ((size_t)sz + 2) / 3 * 4 + 8;
-                char *tmp = (char *)malloc(cap);
-                GoSlice out = {tmp, 0, (ssize_t)cap};
+                jb_reserve(o, cap);
+                GoSlice out = {o->b + o->len, 0, (ssize_t)cap};
                 GoSlice src = {(char *)s, sz, sz};
                 b64encode(&out, &src, 0); /* std alphabet, padded (base64x.StdEncoding) */
-                jb_put(o, tmp, ((size_t)sz + 2) / 3 * 4);
-                free(tmp);
+                o->len += ((size_t)sz + 2) / 3 * 4;
             }
             jb_c(o, '"');
         } else {
@@ -992,28 +992,140 @@ static uint64_t t2j_value(const T2J *c, uint32_t td, TRd *r, JBuf *o)
     return T2J_ERR(DG_T2J_E_UNSUPPORTED, r->p, t->ttype);
 }
 
-/* BinaryConv.Do (conv/t2j/conv.go:43-66 + impl.go:74-91): one message.
- * Returns the status word; *out_len = JSON bytes (written if <= cap). */
+static void t2j_init(T2J *c, const uint8_t *blob, const uint8_t *side, uint64_t opts)
+{
+    c->blob = blob;
+    c->h = (const dg_desc_hdr *)blob;
+    c->T = (const dg_type *)(blob + c->h->off_types);
+    c->S = (const dg_struct *)(blob + c->h->off_structs);
+    c->F = (const dg_field *)(blob + c->h->off_fields);
+    c->R = (const uint64_t *)(blob + c->h->off_reqwords);
+    const dg_t2j_hdr *xh = (const dg_t2j_hdr *)side;
+    c->X = (const dg_t2j_field *)(side + xh->off_fields);
+    c->XP = (const char *)(side + xh->off_pool);
+    c->opts = opts;
+}
+
+/* BinaryConv.Do (conv/t2j/conv.go:50-75 + impl.go:74-187): one message into
+ * o (reset first; the caller's buffer is reused like conv.NewBytes' pool).
+ * Returns the status word; on success the JSON is o->b[0, o->len). */
+static uint64_t t2j_do(const T2J *c, uint32_t root, const uint8_t *thrift, size_t n, JBuf *o)
+{
+    TRd r = {thrift, n, 0};
+    o->len = 0;
+    return t2j_value(c, root, &r, o);
+}
+
 uint64_t dgref_t2j(const uint8_t *blob, const uint8_t *side, uint32_t root, const uint8_t *thrift, size_t n,
                    uint64_t opts, uint8_t *out, size_t cap, size_t *out_len)
 {
     T2J c;
-    c.blob = blob;
-    c.h = (const dg_desc_hdr *)blob;
-    c.T = (const dg_type *)(blob + c.h->off_types);
-    c.S = (const dg_struct *)(blob + c.h->off_structs);
-    c.F = (const dg_field *)(blob + c.h->off_fields);
-    c.R = (const uint64_t *)(blob + c.h->off_reqwords);
-    const dg_t2j_hdr *xh = (const dg_t2j_hdr *)side;
-    c.X = (const dg_t2j_field *)(side + xh->off_fields);
-    c.XP = (const char *)(side + xh->off_pool);
-    c.opts = opts;
-    TRd r = {thrift, n, 0};
+    t2j_init(&c, blob, side, opts);
     JBuf o = {(char *)malloc(256), 0, 256};
-    uint64_t e = t2j_value(&c, root, &r, &o);
+    uint64_t e = t2j_do(&c, root, thrift, n, &o);
     *out_len = e ? 0 : o.len;
     if (!e && o.len <= cap)
         memcpy(out, o.b, o.len);
     free(o.b);
     return e;
+}
+
+/* ---- timed batch driver for bench.py's t2j cpu_baseline ----
+ * Same shape as dgref_j2t_timed: pinned threads, byte-balanced contiguous
+ * shards, one untimed pass then `reps` timed ones between barriers; each
+ * message converted into a per-thread reused buffer and copied into its
+ * output slot (Do's copy, conv/t2j/conv.go:67-70). */
+typedef struct {
+    T2J c;
+    uint32_t root;
+    const uint8_t *src;
+    const uint64_t *in_off;
+    uint64_t lo, hi;
+    uint8_t *out;
+    const uint64_t *out_off;
+    uint32_t *out_len;
+    uint64_t *ret;
+    int cpu, tid, reps;
+    pthread_barrier_t *bar;
+    double *best;
+} T2JJob;
+
+static void *run_t2j_timed(void *arg)
+{
+    T2JJob *t = (T2JJob *)arg;
+    if (t->cpu >= 0) {
+        cpu_set_t cs;
+        CPU_ZERO(&cs);
+        CPU_SET(t->cpu, &cs);
+        pthread_setaffinity_np(pthread_self(), sizeof cs, &cs);
+    }
+    JBuf o = {(char *)malloc(1 << 16), 0, 1 << 16};
+    double t0 = 0;
+    for (int rep = -1; rep < t->reps; rep++) {
+        pthread_barrier_wait(t->bar);
+        if (t->tid == 0)
+            t0 = now_s();
+        for (uint64_t i = t->lo; i < t->hi; i++) {
+            uint64_t e = t2j_do(&t->c, t->root, t->src + t->in_off[i], t->in_off[i + 1] - t->in_off[i], &o);
+            uint64_t cap = t->out_off[i + 1] - t->out_off[i];
+            t->ret[i] = e;
+            t->out_len[i] = e ? 0 : (uint32_t)o.len;
+            if (!e && o.len <= cap)
+                memcpy(t->out + t->out_off[i], o.b, o.len);
+        }
+        pthread_barrier_wait(t->bar);
+        if (t->tid == 0 && rep >= 0) {
+            double dt = now_s() - t0;
+            if (*t->best < 0 || dt < *t->best)
+                *t->best = dt;
+        }
+    }
+    free(o.b);
+    return NULL;
+}
+
+int dgref_t2j_timed(const uint8_t *blob, const uint8_t *side, uint32_t root, const uint8_t *src,
+                    const uint64_t *in_off, uint64_t n, uint64_t opts, uint8_t *out, const uint64_t *out_off,
+                    uint32_t *out_len, uint64_t *ret, int nthreads, const int *cpus, int reps, double *best_s)
+{
+    if (nthreads < 1 || reps < 1 || !best_s)
+        return -1;
+    T2JJob *tj = (T2JJob *)calloc(nthreads, sizeof(T2JJob));
+    pthread_t *th = (pthread_t *)calloc(nthreads, sizeof(pthread_t));
+    pthread_barrier_t bar;
+    pthread_barrier_init(&bar, NULL, (unsigned)nthreads);
+    double best = -1;
+    uint64_t total = in_off[n] - in_off[0];
+    uint64_t lo = 0;
+    for (int t = 0; t < nthreads; t++) {
+        uint64_t target = in_off[0] + total * (uint64_t)(t + 1) / nthreads;
+        uint64_t hi = lo;
+        while (hi < n && (t == nthreads - 1 || in_off[hi] < target))
+            hi++;
+        t2j_init(&tj[t].c, blob, side, opts);
+        tj[t].root = root;
+        tj[t].src = src;
+        tj[t].in_off = in_off;
+        tj[t].lo = lo;
+        tj[t].hi = hi;
+        tj[t].out = out;
+        tj[t].out_off = out_off;
+        tj[t].out_len = out_len;
+        tj[t].ret = ret;
+        tj[t].cpu = cpus ? cpus[t] : -1;
+        tj[t].tid = t;
+        tj[t].reps = reps;
+        tj[t].bar = &bar;
+        tj[t].best = &best;
+        lo = hi;
+    }
+    for (int t = 0; t < nthreads; t++)
+        pthread_create(&th[t], NULL, run_t2j_timed, &tj[t]);
+    for (int t = 0; t < nthreads; t++)
+        pthread_join(th[t], NULL);
+    pthread_barrier_destroy(&bar);
+    free(tj);
+    free(th);
+    *best_s = best;
+    return 0;
 }

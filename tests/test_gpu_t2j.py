@@ -234,7 +234,7 @@ def test_device_entry_point(chk):
     a, off = W.arena(msgs)
     n = len(msgs)
     lens = np.diff(off).astype(np.int64)
-    slots = ((lens * 2 + 16 + 7) // 8) * 8  # small on purpose: some overflow
+    slots = ((lens // 2 + 8 + 7) // 8) * 8  # small on purpose: most overflow
     oo = np.zeros(n + 1, dtype=np.int64)
     np.cumsum(slots, out=oo[1:])
     dev = torch.device("cuda:0")
