@@ -81,6 +81,7 @@ struct dg_desc {
     size_t len;
     dg_desc_hdr hdr;
     uint8_t *d_side = nullptr;     /* t2j side table (dg_desc_attach_t2j) */
+    std::vector<uint8_t> hblob;    /* host copy of the blob (launch decisions) */
     size_t side_len = 0;
 };
 

@@ -13,7 +13,7 @@
 #include <mutex>
 #include <vector>
 
-#include "j2t_small.h"
+#include "j2t_flat.h"
 #include "host_internal.h"
 
 /* ========================================================================== */
@@ -149,7 +149,8 @@ void dg_ctx_destroy(dg_ctx *c)
 
 void *dg_ctx_stream(dg_ctx *c) { return c ? (void *)c->stream : nullptr; }
 
-static int desc_finish(dg_ctx *c, const dg_desc_hdr &h, uint8_t *d_blob, size_t len, dg_desc **out)
+static int desc_finish(dg_ctx *c, const dg_desc_hdr &h, uint8_t *d_blob, size_t len, const void *host_blob,
+                       dg_desc **out)
 {
     if (h.magic != DG_DESC_MAGIC || h.version < 1 || h.version > DG_DESC_VERSION || h.total_len > len)
         return set_err(DG_E_DESC, "bad descriptor blob header");
@@ -158,8 +159,33 @@ static int desc_finish(dg_ctx *c, const dg_desc_hdr &h, uint8_t *d_blob, size_t 
     d->d_blob = d_blob;
     d->len = len;
     d->hdr = h;
+    d->hblob.assign((const uint8_t *)host_blob, (const uint8_t *)host_blob + h.total_len);
     *out = d;
     return DG_OK;
+}
+
+/* The flat-struct kernel applies: the root is a struct of at most 64 fields,
+ * all scalars or strings, without HTTP-mapped fields under F_ENABLE_HM, and
+ * the blob fits its LDS copy. */
+static bool flat_root(const dg_desc *d, uint32_t root, uint64_t flags)
+{
+    const dg_desc_hdr &h = d->hdr;
+    if (d->hblob.size() < h.total_len || h.version < 2 || h.total_len > FL_DESC || root >= h.n_types) return false;
+    const uint8_t *b = d->hblob.data();
+    const dg_type *T = (const dg_type *)(b + h.off_types);
+    if (T[root].ttype != DG_T_STRUCT) return false;
+    const dg_struct &sd = ((const dg_struct *)(b + h.off_structs))[T[root].st];
+    if (sd.req_words != 1 || ((flags & DG_F_ENABLE_HM) && (sd.flags & DG_SF_HTTP_MAPPING))) return false;
+    const dg_field *F = (const dg_field *)(b + h.off_fields);
+    for (uint32_t k = 0; k < sd.n_fields; k++) {
+        switch (T[F[sd.field_begin + k].type].ttype) {
+        case DG_T_BOOL: case DG_T_BYTE: case DG_T_I16: case DG_T_I32: case DG_T_I64: case DG_T_DOUBLE: case DG_T_STRING:
+            break;
+        default:
+            return false;
+        }
+    }
+    return true;
 }
 
 int dg_desc_create(dg_ctx *c, const void *blob, size_t len, dg_desc **out)
@@ -172,7 +198,7 @@ int dg_desc_create(dg_ctx *c, const void *blob, size_t len, dg_desc **out)
     uint8_t *d_blob;
     HIPCHK(hipMalloc(&d_blob, len));
     HIPCHK(hipMemcpy(d_blob, blob, len, hipMemcpyHostToDevice));
-    return desc_finish(c, h, d_blob, len, out);
+    return desc_finish(c, h, d_blob, len, blob, out);
 }
 
 int dg_desc_create_device(dg_ctx *c, const void *d_src, size_t len, dg_desc **out)
@@ -182,9 +208,12 @@ int dg_desc_create_device(dg_ctx *c, const void *d_src, size_t len, dg_desc **ou
     uint8_t *d_blob;
     HIPCHK(hipMalloc(&d_blob, len));
     HIPCHK(hipMemcpy(d_blob, d_src, len, hipMemcpyDeviceToDevice));
+    std::vector<uint8_t> hb(len);
+    HIPCHK(hipMemcpy(hb.data(), d_blob, len, hipMemcpyDeviceToHost));
     dg_desc_hdr h;
-    HIPCHK(hipMemcpy(&h, d_blob, sizeof h, hipMemcpyDeviceToHost));
-    return desc_finish(c, h, d_blob, len, out);
+    memcpy(&h, hb.data(), sizeof h);
+    if (h.total_len > len) return set_err(DG_E_DESC, "bad descriptor blob");
+    return desc_finish(c, h, d_blob, len, hb.data(), out);
 }
 
 void dg_desc_destroy(dg_desc *d)
@@ -247,7 +276,9 @@ static int enqueue(dg_ctx *c, Scratch *x, const dg_desc *d, uint32_t root, const
     int rc = ensure_fast_ws(x, n);
     if (rc) return rc;
     const bool no_wave = (flags & DG_F_NO_WAVE_PATH) != 0;
-    flags &= ~DG_F_NO_WAVE_PATH;
+    const char *fl_env = getenv("DG_FLAT");
+    const bool use_flat = fl_env ? atoi(fl_env) != 0 : (flags & DG_F_FLAT_PATH) != 0;
+    flags &= ~(DG_F_NO_WAVE_PATH | DG_F_FLAT_PATH);
     Params P;
     P.root = root;
     P.json = json;
@@ -312,8 +343,18 @@ static int enqueue(dg_ctx *c, Scratch *x, const dg_desc *d, uint32_t root, const
         S.hdr = d->hdr;
         S.bail_count = x->d_counts;
         S.bail_list = x->d_bail_list;
-        const uint64_t mpb = (uint64_t)SM_WAVES * (uint64_t)(mpw >= 64 ? 64 : mpw == 16 ? 16 : 32);
-        launch_small_kernel(mpw, dim3((uint32_t)((n + mpb - 1) / mpb)), s, P1, S);
+        if (use_flat && flat_root(d, root, flags)) {
+            /* flat root struct: a lane group per message, a lane per field */
+            FlatParams FP;
+            FP.blob = d->d_blob;
+            FP.hdr = d->hdr;
+            FP.bail_count = x->d_counts;
+            FP.bail_list = x->d_bail_list;
+            launch_flat_kernel(dim3((uint32_t)((n + FL_MPB - 1) / FL_MPB)), s, P1, FP);
+        } else {
+            const uint64_t mpb = (uint64_t)SM_WAVES * (uint64_t)(mpw >= 64 ? 64 : mpw == 16 ? 16 : 32);
+            launch_small_kernel(mpw, dim3((uint32_t)((n + mpb - 1) / mpb)), s, P1, S);
+        }
         HIPCHK(hipGetLastError());
         if (need_wave) {
             WaveParams W;

@@ -237,16 +237,6 @@ struct WOut {
     }
 };
 
-/* a writer that only counts (output lengths before the offsets are known) */
-struct CountOut_unused {
-    uint64_t len = 0;
-    DGI void wle(uint64_t, uint32_t n) { len += n; }
-    DGI void w8(uint8_t) { len += 1; }
-    DGI void w16(uint16_t) { len += 2; }
-    DGI void w32(uint32_t) { len += 4; }
-    DGI void w64(uint64_t) { len += 8; }
-};
-
 /* big-endian u32 at an arbitrary byte address, byte-exact */
 DGI void put_be32(gu8 *p, uint32_t v)
 {

@@ -328,7 +328,7 @@ struct T2JRd {
 
 DGI bool ttype_valid(uint8_t t) /* thrift/descriptor.go:60-67 */
 {
-    return t <= 17 && ((0x3FDDFu >> t) & 1); /* 0 1 2 3 4 6 8 10 11 12 13 14 15 16 17 */
+    return t <= 17 && ((0x3FD5Fu >> t) & 1); /* 0 1 2 3 4 6 8 10 11 12 13 14 15 16 17 */
 }
 DGI uint32_t fixed_size(uint8_t t) /* typeSize, thrift/binary_skip.go:26-41 */
 {

@@ -20,6 +20,8 @@
 #define DG_F_VALIDATE_UTF8 (1ull << 16) /* extension: reject invalid UTF-8 in strings */
 #define DG_F_NO_FAST_PATH (1ull << 17)  /* extension: run every message on the exact machine (testing) */
 #define DG_F_NO_WAVE_PATH (1ull << 18)  /* extension: skip the wave-per-message kernel, lane kernel only (testing) */
+#define DG_F_FLAT_PATH (1ull << 19)     /* extension: flat root structs on the field-parallel kernel (j2t_flat.h);
+                                           faster when key order varies between messages, slower on uniform batches */
 
 /* library-internal per-message statuses (code byte values the reference never
  * produces). The host entry points resolve them before returning; the device

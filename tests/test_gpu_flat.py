@@ -1,0 +1,127 @@
+"""GPU parity of the flat-struct kernel (j2t_flat.h: a lane group per
+message, a lane per field; selected by DG_F_FLAT_PATH) against the
+reference's own engine (oracle/_ref), byte for byte and status word for
+status word; and against the small kernel on the same batches."""
+import random
+
+import numpy as np
+import pytest
+
+import fuzz
+import oracle
+from dynamicgo_amd import conv, thrift as T, workloads as W
+from test_gpu_parity import _raw_batch
+
+pytestmark = pytest.mark.gpu
+
+FLAT = 1 << 19  # DG_F_FLAT_PATH
+
+
+def _chk():
+    return oracle.RefOracle() or oracle.PortOracle()
+
+
+def flat_desc():
+    """A flat struct with every scalar type, binary, js_conv fields,
+    required / default / optional fields, an alias and a non-IDL-order id."""
+    return T.struct_type("Flat", [
+        T.FieldDescriptor(1, "b", T.builtin("bool"), T.OPTIONAL),
+        T.FieldDescriptor(2, "y", T.builtin("byte"), T.OPTIONAL),
+        T.FieldDescriptor(3, "s16", T.builtin("i16"), T.DEFAULT),
+        T.FieldDescriptor(4, "s32", T.builtin("i32"), T.OPTIONAL),
+        T.FieldDescriptor(5, "s64", T.builtin("i64"), T.OPTIONAL),
+        T.FieldDescriptor(6, "d", T.builtin("double"), T.OPTIONAL),
+        T.FieldDescriptor(7, "str", T.builtin("string"), T.OPTIONAL, alias="Str"),
+        T.FieldDescriptor(8, "bin", T.builtin("binary"), T.OPTIONAL),
+        T.FieldDescriptor(9, "vm64", T.builtin("i64"), T.OPTIONAL, vm=T.VM_JSCONV),
+        T.FieldDescriptor(10, "vm16", T.builtin("i16"), T.OPTIONAL, vm=T.VM_JSCONV),
+        T.FieldDescriptor(11, "vms", T.builtin("string"), T.OPTIONAL, vm=T.VM_JSCONV),
+        T.FieldDescriptor(12, "req", T.builtin("i32"), T.REQUIRED),
+        T.FieldDescriptor(40, "far", T.builtin("double"), T.DEFAULT),
+    ])
+
+
+def _compare(flat, msgs, flags):
+    chk = _chk()
+    bad = []
+    outs, rets = _raw_batch(flat, msgs, flags)
+    er, eo = chk.j2t_batch(flat, msgs, flags & 0xFFFF)
+    for i in range(len(msgs)):
+        if int(rets[i]) != int(er[i]) or outs[i] != eo[i]:
+            bad.append((i, msgs[i][:120], hex(int(rets[i])), hex(int(er[i]))))
+    return bad
+
+
+@pytest.mark.parametrize("flags", [0x1, 0x0, 0x5, 0x7, 0x41, 0x23, 0x83, 0x11, 0x201])
+def test_flat_fuzz_vs_oracle(flags):
+    rng = random.Random(500 + flags)
+    for td in (flat_desc(), W.simple_desc()):
+        fl = T.flatten(td)
+        msgs = [fuzz.gen_message(rng, td, mutate_p=rng.random() < 0.3) for _ in range(1500)]
+        bad = _compare(fl, msgs, flags | FLAT)
+        assert not bad, bad[:4]
+
+
+def test_flat_clean_messages_stay_on_the_flat_kernel():
+    """Well-formed C2 batches: every message is converted by the flat kernel
+    (no bail to the list pass), identical to the oracle and to the small
+    kernel."""
+    ctx = conv.default_context()
+    rng = random.Random(42)
+    td = W.simple_desc()
+    fl = T.flatten(td)
+    msgs = W.gen_flat_batch(rng, 20000)
+    ctx.stats(reset=True)
+    o1, r1 = _raw_batch(fl, msgs, 0x1 | FLAT)
+    bails, _ = ctx.stats(reset=True)
+    o2, r2 = _raw_batch(fl, msgs, 0x1)
+    assert o1 == o2 and list(r1) == list(r2)
+    assert not any(int(r) for r in r1)
+    assert bails == 0, bails
+    assert not _compare(fl, msgs[:3000], 0x1 | FLAT)
+
+
+@pytest.mark.parametrize("variant", ["c2x", "c2s", "ws", "escapes", "unknown", "dups"])
+def test_flat_variants(variant):
+    rng = random.Random(7)
+    td = W.simple_desc()
+    fl = T.flatten(td)
+    flags = 0x1
+    if variant == "c2x":
+        msgs, flags = W.gen_flat_batch(rng, 4000), 0x7
+    elif variant == "c2s":
+        msgs = W.gen_flat_batch_shuffled(rng, 4000)
+    elif variant == "ws":
+        msgs = [fuzz.spacify(random.Random(k), m.decode()).encode() for k, m in enumerate(W.gen_flat_batch(rng, 3000))]
+        msgs = [b"  \n" + m + b" \t" for m in msgs]
+    elif variant == "escapes":
+        msgs = [('{"StringField":"a\\nb\\u00e9\\ud83d\\ude00\\t","ByteField":-1,"BinaryField":"%s"}' %
+                 rng.choice(["", "QQ==", "QUI=", "QUJD", "QUJDRA==", "QUJDREVG"])).encode() for _ in range(500)]
+        msgs += [b'{"StringField":"q\\"x"}', b'{"StringField":"b\\\\"}', b'{"StringField":"\\/"}']
+    elif variant == "unknown":
+        msgs = [('{"x%d":%s,"I32Field":%d,"zz":"%s","DoubleField":1.5}' %
+                 (k, rng.choice(["1", "true", "\"s\"", "[1]", "{}", "null", "-2.5e3"]), k, "v" * (k % 9)))
+                .encode() for k in range(2000)]
+    else:
+        msgs = [('{"I32Field":%d,"I32Field":%d,"StringField":"a","StringField":"bc"}' % (k, -k)).encode()
+                for k in range(1000)]
+    for extra in (FLAT, 0):
+        bad = _compare(fl, msgs, flags | extra)
+        assert not bad, (extra, bad[:4])
+
+
+def test_flat_edges():
+    td = flat_desc()
+    fl = T.flatten(td)
+    msgs = [b"", b"{}", b" { } ", b"{", b"}", b'{"req":1}', b'{"req":1,}', b'{,"req":1}', b'{"req":1 "b":true}',
+            b'{"req":1}x', b'{"req":1} {}', b'[1]', b'"s"', b'1', b'null', b'{"req":null}', b'{"req":1,"b":nul}',
+            b'{"req":1,"Str":"' + b"x" * 400 + b'"}', b'{"req":1,"Str":"' + b"x" * 600 + b'"}',
+            b'{"req":1,"str":"by name"}', b'{"req":1,"vm64":"123","vm16":"-7","vms":42}', b'{"req":1,"vm64":""}',
+            b'{"req":2147483648}', b'{"req":1,"y":128}', b'{"req":1,"d":1e400}', b'{"req":1,"s64":"5"}',
+            b'{"req":1,"bin":"QQ=="}', b'{"req":1,"bin":"QR=="}', b'{"req":1,"bin":"Q==="}', b'{"req":1,"bin":"QQ"}',
+            b'{"req":1,"b":true,"b":false}', b'{"\\u0072eq":1}', b'{"req":1,"Str":"\xff\xfe"}',
+            b'{"req" : 1 , "far" : 2.5 }', b'{"req":1,"far":-0.0,"s16":32767}']
+    for flags in (0x1, 0x0, 0x7, 0x23, 0x5):
+        for extra in (FLAT, 0):
+            bad = _compare(fl, msgs, flags | extra)
+            assert not bad, (hex(flags), extra, bad[:4])

@@ -1,4 +1,4 @@
-"""Build experiment variants of the library (wave-kernel occupancy knobs):
+"""Build experiment variants of the library (wave / flat kernel knobs):
 python tools/build_variants.py NAME=-DFLAG=..,-DFLAG=.. ...  -> dynamicgo_amd/libdgj2t_NAME.so"""
 import os
 import sys
@@ -10,5 +10,7 @@ for spec in sys.argv[1:]:
     name, flags = spec.split("=", 1)
     fl = tuple(flags.split(","))
     out = os.path.join(b.ROOT, "dynamicgo_amd", f"libdgj2t_{name}.so")
-    b.build_hip(out=out, unit_flags={"j2t_kern_wave.hip": fl, "j2t_host.hip": fl})
+    units = ("j2t_kern_flat.hip", "j2t_host.hip") if all(f.startswith("-DDG_FL_") for f in fl) else \
+        ("j2t_kern_wave.hip", "j2t_host.hip", "j2t_kern_flat.hip")
+    b.build_hip(out=out, unit_flags={u: fl for u in units})
     print("built", out, flush=True)

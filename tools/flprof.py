@@ -1,0 +1,50 @@
+"""Phase breakdown of the flat kernel (a -DDG_FLPROF build, tools/build_variants.py flprof=-DDG_FL_PROF...):
+on the GPU: DG_LIB_PATH=dynamicgo_amd/libdgj2t_flprof.so DG_ALLOW_STALE=1 python tools/flprof.py c2"""
+import ctypes as C
+import os
+import random
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+import torch
+
+from dynamicgo_amd import _lib, conv, workloads as W
+from dynamicgo_amd.thrift import flatten
+
+cfg = sys.argv[1] if len(sys.argv) > 1 else "c2"
+td, msgs = {"c2": lambda: (W.simple_desc(), W.gen_flat_batch(random.Random(42), 65536)),
+            "c2s": lambda: (W.simple_desc(), W.gen_flat_batch_shuffled(random.Random(42), 65536))}[cfg]()
+n = len(msgs)
+flat = flatten(td)
+a, off = W.arena(msgs)
+slots = np.zeros(n + 1, dtype=np.int64)
+np.cumsum((np.diff(off).astype(np.int64) * 4 + 64 + 7) // 8 * 8, out=slots[1:])
+dev = torch.device("cuda:0")
+ctx = conv.Context(0)
+dh = ctx.desc(flat)
+d_json = torch.from_numpy(a).to(dev)
+d_in = torch.from_numpy(off.astype(np.int64)).to(dev)
+d_out = torch.empty(int(slots[-1]) + 64, dtype=torch.uint8, device=dev)
+d_oo = torch.from_numpy(slots).to(dev)
+d_ol = torch.zeros(n, dtype=torch.int32, device=dev)
+d_ret = torch.zeros(n, dtype=torch.int64, device=dev)
+L = _lib.lib()
+ms = C.c_float(0)
+cnt = (C.c_uint64 * 16)()
+args = (ctx.h, dh, flat.root_type, d_json.data_ptr(), d_in.data_ptr(), n, 1, d_out.data_ptr(), d_oo.data_ptr(),
+        d_ol.data_ptr(), d_ret.data_ptr())
+_lib.check(L.dg_bench_device(*args, 1, C.byref(ms)))
+_lib.check(L.dg_ctx_counters(ctx.h, cnt, 16, 1))
+reps = 5
+_lib.check(L.dg_bench_device(*args, reps, C.byref(ms)))
+_lib.check(L.dg_ctx_counters(ctx.h, cnt, 16, 1))
+c = list(cnt)[2:10]
+names = ["stage+desc+barrier", "structure", "barrier 1", "parse", "barrier 2", "prefix+barrier", "write",
+         "barrier 4"]
+waves = n // 8 // 32  # 8 messages (64 lanes) per wave; 1 block in 32 sampled
+tot = sum(c)
+print(f"{cfg}: {ms.value / reps * 1000:.1f} us/step (instrumented), ok={(d_ret.cpu().numpy() == 0).sum()}")
+for k, nm in enumerate(names):
+    print("  %-20s %6.2f%%  %9.0f cycles/wave" % (nm, 100 * c[k] / max(1, tot), c[k] / reps / waves))
+print("  total %.0f cycles/wave" % (tot / reps / waves))
