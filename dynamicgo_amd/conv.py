@@ -35,6 +35,8 @@ F_WRITE_OPTIONAL = 1 << 7
 F_TRACE_BACK = 1 << 8
 F_NO_WRITE_BASE = 1 << 9
 F_VALIDATE_UTF8 = 1 << 16  # extension, off by default
+F_FLAT_PATH = 1 << 19      # extension: flat root structs on the field-parallel kernel
+F_HM_SPLIT = 1 << 20       # extension: root HTTP mappings written by the host (do_batch_hm_split)
 
 DG_ST_OUT_OVERFLOW = 0xF0
 DG_ST_DEEP = 0xF1
@@ -264,7 +266,21 @@ class BinaryConv:
         if out:
             buf.extend(out)
 
-    def do_batch(self, desc, msgs: Sequence[bytes]) -> Tuple[List[bytes], np.ndarray]:
+    def do_batch_hm_split(self, desc, msgs: Sequence[bytes], prefixes: Sequence[bytes]):
+        """EnableHttpMapping, pre-split on the host: the
+        Go host has run handleHttpMappings (conv/j2t/impl.go:243-292) for the
+        ROOT struct and produced prefixes[i], its mapped fields' Thrift bytes;
+        the GPU converts the bodies with DG_F_HM_SPLIT (mapped keys skipped,
+        mapped fields counted as set) and each result is prefix + body (pass
+        b"" for a root without mapped fields). A nested struct with mapped
+        fields still returns ERR_HM (19)."""
+        if len(prefixes) != len(msgs):
+            raise ValueError("one prefix per message")
+        outs, rets = self.do_batch(desc, msgs, extra_flags=F_HTTP_MAPPING | F_HM_SPLIT)
+        # a null body converts to nothing: no struct, no mapped fields
+        return [p + o if int(r) == 0 and o else b"" for p, o, r in zip(prefixes, outs, rets)], rets
+
+    def do_batch(self, desc, msgs: Sequence[bytes], extra_flags: int = 0) -> Tuple[List[bytes], np.ndarray]:
         """Batch of independent messages -> (outputs, packed statuses)."""
         self._check_opts()
         flat = self._flat(desc)
@@ -280,14 +296,15 @@ class BinaryConv:
         out = np.zeros(cap, dtype=np.uint8)
         need = C.c_uint64(0)
         L = _lib.lib()
+        flags = to_flags(self.opts) | extra_flags
         rc = L.dg_j2t_batch_host(ctx.h, ctx.desc(flat), flat.root_type, arena.ctypes.data, in_off.ctypes.data,
-                                 n, to_flags(self.opts), out.ctypes.data, cap, out_off.ctypes.data,
+                                 n, flags, out.ctypes.data, cap, out_off.ctypes.data,
                                  rets.ctypes.data, C.byref(need))
         if rc == -3 and need.value > cap:
             cap = int(need.value) + 64
             out = np.zeros(cap, dtype=np.uint8)
             rc = L.dg_j2t_batch_host(ctx.h, ctx.desc(flat), flat.root_type, arena.ctypes.data,
-                                     in_off.ctypes.data, n, to_flags(self.opts), out.ctypes.data, cap,
+                                     in_off.ctypes.data, n, flags, out.ctypes.data, cap,
                                      out_off.ctypes.data, rets.ctypes.data, C.byref(need))
         _lib.check(rc)
         outs = [out[int(out_off[i]):int(out_off[i + 1])].tobytes() for i in range(n)]

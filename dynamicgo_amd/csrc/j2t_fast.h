@@ -73,10 +73,11 @@ typedef const __attribute__((address_space(3))) double lds_f64;
 /* F_ENABLE_HM is in: its only effects are on structs with HTTP-mapped fields
  * (ERR_HM at entry native/thrift.c:1119-1123, mapped keys skipped
  * native/thrift.c:725), which the fast paths decline; ERR_HM_END needs
- * F_TRACE_BACK, which stays out */
+ * F_TRACE_BACK, which stays out. DG_F_HM_SPLIT only changes what the exact
+ * machine does at such a struct (j2t_machine.h), so it is in too. */
 constexpr uint64_t FAST_FLAGS = DG_F_ALLOW_UNKNOWN | DG_F_WRITE_DEFAULT | DG_F_ENABLE_VM | DG_F_ENABLE_I2S |
                                 DG_F_WRITE_REQUIRE | DG_F_NO_BASE64 | DG_F_WRITE_OPTIONAL | DG_F_NO_WRITE_BASE |
-                                DG_F_ENABLE_HM;
+                                DG_F_ENABLE_HM | DG_F_HM_SPLIT;
 
 /* small power tables, copied to LDS by the kernel prologue */
 struct FastTabs {

@@ -686,7 +686,15 @@ struct Machine {
                         for (uint32_t w = 0; w < sd.req_words; w++) ws.reqarena[reqlen + w] = D.R[sd.req_begin + w];
                         reqlen += sd.req_words;
                     }
-                    if ((flag & DG_F_ENABLE_HM) && (sd.flags & DG_SF_HTTP_MAPPING)) return pack0(E_HM, (uint64_t)(p - 1));
+                    if ((flag & DG_F_ENABLE_HM) && (sd.flags & DG_SF_HTTP_MAPPING)) {
+                        /* ERR_HM (native/thrift.c:1119-1123) -> handleHttpMappings; pre-split
+                         * (DG_F_HM_SPLIT): the host wrote the root's mapped fields, which
+                         * reqs.Set(id, Optional) marks as set (conv/j2t/impl.go:284) */
+                        if (!(flag & DG_F_HM_SPLIT) || sp != 1) return pack0(E_HM, (uint64_t)(p - 1)); /* root: vt[0] */
+                        for (uint32_t k = 0; k < sd.n_fields; k++)
+                            if (ldrec(&D.F[sd.field_begin + k]).flags & DG_FF_HTTP_MAPPING)
+                                bm_set_req(nx, sd, k, DG_REQ_OPTIONAL);
+                    }
                 } else {
                     out.w8(TY(t.key).ttype);
                     out.w8(TY(t.elem).ttype);

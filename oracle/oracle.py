@@ -77,6 +77,23 @@ class _Base:
                 raise RuntimeError("oracle output exceeded harness capacity")
         return 0, out.raw[:ol.value]
 
+    def j2t_hm(self, flat, json: bytes, flags: int, prefix: bytes, root: Optional[int] = None) -> Tuple[int, bytes]:
+        """One message with the root's HTTP-mapped fields written by the host
+        as `prefix` (handleHttpMappings emulation, reference harness only)."""
+        f = getattr(self.lib, self.p + "j2t_hm")
+        f.restype = C.c_uint64
+        f.argtypes = [C.c_void_p, C.c_uint32, C.c_char_p, C.c_size_t, C.c_uint64, C.c_char_p, C.c_size_t,
+                      C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]
+        d = self._desc(flat.blob)
+        root = flat.root_type if root is None else root
+        cap = 16 * len(json) + len(prefix) + 65536
+        out = C.create_string_buffer(cap)
+        ol = C.c_size_t(0)
+        ret = f(d, root, json, len(json), flags, prefix, len(prefix), out, cap, C.byref(ol))
+        if ret != 0:
+            return int(ret), b""
+        return 0, out.raw[:ol.value]
+
     def j2t_batch(self, flat, msgs: Sequence[bytes], flags: int, nthreads: int = 1,
                   root: Optional[int] = None, slot_factor: int = 4, slot_pad: int = 64):
         """Batch API over an arena: returns (rets u64[n], outs list[bytes])."""

@@ -240,6 +240,14 @@ static void ensure(char **p, size_t *cap, size_t need)
 }
 
 /* One BinaryConv.Do. Returns the packed reference ret; *out_len = bytes. */
+/* handleHttpMappings emulation for the pre-split tests (DG_F_HM_SPLIT): at
+ * the ROOT struct's ERR_HM the Go host writes the mapped fields (here: the
+ * caller's prefix bytes, as if every value was found) and marks each as set
+ * (reqs.Set(id, Optional), conv/j2t/impl.go:243-292), then resumes. */
+static const uint8_t *g_hm_prefix;
+static size_t g_hm_len;
+static int g_hm_on;
+
 static uint64_t ref_do(RefCtx *c, RefDesc *d, uint32_t root, const uint8_t *json, size_t n,
                        uint64_t flags, uint8_t *out, size_t out_cap, size_t *out_len)
 {
@@ -351,6 +359,27 @@ static uint64_t ref_do(RefCtx *c, RefDesc *d, uint32_t root, const uint8_t *json
             fsm->vt[fsm->sp - 1].jp = p; /* SetPos */
             continue;
         }
+        if (e == ERR_HM && g_hm_on && fsm->sp == 1) {
+            J2TState *v = &fsm->vt[0];
+            const tStructDesc *st = v->td->st;
+            for (size_t k = 0; k < st->ids.len; k++) {
+                const tFieldDesc *f = ((tFieldDesc **)st->ids.buf)[k];
+                if (f && f->http_mappings.len) bm_set_req(v->ex.es.reqs, f->ID, REQ_OPTIONAL);
+            }
+            if (buf.len + g_hm_len > buf.cap) {
+                size_t nc = (buf.len + g_hm_len) * 2 + 64;
+                char *nb = (char *)malloc(nc + 64);
+                memcpy(nb, buf.buf, buf.len);
+                free(c->buf);
+                c->buf = nb;
+                c->buf_cap = nc + 64;
+                buf.buf = nb;
+                buf.cap = nc;
+            }
+            memcpy(buf.buf + buf.len, g_hm_prefix, g_hm_len);
+            buf.len += g_hm_len;
+            continue;
+        }
         break; /* real error or host callback (ERR_HM/HM_END/VM_END) */
     }
     if (ret != 0)
@@ -362,6 +391,21 @@ static uint64_t ref_do(RefCtx *c, RefDesc *d, uint32_t root, const uint8_t *json
 }
 
 static RefCtx *g_ctx;
+
+/* one message with the root's HTTP-mapped fields written by the "host" as
+ * `prefix` (see g_hm_*); flags should include F_ENABLE_HM */
+uint64_t dgref_j2t_hm(void *desc, uint32_t root, const uint8_t *json, size_t n, uint64_t flags,
+                      const uint8_t *prefix, size_t plen, uint8_t *out, size_t out_cap, size_t *out_len)
+{
+    if (!g_ctx)
+        g_ctx = ctx_new();
+    g_hm_prefix = prefix;
+    g_hm_len = plen;
+    g_hm_on = 1;
+    uint64_t r = ref_do(g_ctx, (RefDesc *)desc, root, json, n, flags, out, out_cap, out_len);
+    g_hm_on = 0;
+    return r;
+}
 
 uint64_t dgref_j2t(void *desc, uint32_t root, const uint8_t *json, size_t n, uint64_t flags,
                    uint8_t *out, size_t out_cap, size_t *out_len)

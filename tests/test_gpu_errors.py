@@ -82,3 +82,41 @@ def test_recurse_exceed_max():
     deep.elem = deep  # list<list<...>>, a cyclic descriptor (cycles are allowed, SelfRef)
     e = _check(deep, b"[" * 4200 + b"]" * 4200, conv.Options(), "ErrStackOverflow", "stack 4096 overflow")
     assert e.code == 7
+
+
+# ---- HTTP-mapping pre-split (DG_F_HM_SPLIT) ----
+HM, HM_SPLIT = 0x8, 1 << 20
+
+
+@pytest.mark.parametrize("method,flags", [("NestingMethod", 0x1), ("NestingMethod", 0x7), ("NestingMethod", 0x83),
+                                          ("Nesting2Method", 0x1)])
+def test_hm_split_vs_reference(method, flags):
+    """The root struct's HTTP-mapped fields written by the host (the prefix),
+    the body converted on the GPU: prefix + GPU bytes == the reference FSM
+    resumed after handleHttpMappings (mapped keys in the body skipped, mapped
+    fields counted as set). Nested mapped structs still return ERR_HM."""
+    import random
+    import fuzz
+    from schemas import idl_desc
+    from test_gpu_parity import _raw_batch
+    ref = oracle.RefOracle()
+    if ref is None:
+        pytest.skip("oracle/_ref not built")
+    td = idl_desc("baseline.thrift", method)
+    fl = T.flatten(td)
+    rng = random.Random(77 + flags)
+    msgs = [fuzz.gen_message(rng, td, mutate_p=rng.random() < 0.3) for _ in range(400)]
+    prefix = b"\x0b\x00\x01\x00\x00\x00\x02hm" + b"\x08\x00\x04\x00\x00\x00\x07"
+    outs, rets = _raw_batch(fl, msgs, flags | HM | HM_SPLIT)
+    # the host writes a prefix only when the root struct has mapped fields and
+    # the body is a struct (a null body converts to nothing)
+    root_hm = any(f.http_mappings for f in td.struct.fields)
+    bad = []
+    for i, m in enumerate(msgs):
+        if not m:  # an empty body is the Go prelude's (handleHttpMappings with nobody=true, impl.go:52-82)
+            continue
+        er, eo = ref.j2t_hm(fl, m, flags | HM, prefix)
+        got = (prefix if root_hm else b"") + outs[i] if int(rets[i]) == 0 and outs[i] else b""
+        if int(rets[i]) != er or got != eo:
+            bad.append((m[:80], hex(int(rets[i])), hex(er), got[:40], eo[:40]))
+    assert not bad, bad[:4]

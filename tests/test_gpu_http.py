@@ -61,3 +61,21 @@ def test_httpconv_batch_framed_on_gpu():
                 assert o == (hc.top + eo + hc.bottom if er == 0 else b""), (method, b[:80])
             if method == "NestingMethod":
                 assert all((int(r) & 0xFF) in (19, 9) for r in rets[:300]), "expected ERR_HM on mapped structs"
+
+
+def test_do_batch_hm_split_mirror():
+    """BinaryConv.do_batch_hm_split: the Python mirror of the pre-split flow
+    (prefix from the host + GPU body) equals the resumed reference."""
+    import oracle
+    from schemas import idl_desc
+    ref = oracle.RefOracle()
+    if ref is None:
+        pytest.skip("oracle/_ref not built")
+    td = idl_desc("baseline.thrift", "NestingMethod")
+    fl = T.flatten(td)
+    bodies = [b'{"String":"x","I64":5,"ListString":["a"],"Double":1.5}', b'{}', b'{"I32":7,"Byte":1}', b'{"I64":']
+    prefixes = [b"\x0b\x00\x01\x00\x00\x00\x01h", b"", b"\x04\x00\x03" + bytes(8), b"\x08\x00\x04\x00\x00\x00\x01"]
+    outs, rets = conv.BinaryConv(conv.Options()).do_batch_hm_split(td, bodies, prefixes)
+    for b, p, o, r in zip(bodies, prefixes, outs, rets):
+        er, eo = ref.j2t_hm(fl, b, 0x1 | 0x8, p)
+        assert (int(r), o) == (er, eo)
