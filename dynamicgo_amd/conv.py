@@ -35,8 +35,9 @@ F_WRITE_OPTIONAL = 1 << 7
 F_TRACE_BACK = 1 << 8
 F_NO_WRITE_BASE = 1 << 9
 F_VALIDATE_UTF8 = 1 << 16  # extension, off by default
-F_FLAT_PATH = 1 << 19      # extension: flat root structs on the field-parallel kernel
+F_FLAT_PATH = 1 << 19      # extension: force the field-major flat kernel (default for flat roots, messages <= 256 B)
 F_HM_SPLIT = 1 << 20       # extension: root HTTP mappings written by the host (do_batch_hm_split)
+F_NO_FLAT_PATH = 1 << 21   # extension: the lane-per-message small kernel even for a flat root (testing)
 
 DG_ST_OUT_OVERFLOW = 0xF0
 DG_ST_DEEP = 0xF1

@@ -1,73 +1,125 @@
 /*
- * j2t_flat.h — the flat-struct kernel: one GROUP of FL_G lanes per message,
- * one lane per FIELD.
+ * j2t_flat.h — the flat-struct kernel: field-major conversion of small
+ * messages whose root struct has only scalar and string fields (C2's
+ * baseline.Simple, conv/j2t/conv_test.go's Simple).
  *
- * For a root struct whose fields are all scalars or strings (C2's
- * baseline.Simple, conv/j2t/conv_test.go's Simple), a message is
- *     ws '{' ws "key" ws ':' ws value ws (',' ...)* '}' ws
- * and every field can be converted on its own once its span is known. The
- * lane-per-message kernel (j2t_small.h) walks the message byte-serially in
- * one lane; here the group first finds the top-level commas in parallel
- * (each lane classifies 64 bytes: quote parity with a prefix XOR carried
- * across the group, commas and brackets outside strings), then lane k
- * converts field k -- key lookup, value parse, Thrift size -- the group
- * prefix-sums the sizes, and every lane writes its field at its offset.
+ * A message is   ws '{' ws "key" ws ':' ws value ws (',' ...)* '}' ws
+ * and once the top-level commas and colons are known every field converts on
+ * its own. The lane-per-message kernel (j2t_small.h) walks a message
+ * byte-serially in one lane, so a 64K batch is one wave per SIMD and every
+ * latency is exposed. Here a block of 8 waves takes 64 messages:
+ *
+ *  1. structure: 8 lanes per message, each classifies 40 aligned bytes of the
+ *     staged message into bit masks (quote, backslash, comma, colon, bracket);
+ *     the in-string mask is a prefix XOR of the quote bits carried across the
+ *     8 lanes with DPP; commas and colons outside strings are recorded (with
+ *     the count of quotes before each comma).
+ *  2. fields, field-major: wave w converts field w (+8r) of all 64 messages,
+ *     so the lanes of a wave hold the same field of 64 messages -- the same
+ *     type, the same code path. Key lookup (the predicted IDL-order field,
+ *     else the name table), value parse and Thrift size.
+ *  3. every lane reads the sizes of the fields before its own (one barrier),
+ *     writes its field into the message's LDS output stage, and the 8 lanes of
+ *     a message copy the stage to the slot with whole-word stores.
+ *
  * JSON fields are written in input order, exactly as j2t_fsm_exec writes them
- * (native/thrift.c:765-1187, one tb_write_field_begin + value per key).
- *
- * Anything outside that shape -- nesting, null values, escaped keys, a
- * backslash before '"' or '\\', unset fields that need writing, errors --
- * is declined to the bail list, whose list pass (lane kernel fast path, then
- * the exact machine) produces the reference's bytes or error. Messages
- * longer than big_max go to the wave kernel's list as in the small kernel.
+ * (native/thrift.c:765-1187: tb_write_field_begin + value per key,
+ * native/thrift.c:312-420 for the values). Anything outside that shape --
+ * nesting, null values, escaped keys, a backslash before '"' or '\\', unset
+ * fields that need writing, any error -- goes to the bail list, whose list
+ * pass (lane kernel fast path, then the exact machine) produces the
+ * reference's bytes or error. Messages longer than big_max go to the wave
+ * kernel's list as in the small kernel.
  */
 #pragma once
 #include "j2t_small.h"
 
 namespace dg {
 
-constexpr uint32_t FL_G = 8;                      /* lanes per message */
-#ifndef DG_FL_WAVES
-#define DG_FL_WAVES 4
-#endif
+constexpr uint32_t FL_G = 8;                     /* lanes per message in the structure phase */
+constexpr uint32_t FL_WAVES = 8;                 /* waves per block = field slots per round */
+constexpr uint32_t FL_MPB = 64;                  /* messages per block (= lanes of a wave in phase 2) */
+constexpr uint32_t FL_LW = 5;                    /* aligned words per structure lane: 8 x 40 B >= 256 + 7 */
+constexpr uint32_t FL_MAXLEN = 256;              /* longest message on this kernel */
+constexpr uint32_t FL_SLOTW = FL_MAXLEN / 8;     /* words per message when the block's span is not staged */
+constexpr uint32_t FL_STAGEW = FL_MPB * FL_SLOTW;/* 16 KiB */
+constexpr uint32_t FL_SLACKW = FL_G * FL_LW + 2; /* reads past the last message stay in the array */
+constexpr uint32_t FL_MAXF = 24;                 /* fields per message (top-level commas + 1) */
+constexpr uint32_t FL_OUTW = 24;                 /* output stage per message (words): 192 B */
+constexpr uint32_t FL_DESC = 16 * 1024;          /* descriptor bytes in LDS (dynamic) */
+constexpr uint32_t FL_INLINE = 16;               /* longer string / base64 bodies are written as chunk tasks */
+constexpr uint32_t FL_CHUNK = 32;                /* input bytes per chunk task */
+constexpr uint32_t FL_MAXTASK = 512;             /* chunk tasks per block (more: the message declines) */
 #ifndef DG_FL_WPE
-#define DG_FL_WPE 4 /* waves per SIMD the register budget is cut for (LDS allows 4) */
+#define DG_FL_WPE 4 /* waves per SIMD the register budget is cut for */
 #endif
-constexpr uint32_t FL_WAVES = DG_FL_WAVES;        /* waves per block */
-constexpr uint32_t FL_MPW = 64 / FL_G;            /* messages per wave */
-constexpr uint32_t FL_MPB = FL_WAVES * FL_MPW;    /* messages per block */
-constexpr uint32_t FL_MAXLEN = 64 * FL_G;         /* bytes a group classifies (64 per lane) */
-constexpr uint32_t FL_IN_WORDS = FL_MAXLEN / 8 + 3;
-constexpr uint32_t FL_MAXSEP = 48;                /* top-level commas per message */
-constexpr uint32_t FL_OUTW = 64;                  /* output stage per message (words): 512 B */
-constexpr uint32_t FL_DESC = 16 * 1024;           /* descriptor bytes in LDS (dynamic) */
-constexpr uint32_t FL_FPR = 64 * FL_WAVES / FL_MPB; /* fields per message per round (phase 2) */
 
-/* group (FL_G lanes) collectives on 32-bit values */
-DGI uint32_t grp_incl_sum(uint32_t v, uint32_t g)
+/* ---- group (8 lanes, half a DPP row) collectives; converged code only ---- */
+#define DG_DPP(v, ctrl) ((uint32_t)__builtin_amdgcn_update_dpp(0, (int)(v), (ctrl), 0xF, 0xF, false))
+DGI uint32_t g8_incl_sum(uint32_t v, uint32_t g)
 {
-#pragma unroll
-    for (uint32_t d = 1; d < FL_G; d <<= 1) {
-        const uint32_t u = (uint32_t)__shfl_up((int)v, d, FL_G);
-        if (g >= d) v += u;
-    }
+    uint32_t t = DG_DPP(v, 0x111); /* row_shr:1 */
+    v += g >= 1 ? t : 0u;
+    t = DG_DPP(v, 0x112); /* row_shr:2 */
+    v += g >= 2 ? t : 0u;
+    t = DG_DPP(v, 0x114); /* row_shr:4 */
+    v += g >= 4 ? t : 0u;
     return v;
 }
-DGI uint32_t grp_sum(uint32_t v)
+DGI uint32_t g8_sum(uint32_t v)
 {
-#pragma unroll
-    for (uint32_t d = 1; d < FL_G; d <<= 1) v += (uint32_t)__shfl_xor((int)v, d, FL_G);
+    v += DG_DPP(v, 0xB1);  /* quad_perm [1,0,3,2] */
+    v += DG_DPP(v, 0x4E);  /* quad_perm [2,3,0,1] */
+    v += DG_DPP(v, 0x141); /* row_half_mirror: lane i <- 7-i, the other quad */
     return v;
 }
-DGI uint32_t grp_or(uint32_t v)
+/* the value of the next lane of the group (0 for the last lane) */
+DGI uint32_t g8_next(uint32_t v, uint32_t g)
 {
-#pragma unroll
-    for (uint32_t d = 1; d < FL_G; d <<= 1) v |= (uint32_t)__shfl_xor((int)v, d, FL_G);
-    return v;
+    const uint32_t t = DG_DPP(v, 0x101); /* row_shl:1 */
+    return g < 7 ? t : 0u;
 }
 
 /* 0x80 in each byte of w (32-bit half) equal to c */
 DGI uint32_t eq32(uint32_t w, uint32_t cc) { return zb32(w ^ cc); }
+/* the 0x80 flags of a 32-bit half -> 4 bits (byte k -> bit k) */
+DGI uint32_t nib(uint32_t m80) { return (((m80 >> 7) * 0x00204081u) >> 21) & 0xFu; }
+/* byte-class bits of an 8-byte word (byte k -> bit k) */
+DGI uint32_t cls8(uint32_t lo, uint32_t hi, uint32_t cc) { return nib(eq32(lo, cc)) | (nib(eq32(hi, cc)) << 4); }
+
+/* The staged message in LDS, the SrcT interface without SrcT's one-word
+ * cache: every access is its own LDS read, so independent reads overlap
+ * instead of chaining through the cache tag (and no per-lane branch). */
+struct LSrc {
+    typedef int32_t idx;
+    const __attribute__((address_space(3))) uint64_t *w8;
+    int32_t off0;
+    int32_t n;
+    DGI void init(const __attribute__((address_space(3))) uint64_t *words, int32_t off, int32_t len)
+    {
+        w8 = words;
+        off0 = off;
+        n = len;
+    }
+    DGI uint8_t raw(int32_t i) const
+    {
+        return ((const __attribute__((address_space(3))) uint8_t *)w8)[off0 + i];
+    }
+    DGI uint8_t at(int32_t i) const { return (uint32_t)i < (uint32_t)n ? raw(i) : 0; }
+    /* 8 bytes at [i, i+8), first byte lowest (the stage has slack words past the end) */
+    DGI uint64_t get8(int32_t i) const
+    {
+        const uint32_t b = (uint32_t)(off0 + i), k = b >> 3, sh = (b & 7) << 3;
+        const uint64_t lo = w8[k], hi = w8[k + 1];
+        return (lo >> sh) | ((hi << 1) << (63 - sh));
+    }
+    DGI LSrc sub(int32_t s0, int32_t len) const
+    {
+        LSrc r;
+        r.init(w8, off0 + s0, len);
+        return r;
+    }
+};
 
 /* A byte writer into an 8-aligned buffer (global: the output slot; LDS: a
  * message's output stage) starting at an arbitrary byte offset; several
@@ -157,24 +209,41 @@ DGI uint32_t skip_ws(S &s, uint32_t p)
     return p;
 }
 
-/* field k's span [sk, ek): parse and size it; false = decline the message */
+/* does src[s0, s0+nb) hold byte ch */
+template <class S>
+DGI bool has_byte(S &src, uint32_t s0, uint32_t nb, uint8_t ch)
+{
+    for (uint32_t j = 0; j < nb; j += 8) {
+        uint64_t m = eqbytes(src.get8((typename S::idx)(s0 + j)), ch);
+        if (nb - j < 8) m &= (1ull << ((nb - j) << 3)) - 1;
+        if (m) return true;
+    }
+    return false;
+}
+
+/* Field k: bytes (sk, ek) between its separators, its colon at ck, nq quotes
+ * inside. Key lookup, value parse and Thrift size; false = decline the
+ * message. Every quote of the message is a delimiter (phase 1 declined \" and
+ * \\), so a field holds exactly the key's two quotes, plus two when the value
+ * is a string: the key and a string value are delimited without scanning. */
 template <class S, class DV>
-DGI bool flat_parse(const DV &D, const dg_struct &sd, S &src, uint32_t sk, uint32_t ek, uint32_t k, uint64_t flag,
-                    const FastTabs &tb, FField &F)
+DGI bool fl_field(const DV &D, const dg_struct &sd, S &src, uint32_t sk, uint32_t ck, uint32_t ek, uint32_t nq,
+                  bool hasbs, uint32_t k, uint64_t flag, const FastTabs &tb, FField &F)
 {
     typedef typename S::idx SI;
-    uint32_t p = skip_ws(src, sk);
-    if (p >= ek || src.raw((SI)p) != '"') return false;
-    const uint32_t k0 = p + 1;
-    bool esc;
-    int64_t e = advance_string(src, k0, esc);
-    if (e < 0 || esc || (uint64_t)e > ek) return false;
-    const uint32_t kn = (uint32_t)e - 1 - k0;
-    p = skip_ws(src, (uint32_t)e);
-    if (p >= ek || src.raw((SI)p) != ':') return false;
-    p = skip_ws(src, p + 1);
-    if (p >= ek) return false;
-    /* the key: predicted (field k in IDL order), else the name table */
+    const uint32_t p = skip_ws(src, sk);
+    uint32_t q = ck;
+    while (q > p && isspace_(src.raw((SI)(q - 1)))) q--;
+    if (q < p + 2 || src.raw((SI)p) != '"' || src.raw((SI)(q - 1)) != '"') return false;
+    const uint32_t k0 = p + 1, kn = q - 1 - k0;
+    const uint32_t v0 = skip_ws(src, ck + 1);
+    uint32_t ve = ek;
+    while (ve > v0 && isspace_(src.raw((SI)(ve - 1)))) ve--;
+    if (v0 >= ve) return false;
+    const uint8_t c = src.raw((SI)v0);
+    if (nq != (c == '"' ? 4u : 2u)) return false;
+    if (hasbs && has_byte(src, k0, kn, '\\')) return false; /* escaped key: unquoted before lookup -> the list pass */
+    /* the key (native/thrift.c:668-763): predicted (field k in IDL order), else the name table */
     int32_t fi = -1;
     dg_field f;
     if (k < sd.n_fields) {
@@ -201,40 +270,34 @@ DGI bool flat_parse(const DV &D, const dg_struct &sd, S &src, uint32_t sk, uint3
         }
         if (fi >= 0) f = ldrec(&D.F[fi]);
     }
-    /* the value */
-    const uint8_t c = src.raw((SI)p);
+    /* the value, [v0, ve) */
     uint32_t vk;
     uint32_t vs0 = 0, vnb = 0;
     bool vesc = false, isint = false, bv = false;
     int64_t iv = 0;
     double dv = 0.0;
     if (c == '"') {
-        vs0 = p + 1;
-        e = advance_string(src, vs0, vesc);
-        if (e < 0 || (uint64_t)e > ek) return false;
-        vnb = (uint32_t)e - 1 - vs0;
-        p = (uint32_t)e;
+        if (ve - v0 < 2 || src.raw((SI)(ve - 1)) != '"') return false;
+        vs0 = v0 + 1;
+        vnb = ve - 1 - vs0;
+        vesc = hasbs && has_byte(src, vs0, vnb, '\\');
         vk = FV_STR;
     } else if (c == '-' || (uint8_t)(c - '0') <= 9) {
-        SI q = (SI)p;
-        vs0 = p;
-        if (!fast_vnumber(src, q, tb, iv, dv, isint)) return false;
-        p = (uint32_t)q;
-        vnb = p - vs0;
+        SI qq = (SI)v0;
+        if (!fast_vnumber(src, qq, tb, iv, dv, isint) || (uint32_t)qq != ve) return false;
+        vs0 = v0;
+        vnb = ve - v0;
         vk = FV_NUM;
     } else if (c == 't') {
-        if (p + 4 > ek || (uint32_t)src.get8((SI)p) != VS_TRUE) return false;
-        p += 4;
+        if (ve - v0 != 4 || (uint32_t)src.get8((SI)v0) != VS_TRUE) return false;
         bv = true;
         vk = FV_BOOL;
     } else if (c == 'f') {
-        if (p + 5 > ek || (uint32_t)src.get8((SI)(p + 1)) != VS_ALSE) return false;
-        p += 5;
+        if (ve - v0 != 5 || (uint32_t)src.get8((SI)(v0 + 1)) != VS_ALSE) return false;
         vk = FV_BOOL;
     } else {
         return false; /* null, containers, garbage: the list pass */
     }
-    if (skip_ws(src, p) != ek) return false;
     F.fi = fi;
     if (fi < 0 || ((f.flags & DG_FF_REQUEST_BASE) && (flag & DG_F_NO_WRITE_BASE))) {
         if (fi < 0 && !(flag & DG_F_ALLOW_UNKNOWN)) return false; /* ERR_UNKNOWN_FIELD */
@@ -243,8 +306,9 @@ DGI bool flat_parse(const DV &D, const dg_struct &sd, S &src, uint32_t sk, uint3
         F.size = 0;
         return true;
     }
-    const uint8_t tt = ldrec(&D.T[f.type]).ttype;
-    const bool bin = (ldrec(&D.T[f.type]).flags & DG_TF_BINARY) && !(flag & DG_F_NO_BASE64);
+    const dg_type ft = ldrec(&D.T[f.type]);
+    const uint8_t tt = ft.ttype;
+    const bool bin = (ft.flags & DG_TF_BINARY) && !(flag & DG_F_NO_BASE64);
     F.tt = tt;
     F.id = f.id;
     F.i16q = false;
@@ -255,8 +319,8 @@ DGI bool flat_parse(const DV &D, const dg_struct &sd, S &src, uint32_t sk, uint3
         if (vk == FV_STR && tt != DG_T_STRING) {
             if (vnb == 0 || vesc) return false; /* "" -> default write: the list pass */
             S sub = src.sub((SI)vs0, (SI)vnb);
-            SI q = 0;
-            if (!fast_vnumber(sub, q, tb, iv, dv, isint) || (uint32_t)q != vnb) return false;
+            SI qq = 0;
+            if (!fast_vnumber(sub, qq, tb, iv, dv, isint) || (uint32_t)qq != vnb) return false;
             vk = FV_NUM;
         } else if (vk == FV_NUM && tt == DG_T_STRING) {
             vk = FV_NUMSTR; /* the number's text as the string */
@@ -309,59 +373,127 @@ DGI bool flat_parse(const DV &D, const dg_struct &sd, S &src, uint32_t sk, uint3
     return true;
 }
 
-/* write a parsed field (header + value) */
+/* a piece of a string body: src[s0, s0+n) copied */
 template <class S, class O>
-DGI bool flat_write(S &src, const FField &F, O &o)
+DGI void body_copy(S &src, uint32_t s0, uint32_t n, O &o)
+{
+    fast_copy(src, (typename S::idx)s0, (typename S::idx)n, o);
+}
+/* a piece of a canonical padded base64 body, src[s0, s0+n) (n % 4 == 0);
+ * `last`: the piece holds the final quantum, which may carry '=' */
+template <class S, class O>
+DGI bool body_b64(S &src, uint32_t s0, uint32_t n, bool last, O &o)
 {
     typedef typename S::idx SI;
-    if (F.kind == FV_NONE) return true;
+    uint32_t ip = 0;
+    const uint32_t full = last && n >= 4 ? n - 4 : n;
+    for (; ip + 8 <= full; ip += 8) {
+        uint64_t v;
+        if (!b64_8(src.get8((SI)(s0 + ip)), v)) return false;
+        o.wle(v, 6);
+    }
+    for (; ip < full; ip += 4) {
+        uint32_t v;
+        if (!b64_4((uint32_t)src.get8((SI)(s0 + ip)), v)) return false;
+        o.wle(v, 3);
+    }
+    if (last && n >= 4) {
+        uint32_t w = (uint32_t)src.get8((SI)(s0 + ip));
+        const uint32_t c2 = (w >> 16) & 0xFF, c3 = w >> 24;
+        const uint32_t keep = c3 == '=' ? (c2 == '=' ? 1u : 2u) : 3u;
+        if (c3 == '=') w = (w & 0x00FFFFFFu) | ((uint32_t)'A' << 24);
+        if (c2 == '=') w = (w & 0xFF00FFFFu) | ((uint32_t)'A' << 16);
+        uint32_t v;
+        if (!b64_4(w, v)) return false;
+        o.wle(v, keep); /* decode_block keeps nb-1 bytes; the padding bits are not checked */
+    }
+    return true;
+}
+
+/* write a parsed field: header, then the value (j2t_number/j2t_string/
+ * j2t_binary, native/thrift.c:312-420). Returns 0 = error, 1 = written,
+ * 2 = header and length written, the body (> FL_INLINE bytes of a string
+ * without escapes or of canonical base64) is left to chunk tasks. */
+template <class S, class O>
+DGI uint32_t flat_write(S &src, const FField &F, O &o)
+{
+    typedef typename S::idx SI;
+    if (F.kind == FV_NONE) return 1;
     o.wle((uint32_t)F.tt | ((uint32_t)__builtin_bswap16(F.id) << 8), 3);
     switch (F.kind) {
-    case FV_BOOL: o.w8((uint8_t)F.iv); return true;
+    case FV_BOOL: o.w8((uint8_t)F.iv); return 1;
     case FV_NUM:
         if (F.i16q) {
             emit_number(o, DG_T_I16, F.isint, F.iv, F.dv);
             emit_number(o, DG_T_BYTE, F.isint, F.iv, F.dv);
-            return true;
+            return 1;
         }
-        return emit_number(o, F.tt, F.isint, F.iv, F.dv);
+        return emit_number(o, F.tt, F.isint, F.iv, F.dv) ? 1u : 0u;
     case FV_NUMSTR:
-        o.w32(F.nb);
-        fast_copy(src, (SI)F.s0, (SI)F.nb, o);
-        return true;
     case FV_STR:
+        o.w32(F.kind == FV_NUMSTR ? F.nb : F.size - 7);
+        if (F.esc) return fast_unquote(src, (SI)F.s0, (SI)F.nb, o) ? 1u : 0u;
+        if (F.nb > FL_INLINE) return 2;
+        body_copy(src, F.s0, F.nb, o);
+        return 1;
+    default: /* FV_BIN: canonical padded base64 */
         o.w32(F.size - 7);
-        if (F.esc) return fast_unquote(src, (SI)F.s0, (SI)F.nb, o);
-        fast_copy(src, (SI)F.s0, (SI)F.nb, o);
-        return true;
-    default: { /* FV_BIN: canonical padded base64 */
-        o.w32(F.size - 7);
-        uint32_t ip = 0;
-        const uint32_t full = F.nb >= 4 ? F.nb - 4 : 0; /* the last quantum may hold '=' */
-        for (; ip + 8 <= full; ip += 8) {
-            uint64_t v;
-            if (!b64_8(src.get8((SI)(F.s0 + ip)), v)) return false;
-            o.wle(v, 6);
-        }
-        for (; ip < full; ip += 4) {
-            uint32_t v;
-            if (!b64_4((uint32_t)src.get8((SI)(F.s0 + ip)), v)) return false;
-            o.wle(v, 3);
-        }
-        if (F.nb >= 4) {
-            uint32_t w = (uint32_t)src.get8((SI)(F.s0 + ip));
-            const uint32_t c2 = (w >> 16) & 0xFF, c3 = w >> 24;
-            const uint32_t keep = c3 == '=' ? (c2 == '=' ? 1u : 2u) : 3u;
-            if (c3 == '=') w = (w & 0x00FFFFFFu) | ((uint32_t)'A' << 24);
-            if (c2 == '=') w = (w & 0xFF00FFFFu) | ((uint32_t)'A' << 16);
-            uint32_t v;
-            if (!b64_4(w, v)) return false;
-            o.wle(v, keep); /* decode_block keeps nb-1 bytes; the padding bits are not checked */
-        }
-        return true;
-    }
+        if (F.nb > FL_INLINE) return 2;
+        return body_b64(src, F.s0, F.nb, true, o) ? 1u : 0u;
     }
 }
+
+/* An output writer into a message's LDS stage (zeroed beforehand) from an
+ * arbitrary byte offset: whole words are stored, the partial words at the two
+ * ends of the range -- shared with the neighbouring fields -- are OR-ed in
+ * (the bytes outside the range are zero in them). */
+struct LOr {
+    typedef __attribute__((address_space(3))) uint64_t L64;
+    L64 *b;
+    uint32_t len;
+    uint64_t wbuf;
+    bool edge; /* the current word is shared with the field before */
+    DGI void init(L64 *base, uint32_t start)
+    {
+        b = base;
+        len = start;
+        wbuf = 0;
+        edge = (start & 7) != 0;
+    }
+    DGI void put_word(uint32_t wi, uint64_t v)
+    {
+        if (!edge) {
+            b[wi] = v;
+        } else {
+            __hip_atomic_fetch_or((uint64_t *)(void *)&b[wi], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            edge = false;
+        }
+    }
+    DGI void wle(uint64_t v, uint32_t n)
+    {
+        const uint32_t used = len & 7, sh = used << 3;
+        if (n < 8) v &= (1ull << (n << 3)) - 1;
+        const uint64_t low = (wbuf & ((1ull << sh) - 1)) | (v << sh);
+        const uint64_t high = used ? (v >> (64 - sh)) : 0;
+        const uint32_t wi = len >> 3;
+        len += n;
+        if (used + n >= 8) {
+            put_word(wi, low);
+            wbuf = high;
+        } else {
+            wbuf = low;
+        }
+    }
+    DGI void w8(uint8_t v) { wle(v, 1); }
+    DGI void w16(uint16_t v) { wle(__builtin_bswap16(v), 2); }
+    DGI void w32(uint32_t v) { wle(__builtin_bswap32(v), 4); }
+    DGI void w64(uint64_t v) { wle(__builtin_bswap64(v), 8); }
+    DGI void finish()
+    {
+        if (len & 7)
+            __hip_atomic_fetch_or((uint64_t *)(void *)&b[len >> 3], wbuf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+};
 
 struct FlatParams {
     const uint8_t *blob;
@@ -371,7 +503,7 @@ struct FlatParams {
 };
 
 /* -DDG_FLPROF: cycles per wave by phase (s_memtime at the marks, summed
- * into P.stats[2..] by each wave's first lane) */
+ * into P.stats[2..] by each wave's first lane, 1 block in 32 sampled) */
 #ifdef DG_FLPROF
 #define FLP_DECL uint64_t flp_t = __builtin_amdgcn_s_memtime(); uint64_t flp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #define FLP(k)                                              \
@@ -382,7 +514,7 @@ struct FlatParams {
     } while (0)
 #define FLP_END()                                                                        \
     do {                                                                                 \
-        if ((threadIdx.x & 63) == 0 && (blockIdx.x & 31) == 0) /* sampled: 1 block in 32 */ \
+        if ((threadIdx.x & 63) == 0 && (blockIdx.x & 31) == 0)                           \
             for (int k_ = 0; k_ < 8; k_++) atomicAdd(&P.stats[2 + k_], (unsigned long long)flp[k_]); \
     } while (0)
 #else
@@ -391,277 +523,385 @@ struct FlatParams {
 #define FLP_END()
 #endif
 
-/* per message of the block, between the phases */
-struct FlatMsg {
-    uint32_t ok;      /* still on the flat path */
-    uint32_t open, close, nf;
-    uint32_t base;    /* output bytes written by the previous rounds */
-    uint32_t plo, phi;/* present fields (struct field-index bits) */
-    uint32_t a7n;     /* message start & 7 | length << 3 (0 when not staged) */
-    uint64_t oa, cap; /* output slot */
+/* the field slot of wave w: waves w and w+4 share a SIMD, so the first
+ * fields (often the short scalars) are paired with the last ones */
+DGI uint32_t fl_slot(uint32_t w) { return (w & 3) * 2 + (w >> 2); }
+
+/* per-message state of the block, one array per member (lane = message:
+ * consecutive banks) */
+struct FlatLds {
+    uint64_t in[FL_STAGEW + FL_SLACKW];     /* the staged JSON */
+    uint64_t out[FL_MPB * FL_OUTW];         /* output stages, zeroed */
+    uint64_t task[FL_MAXTASK];              /* chunk tasks */
+    uint64_t oa[FL_MPB];                    /* output slot */
+    uint32_t cap[FL_MPB];
+    uint32_t ok[FL_MPB];                    /* still on the flat path (any lane may clear it) */
+    uint32_t n[FL_MPB];                     /* JSON length */
+    uint32_t lw[FL_MPB];                    /* LDS word of the first aligned word << 3 | arena offset & 7 */
+    uint32_t oc[FL_MPB];                    /* open | close << 16 */
+    uint32_t nfq[FL_MPB];                   /* fields | quotes << 8 | backslash seen << 31 */
+    uint32_t plo[FL_MPB], phi[FL_MPB];      /* present fields (struct field-index bits) */
+    uint32_t big[FL_MPB];                   /* listed for the wave kernel */
+    uint32_t nbytes[FL_MPB];                /* Thrift bytes before STOP */
+    uint32_t sep[FL_MAXF * FL_MPB];         /* [k][m]: comma position | quotes before it << 16 */
+    uint16_t col[FL_MAXF * FL_MPB];         /* [k][m]: colon position */
+    uint32_t size[2 * FL_WAVES * FL_MPB];   /* [round & 1][slot][m] */
+    uint32_t rounds, ntask;
+    uint64_t p10u[20];
+    double p10d[23];
 };
 
 template <int V>
 __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(DG_FL_WPE))) void j2t_flat_kernel(
     Params P, FlatParams S)
 {
-    __shared__ __attribute__((aligned(16))) uint64_t s_in[FL_MPB * FL_IN_WORDS];
-    __shared__ uint16_t s_sep[FL_MPB * FL_MAXSEP];
-    __shared__ FlatMsg s_msg[FL_MPB];
-    __shared__ uint32_t s_size[FL_FPR * FL_MPB];
-    __shared__ __attribute__((aligned(16))) uint64_t s_out[FL_MPB * FL_OUTW];
-    __shared__ uint32_t s_rounds;
-    __shared__ uint64_t s_p10u[20];
-    __shared__ double s_p10d[23];
+    __shared__ __attribute__((aligned(16))) FlatLds L;
     extern __shared__ __attribute__((aligned(16))) uint64_t s_fdesc[];
     FLP_DECL
-    const uint32_t tid = threadIdx.x, lane = tid & 63, g = lane & (FL_G - 1);
-    const uint32_t m = tid / FL_G; /* phase 1: the message of this lane's group */
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint64_t b0 = (uint64_t)blockIdx.x * FL_MPB;
+    const uint64_t b1 = b0 + FL_MPB < P.n ? b0 + FL_MPB : P.n;
+
+    /* ---- 0. the block's JSON span to LDS (16-byte coalesced), the descriptor,
+     *      per-message offsets; the output stage zeroed ---- */
+    const uint64_t lo = P.in_off[b0], hi = P.in_off[b1];
+    const uint64_t base = lo & ~15ull;
+    const bool staged = hi - base <= (uint64_t)FL_STAGEW * 8;
+    if (staged) {
+        const uint4 *gs = (const uint4 *)(P.json + base); /* arena: 16 readable bytes past the end */
+        uint4 *ls = (uint4 *)L.in;
+        const uint32_t nw = (uint32_t)((hi - base + 15) >> 4);
+        for (uint32_t k = tid; k < nw; k += 64 * FL_WAVES) ls[k] = gs[k];
+    }
     {
         const uint4 *gd = (const uint4 *)S.blob;
         uint4 *ld = (uint4 *)s_fdesc;
         for (uint32_t k = tid; k < (S.hdr.total_len + 15) / 16; k += 64 * FL_WAVES) ld[k] = gd[k];
     }
+    for (uint32_t k = tid; k < FL_MPB * FL_OUTW / 2; k += 64 * FL_WAVES) ((uint4 *)L.out)[k] = make_uint4(0, 0, 0, 0);
     if (tid < 20) {
         uint64_t v = 1;
         for (uint32_t k = 0; k < tid; k++) v *= 10;
-        s_p10u[tid] = v;
+        L.p10u[tid] = v;
     }
-    if (tid < 23) s_p10d[tid] = P10[tid];
-    if (tid == 0) s_rounds = 0;
-    const uint64_t b0 = (uint64_t)blockIdx.x * FL_MPB;
-    const uint64_t i = b0 + m;
-    const bool have = i < P.n;
-    uint64_t a = 0, b = 0;
-    if (have) {
-        a = P.in_off[i];
-        b = P.in_off[i + 1];
+    if (tid < 23) L.p10d[tid] = P10[tid];
+    if (tid == 0) {
+        L.rounds = 0;
+        L.ntask = 0;
     }
-    const uint64_t n64 = b - a;
-    const bool big = have && P.big_list && n64 > P.big_max;
-    bool ok = have && !big && n64 > 0 && n64 <= FL_MAXLEN;
-    /* stage the message's aligned words (a slack word past the end) */
-    if (ok) {
-        const uint32_t nw = (uint32_t)(((b + 7) >> 3) - (a >> 3)) + 1;
-        const glb_u64 *gsrc = (const glb_u64 *)(const void *)P.json + (a >> 3); /* arena: 16 readable bytes past the end */
-        for (uint32_t w = g; w < nw; w += FL_G) s_in[m * FL_IN_WORDS + w] = gsrc[w];
-    }
-    if (big && g == 0) {
-        const uint32_t q = __hip_atomic_fetch_add(P.big_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        P.big_list[q] = (uint32_t)i;
-    }
-    __syncthreads();
-    FLP(0);
-    const auto D = desc_view<3>((const __attribute__((address_space(3))) uint8_t *)(void *)s_fdesc, S.hdr);
-    const FastTabs tb{(const __attribute__((address_space(3))) uint64_t *)(void *)s_p10u, (lds_f64 *)(void *)s_p10d};
-    const dg_type rt = ldrec(&D.T[P.root]);
-    const dg_struct sd = ldrec(&D.S[rt.st]);
-
-    /* ---- 1. structure (a group of FL_G lanes per message): this lane's 64
-     *      bytes [64g, 64g+64) -> the top-level commas ---- */
-    {
-        const uint32_t n = ok ? (uint32_t)n64 : 0;
-        SrcT<lds_u64, int32_t> src;
-        src.init((lds_u64 *)(void *)&s_in[m * FL_IN_WORDS], (int32_t)(a & 7), (int32_t)n);
-        uint32_t nsep = 0, nbrk = 0, bad = 0;
-        uint64_t cm[8]; /* commas outside strings (0x80 per byte), per word */
-        uint32_t lane_q = 0;
-        {
-            uint64_t qm[8], sm[8], bm[8];
-            const uint32_t base = 64 * g;
-#pragma unroll
-            for (uint32_t j = 0; j < 8; j++) {
-                const uint32_t at = base + 8 * j;
-                uint64_t w = at < n ? src.get8((int32_t)at) : 0;
-                if (at < n && at + 8 > n) w &= (1ull << ((n - at) << 3)) - 1; /* bytes past the end: 0 */
-                const uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
-                const uint32_t l20 = lo | 0x20202020u, h20 = hi | 0x20202020u;
-                qm[j] = (uint64_t)eq32(lo, 0x22222222u) | ((uint64_t)eq32(hi, 0x22222222u) << 32);
-                bm[j] = (uint64_t)eq32(lo, 0x5C5C5C5Cu) | ((uint64_t)eq32(hi, 0x5C5C5C5Cu) << 32);
-                cm[j] = (uint64_t)eq32(lo, 0x2C2C2C2Cu) | ((uint64_t)eq32(hi, 0x2C2C2C2Cu) << 32);
-                sm[j] = (uint64_t)(eq32(l20, 0x7B7B7B7Bu) | eq32(l20, 0x7D7D7D7Du)) |
-                        ((uint64_t)(eq32(h20, 0x7B7B7B7Bu) | eq32(h20, 0x7D7D7D7Du)) << 32); /* { } [ ] */
-                lane_q += (uint32_t)__builtin_popcountll(qm[j]);
-            }
-            /* a backslash before '"' or '\\' (escaped quote or backslash) -> decline */
-#pragma unroll
-            for (uint32_t j = 0; j < 8; j++) {
-                const uint64_t nxt = ((qm[j] | bm[j]) >> 8) | (j < 7 ? (qm[j + 1] | bm[j + 1]) << 56 : 0);
-                if (bm[j] & nxt) bad = 1;
-            }
-            const uint32_t next_first = (uint32_t)__shfl_down((int)(uint32_t)((qm[0] | bm[0]) & 0x80), 1, FL_G);
-            if (g + 1 < FL_G && (bm[7] >> 63) && next_first) bad = 1;
-            /* quote parity: prefix XOR over the bytes, carried across words and lanes */
-            const uint32_t incl = grp_incl_sum(lane_q, g);
-            uint32_t inside = (incl - lane_q) & 1;
-#pragma unroll
-            for (uint32_t j = 0; j < 8; j++) {
-                uint64_t x = qm[j] >> 7; /* 1 per quote byte */
-                x ^= x << 8;
-                x ^= x << 16;
-                x ^= x << 32;
-                x = (x << 8) - x; /* 0xFF in each byte where the parity is odd */
-                const uint64_t ins = x ^ (inside ? ~0ull : 0ull); /* inside a string, opening quote included */
-                inside ^= (uint32_t)(__builtin_popcountll(qm[j]) & 1);
-                cm[j] &= ~ins;
-                nsep += (uint32_t)__builtin_popcountll(cm[j]);
-                nbrk += (uint32_t)__builtin_popcountll(sm[j] & ~ins);
-            }
-            bad |= (uint32_t)__shfl(incl, FL_G - 1, FL_G) & 1; /* an unterminated string */
-        }
-        const uint32_t sep_incl = grp_incl_sum(nsep, g);
-        const uint32_t sep_tot = (uint32_t)__shfl(sep_incl, FL_G - 1, FL_G);
-        const uint32_t brk_tot = grp_sum(nbrk);
-        bad = grp_or(bad);
-        ok = ok && !bad && brk_tot == 2 && sep_tot < FL_MAXSEP;
-        if (ok) {
-            __attribute__((address_space(3))) uint16_t *sep =
-                (__attribute__((address_space(3))) uint16_t *)(void *)&s_sep[m * FL_MAXSEP];
-            uint32_t idx = sep_incl - nsep;
-#pragma unroll
-            for (uint32_t j = 0; j < 8; j++) {
-                uint64_t c = cm[j];
-                while (c) {
-                    const uint32_t bit = (uint32_t)__builtin_ctzll(c);
-                    c &= c - 1;
-                    sep[idx++] = (uint16_t)(64 * g + 8 * j + (bit >> 3));
+    if (tid < FL_MPB) {
+        uint32_t ok = 0, n = 0, lw = 0, big = 0, cap = 0;
+        uint64_t oa = 0;
+        const uint64_t i = b0 + tid;
+        if (i < b1) {
+            const uint64_t a = P.in_off[i], b = P.in_off[i + 1];
+            const uint64_t n64 = b - a;
+            oa = P.out_off[i];
+            cap = (uint32_t)min(P.out_off[i + 1] - oa, (uint64_t)0xFFFFFFFFu);
+            if (P.big_list && (n64 > P.big_max || n64 > FL_MAXLEN)) { /* the wave kernel */
+                big = 1;
+                const uint32_t q = __hip_atomic_fetch_add(P.big_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                P.big_list[q] = (uint32_t)i;
+            } else if (n64 > 0 && n64 <= FL_MAXLEN) {
+                n = (uint32_t)n64;
+                if (staged) {
+                    ok = 1;
+                    lw = (uint32_t)(((a - base) >> 3) << 3) | (uint32_t)(a & 7);
+                } else if ((a & 7) + n64 <= FL_MAXLEN) {
+                    ok = 1;
+                    lw = (tid * FL_SLOTW) << 3 | (uint32_t)(a & 7);
                 }
             }
         }
-        if (g == 0) {
-            /* the braces: the first and last non-space bytes */
-            uint32_t open = 0, close = 0, nf = 0;
-            if (ok) {
-                open = skip_ws(src, 0);
-                close = n - 1;
-                while (close > open && isspace_(src.raw((int32_t)close))) close--;
-                ok = open < close && src.raw((int32_t)open) == '{' && src.raw((int32_t)close) == '}';
-                nf = sep_tot + 1;
-                if (ok && sep_tot == 0 && skip_ws(src, open + 1) == close) nf = 0; /* {} */
+        L.ok[tid] = ok;
+        L.n[tid] = n;
+        L.lw[tid] = lw;
+        L.big[tid] = big;
+        L.oa[tid] = oa;
+        L.cap[tid] = cap;
+        L.plo[tid] = 0;
+        L.phi[tid] = 0;
+        L.oc[tid] = 0;
+        L.nfq[tid] = 0;
+    }
+    __syncthreads();
+    const uint32_t m1 = tid >> 3, g = tid & 7; /* phases 1 and 4: 8 lanes per message */
+    if (!staged) {
+        /* a span too long for the stage (large messages in between): each
+         * message that fits its own 256-byte slot is copied there */
+        if (L.ok[m1]) {
+            const uint64_t a = P.in_off[b0 + m1];
+            const uint32_t nw = (uint32_t)(((a & 7) + L.n[m1] + 7) >> 3);
+            const glb_u64 *gsrc = (const glb_u64 *)(const void *)P.json + (a >> 3);
+            for (uint32_t w = g; w < nw; w += FL_G) L.in[(L.lw[m1] >> 3) + w] = gsrc[w];
+        }
+        __syncthreads();
+    }
+    FLP(0);
+    const auto D = desc_view<3>((const __attribute__((address_space(3))) uint8_t *)(void *)s_fdesc, S.hdr);
+    const FastTabs tb{(const __attribute__((address_space(3))) uint64_t *)(void *)L.p10u, (lds_f64 *)(void *)L.p10d};
+    const dg_type rt = ldrec(&D.T[P.root]);
+    const dg_struct sd = ldrec(&D.S[rt.st]);
+
+    /* ---- 1. structure: lane g of a message classifies the aligned words
+     *      [5g, 5g+5) of it (bit b of a lane = message byte 40g + b - a7) ---- */
+    {
+        const bool on = L.ok[m1] != 0;
+        const uint32_t n = L.n[m1], lwa = L.lw[m1], a7 = lwa & 7, lw = lwa >> 3;
+        const uint32_t nwords = on ? (a7 + n + 7) >> 3 : 0; /* aligned words of the message */
+        uint32_t q80[2 * FL_LW], ck[2 * FL_LW];            /* per 32-bit half: quotes; commas | colons >> 1 */
+        uint32_t nq = 0, anybs = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < FL_LW; j++) {
+            const uint32_t wi = FL_LW * g + j;
+            uint64_t w = 0;
+            if (wi < nwords) {
+                w = L.in[lw + wi];
+                const int32_t wb = (int32_t)(wi * 8) - (int32_t)a7; /* message position of the word's byte 0 */
+                if (wb < 0) w &= ~0ull << ((uint32_t)(-wb) << 3);
+                if (wb + 8 > (int32_t)n) w &= (1ull << ((uint32_t)((int32_t)n - wb) << 3)) - 1;
             }
-            FlatMsg fm;
-            fm.ok = ok ? 1u : 0u;
-            fm.open = open;
-            fm.close = close;
-            fm.nf = nf;
-            fm.base = 0;
-            fm.plo = fm.phi = 0;
-            fm.a7n = (uint32_t)(a & 7) | (n << 3);
-            fm.oa = have ? P.out_off[i] : 0;
-            fm.cap = have ? P.out_off[i + 1] - fm.oa : 0;
-            s_msg[m] = fm;
-            if (ok) atomicMax(&s_rounds, (nf + FL_FPR - 1) / FL_FPR);
+#pragma unroll
+            for (uint32_t h = 0; h < 2; h++) {
+                const uint32_t x = (uint32_t)(w >> (32 * h));
+                q80[2 * j + h] = eq32(x, 0x22222222u);
+                ck[2 * j + h] = eq32(x, 0x2C2C2C2Cu) | (eq32(x, 0x3A3A3A3Au) >> 1);
+                anybs |= eq32(x, 0x5C5C5C5Cu);
+                nq += (uint32_t)__builtin_popcount(q80[2 * j + h]);
+            }
+        }
+        /* quote parity: prefix XOR of the quote bytes, carried across halves and the group */
+        const uint32_t qx = g8_incl_sum(nq, g) - nq;
+        uint32_t carry = qx & 1, nc = 0, nk = 0;
+#pragma unroll
+        for (uint32_t h = 0; h < 2 * FL_LW; h++) {
+            uint32_t x = q80[h] >> 7;
+            x ^= x << 8;
+            x ^= x << 16;
+            const uint32_t ins = ((x << 8) - x) ^ (carry ? ~0u : 0u); /* 0xFF: inside a string (opening quote included) */
+            carry ^= (uint32_t)__builtin_popcount(q80[h]) & 1;
+            ck[h] &= ~ins;
+            nc += (uint32_t)__builtin_popcount(ck[h] & 0x80808080u);
+            nk += (uint32_t)__builtin_popcount(ck[h] & 0x40404040u);
+        }
+        const uint32_t pk = nc | (nk << 10) | (nq << 20);
+        const uint32_t pin = g8_incl_sum(pk, g);
+        const uint32_t ptot = g8_sum(pk);
+        const uint32_t hasbs = g8_sum(anybs ? 1u : 0u);
+        uint32_t bad = 0;
+        if (hasbs) {
+            /* a backslash before '"' or '\\' (an escaped quote or backslash) -> decline,
+             * so every quote is a delimiter */
+            uint64_t bw[FL_LW], qw[FL_LW];
+#pragma unroll
+            for (uint32_t j = 0; j < FL_LW; j++) {
+                const uint32_t wi = FL_LW * g + j;
+                uint64_t w = 0;
+                if (wi < nwords) {
+                    w = L.in[lw + wi];
+                    const int32_t wb = (int32_t)(wi * 8) - (int32_t)a7;
+                    if (wb < 0) w &= ~0ull << ((uint32_t)(-wb) << 3);
+                    if (wb + 8 > (int32_t)n) w &= (1ull << ((uint32_t)((int32_t)n - wb) << 3)) - 1;
+                }
+                bw[j] = eqbytes(w, '\\');
+                qw[j] = bw[j] | eqbytes(w, '"');
+            }
+            const uint32_t nxt = g8_next((uint32_t)(qw[0] & 0x80), g); /* the next lane's first byte */
+            uint64_t bb = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < FL_LW; j++)
+                bb |= bw[j] & ((qw[j] >> 8) | (j + 1 < FL_LW ? qw[j + 1] << 56 : (uint64_t)nxt << 56));
+            bad = g8_sum(bb ? 1u : 0u);
+        }
+        if (on) {
+            uint32_t ci = (pin & 0x3FF) - nc, ki = ((pin >> 10) & 0x3FF) - nk, qc = qx;
+#pragma unroll
+            for (uint32_t h = 0; h < 2 * FL_LW; h++) {
+                const uint32_t pos0 = 40 * g + 4 * h - a7; /* message position of the half's byte 0 */
+                uint32_t c = ck[h] & 0x80808080u, k = ck[h] & 0x40404040u;
+                while (c) {
+                    const uint32_t bit = (uint32_t)__builtin_ctz(c);
+                    c &= c - 1;
+                    if (ci < FL_MAXF)
+                        L.sep[ci * FL_MPB + m1] =
+                            (pos0 + (bit >> 3)) | ((qc + (uint32_t)__builtin_popcount(q80[h] & ((1u << bit) - 1))) << 16);
+                    ci++;
+                }
+                while (k) {
+                    const uint32_t bit = (uint32_t)__builtin_ctz(k);
+                    k &= k - 1;
+                    if (ki < FL_MAXF) L.col[ki * FL_MPB + m1] = (uint16_t)(pos0 + (bit >> 3));
+                    ki++;
+                }
+                qc += (uint32_t)__builtin_popcount(q80[h]);
+            }
+        }
+        if (g == 0 && on) {
+            LSrc src;
+            src.init((const __attribute__((address_space(3))) uint64_t *)(void *)&L.in[lw], (int32_t)a7, (int32_t)n);
+            const uint32_t open = skip_ws(src, 0);
+            uint32_t close = n - 1;
+            while (close > open && isspace_(src.raw((int32_t)close))) close--;
+            const uint32_t nsep = ptot & 0x3FF, ncol = (ptot >> 10) & 0x3FF, qtot = ptot >> 20;
+            bool ok = !bad && open < close && src.raw((int32_t)open) == '{' && src.raw((int32_t)close) == '}' &&
+                      !(qtot & 1) && nsep + 1 < FL_MAXF;
+            uint32_t nf = nsep + 1;
+            if (ok && nsep == 0 && ncol == 0 && skip_ws(src, open + 1) == close) nf = 0; /* {} */
+            ok = ok && ncol == nf;
+            L.ok[m1] = ok ? 1u : 0u;
+            L.oc[m1] = open | (close << 16);
+            L.nfq[m1] = nf | (qtot << 8) | (hasbs ? 1u << 31 : 0u);
+            if (ok) atomicMax(&L.rounds, (nf + FL_WAVES - 1) / FL_WAVES);
         }
     }
     FLP(1);
     __syncthreads();
     FLP(2);
+#if defined(DG_FL_STOP) && DG_FL_STOP == 1
+    return;
+#endif
 
-    /* ---- 2. fields, field-major: lane (fs, mm) converts field r*FL_FPR + fs
-     *      of message mm, so a wave's lanes hold the same field of many
-     *      messages (same type, same path) ---- */
-    const uint32_t mm = tid % FL_MPB, fs = tid / FL_MPB;
-    const uint32_t a7n = s_msg[mm].a7n;
-    const uint64_t oa = s_msg[mm].oa;
-    SrcT<lds_u64, int32_t> src;
-    src.init((lds_u64 *)(void *)&s_in[mm * FL_IN_WORDS], (int32_t)(a7n & 7), (int32_t)(a7n >> 3));
-    const uint32_t rounds = s_rounds;
-    for (uint32_t r = 0; r < rounds; r++) {
-        const FlatMsg fm = s_msg[mm];
-        const uint32_t k = r * FL_FPR + fs;
-        FField F;
-        F.size = 0;
-        F.kind = FV_NONE;
-        const bool mine = fm.ok && k < fm.nf;
-        if (mine) {
-            const __attribute__((address_space(3))) uint16_t *sep =
-                (const __attribute__((address_space(3))) uint16_t *)(void *)&s_sep[mm * FL_MAXSEP];
-            const uint32_t sk = k == 0 ? fm.open + 1 : (uint32_t)sep[k - 1] + 1;
-            const uint32_t ek = k == fm.nf - 1 ? fm.close : (uint32_t)sep[k];
-            if (!flat_parse(D, sd, src, sk, ek, k, P.flag, tb, F)) {
-                s_msg[mm].ok = 0; /* any lane may clear it */
-                F.size = 0;
-            } else if (F.fi >= 0) {
-                const uint32_t bit = (uint32_t)F.fi - sd.field_begin;
-                if (bit < 32) atomicOr(&s_msg[mm].plo, 1u << bit);
-                else atomicOr(&s_msg[mm].phi, 1u << (bit - 32));
-            }
-        }
-        s_size[fs * FL_MPB + mm] = F.size;
-        FLP(3);
-        __syncthreads();
-        FLP(4);
-        /* offsets: one lane per message adds up the round's sizes in field order */
-        if (tid < FL_MPB) {
-            FlatMsg &q = s_msg[tid];
-            uint32_t off = q.base;
-#pragma unroll
-            for (uint32_t f = 0; f < FL_FPR; f++) {
-                const uint32_t sz = s_size[f * FL_MPB + tid];
-                s_size[f * FL_MPB + tid] = off;
-                off += sz;
-            }
-            /* room for STOP in the stage and (word-rounded) in the slot; else the list pass */
-            if (off + 1 > FL_OUTW * 8 || (((uint64_t)off + 8) & ~7ull) > q.cap) q.ok = 0;
-            q.base = off;
-        }
-        __syncthreads();
-        FLP(5);
-        if (mine && s_msg[mm].ok && F.size) {
-            LOut o;
-            o.init((LOut::B8 *)(void *)&s_out[mm * FL_OUTW], s_size[fs * FL_MPB + mm]);
-            const bool wok = flat_write(src, F, o);
-            o.finish();
-            if (!wok) s_msg[mm].ok = 0;
-        }
-        FLP(6);
-        __syncthreads();
-        FLP(7);
-    }
-    /* ---- 3. per message: requires and STOP (one lane per message), then the
-     *      staged output to the slot (a group per message, word stores) ---- */
-    if (tid < FL_MPB && b0 + tid < P.n) {
-        const uint64_t ii = b0 + tid;
-        FlatMsg &q = s_msg[tid];
-        bool good = q.ok != 0;
-        if (good) {
-            const uint64_t present = (uint64_t)q.plo | ((uint64_t)q.phi << 32);
-            uint64_t bits = D.R[sd.req_begin] & ~present;
-            const uint64_t flag = P.flag;
-            while (bits) { /* unset fields that error or need a default write -> the list pass */
-                const uint32_t kk = (uint32_t)__builtin_ctzll(bits);
-                bits &= bits - 1;
-                const dg_field f = ldrec(&D.F[sd.field_begin + kk]);
-                if (f.flags & DG_FF_REQUEST_BASE) continue;
-                if (f.required == DG_REQ_REQUIRED || ((flag & DG_F_WRITE_DEFAULT) && f.required == DG_REQ_DEFAULT) ||
-                    ((flag & DG_F_WRITE_OPTIONAL) && f.required == DG_REQ_OPTIONAL)) {
-                    good = false;
-                    break;
+    /* ---- 2./3. fields, field-major: wave w converts field fl_slot(w) + 8r
+     *      of the block's messages (lane = message) ---- */
+    {
+        const uint32_t mm = lane, fs = fl_slot(wave);
+        const uint32_t ok0 = L.ok[mm], lwa = L.lw[mm], oc = L.oc[mm], nfq = L.nfq[mm];
+        const uint32_t nf = nfq & 0xFF, qtot = (nfq >> 8) & 0x3FF;
+        const bool hasbs = (nfq >> 31) != 0;
+        LSrc src;
+        src.init((const __attribute__((address_space(3))) uint64_t *)(void *)&L.in[lwa >> 3], (int32_t)(lwa & 7), (int32_t)L.n[mm]);
+        const uint32_t rounds = L.rounds;
+        uint32_t nbytes = 0;
+        for (uint32_t r = 0; r < rounds; r++) {
+            const uint32_t k = r * FL_WAVES + fs;
+            FField F;
+            F.size = 0;
+            F.kind = FV_NONE;
+            if (ok0 && k < nf) {
+                const uint32_t e0 = k ? L.sep[(k - 1) * FL_MPB + mm] : 0;
+                const uint32_t sk = k ? (e0 & 0xFFFF) + 1 : (oc & 0xFFFF) + 1, q0 = e0 >> 16;
+                uint32_t ek = oc >> 16, q1 = qtot;
+                if (k + 1 < nf) {
+                    const uint32_t e1 = L.sep[k * FL_MPB + mm];
+                    ek = e1 & 0xFFFF;
+                    q1 = e1 >> 16;
+                }
+                const uint32_t ck = L.col[k * FL_MPB + mm];
+                if (!(ck >= sk && ck < ek && fl_field(D, sd, src, sk, ck, ek, q1 - q0, hasbs, k, P.flag, tb, F))) {
+                    L.ok[mm] = 0;
+                    F.size = 0;
+                    F.kind = FV_NONE;
+                } else if (F.fi >= 0) {
+                    const uint32_t bit = (uint32_t)F.fi - sd.field_begin;
+                    if (bit < 32) atomicOr(&L.plo[mm], 1u << bit);
+                    else atomicOr(&L.phi[mm], 1u << (bit - 32));
                 }
             }
-        }
-        if (good) {
-            ((__attribute__((address_space(3))) uint8_t *)(void *)&s_out[tid * FL_OUTW])[q.base] = 0; /* STOP */
-        } else {
-            q.ok = 0;
-            const uint64_t lo8 = P.in_off[ii], hi8 = P.in_off[ii + 1];
-            if (!(P.big_list && hi8 - lo8 > P.big_max)) { /* not the wave kernel's */
-                const uint32_t qq = atomicAdd(S.bail_count, 1u);
-                S.bail_list[qq] = (uint32_t)ii;
+            uint32_t *sz = &L.size[(r & 1) * FL_WAVES * FL_MPB];
+            sz[fs * FL_MPB + mm] = F.size;
+            FLP(3);
+            __syncthreads();
+            FLP(4);
+#if defined(DG_FL_STOP) && DG_FL_STOP == 2
+            continue;
+#endif
+            uint32_t off = nbytes, tot = 0;
+#pragma unroll
+            for (uint32_t f = 0; f < FL_WAVES; f++) {
+                const uint32_t v = sz[f * FL_MPB + mm];
+                off += f < fs ? v : 0u;
+                tot += v;
             }
+            nbytes += tot;
+            if (F.size) {
+                uint32_t wr = 0;
+                if (off + F.size <= FL_OUTW * 8) {
+                    LOr o;
+                    o.init((LOr::L64 *)(void *)&L.out[mm * FL_OUTW], off);
+                    wr = flat_write(src, F, o);
+                    o.finish();
+                }
+                if (wr == 2) {
+                    /* the body as chunk tasks of FL_CHUNK input bytes */
+                    const bool b64 = F.kind == FV_BIN;
+                    const uint32_t nch = (F.nb + FL_CHUNK - 1) / FL_CHUNK;
+                    const uint32_t t0 = atomicAdd(&L.ntask, nch);
+                    if (t0 + nch <= FL_MAXTASK) {
+                        for (uint32_t c = 0; c < nch; c++) {
+                            const uint32_t cs = c * FL_CHUNK, cn = min(FL_CHUNK, F.nb - cs);
+                            const uint32_t dst = off + 7 + (b64 ? c * (FL_CHUNK / 4 * 3) : cs);
+                            L.task[t0 + c] = (uint64_t)mm | ((uint64_t)b64 << 6) | ((uint64_t)(c + 1 == nch) << 7) |
+                                             ((uint64_t)(F.s0 + cs) << 8) | ((uint64_t)cn << 20) | ((uint64_t)dst << 32);
+                        }
+                    } else {
+                        wr = 0;
+                    }
+                }
+                if (!wr) L.ok[mm] = 0;
+            }
+            FLP(5);
+        }
+        if (fs == 0) L.nbytes[mm] = nbytes;
+    }
+    FLP(6);
+    __syncthreads();
+    /* ---- 3b. chunk tasks: long string / base64 bodies, spread over the block ---- */
+    {
+        const uint32_t nt = min(L.ntask, FL_MAXTASK);
+        for (uint32_t t = tid; t < nt; t += 64 * FL_WAVES) {
+            const uint64_t tk = L.task[t];
+            const uint32_t m = (uint32_t)tk & 63, s0 = (uint32_t)(tk >> 8) & 0xFFF, cn = (uint32_t)(tk >> 20) & 0xFFF;
+            const uint32_t lwa = L.lw[m];
+            LSrc src;
+            src.init((const __attribute__((address_space(3))) uint64_t *)(void *)&L.in[lwa >> 3], (int32_t)(lwa & 7), (int32_t)L.n[m]);
+            LOr o;
+            o.init((LOr::L64 *)(void *)&L.out[m * FL_OUTW], (uint32_t)(tk >> 32));
+            bool cok = true;
+            if ((tk >> 6) & 1) cok = body_b64(src, s0, cn, ((tk >> 7) & 1) != 0, o);
+            else body_copy(src, s0, cn, o);
+            o.finish();
+            if (!cok) L.ok[m] = 0;
         }
     }
     __syncthreads();
-    if (!have || !s_msg[m].ok) return;
+    FLP(7);
+
+    /* ---- 4. per message (8 lanes): unset fields, then the stage (STOP is
+     *      the zero byte after the fields) to the slot with word stores ---- */
     {
-        const uint32_t len = s_msg[m].base + 1;
-        const uint64_t oa1 = s_msg[m].oa;
-        gu64 *dst = (gu64 *)(void *)(P.out + oa1);
-        const __attribute__((address_space(3))) uint64_t *st = (const __attribute__((address_space(3))) uint64_t *)(void *)&s_out[m * FL_OUTW];
-        for (uint32_t w = g; w < (len + 7) / 8; w += FL_G) dst[w] = st[w];
-        if (g == 0) {
-            P.ret[i] = 0;
-            P.out_len[i] = len;
+        const uint64_t i = b0 + m1;
+        if (i < b1) {
+            const uint32_t len = L.nbytes[m1] + 1;
+            bool good = L.ok[m1] && len <= FL_OUTW * 8 && len <= L.cap[m1];
+            if (good) {
+                const uint64_t present = (uint64_t)L.plo[m1] | ((uint64_t)L.phi[m1] << 32);
+                uint64_t bits = D.R[sd.req_begin] & ~present;
+                const uint64_t flag = P.flag;
+                while (bits) { /* unset fields that error or need a default write -> the list pass */
+                    const uint32_t kk = (uint32_t)__builtin_ctzll(bits);
+                    bits &= bits - 1;
+                    const dg_field f = ldrec(&D.F[sd.field_begin + kk]);
+                    if (f.flags & DG_FF_REQUEST_BASE) continue;
+                    if (f.required == DG_REQ_REQUIRED || ((flag & DG_F_WRITE_DEFAULT) && f.required == DG_REQ_DEFAULT) ||
+                        ((flag & DG_F_WRITE_OPTIONAL) && f.required == DG_REQ_OPTIONAL)) {
+                        good = false;
+                        break;
+                    }
+                }
+            }
+            if (good) {
+                gu64 *dst = (gu64 *)(void *)(P.out + L.oa[m1]);
+                const __attribute__((address_space(3))) uint64_t *st =
+                    (const __attribute__((address_space(3))) uint64_t *)(void *)&L.out[m1 * FL_OUTW];
+                for (uint32_t w = g; w < (len + 7) / 8; w += FL_G) dst[w] = st[w];
+                if (g == 0) {
+                    P.ret[i] = 0;
+                    P.out_len[i] = len;
+                }
+            } else if (g == 0 && !L.big[m1]) {
+                const uint32_t qq = atomicAdd(S.bail_count, 1u);
+                S.bail_list[qq] = (uint32_t)i;
+            }
         }
     }
     FLP_END();

@@ -276,9 +276,13 @@ static int enqueue(dg_ctx *c, Scratch *x, const dg_desc *d, uint32_t root, const
     int rc = ensure_fast_ws(x, n);
     if (rc) return rc;
     const bool no_wave = (flags & DG_F_NO_WAVE_PATH) != 0;
+    /* flat roots go to the field-major flat kernel when the batch's messages
+     * fit it (max_len unknown: longer ones are listed for the wave kernel) */
     const char *fl_env = getenv("DG_FLAT");
-    const bool use_flat = fl_env ? atoi(fl_env) != 0 : (flags & DG_F_FLAT_PATH) != 0;
-    flags &= ~(DG_F_NO_WAVE_PATH | DG_F_FLAT_PATH);
+    const bool use_flat = fl_env ? atoi(fl_env) != 0
+                                 : (flags & DG_F_FLAT_PATH) != 0 ||
+                                       (!(flags & DG_F_NO_FLAT_PATH) && (max_len == 0 || max_len <= FL_MAXLEN));
+    flags &= ~(DG_F_NO_WAVE_PATH | DG_F_FLAT_PATH | DG_F_NO_FLAT_PATH);
     Params P;
     P.root = root;
     P.json = json;

@@ -20,14 +20,15 @@
 #define DG_F_VALIDATE_UTF8 (1ull << 16) /* extension: reject invalid UTF-8 in strings */
 #define DG_F_NO_FAST_PATH (1ull << 17)  /* extension: run every message on the exact machine (testing) */
 #define DG_F_NO_WAVE_PATH (1ull << 18)  /* extension: skip the wave-per-message kernel, lane kernel only (testing) */
-#define DG_F_FLAT_PATH (1ull << 19)     /* extension: flat root structs on the field-parallel kernel (j2t_flat.h);
-                                           faster when key order varies between messages, slower on uniform batches */
+#define DG_F_FLAT_PATH (1ull << 19)     /* extension: force the field-major flat kernel (j2t_flat.h) for a flat root
+                                           struct (the default whenever the batch's messages are <= 256 B) */
 #define DG_F_HM_SPLIT (1ull << 20)      /* extension, with F_ENABLE_HM: the host has already written the ROOT struct's
                                            HTTP-mapped fields (handleHttpMappings, conv/j2t/impl.go:243-292, every
                                            value found); the root raises no ERR_HM, its mapped fields count as set
                                            and their JSON keys are skipped (native/thrift.c:725). The output is the
                                            body part: the host puts its mapped-field bytes in front. Nested structs
                                            with mapped fields still return ERR_HM. */
+#define DG_F_NO_FLAT_PATH (1ull << 21)  /* extension: lane-per-message small kernel even for a flat root (testing) */
 
 /* library-internal per-message statuses (code byte values the reference never
  * produces). The host entry points resolve them before returning; the device

@@ -1,7 +1,8 @@
-"""GPU parity of the flat-struct kernel (j2t_flat.h: a lane group per
-message, a lane per field; selected by DG_F_FLAT_PATH) against the
+"""GPU parity of the flat-struct kernel (j2t_flat.h: field-major, the
+default for flat root structs; forced by DG_F_FLAT_PATH) against the
 reference's own engine (oracle/_ref), byte for byte and status word for
-status word; and against the small kernel on the same batches."""
+status word; and against the lane-per-message small kernel
+(DG_F_NO_FLAT_PATH) on the same batches."""
 import random
 
 import numpy as np
@@ -15,6 +16,7 @@ from test_gpu_parity import _raw_batch
 pytestmark = pytest.mark.gpu
 
 FLAT = 1 << 19  # DG_F_FLAT_PATH
+NO_FLAT = 1 << 21  # DG_F_NO_FLAT_PATH
 
 
 def _chk():
@@ -74,7 +76,7 @@ def test_flat_clean_messages_stay_on_the_flat_kernel():
     ctx.stats(reset=True)
     o1, r1 = _raw_batch(fl, msgs, 0x1 | FLAT)
     bails, _ = ctx.stats(reset=True)
-    o2, r2 = _raw_batch(fl, msgs, 0x1)
+    o2, r2 = _raw_batch(fl, msgs, 0x1 | NO_FLAT)
     assert o1 == o2 and list(r1) == list(r2)
     assert not any(int(r) for r in r1)
     assert bails == 0, bails
@@ -105,7 +107,7 @@ def test_flat_variants(variant):
     else:
         msgs = [('{"I32Field":%d,"I32Field":%d,"StringField":"a","StringField":"bc"}' % (k, -k)).encode()
                 for k in range(1000)]
-    for extra in (FLAT, 0):
+    for extra in (FLAT, 0, NO_FLAT):
         bad = _compare(fl, msgs, flags | extra)
         assert not bad, (extra, bad[:4])
 
@@ -122,6 +124,6 @@ def test_flat_edges():
             b'{"req":1,"b":true,"b":false}', b'{"\\u0072eq":1}', b'{"req":1,"Str":"\xff\xfe"}',
             b'{"req" : 1 , "far" : 2.5 }', b'{"req":1,"far":-0.0,"s16":32767}']
     for flags in (0x1, 0x0, 0x7, 0x23, 0x5):
-        for extra in (FLAT, 0):
+        for extra in (FLAT, 0, NO_FLAT):
             bad = _compare(fl, msgs, flags | extra)
             assert not bad, (hex(flags), extra, bad[:4])

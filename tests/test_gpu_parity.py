@@ -280,24 +280,32 @@ def _lean_decline_msgs(rng):
     return simple, nest
 
 
+NO_FLAT = 1 << 21  # DG_F_NO_FLAT_PATH: the small kernel even for flat roots
+
+
+@pytest.mark.parametrize("route", [0, NO_FLAT])
 @pytest.mark.parametrize("flags", [1, 1 | 2, 1 | 32, 1 | 128, 1 | 2 | 32 | 128, 0])
-def test_small_kernel_declines_vs_oracle(flags):
+def test_small_kernel_declines_vs_oracle(flags, route):
     """The small kernel leaves unknown-field skips, numeric map keys and
     default writes to the list pass (full fast path, then the exact machine):
-    the hybrid route must still be bit-exact with the oracle on them."""
+    the hybrid route must still be bit-exact with the oracle on them (route 0:
+    Simple takes the flat kernel, NO_FLAT: the small kernel)."""
     simple, nest = _lean_decline_msgs(random.Random(7 + flags))
     chk = _checker()
     for fl, msgs in ((T.flatten(W.simple_desc()), simple), (T.flatten(W.nesting_desc()), nest)):
         assert max(len(m) for m in msgs) <= 512
-        outs, rets = _raw_batch(fl, msgs, flags)
+        outs, rets = _raw_batch(fl, msgs, flags | route)
         for m, o, r in zip(msgs, outs, rets):
             assert (int(r), o) == chk.j2t(fl, m, flags), m[:200]
 
 
-def test_small_kernel_wave_staging_vs_oracle():
+@pytest.mark.parametrize("route", [0, NO_FLAT])
+def test_small_kernel_wave_staging_vs_oracle(route):
     """Blocks whose JSON span does not fit the stage (large messages between
     small ones) stage per wave; waves whose small messages still do not fit
-    read global memory. Both must be bit-exact with the oracle."""
+    read global memory. Both must be bit-exact with the oracle. (Route 0: the
+    flat kernel stages per message and lists 257-512 B messages for the wave
+    kernel.)"""
     rng = random.Random(11)
     fl = T.flatten(W.simple_desc())
     msgs = []
@@ -311,7 +319,7 @@ def test_small_kernel_wave_staging_vs_oracle():
             else:
                 msgs.append(W.simple_obj(rng).encode())
     chk = _checker()
-    outs, rets = _raw_batch(fl, msgs, 1)
+    outs, rets = _raw_batch(fl, msgs, 1 | route)
     for m, o, r in zip(msgs, outs, rets):
         assert (int(r), o) == chk.j2t(fl, m, 1), m[:120]
 

@@ -1,5 +1,5 @@
-"""Phase breakdown of the flat kernel (a -DDG_FLPROF build, tools/build_variants.py flprof=-DDG_FL_PROF...):
-on the GPU: DG_LIB_PATH=dynamicgo_amd/libdgj2t_flprof.so DG_ALLOW_STALE=1 python tools/flprof.py c2"""
+"""Per-field-slot parse/write cycles of the flat kernel (a -DDG_FLPROF2 build of j2t_kern_flat.hip):
+on the GPU: DG_FLAT=1 DG_LIB_PATH=dynamicgo_amd/libdgj2t_flprof2.so DG_ALLOW_STALE=1 python tools/flprof2.py c2"""
 import ctypes as C
 import os
 import random
@@ -39,12 +39,9 @@ _lib.check(L.dg_ctx_counters(ctx.h, cnt, 16, 1))
 reps = 5
 _lib.check(L.dg_bench_device(*args, reps, C.byref(ms)))
 _lib.check(L.dg_ctx_counters(ctx.h, cnt, 16, 1))
-c = list(cnt)[2:10]
-names = ["stage+desc+barrier", "structure", "barrier 1", "parse", "barrier 2", "prefix+write", "tail",
-         "barrier 4"]
-waves = n // 8 // 32  # 8 waves per 64-message block; 1 block in 32 sampled
-tot = sum(c)
-print(f"{cfg}: {ms.value / reps * 1000:.1f} us/step (instrumented), ok={(d_ret.cpu().numpy() == 0).sum()}")
-for k, nm in enumerate(names):
-    print("  %-20s %6.2f%%  %9.0f cycles/wave" % (nm, 100 * c[k] / max(1, tot), c[k] / reps / waves))
-print("  total %.0f cycles/wave" % (tot / reps / waves))
+c = list(cnt)
+blocks = (n + 63) // 64 // 32 + 0.0  # 1 block in 32 sampled
+print(f"{cfg}: {ms.value / reps * 1000:.1f} us/step (instrumented)")
+for w in range(8):
+    print("  slot %d  parse %8.0f cycles/wave   write %8.0f" % (w, c[2 + w] / reps / blocks,
+                                                             (c[10 + w] / reps / blocks) if w < 6 else 0))

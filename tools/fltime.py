@@ -1,5 +1,5 @@
-"""Phase breakdown of the flat kernel (a -DDG_FLPROF build, tools/build_variants.py flprof=-DDG_FL_PROF...):
-on the GPU: DG_LIB_PATH=dynamicgo_amd/libdgj2t_flprof.so DG_ALLOW_STALE=1 python tools/flprof.py c2"""
+"""Time the flat path (DG_FLAT=1) of whatever library DG_LIB_PATH names on C2, no checks
+(for ablation builds that stop early): python tools/fltime.py [c2|c2s]"""
 import ctypes as C
 import os
 import random
@@ -31,20 +31,11 @@ d_ol = torch.zeros(n, dtype=torch.int32, device=dev)
 d_ret = torch.zeros(n, dtype=torch.int64, device=dev)
 L = _lib.lib()
 ms = C.c_float(0)
-cnt = (C.c_uint64 * 16)()
 args = (ctx.h, dh, flat.root_type, d_json.data_ptr(), d_in.data_ptr(), n, 1, d_out.data_ptr(), d_oo.data_ptr(),
         d_ol.data_ptr(), d_ret.data_ptr())
-_lib.check(L.dg_bench_device(*args, 1, C.byref(ms)))
-_lib.check(L.dg_ctx_counters(ctx.h, cnt, 16, 1))
-reps = 5
-_lib.check(L.dg_bench_device(*args, reps, C.byref(ms)))
-_lib.check(L.dg_ctx_counters(ctx.h, cnt, 16, 1))
-c = list(cnt)[2:10]
-names = ["stage+desc+barrier", "structure", "barrier 1", "parse", "barrier 2", "prefix+write", "tail",
-         "barrier 4"]
-waves = n // 8 // 32  # 8 waves per 64-message block; 1 block in 32 sampled
-tot = sum(c)
-print(f"{cfg}: {ms.value / reps * 1000:.1f} us/step (instrumented), ok={(d_ret.cpu().numpy() == 0).sum()}")
-for k, nm in enumerate(names):
-    print("  %-20s %6.2f%%  %9.0f cycles/wave" % (nm, 100 * c[k] / max(1, tot), c[k] / reps / waves))
-print("  total %.0f cycles/wave" % (tot / reps / waves))
+_lib.check(L.dg_bench_device(*args, 3, C.byref(ms)))
+best = 1e9
+for _ in range(5):
+    _lib.check(L.dg_bench_device(*args, 20, C.byref(ms)))
+    best = min(best, ms.value / 20)
+print(f"{os.environ.get('DG_LIB_PATH', 'libdgj2t.so')} {cfg}: {best * 1000:.1f} us/step ok={(d_ret.cpu().numpy() == 0).sum()}")
