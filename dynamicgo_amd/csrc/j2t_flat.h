@@ -400,6 +400,7 @@ DGI bool body_b64(S &src, uint32_t s0, uint32_t n, bool last, O &o)
     if (last && n >= 4) {
         uint32_t w = (uint32_t)src.get8((SI)(s0 + ip));
         const uint32_t c2 = (w >> 16) & 0xFF, c3 = w >> 24;
+        if (c2 == '=' && c3 != '=') return false; /* "xx=y": a decode error in the reference */
         const uint32_t keep = c3 == '=' ? (c2 == '=' ? 1u : 2u) : 3u;
         if (c3 == '=') w = (w & 0x00FFFFFFu) | ((uint32_t)'A' << 24);
         if (c2 == '=') w = (w & 0xFF00FFFFu) | ((uint32_t)'A' << 16);

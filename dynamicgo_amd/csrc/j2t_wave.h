@@ -73,7 +73,6 @@ constexpr uint32_t WV_NOEND = 0xFFFFFFFFu;     /* string not closed (yet) */
 constexpr uint32_t WV_POSMASK = (1u << 29) - 1;
 constexpr uint32_t WV_MSG = DG_WV_MSG;         /* messages up to this (minus 16) are staged in LDS */
 constexpr uint32_t WV_DESC = 16384;            /* the wave path needs the descriptor in LDS (dynamic, sized to it) */
-constexpr uint32_t WV_LONG = 192;              /* strings longer than this are copied/decoded by the whole wave */
 constexpr uint32_t WV_BLOCKS_PER_CU = DG_WV_BPC; /* persistent grid: blocks of 4 waves per CU */
 constexpr uint32_t WV_MIN_DEFAULT = 512;       /* messages longer than this go to the wave kernel (DG_WAVE_MIN) */
 constexpr uint32_t WV_REQMASKS = 64;           /* per-struct REQUIRED-field masks kept in LDS */
@@ -105,8 +104,18 @@ struct WaveLds {
     uint32_t tpos[WV_RING]; /* kind << 29 | position */
     uint32_t tend[WV_RING]; /* string: closing quote position; scalar: one past its last byte */
     uint32_t trec[WV_RING]; /* key: field index / TR_* */
+    uint8_t tbs[WV_RING];   /* string: a backslash inside (set by the scan) */
     CRec crec[64 + WV_MAXD + 1];
+    /* the page's string / base64 bodies as chunk tasks, per token lane */
+    uint32_t cinc[64];      /* inclusive prefix of chunk counts */
+    uint32_t cbs[64];       /* body source position */
+    uint32_t cbd[64];       /* body output offset in the slot */
+    uint32_t cbn[64];       /* body length | base64 << 31 */
 };
+#ifndef DG_WV_CH
+#define DG_WV_CH 32
+#endif
+constexpr uint32_t WV_CH = DG_WV_CH; /* input bytes per body chunk task (a multiple of 8) */
 
 struct WaveParams {
     const uint8_t *blob; /* descriptor blob (device) */
@@ -258,19 +267,6 @@ DGI uint32_t num_size(uint8_t tt)
     return 0;
 }
 
-/* any '\\' in src[s0, s0+n) */
-template <class S>
-DGI bool has_bslash(S &src, int64_t s0, int64_t n)
-{
-    for (int64_t i = 0; i < n; i += 8) {
-        uint64_t m = eqbytes(src.get8(s0 + i), 0x5C);
-        int64_t rem = n - i;
-        if (rem < 8) m &= (1ull << (rem << 3)) - 1;
-        if (m) return true;
-    }
-    return false;
-}
-
 /* decoded length of a standard-padded base64 body of nb chars (nb % 4 == 0),
  * or -1 for a shape the wave path leaves to the exact machine */
 template <class S>
@@ -283,43 +279,6 @@ DGI int64_t b64_len(S &src, int64_t s0, int64_t nb)
     return nb / 4 * 3 - pad;
 }
 
-/* b64decode (native/base64.c:659-817, mode 0) of a body of nb chars whose
- * length b64_len accepted: 8 chars -> 6 bytes per step (b64_8), then whole
- * quanta; a final quantum "xx==" / "xxx=" keeps the top 1 / 2 bytes like
- * decode_block (native/base64.c:600-631). false = anything else (\r, \n,
- * '=' inside, characters outside the alphabet): left to the exact machine. */
-template <class S, class O>
-DGI bool b64_decode_wave(S &src, int64_t s0, int64_t nb, O &out)
-{
-    int64_t ip = 0;
-    uint64_t o;
-    while (ip + 8 <= nb && b64_8(src.get8(s0 + ip), o)) {
-        out.wle(o, 6);
-        ip += 8;
-    }
-    while (ip < nb) {
-        int a = b64v(src.raw(s0 + ip)), b = b64v(src.raw(s0 + ip + 1));
-        uint8_t c2 = src.raw(s0 + ip + 2), c3 = src.raw(s0 + ip + 3);
-        int c = b64v(c2), d = b64v(c3);
-        bool last = ip + 4 == nb;
-        if (a < 0 || b < 0) return false;
-        uint32_t v = ((uint32_t)a << 18) | ((uint32_t)b << 12);
-        uint32_t keep = 3;
-        if (c >= 0 && d >= 0) {
-            v |= ((uint32_t)c << 6) | (uint32_t)d;
-        } else if (last && c >= 0 && c3 == '=') {
-            v |= (uint32_t)c << 6;
-            keep = 2;
-        } else if (last && c2 == '=' && c3 == '=') {
-            keep = 1;
-        } else {
-            return false;
-        }
-        out.wle(((v >> 16) & 0xff) | (((v >> 8) & 0xff) << 8) | ((uint64_t)(v & 0xff) << 16), keep);
-        ip += 4;
-    }
-    return true;
-}
 
 /* j2t_write_unset_fields (native/thrift.c:258-310) for one struct instance
  * whose remaining requires bits are `bits`: false = ERR_NULL_REQUIRED (bail) */
@@ -400,29 +359,38 @@ DGI void coop_copy(S &src, int64_t s0, int64_t nb, gu8 *dst, uint32_t lane)
     }
 }
 
-/* base64 body src[s0, s0+nb) (nb % 4 == 0) -> dst, by the 64 lanes: 8 chars ->
- * 6 bytes per lane and step, the last 4..8 chars (padding) by lane 0 */
-template <class S>
-DGI bool coop_b64(S &src, int64_t s0, int64_t nb, gu8 *dst, uint32_t want, uint32_t lane)
+
+/* a chunk of a canonical padded base64 body: src[s0, s0+n) (n % 4 == 0);
+ * `last`: the chunk holds the final quantum, "xx==" / "xxx=" keeping 1 / 2
+ * bytes like decode_block (native/base64.c:600-631). false = a character
+ * outside the alphabet or '=' anywhere else: the exact machine reports it. */
+template <class S, class O>
+DGI bool chunk_b64(S &src, int64_t s0, int64_t n, bool last, O &o)
 {
-    const int64_t full = nb >= 8 ? (nb - 4) >> 3 : 0;
-    bool ok = true;
-    for (int64_t g = lane; g < full; g += 64) {
-        uint64_t o;
-        if (!b64_8(src.get8(s0 + 8 * g), o)) ok = false;
-        WOut w;
-        w.init(dst + 6 * g);
-        w.wle(o, 6);
-        w.finish();
+    int64_t ip = 0;
+    const int64_t full = last && n >= 4 ? n - 4 : n;
+    for (; ip + 8 <= full; ip += 8) {
+        uint64_t v;
+        if (!b64_8(src.get8(s0 + ip), v)) return false;
+        o.wle(v, 6);
     }
-    if (lane == 0) {
-        WOut w;
-        w.init(dst + 6 * full);
-        if (!b64_decode_wave(src, s0 + 8 * full, nb - 8 * full, w)) ok = false;
-        w.finish();
-        if (w.len + 6 * (uint64_t)full != want) ok = false;
+    for (; ip < full; ip += 4) {
+        uint32_t v;
+        if (!b64_4((uint32_t)src.get8(s0 + ip), v)) return false;
+        o.wle(v, 3);
     }
-    return ok;
+    if (last && n >= 4) {
+        uint32_t w = (uint32_t)src.get8(s0 + ip);
+        const uint32_t c2 = (w >> 16) & 0xFF, c3 = w >> 24;
+        if (c2 == '=' && c3 != '=') return false;
+        const uint32_t keep = c3 == '=' ? (c2 == '=' ? 1u : 2u) : 3u;
+        if (c3 == '=') w = (w & 0x00FFFFFFu) | ((uint32_t)'A' << 24);
+        if (c2 == '=') w = (w & 0xFF00FFFFu) | ((uint32_t)'A' << 16);
+        uint32_t v;
+        if (!b64_4(w, v)) return false;
+        o.wle(v, keep);
+    }
+    return true;
 }
 
 /* the exact number parser, out of line (rare: keeps the kernel small) */
@@ -520,7 +488,20 @@ DGI void scan_chunk(uint32_t x, int64_t head, int64_t len, uint32_t chunk, ScanS
             uint32_t kind = ((stm >> j) & 1) ? (knib >> (3 * j)) & 7 : ((openq >> j) & 1) ? K_STRING : K_SCALAR;
             L.tpos[k & WV_RMASK] = (kind << 29) | (uint32_t)(p0 + j);
             L.tend[k & WV_RMASK] = WV_NOEND;
+            L.tbs[k & WV_RMASK] = 0;
             k++;
+        }
+    }
+    /* backslashes inside a string mark the open string: the last token
+     * started before them (after every token write of the chunk) */
+    const uint32_t bsi = bs & instr;
+    if (bsi) {
+#pragma unroll
+        for (uint32_t j = 0; j < 4; j++) {
+            if ((bsi >> j) & 1) {
+                uint32_t kb = st.produced + pre + (uint32_t)__builtin_popcount(tok & ((1u << j) - 1));
+                L.tbs[(kb - 1) & WV_RMASK] = 1;
+            }
         }
     }
     /* terminators, after every token write of the chunk: the token a
@@ -648,7 +629,7 @@ DGI bool wave_run(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L
         bool kesc = false;
         if (alive && keyish) {
             const int64_t k0 = pos + 1, kl = te - k0;
-            kesc = has_bslash(src, k0, kl);
+            kesc = L.tbs[t & WV_RMASK] != 0;
             for (int64_t j = 0; j < kl; j += 8) {
                 uint64_t w = src.get8(k0 + j);
                 const int64_t r = kl - j < 8 ? kl - j : 8;
@@ -781,7 +762,7 @@ DGI bool wave_run(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L
                 cs = pos + 1;
                 cn = te - cs;
                 tt = ldrec(&D.T[ldrec(&D.T[pt]).key]).ttype;
-                esc = has_bslash(src, cs, cn);
+                esc = L.tbs[t & WV_RMASK] != 0;
                 if (esc) bad = true;
                 if (tt == DG_T_STRING) {
                     hv = __builtin_bswap32((uint32_t)cn);
@@ -805,7 +786,7 @@ DGI bool wave_run(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L
                 cn = te - cs;
                 if (tt != DG_T_STRING) bad = true;
                 isbin = (flag & DG_F_NO_BASE64) == 0 && (vt.flags & DG_TF_BINARY);
-                if (!isbin) esc = has_bslash(src, cs, cn);
+                if (!isbin) esc = L.tbs[t & WV_RMASK] != 0; /* a backslash inside (the scan marked it) */
                 hn = 4;
             } else if (kind == K_LBRACE) {
                 if (L.crec[lane].flags & CF_MAP) {
@@ -925,19 +906,19 @@ DGI bool wave_run(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L
         if (O + tot > cap) return false; /* slot overflow: the exact machine reports it */
         if (alive && op) L.crec[lane].outpos = (uint32_t)opos;
 
-        /* emit: header, then the body, through one writer per lane */
+        /* emit: header, then the body, through one writer per lane; bodies
+         * without escapes (copies) and base64 bodies go to chunk tasks below */
         bool deferred = false;
+        const bool live = alive && !skip && !isnull;
+        const bool chunked = live && cn > 0 && isval && (isbin || !esc);
         {
             WOut w;
             w.init(ob + opos);
-            const bool live = alive && !skip && !isnull;
             if (live && cl && hn == 1 && reqs) unset_fields(D, csd, reqs, flag, w); /* before the STOP */
             if (live && hn) w.wle(hv, hn);
             if (live && ns >= 0 && hn == 0) emit_number(w, tt, isint, iv, dv);
-            if (live && cn > (int64_t)WV_LONG && isval && (isbin || !esc)) deferred = true; /* whole wave, below */
-            else if (live && isbin) {
-                if (!b64_decode_wave(src, cs, cn, w)) bad = true;
-            } else if (live && esc && isval) {
+            if (chunked) deferred = true; /* chunk tasks, below */
+            else if (live && esc && isval) {
                 fast_unquote(src, cs, cn, w);
             } else if (live && cn > 0) {
                 fast_copy(src, cs, cn, w);
@@ -951,19 +932,39 @@ DGI bool wave_run(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L
                 put_be32(ob + L.crec[ci].outpos + ((pf & CF_MAP) ? 2 : 1), L.crec[ci].count);
         }
         WP(6);
-        /* long strings: one at a time, by all 64 lanes */
-        for (uint64_t dm = ballot(deferred); dm; dm &= dm - 1) {
-            const int l = (int)__builtin_ctzll(dm);
-            const int64_t s0 = (int64_t)__builtin_amdgcn_readlane((int)pos, l) + 1;
-            const int64_t nb = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)te, l) - s0;
-            const uint64_t d0 = (((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(opos >> 32), l)) << 32) |
-                                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)opos, l);
-            const uint32_t want = (uint32_t)__builtin_amdgcn_readlane((int)ln, l) - 4;
-            gu8 *dst = ob + d0 + 4;
-            if (__builtin_amdgcn_readlane((int)isbin, l)) {
-                if (!coop_b64(src, s0, nb, dst, want, lane)) bad = true;
-            } else {
-                coop_copy(src, s0, nb, dst, lane);
+        /* string / base64 bodies: WV_CH-byte chunk tasks over the 64 lanes
+         * (task c belongs to the first lane whose inclusive chunk count
+         * exceeds c), so the page's longest string no longer sets the time */
+        {
+            const uint32_t nch = deferred ? (uint32_t)((cn + WV_CH - 1) / WV_CH) : 0u;
+            const uint32_t cinc = wave_incl_sum(nch, lane);
+            const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)cinc, 63);
+            if (T) {
+                L.cinc[lane] = cinc;
+                L.cbs[lane] = (uint32_t)cs;
+                L.cbd[lane] = (uint32_t)(opos + 4);
+                L.cbn[lane] = (uint32_t)cn | (isbin ? 0x80000000u : 0u);
+                __builtin_amdgcn_wave_barrier();
+                for (uint32_t c = lane; c < T; c += 64) {
+                    uint32_t l = 0;
+#pragma unroll
+                    for (uint32_t step = 32; step; step >>= 1)
+                        if (L.cinc[l + step - 1] <= c) l += step;
+                    const uint32_t bn = L.cbn[l], blen = bn & 0x7FFFFFFFu;
+                    const uint32_t lch = (blen + WV_CH - 1) / WV_CH;
+                    const uint32_t k = c - (L.cinc[l] - lch);
+                    const int64_t s0 = (int64_t)L.cbs[l] + (int64_t)k * WV_CH;
+                    const int64_t n = (int64_t)min(WV_CH, blen - k * WV_CH);
+                    WOut w;
+                    if (bn >> 31) {
+                        w.init(ob + L.cbd[l] + (uint64_t)k * (WV_CH / 4 * 3));
+                        if (!chunk_b64(src, s0, n, k + 1 == lch, w)) bad = true;
+                    } else {
+                        w.init(ob + L.cbd[l] + (uint64_t)k * WV_CH);
+                        fast_copy(src, s0, n, w);
+                    }
+                    w.finish();
+                }
             }
         }
         if (ballot(bad)) return false;

@@ -122,7 +122,11 @@ def test_flat_edges():
             b'{"req":2147483648}', b'{"req":1,"y":128}', b'{"req":1,"d":1e400}', b'{"req":1,"s64":"5"}',
             b'{"req":1,"bin":"QQ=="}', b'{"req":1,"bin":"QR=="}', b'{"req":1,"bin":"Q==="}', b'{"req":1,"bin":"QQ"}',
             b'{"req":1,"b":true,"b":false}', b'{"\\u0072eq":1}', b'{"req":1,"Str":"\xff\xfe"}',
-            b'{"req" : 1 , "far" : 2.5 }', b'{"req":1,"far":-0.0,"s16":32767}']
+            b'{"req" : 1 , "far" : 2.5 }', b'{"req":1,"far":-0.0,"s16":32767}',
+            b'{"req":1,"bin":"QQ=A"}', b'{"req":1,"bin":"Q=A="}', b'{"req":1,"bin":"QUJDRA=A"}',
+            b'{"req":1,"bin":"QUJDREVGR0hJSktMTU5PUFFSU1RVVldYWVo=A"}',
+            b'{"req":1,"bin":"QUJDREVGR0hJSktMTU5PUFFSU1RVVldYWVpbXF1eX2BhYmNkZWZnaA=="}',
+            b'{"req":1,"Str":"0123456789abcdefghijklmnopqrstuvwxyz0123456789abcdefghij"}']
     for flags in (0x1, 0x0, 0x7, 0x23, 0x5):
         for extra in (FLAT, 0, NO_FLAT):
             bad = _compare(fl, msgs, flags | extra)

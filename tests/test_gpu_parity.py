@@ -2,6 +2,7 @@
 generated golden vectors and the oracle, bit-exact (integer/byte work: Thrift
 bytes and packed status words must be identical)."""
 import random
+import zlib
 
 import numpy as np
 import pytest
@@ -79,7 +80,10 @@ def test_fuzz_vs_oracle(which):
           "null": lambda: idl_desc("null.thrift", "NullTest")}[which]()
     fl = T.flatten(td)
     chk = _checker()
-    rng = random.Random(hash(which) & 0xffff)
+    # a fixed seed per schema (str hash() is salted per process); see
+    # tests/test_oracle.py::test_unterminated_string_block_tail for the one
+    # malformed-input class where the reference's verdict is undefined
+    rng = random.Random(zlib.crc32(which.encode()) & 0xffff)
     for flags in (0x1, 0x0, 0x11, 0x5, 0x23, 0x83, 0x41, 0x100, 0x201, NO_FAST | 0x1, NO_FAST | 0x83,
                   NO_WAVE | 0x1, NO_WAVE | 0x83):
         msgs = [fuzz.gen_message(rng, td, mutate_p=rng.random() < 0.5) for _ in range(300)]

@@ -50,6 +50,10 @@ def _must_wave_cases():
     cases.append(b'{"BinaryField":"QQ=="}')
     cases.append(b'{"BinaryField":"QUI="}')
     cases.append(b'{"BinaryField":""}')
+    for n in (28, 32, 36, 60, 64, 68, 92, 96, 100):                           # base64 chunk-task boundaries
+        cases.append(b'{"ByteField":2,"BinaryField":"' + (b"QUJD" * 40)[:n - 4] + b'QQ==","I32Field":1}')
+    for n in (7, 8, 9, 31, 32, 33, 63, 64, 65, 100):                          # copy chunk-task boundaries
+        cases.append(b'{"StringField":"' + bytes(97 + (i % 26) for i in range(n)) + b'","ByteField":4}')
     cases.append(b'{"DoubleField":-0,"I64Field":-9223372036854775808,"I32Field":1.9,"ByteField":-129}')
     cases.append(b'{"DoubleField":1e22,"I64Field":123456789012345678,"I32Field":2147483648}')
     cases.append(b'{"DoubleField":0.1e-5,"I64Field":99999999999999999999}')   # overflow -> double -> cvt
@@ -81,6 +85,7 @@ def _may_bail_cases():
         b'{"ByteField":1} trailing "junk',
         b'{"ByteField":01}', b'{"ByteField":1,}', b'{"ByteField" 1}', b'{"ByteField":tru}', b'{"ByteField":[1]}',
         b'{"StringField":"abc', b'{"BinaryField":"QQ"}', b'{"BinaryField":"Q\\nQ=="}', b'{"DoubleField":1e400}',
+        b'{"BinaryField":"QQ=A"}', b'{"BinaryField":"' + b"QUJD" * 20 + b'QQ=A"}',   # '=' then a letter: decode error
         b'{"StringField":"\\ud800"}', b'{"StringField":"\\x"}', b"[1]", b"", b"null", b"  {}  ", b"{",
         b'{"ByteField":1]', b'{"a":[1,2}', b'{"ByteField":1e2}', b'{"I32Field":"12"}',
     ]

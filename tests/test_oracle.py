@@ -103,3 +103,23 @@ def test_utf8_validation_extension(body, bad):
         assert r1 == (_pack(2, body[bad], len(pre) + bad), b"")
     # binary fields are base64 text, not validated
     assert chk.j2t(fl, b'{"BinaryField":"\xff"}', 1 | UTF8_FLAG) == chk.j2t(fl, b'{"BinaryField":"\xff"}', 1)
+
+
+def test_unterminated_string_block_tail():
+    """The one malformed-input class where the reference's verdict is
+    undefined: an unterminated string whose bytes after the opening quote end
+    exactly at a SIMD block boundary. advance_string (native/scanning.c:130-375)
+    then skips its scalar tail loop and tests `if (ch == '"')` on an
+    uninitialised `ch` (declared at :132, only assigned inside the loop at
+    :342). The restatement (and the GPU) report ERR_EOF at the end, as for
+    every other unterminated string; whatever the compiled reference returns
+    there depends on a stale register. Any other tail length agrees."""
+    ref = oracle.RefOracle()
+    port = oracle.PortOracle()
+    fl = T.flatten(probe("D3"))
+    for k in range(1, 70):
+        m = b'{"x":1,"y":"' + b"a" * k
+        r, _ = port.j2t(fl, m, 1)
+        assert r & 0xFF == 1 and (r >> 8) & 0xFFFFFFFF == len(m), (k, hex(r))  # ERR_EOF at len
+        if ref is not None and k % 32:
+            assert ref.j2t(fl, m, 1)[0] == r, k
