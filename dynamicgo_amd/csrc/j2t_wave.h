@@ -113,7 +113,7 @@ struct WaveLds {
     uint32_t cbn[64];       /* body length | base64 << 31 */
 };
 #ifndef DG_WV_CH
-#define DG_WV_CH 32
+#define DG_WV_CH 8
 #endif
 constexpr uint32_t WV_CH = DG_WV_CH; /* input bytes per body chunk task (a multiple of 8) */
 
