@@ -393,6 +393,44 @@ DGI bool chunk_b64(S &src, int64_t s0, int64_t n, bool last, O &o)
     return true;
 }
 
+/* A number token's bytes held in registers: the 5 aligned words covering
+ * [p, p + 32) of the message, loaded together (one wait) instead of the
+ * dependent word-at-a-time loads of the parse loops. Tokens up to RS_MAX
+ * bytes use it; longer ones take the exact parser. */
+constexpr int64_t RS_MAX = 24;
+struct RSrc {
+    typedef int64_t idx;
+    uint64_t w0, w1, w2, w3, w4;
+    uint32_t sh; /* byte offset of the token's first byte in w0 */
+    int64_t n;
+    template <class S>
+    DGI void load(const S &src, int64_t p, int64_t len)
+    {
+        const int64_t b = src.off0 + p;
+        const uint64_t *q = src.w8 + (b >> 3);
+        sh = (uint32_t)(b & 7);
+        n = len;
+        const uint32_t need = (sh + (uint32_t)len + 8 + 7) >> 3; /* words up to get8(n) */
+        w0 = q[0];
+        w1 = need > 1 ? q[1] : 0;
+        w2 = need > 2 ? q[2] : 0;
+        w3 = need > 3 ? q[3] : 0;
+        w4 = need > 4 ? q[4] : 0;
+    }
+    DGI uint64_t word(uint32_t j) const { return j == 0 ? w0 : j == 1 ? w1 : j == 2 ? w2 : j == 3 ? w3 : w4; }
+    DGI uint8_t raw(int64_t i) const
+    {
+        const uint32_t b = sh + (uint32_t)i;
+        return (uint8_t)(word(b >> 3) >> ((b & 7) << 3));
+    }
+    DGI uint8_t at(int64_t i) const { return (uint64_t)i < (uint64_t)n ? raw(i) : 0; }
+    DGI uint64_t get8(int64_t i) const
+    {
+        const uint32_t b = sh + (uint32_t)i, j = b >> 3, s8 = (b & 7) << 3;
+        return (word(j) >> s8) | ((word(j + 1) << 1) << (63 - s8));
+    }
+};
+
 /* the exact number parser, out of line (rare: keeps the kernel small) */
 __device__ __noinline__ void vnumber_slow(SrcT<const uint64_t> src, int64_t &p, JState &js, gu8 *dbuf)
 {
@@ -822,10 +860,20 @@ DGI bool wave_run(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L
                     hn = 1;
                 }
             } else {
-                S ks = src.sub(ns, nn);
                 int64_t q = 0;
-                if (!fast_vnumber(ks, q, tb, iv, dv, isint)) slow = true;
-                else if (whole && q != nn) bad = true;
+#if defined(DG_WV_ABL) && (DG_WV_ABL & 16)
+                q = nn; iv = nn; isint = true; /* ablation: no number parse */
+                if (0) slow = true;
+#else
+                if (nn > RS_MAX) {
+                    slow = true; /* long numbers (big decimals, long map keys): the exact parser */
+                } else {
+                    RSrc ks;
+                    ks.load(src, ns, nn);
+                    if (!fast_vnumber(ks, q, tb, iv, dv, isint)) slow = true;
+                    else if (whole && q != nn) bad = true;
+                }
+#endif
                 if (!skip && !num_size(tt)) bad = true;
             }
         }
@@ -915,6 +963,9 @@ DGI bool wave_run(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L
             WOut w;
             w.init(ob + opos);
             if (live && cl && hn == 1 && reqs) unset_fields(D, csd, reqs, flag, w); /* before the STOP */
+#if defined(DG_WV_ABL) && (DG_WV_ABL & 4)
+            w.dry = true; /* ablation: no header/number stores */
+#endif
             if (live && hn) w.wle(hv, hn);
             if (live && ns >= 0 && hn == 0) emit_number(w, tt, isint, iv, dv);
             if (chunked) deferred = true; /* chunk tasks, below */
@@ -945,7 +996,11 @@ DGI bool wave_run(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L
                 L.cbd[lane] = (uint32_t)(opos + 4);
                 L.cbn[lane] = (uint32_t)cn | (isbin ? 0x80000000u : 0u);
                 __builtin_amdgcn_wave_barrier();
+#if defined(DG_WV_ABL) && (DG_WV_ABL & 8)
+                for (uint32_t c = lane; c < 0; c += 64) { /* ablation: no body tasks */
+#else
                 for (uint32_t c = lane; c < T; c += 64) {
+#endif
                     uint32_t l = 0;
 #pragma unroll
                     for (uint32_t step = 32; step; step >>= 1)
