@@ -39,7 +39,7 @@ namespace dg {
 constexpr uint32_t FL_G = 8;                     /* lanes per message in the structure phase */
 constexpr uint32_t FL_WAVES = 8;                 /* waves per block = field slots per round */
 constexpr uint32_t FL_MPB = 64;                  /* messages per block (= lanes of a wave in phase 2) */
-constexpr uint32_t FL_LW = 5;                    /* aligned words per structure lane: 8 x 40 B >= 256 + 7 */
+constexpr uint32_t FL_LW = 5;                    /* aligned words a structure lane may read: 4 + word 32 (lane 7) */
 constexpr uint32_t FL_MAXLEN = 256;              /* longest message on this kernel */
 constexpr uint32_t FL_SLOTW = FL_MAXLEN / 8;     /* words per message when the block's span is not staged */
 constexpr uint32_t FL_STAGEW = FL_MPB * FL_SLOTW;/* 16 KiB */
@@ -645,16 +645,16 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
     const dg_struct sd = ldrec(&D.S[rt.st]);
 
     /* ---- 1. structure: lane g of a message classifies the aligned words
-     *      [5g, 5g+5) of it (bit b of a lane = message byte 40g + b - a7) ---- */
+     *      [4g, 4g+4) of it, lane 7 also word 32 when the message reaches it
+     *      (bit b of a lane = message byte 32g + b - a7) ---- */
     {
         const bool on = L.ok[m1] != 0;
         const uint32_t n = L.n[m1], lwa = L.lw[m1], a7 = lwa & 7, lw = lwa >> 3;
-        const uint32_t nwords = on ? (a7 + n + 7) >> 3 : 0; /* aligned words of the message */
-        uint32_t q80[2 * FL_LW], ck[2 * FL_LW];            /* per 32-bit half: quotes; commas | colons >> 1 */
-        uint32_t nq = 0, anybs = 0;
-#pragma unroll
-        for (uint32_t j = 0; j < FL_LW; j++) {
-            const uint32_t wi = FL_LW * g + j;
+        const uint32_t nwords = on ? (a7 + n + 7) >> 3 : 0; /* aligned words of the message (<= 33) */
+        /* word 32 (messages of 250-256 B): a wave-uniform extra step */
+        const bool x5 = __builtin_amdgcn_ballot_w64(g == 7 && nwords > 32) != 0;
+        auto word = [&](uint32_t j) -> uint64_t {
+            const uint32_t wi = j < 4 ? 4 * g + j : (g == 7 ? 32u : 0xFFFFu);
             uint64_t w = 0;
             if (wi < nwords) {
                 w = L.in[lw + wi];
@@ -662,6 +662,12 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
                 if (wb < 0) w &= ~0ull << ((uint32_t)(-wb) << 3);
                 if (wb + 8 > (int32_t)n) w &= (1ull << ((uint32_t)((int32_t)n - wb) << 3)) - 1;
             }
+            return w;
+        };
+        uint32_t q80[10], ck[10]; /* per 32-bit half: quotes; commas | colons >> 1 */
+        uint32_t nq = 0, anybs = 0;
+        auto classify = [&](uint32_t j) {
+            const uint64_t w = word(j);
 #pragma unroll
             for (uint32_t h = 0; h < 2; h++) {
                 const uint32_t x = (uint32_t)(w >> (32 * h));
@@ -670,12 +676,15 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
                 anybs |= eq32(x, 0x5C5C5C5Cu);
                 nq += (uint32_t)__builtin_popcount(q80[2 * j + h]);
             }
-        }
+        };
+#pragma unroll
+        for (uint32_t j = 0; j < 4; j++) classify(j);
+        q80[8] = q80[9] = ck[8] = ck[9] = 0;
+        if (x5) classify(4);
         /* quote parity: prefix XOR of the quote bytes, carried across halves and the group */
         const uint32_t qx = g8_incl_sum(nq, g) - nq;
         uint32_t carry = qx & 1, nc = 0, nk = 0;
-#pragma unroll
-        for (uint32_t h = 0; h < 2 * FL_LW; h++) {
+        auto parity = [&](uint32_t h) {
             uint32_t x = q80[h] >> 7;
             x ^= x << 8;
             x ^= x << 16;
@@ -684,6 +693,12 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
             ck[h] &= ~ins;
             nc += (uint32_t)__builtin_popcount(ck[h] & 0x80808080u);
             nk += (uint32_t)__builtin_popcount(ck[h] & 0x40404040u);
+        };
+#pragma unroll
+        for (uint32_t h = 0; h < 8; h++) parity(h);
+        if (x5) {
+            parity(8);
+            parity(9);
         }
         const uint32_t pk = nc | (nk << 10) | (nq << 20);
         const uint32_t pin = g8_incl_sum(pk, g);
@@ -693,32 +708,25 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
         if (hasbs) {
             /* a backslash before '"' or '\\' (an escaped quote or backslash) -> decline,
              * so every quote is a delimiter */
-            uint64_t bw[FL_LW], qw[FL_LW];
+            uint64_t bw[5], qw[5];
 #pragma unroll
-            for (uint32_t j = 0; j < FL_LW; j++) {
-                const uint32_t wi = FL_LW * g + j;
-                uint64_t w = 0;
-                if (wi < nwords) {
-                    w = L.in[lw + wi];
-                    const int32_t wb = (int32_t)(wi * 8) - (int32_t)a7;
-                    if (wb < 0) w &= ~0ull << ((uint32_t)(-wb) << 3);
-                    if (wb + 8 > (int32_t)n) w &= (1ull << ((uint32_t)((int32_t)n - wb) << 3)) - 1;
-                }
+            for (uint32_t j = 0; j < 5; j++) {
+                const uint64_t w = word(j);
                 bw[j] = eqbytes(w, '\\');
                 qw[j] = bw[j] | eqbytes(w, '"');
             }
             const uint32_t nxt = g8_next((uint32_t)(qw[0] & 0x80), g); /* the next lane's first byte */
             uint64_t bb = 0;
 #pragma unroll
-            for (uint32_t j = 0; j < FL_LW; j++)
-                bb |= bw[j] & ((qw[j] >> 8) | (j + 1 < FL_LW ? qw[j + 1] << 56 : (uint64_t)nxt << 56));
+            for (uint32_t j = 0; j < 4; j++)
+                bb |= bw[j] & ((qw[j] >> 8) | (j < 3 ? qw[j + 1] << 56 : (g == 7 ? qw[4] : (uint64_t)nxt) << 56));
+            bb |= bw[4] & (qw[4] >> 8);
             bad = g8_sum(bb ? 1u : 0u);
         }
         if (on) {
             uint32_t ci = (pin & 0x3FF) - nc, ki = ((pin >> 10) & 0x3FF) - nk, qc = qx;
-#pragma unroll
-            for (uint32_t h = 0; h < 2 * FL_LW; h++) {
-                const uint32_t pos0 = 40 * g + 4 * h - a7; /* message position of the half's byte 0 */
+            auto record = [&](uint32_t h) {
+                const uint32_t pos0 = 32 * g + 4 * h - a7; /* message position of the half's byte 0 */
                 uint32_t c = ck[h] & 0x80808080u, k = ck[h] & 0x40404040u;
                 while (c) {
                     const uint32_t bit = (uint32_t)__builtin_ctz(c);
@@ -735,6 +743,12 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
                     ki++;
                 }
                 qc += (uint32_t)__builtin_popcount(q80[h]);
+            };
+#pragma unroll
+            for (uint32_t h = 0; h < 8; h++) record(h);
+            if (x5) {
+                record(8);
+                record(9);
             }
         }
         if (g == 0 && on) {
