@@ -195,17 +195,23 @@ def e2e_host_path(L, ctx, dh, root, flags, arena, off, dev, flat, chunks: int = 
         lens = np.diff(o)
         slots = np.zeros(b - a + 1, dtype=np.int64)
         np.cumsum((lens * 4 + 64 + 7) & ~7, out=slots[1:])
-        h_json = torch.from_numpy(np.concatenate([arena[lo:hi], np.zeros(64, np.uint8)])).pin_memory()
-        h_in = torch.from_numpy(o).pin_memory()
-        C.append(dict(n=b - a, a=a, b=b, h_json=h_json, h_in=h_in, max_len=int(lens.max()) if b > a else 0,
-                      d_json=torch.empty_like(h_json, device=dev), d_in=torch.empty_like(h_in, device=dev),
+        # one upload per chunk: [offsets (8 (n+1)) | JSON + 64 B pad]; one
+        # download: [ret (8 n) | out_len (4 n, padded to 8) | packed Thrift]
+        m = b - a
+        nj = hi - lo + 64
+        h_up = torch.zeros(8 * (m + 1) + nj, dtype=torch.uint8).pin_memory()
+        h_up[:8 * (m + 1)].view(torch.int64).copy_(torch.from_numpy(o))
+        h_up[8 * (m + 1):8 * (m + 1) + hi - lo].copy_(torch.from_numpy(np.ascontiguousarray(arena[lo:hi])))
+        d_up = torch.empty_like(h_up, device=dev)
+        olw = (4 * m + 7) // 8 * 8
+        d_down = torch.empty(8 * m + olw + int(slots[-1]) + 64, dtype=torch.uint8, device=dev)
+        C.append(dict(n=m, a=a, b=b, h_up=h_up, d_up=d_up, max_len=int(lens.max()) if b > a else 0,
+                      d_in=d_up[:8 * (m + 1)].view(torch.int64), d_json=d_up[8 * (m + 1):],
                       d_out=torch.empty(int(slots[-1]) + 64, dtype=torch.uint8, device=dev),
-                      d_oo=torch.from_numpy(slots).to(dev), d_ol=torch.zeros(b - a, dtype=torch.int32, device=dev),
-                      d_ret=torch.zeros(b - a, dtype=torch.int64, device=dev),
+                      d_oo=torch.from_numpy(slots).to(dev), d_down=d_down,
+                      d_ret=d_down[:8 * m].view(torch.int64), d_ol=d_down[8 * m:8 * m + 4 * m].view(torch.int32),
+                      d_pack=d_down[8 * m + olw:], head=8 * m + olw,
                       d_doff=torch.zeros(b - a + 1, dtype=torch.int64, device=dev),
-                      d_pack=torch.empty(int(slots[-1]) + 64, dtype=torch.uint8, device=dev),
-                      h_ol=torch.empty(b - a, dtype=torch.int32).pin_memory(),
-                      h_ret=torch.empty(b - a, dtype=torch.int64).pin_memory(),
                       h_doff=torch.empty(b - a + 1, dtype=torch.int64).pin_memory()))
     streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
 
@@ -213,8 +219,7 @@ def e2e_host_path(L, ctx, dh, root, flags, arena, off, dev, flat, chunks: int = 
         for k, c in enumerate(C):
             st = streams[k % 2]
             with torch.cuda.stream(st):
-                c["d_json"].copy_(c["h_json"], non_blocking=True)
-                c["d_in"].copy_(c["h_in"], non_blocking=True)
+                c["d_up"].copy_(c["h_up"], non_blocking=True)
                 _lib.check(L.dg_j2t_batch_device_ml(ctx.h, dh, root, c["d_json"].data_ptr(), c["d_in"].data_ptr(),
                                                     c["n"], flags, c["d_out"].data_ptr(), c["d_oo"].data_ptr(),
                                                     c["d_ol"].data_ptr(), c["d_ret"].data_ptr(), None,
@@ -222,10 +227,9 @@ def e2e_host_path(L, ctx, dh, root, flags, arena, off, dev, flat, chunks: int = 
                 _lib.check(L.dg_pack_device_scan(ctx.h, c["d_out"].data_ptr(), c["d_oo"].data_ptr(),
                                                  c["d_ol"].data_ptr(), c["n"], c["d_pack"].data_ptr(),
                                                  c["d_doff"].data_ptr(), st.cuda_stream))
-                c["h_ol"].copy_(c["d_ol"], non_blocking=True)
-                c["h_ret"].copy_(c["d_ret"], non_blocking=True)
                 if sizes is not None:
-                    c["h_pack"][:sizes[k]].copy_(c["d_pack"][:sizes[k]], non_blocking=True)
+                    nd = c["head"] + sizes[k]
+                    c["h_down"][:nd].copy_(c["d_down"][:nd], non_blocking=True)
                 else:
                     c["h_doff"].copy_(c["d_doff"], non_blocking=True)
         for st in streams:
@@ -234,7 +238,7 @@ def e2e_host_path(L, ctx, dh, root, flags, arena, off, dev, flat, chunks: int = 
     run(None)  # learn each chunk's packed size (deterministic)
     sizes = [int(c["h_doff"][-1]) for c in C]
     for c, sz in zip(C, sizes):
-        c["h_pack"] = torch.empty(max(sz, 1), dtype=torch.uint8).pin_memory()
+        c["h_down"] = torch.empty(c["head"] + max(sz, 1), dtype=torch.uint8).pin_memory()
     best = None
     for _ in range(reps):
         torch.cuda.synchronize()
@@ -249,7 +253,9 @@ def e2e_host_path(L, ctx, dh, root, flags, arena, off, dev, flat, chunks: int = 
     er, eo = chk.j2t_arena(flat, arena, off, flags, nthreads=min(CPU_SHARE, os.cpu_count() or 1))
     bad = 0
     for k, c in enumerate(C):
-        pk, doff, rets = c["h_pack"].numpy(), c["h_doff"].numpy(), c["h_ret"].numpy()
+        hd = c["h_down"].numpy()
+        rets = hd[:8 * c["n"]].view(np.int64)
+        pk, doff = hd[c["head"]:], c["h_doff"].numpy()
         for i in range(c["n"]):
             g = c["a"] + i
             if int(rets[i]) != int(er[g]) or pk[doff[i]:doff[i + 1]].tobytes() != eo[g]:
@@ -275,9 +281,9 @@ def e2e_host_path(L, ctx, dh, root, flags, arena, off, dev, flat, chunks: int = 
     return {"value": round(json_bytes / best / 1e9, 3), "unit": "GB/s", "ms": round(best * 1e3, 3),
             "thrift_bytes": thrift, "chunks": chunks, "streams": 2, "checked_vs_oracle": n,
             "h2d_gbs_alone": round(json_bytes / t_h2d / 1e9, 2), "d2h_gbs_alone": round(thrift / t_d2h / 1e9, 2),
-            "method": "pinned H2D (JSON+offsets) -> convert -> dg_pack_device_scan -> D2H (packed Thrift + "
-                      "out_len + ret), chunks alternating over 2 streams of one context, wall clock, best of %d"
-                      % reps}
+            "method": "per chunk one pinned H2D (offsets + JSON) -> convert -> dg_pack_device_scan -> one D2H "
+                      "(ret + out_len + packed Thrift), chunks alternating over 2 streams of one context, wall "
+                      "clock, best of %d" % reps}
 
 
 # ---------------------------------------------------------------- t2j
@@ -560,7 +566,8 @@ def main(argv=None):
         cpu = cpu_baseline(flat, arena, off, flags)
     e2e = None
     if rank == 0 and world == 1 and not args.no_e2e and args.config in ("c2", "c3"):
-        e2e = e2e_host_path(L, ctx, dh, flat.root_type, flags, arena, off, dev, flat)
+        e2e = e2e_host_path(L, ctx, dh, flat.root_type, flags, arena, off, dev, flat,
+                            chunks=int(os.environ.get("DG_E2E_CHUNKS", "1")))
     c1 = None
     if rank == 0 and args.config == "c1":  # BinaryConv.Do latency: one message, host in -> host out
         cv = conv.BinaryConv(conv.Options(), ctx=ctx)
