@@ -231,15 +231,19 @@ DGI bool fl_field(const DV &D, const dg_struct &sd, S &src, uint32_t sk, uint32_
                   bool hasbs, uint32_t k, uint64_t flag, const FastTabs &tb, FField &F)
 {
     typedef typename S::idx SI;
-    const uint32_t p = skip_ws(src, sk);
-    uint32_t q = ck;
-    while (q > p && isspace_(src.raw((SI)(q - 1)))) q--;
+    /* the four delimiting bytes, read together; spaces around them take the loops */
+    const uint8_t d_s = src.raw((SI)sk), d_q = src.raw((SI)(ck - 1)), d_v = src.raw((SI)(ck + 1)),
+                  d_e = src.raw((SI)(ek - 1));
+    uint32_t p = sk, q = ck, v0 = ck + 1, ve = ek;
+    if (isspace_(d_s) || isspace_(d_q) || isspace_(d_v) || isspace_(d_e) || ck + 1 >= ek) {
+        p = skip_ws(src, sk);
+        while (q > p && isspace_(src.raw((SI)(q - 1)))) q--;
+        v0 = skip_ws(src, ck + 1);
+        while (ve > v0 && isspace_(src.raw((SI)(ve - 1)))) ve--;
+        if (v0 >= ve) return false;
+    }
     if (q < p + 2 || src.raw((SI)p) != '"' || src.raw((SI)(q - 1)) != '"') return false;
     const uint32_t k0 = p + 1, kn = q - 1 - k0;
-    const uint32_t v0 = skip_ws(src, ck + 1);
-    uint32_t ve = ek;
-    while (ve > v0 && isspace_(src.raw((SI)(ve - 1)))) ve--;
-    if (v0 >= ve) return false;
     const uint8_t c = src.raw((SI)v0);
     if (nq != (c == '"' ? 4u : 2u)) return false;
     if (hasbs && has_byte(src, k0, kn, '\\')) return false; /* escaped key: unquoted before lookup -> the list pass */
