@@ -513,10 +513,13 @@ def main(argv=None):
     stream = torch.cuda.Stream(dev)  # the kernels and the timing events share it
     torch.cuda.set_stream(stream)
 
-    def step():
-        _lib.check(L.dg_j2t_batch_device_ml(ctx.h, dh, flat.root_type, d_json.data_ptr(), d_in.data_ptr(), n, flags,
-                                            d_out.data_ptr(), d_oo.data_ptr(), d_ol.data_ptr(), d_ret.data_ptr(),
-                                            d_pend.data_ptr(), stream.cuda_stream, max_len))
+    def step(k=1):
+        # k complete batch conversions enqueued by one C call: the step loop
+        # runs where a production host (Go via cgo, or C) runs it, not in the
+        # Python interpreter (~6 us of ctypes/launch overhead per call)
+        _lib.check(L.dg_j2t_batch_device_iters(ctx.h, dh, flat.root_type, d_json.data_ptr(), d_in.data_ptr(), n,
+                                               flags, d_out.data_ptr(), d_oo.data_ptr(), d_ol.data_ptr(),
+                                               d_ret.data_ptr(), d_pend.data_ptr(), stream.cuda_stream, max_len, k))
 
     ctx.stats(reset=True)
     for _ in range(args.warmup):
@@ -539,8 +542,7 @@ def main(argv=None):
     ev1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(stream)
-    for _ in range(args.steps):
-        step()
+    step(args.steps)
     ev1.record(stream)
     torch.cuda.synchronize()
     if dist:

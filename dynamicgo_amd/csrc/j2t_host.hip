@@ -462,6 +462,22 @@ int dg_j2t_batch_device_ml(dg_ctx *c, const dg_desc *d, uint32_t root, const uin
     return launch(c, d, root, d_json, d_in_off, n, flags, d_out, d_out_off, d_out_len, d_ret, d_pending, s, max_len);
 }
 
+int dg_j2t_batch_device_iters(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *d_json,
+                              const uint64_t *d_in_off, uint64_t n, uint64_t flags, uint8_t *d_out,
+                              const uint64_t *d_out_off, uint32_t *d_out_len, uint64_t *d_ret, uint32_t *d_pending,
+                              void *stream, uint64_t max_len, int iters)
+{
+    if (!c || !d || iters < 0) return set_err(DG_E_INVALID, "bad args");
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    for (int k = 0; k < iters; k++) {
+        int rc = launch(c, d, root, d_json, d_in_off, n, flags, d_out, d_out_off, d_out_len, d_ret, d_pending, s, max_len);
+        if (rc) return rc;
+    }
+    return DG_OK;
+}
+
 int dg_j2t_batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *json, const uint64_t *in_off,
                       uint64_t n, uint64_t flags, uint8_t *out, uint64_t out_cap, uint64_t *out_off, uint64_t *ret,
                       uint64_t *out_need)

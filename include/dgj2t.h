@@ -113,6 +113,15 @@ int dg_j2t_batch_device_ml(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type,
                            const uint64_t *d_out_off, uint32_t *d_out_len, uint64_t *d_ret,
                            uint32_t *d_pending, void *stream, uint64_t max_len);
 
+/* dg_j2t_batch_device_ml enqueued `iters` times back to back in one call
+ * (one lock, no host round trip between batches): a host that re-runs the
+ * same job -- benchmarks, replays -- keeps the GPU fed. Every iteration is a
+ * complete conversion of the batch. */
+int dg_j2t_batch_device_iters(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, const uint8_t *d_json,
+                              const uint64_t *d_in_off, uint64_t n, uint64_t flags, uint8_t *d_out,
+                              const uint64_t *d_out_off, uint32_t *d_out_len, uint64_t *d_ret,
+                              uint32_t *d_pending, void *stream, uint64_t max_len, int iters);
+
 /* Output-slot size the device path uses by default for a message of len bytes. */
 uint64_t dg_slot_bound(uint64_t len);
 
