@@ -213,3 +213,29 @@ def test_pack_device_scan_vs_oracle(n):
     assert got[len(want)] == 0xAB
     exp_off = np.concatenate([[0], np.cumsum([len(o) for o in eo])])
     assert (doff == exp_off).all()
+
+
+@pytest.mark.parametrize("cfg", ["c2", "c5mix"])
+def test_batch_device_iters_vs_oracle(cfg):
+    """dg_j2t_batch_device_iters (the bench's step loop): K back-to-back
+    conversions of one batch leave exactly the oracle's output, on the flat
+    path (C2) and on the small + wave + list pipeline (a C5-style mix)."""
+    import torch
+    rng = random.Random(77)
+    if cfg == "c2":
+        td, msgs = W.simple_desc(), W.gen_flat_batch(rng, 3000)
+    else:
+        td, msgs = W.mixed_desc(), W.gen_mixed_batch(rng, 1500, large_scale=0.05)
+    fl = T.flatten(td)
+    ctx = conv.default_context()
+    dh = ctx.desc(fl)
+    b = DevBatch(msgs)
+    st = torch.cuda.current_stream().cuda_stream
+    for ml in (0, b.max_len):
+        b.out.zero_()
+        b.ret.fill_(-1)
+        _lib.check(_lib.lib().dg_j2t_batch_device_iters(
+            ctx.h, dh, fl.root_type, b.json.data_ptr(), b.in_off.data_ptr(), b.n, 1, b.out.data_ptr(),
+            b.out_off.data_ptr(), b.out_len.data_ptr(), b.ret.data_ptr(), None, st, ml, 3))
+        torch.cuda.synchronize()
+        assert b.results() == _oracle_all(fl, msgs)
