@@ -832,32 +832,41 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
                 tot += v;
             }
             nbytes += tot;
+            uint32_t wr = 1;
             if (F.size) {
-                uint32_t wr = 0;
+                wr = 0;
                 if (off + F.size <= FL_OUTW * 8) {
                     LOr o;
                     o.init((LOr::L64 *)(void *)&L.out[mm * FL_OUTW], off);
                     wr = flat_write(src, F, o);
                     o.finish();
                 }
-                if (wr == 2) {
-                    /* the body as chunk tasks of FL_CHUNK input bytes */
-                    const bool b64 = F.kind == FV_BIN;
-                    const uint32_t nch = (F.nb + FL_CHUNK - 1) / FL_CHUNK;
-                    const uint32_t t0 = atomicAdd(&L.ntask, nch);
-                    if (t0 + nch <= FL_MAXTASK) {
+            }
+            {
+                /* bodies left to chunk tasks of FL_CHUNK input bytes: one LDS
+                 * atomic per wave (lane 63 reserves the wave's total) */
+                const uint32_t nch = wr == 2 ? (F.nb + FL_CHUNK - 1) / FL_CHUNK : 0u;
+                const uint32_t incl = wave_incl_sum(nch, lane);
+                const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+                if (tot) {
+                    uint32_t base = 0;
+                    if (lane == 63) base = atomicAdd(&L.ntask, tot);
+                    base = (uint32_t)__builtin_amdgcn_readlane((int)base, 63);
+                    const uint32_t t0 = base + incl - nch;
+                    if (nch && t0 + nch <= FL_MAXTASK) {
+                        const bool b64 = F.kind == FV_BIN;
                         for (uint32_t c = 0; c < nch; c++) {
                             const uint32_t cs = c * FL_CHUNK, cn = min(FL_CHUNK, F.nb - cs);
                             const uint32_t dst = off + 7 + (b64 ? c * (FL_CHUNK / 4 * 3) : cs);
                             L.task[t0 + c] = (uint64_t)mm | ((uint64_t)b64 << 6) | ((uint64_t)(c + 1 == nch) << 7) |
                                              ((uint64_t)(F.s0 + cs) << 8) | ((uint64_t)cn << 20) | ((uint64_t)dst << 32);
                         }
-                    } else {
+                    } else if (nch) {
                         wr = 0;
                     }
                 }
-                if (!wr) L.ok[mm] = 0;
             }
+            if (!wr) L.ok[mm] = 0;
             FLP(5);
         }
         if (fs == 0) L.nbytes[mm] = nbytes;
