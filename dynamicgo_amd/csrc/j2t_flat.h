@@ -605,8 +605,7 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
             cap = (uint32_t)min(P.out_off[i + 1] - oa, (uint64_t)0xFFFFFFFFu);
             if (P.big_list && (n64 > P.big_max || n64 > FL_MAXLEN)) { /* the wave kernel */
                 big = 1;
-                const uint32_t q = __hip_atomic_fetch_add(P.big_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                P.big_list[q] = (uint32_t)i;
+                list_big(P, i, n64);
             } else if (n64 > 0 && n64 <= FL_MAXLEN) {
                 n = (uint32_t)n64;
                 if (staged) {

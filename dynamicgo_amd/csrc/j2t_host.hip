@@ -295,6 +295,8 @@ static int enqueue(dg_ctx *c, Scratch *x, const dg_desc *d, uint32_t root, const
     P.big_list = nullptr;
     P.big_count = nullptr;
     P.big_max = 0;
+    P.huge_count = nullptr;
+    P.huge_min = WV_HUGE_MIN;
     P.out = out;
     P.out_off = out_off;
     P.out_len = out_len;
@@ -341,6 +343,7 @@ static int enqueue(dg_ctx *c, Scratch *x, const dg_desc *d, uint32_t root, const
             P1.big_list = x->d_big_list;
             P1.big_count = x->d_counts + 1;
             P1.big_max = big_max;
+            P1.huge_count = x->d_counts + 3;
         }
         SmallParams S;
         S.blob = d->d_blob;
@@ -368,6 +371,8 @@ static int enqueue(dg_ctx *c, Scratch *x, const dg_desc *d, uint32_t root, const
             W.bail_list = x->d_bail_list;
             W.list = x->d_big_list;
             W.list_count = x->d_counts + 1;
+            W.huge_count = x->d_counts + 3;
+            W.list_cap = n;
             W.ws = x->ws_wave;
             W.queue = x->d_counts + 2;
             uint64_t wblocks = std::min<uint64_t>((n + WV_WAVES - 1) / WV_WAVES, (uint64_t)c->n_cu * WV_BLOCKS_PER_CU);
@@ -394,6 +399,7 @@ static int enqueue(dg_ctx *c, Scratch *x, const dg_desc *d, uint32_t root, const
         P1.big_list = x->d_big_list;
         P1.big_count = x->d_counts + 1;
         P1.big_max = big_max;
+        P1.huge_count = x->d_counts + 3;
         lane_launch(dim3((uint32_t)blocks), P1);
         HIPCHK(hipGetLastError());
         WaveParams W;
@@ -403,6 +409,8 @@ static int enqueue(dg_ctx *c, Scratch *x, const dg_desc *d, uint32_t root, const
         W.bail_list = x->d_bail_list;
         W.list = x->d_big_list;
         W.list_count = x->d_counts + 1;
+        W.huge_count = x->d_counts + 3;
+        W.list_cap = n;
         W.ws = x->ws_wave;
         W.queue = x->d_counts + 2;
         uint64_t wblocks = std::min<uint64_t>((n + WV_WAVES - 1) / WV_WAVES, (uint64_t)c->n_cu * WV_BLOCKS_PER_CU);

@@ -56,7 +56,24 @@ struct Params {
     uint32_t *big_list;        /* messages longer than big_max are left to the wave kernel via this list */
     uint32_t *big_count;
     uint64_t big_max;
+    uint32_t *huge_count;      /* messages longer than huge_min go to the END of big_list (taken first) */
+    uint64_t huge_min;
 };
+
+/* List message i (len bytes) for the wave kernel. Huge ones are written from
+ * the end of the list and the wave kernel's queue hands them out first: a
+ * C4-size message keeps a wave busy for about a millisecond, so one taken
+ * last would set the kernel's tail. */
+DGI void list_big(const Params &P, uint64_t i, uint64_t len)
+{
+    if (P.huge_count && len > P.huge_min) {
+        const uint32_t q = __hip_atomic_fetch_add(P.huge_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        P.big_list[P.n - 1 - q] = (uint32_t)i;
+    } else {
+        const uint32_t q = __hip_atomic_fetch_add(P.big_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        P.big_list[q] = (uint32_t)i;
+    }
+}
 
 #ifdef DG_PROFILE
 #define PROF_DECL uint64_t prof[16] = {0};
@@ -854,6 +871,7 @@ DGI void deep_pass(const Params &P, const DV &dv, uint32_t *done, uint32_t nbloc
         if (P.reset2) {
             __hip_atomic_store(P.reset2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(P.reset2 + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(P.reset2 + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         __hip_atomic_store(P.deep_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -906,6 +924,7 @@ __global__ __launch_bounds__(LANE_BLOCK) __attribute__((amdgpu_waves_per_eu(1, 1
             if (blockIdx.x == 0 && threadIdx.x == 0 && P.reset2) {
                 __hip_atomic_store(P.reset2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 __hip_atomic_store(P.reset2 + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(P.reset2 + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             return;
         }
@@ -995,8 +1014,7 @@ __global__ __launch_bounds__(LANE_BLOCK) __attribute__((amdgpu_waves_per_eu(1, 1
         bool done = false;
         if (P.big_list && P.in_off[i + 1] - P.in_off[i] > P.big_max) {
             /* a large message: the wave kernel (one wavefront per message) takes it */
-            uint32_t q = __hip_atomic_fetch_add(P.big_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&P.big_list[q], (uint32_t)i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            list_big(P, i, P.in_off[i + 1] - P.in_off[i]);
             done = true;
         } else if (P.fast) {
             uint64_t oa = P.out_off[i], ob = P.out_off[i + 1];

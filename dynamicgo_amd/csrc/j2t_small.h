@@ -106,8 +106,7 @@ __global__ __launch_bounds__(64 * SM_WAVES) __attribute__((amdgpu_waves_per_eu(D
     }
     if (!mine) return;
     if (big) {
-        uint32_t q = __hip_atomic_fetch_add(P.big_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        P.big_list[q] = (uint32_t)i;
+        list_big(P, i, b - a);
         return;
     }
     const auto dv = desc_view<3>((const __attribute__((address_space(3))) uint8_t *)(void *)ldesc, S.hdr);

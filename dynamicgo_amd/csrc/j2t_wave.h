@@ -75,6 +75,7 @@ constexpr uint32_t WV_MSG = DG_WV_MSG;         /* messages up to this (minus 16)
 constexpr uint32_t WV_DESC = 16384;            /* the wave path needs the descriptor in LDS (dynamic, sized to it) */
 constexpr uint32_t WV_BLOCKS_PER_CU = DG_WV_BPC; /* persistent grid: blocks of 4 waves per CU */
 constexpr uint32_t WV_MIN_DEFAULT = 512;       /* messages longer than this go to the wave kernel (DG_WAVE_MIN) */
+constexpr uint64_t WV_HUGE_MIN = 16384;        /* ... and longer than this are queued first */
 constexpr uint32_t WV_REQMASKS = 64;           /* per-struct REQUIRED-field masks kept in LDS */
 
 /* token kinds (3 bits, stored above the 29-bit position) */
@@ -124,6 +125,8 @@ struct WaveParams {
     uint32_t *bail_list;
     const uint32_t *list; /* in: the messages to convert (the lane kernel's large ones) */
     const uint32_t *list_count;
+    const uint32_t *huge_count; /* huge messages listed from the end of `list` (taken first) */
+    uint64_t list_cap;          /* the list's length (the batch size) */
     uint8_t *ws;          /* DCAP bytes of big-decimal digits per wave of the grid */
     uint32_t *queue;      /* next list entry to take (zero at launch; reset by the list-mode lane kernel) */
 };
@@ -1095,7 +1098,12 @@ DGI bool wave_convert(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, L
  * staged in the wave's LDS buffer. Bailed messages are listed for the exact
  * machine (j2t_lane_kernel in list mode). */
 template <int V> /* instantiated in j2t_kern_wave.hip only */
-__global__ __launch_bounds__(64 * WV_WAVES) __attribute__((amdgpu_waves_per_eu(DG_WV_WPE))) void j2t_wave_kernel(
+#ifdef DG_WV_NUMVGPR
+#define DG_WV_VGPR_ATTR __attribute__((amdgpu_num_vgpr(DG_WV_NUMVGPR)))
+#else
+#define DG_WV_VGPR_ATTR
+#endif
+__global__ __launch_bounds__(64 * WV_WAVES) __attribute__((amdgpu_waves_per_eu(DG_WV_WPE))) DG_WV_VGPR_ATTR void j2t_wave_kernel(
     Params P, WaveParams W)
 {
     __shared__ __attribute__((aligned(16))) WaveLds wl[WV_WAVES];
@@ -1106,8 +1114,12 @@ __global__ __launch_bounds__(64 * WV_WAVES) __attribute__((amdgpu_waves_per_eu(D
     __shared__ uint64_t s_p10u[20];
     __shared__ double s_p10d[23];
     const uint32_t tid = threadIdx.x;
-    const uint64_t total = W.list ? (uint64_t)__hip_atomic_load((uint32_t *)W.list_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                  : P.n;
+    const uint64_t nh = W.list && W.huge_count
+                            ? (uint64_t)__hip_atomic_load((uint32_t *)W.huge_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                            : 0;
+    const uint64_t total =
+        W.list ? (uint64_t)__hip_atomic_load((uint32_t *)W.list_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + nh
+               : P.n;
     if ((uint64_t)blockIdx.x * WV_WAVES >= total) return;
     {
         const uint4 *g = (const uint4 *)W.blob;
@@ -1162,7 +1174,7 @@ __global__ __launch_bounds__(64 * WV_WAVES) __attribute__((amdgpu_waves_per_eu(D
         if (lane == 0) kq = __hip_atomic_fetch_add(W.queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint64_t k = (uint32_t)__builtin_amdgcn_readfirstlane((int)kq);
         if (k >= total) break;
-        const uint64_t m = W.list ? (uint64_t)W.list[k] : k;
+        const uint64_t m = W.list ? (uint64_t)(k < nh ? W.list[W.list_cap - 1 - k] : W.list[k - nh]) : k;
         bool ok = wave_convert(P, dv, W.hdr.n_fields, m, wl[wave], mbuf, cls, tb, lane, dbuf,
                                (const __attribute__((address_space(3))) uint64_t *)(void *)s_reqmask);
         if (!ok && lane == 0) {
