@@ -131,3 +131,26 @@ def test_flat_edges():
         for extra in (FLAT, 0, NO_FLAT):
             bad = _compare(fl, msgs, flags | extra)
             assert not bad, (hex(flags), extra, bad[:4])
+
+
+def test_flat_lengths_up_to_256():
+    """Messages of every length up to the flat kernel's 256-byte limit, at
+    every alignment in the arena (structure lanes cover 4 words each; lane 7
+    takes word 32 only when a message reaches it), and just past it (listed
+    for the wave kernel or the list pass)."""
+    td = W.simple_desc()
+    fl = T.flatten(td)
+    msgs = []
+    for n in list(range(180, 262)) + [511, 512, 513]:
+        base = '{"ByteField":1,"I32Field":2,"StringField":"%s","I64Field":3}'
+        pad = n - len(base % "")
+        if pad < 0:
+            continue
+        m = (base % ("s" * pad)).encode()
+        assert len(m) == n
+        for lead in range(8):  # leading spaces: every alignment of the braces and words
+            msgs.append(b" " * lead + m)
+        msgs.append(b'{"StringField":"' + b"," * (n - 19) + b'"}')  # commas inside a string at every word
+    for extra in (FLAT, 0, NO_FLAT):
+        bad = _compare(fl, msgs, 0x1 | extra)
+        assert not bad, (extra, bad[:4])
