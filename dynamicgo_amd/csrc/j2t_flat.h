@@ -9,18 +9,21 @@
  * byte-serially in one lane, so a 64K batch is one wave per SIMD and every
  * latency is exposed. Here a block of 8 waves takes 64 messages:
  *
- *  1. structure: 8 lanes per message, each classifies 40 aligned bytes of the
- *     staged message into bit masks (quote, backslash, comma, colon, bracket);
- *     the in-string mask is a prefix XOR of the quote bits carried across the
- *     8 lanes with DPP; commas and colons outside strings are recorded (with
- *     the count of quotes before each comma).
- *  2. fields, field-major: wave w converts field w (+8r) of all 64 messages,
- *     so the lanes of a wave hold the same field of 64 messages -- the same
- *     type, the same code path. Key lookup (the predicted IDL-order field,
- *     else the name table), value parse and Thrift size.
+ *  1. structure: 8 lanes per message, each classifies 32 aligned bytes of
+ *     the staged message (lane 7 also word 32 when a message reaches it)
+ *     into 0x80-per-byte masks (quote, comma, colon, backslash); the
+ *     in-string mask is a prefix XOR of the quote bytes carried across the 8
+ *     lanes with DPP scans; commas and colons outside strings are recorded
+ *     (with the count of quotes before each comma).
+ *  2. fields, field-major: wave w converts field fl_slot(w) (+8r) of all 64
+ *     messages, so the lanes of a wave hold the same field of 64 messages --
+ *     the same type, the same code path. Key lookup (the predicted IDL-order
+ *     field, else the name table), value parse and Thrift size.
  *  3. every lane reads the sizes of the fields before its own (one barrier),
- *     writes its field into the message's LDS output stage, and the 8 lanes of
- *     a message copy the stage to the slot with whole-word stores.
+ *     writes its field into the message's zeroed LDS output stage (shared
+ *     edge words OR-ed), leaves string/base64 bodies over 16 B to chunk
+ *     tasks that the whole block takes after a barrier, and the 8 lanes of a
+ *     message copy the stage to the slot with whole-word stores.
  *
  * JSON fields are written in input order, exactly as j2t_fsm_exec writes them
  * (native/thrift.c:765-1187: tb_write_field_begin + value per key,
@@ -82,10 +85,6 @@ DGI uint32_t g8_next(uint32_t v, uint32_t g)
 
 /* 0x80 in each byte of w (32-bit half) equal to c */
 DGI uint32_t eq32(uint32_t w, uint32_t cc) { return zb32(w ^ cc); }
-/* the 0x80 flags of a 32-bit half -> 4 bits (byte k -> bit k) */
-DGI uint32_t nib(uint32_t m80) { return (((m80 >> 7) * 0x00204081u) >> 21) & 0xFu; }
-/* byte-class bits of an 8-byte word (byte k -> bit k) */
-DGI uint32_t cls8(uint32_t lo, uint32_t hi, uint32_t cc) { return nib(eq32(lo, cc)) | (nib(eq32(hi, cc)) << 4); }
 
 /* The staged message in LDS, the SrcT interface without SrcT's one-word
  * cache: every access is its own LDS read, so independent reads overlap
@@ -120,64 +119,6 @@ struct LSrc {
         return r;
     }
 };
-
-/* A byte writer into an 8-aligned buffer (global: the output slot; LDS: a
- * message's output stage) starting at an arbitrary byte offset; several
- * lanes write disjoint ranges of the same buffer. Whole words inside the
- * range are stored as words, the partial words at its two ends byte by byte
- * (those bytes' neighbours belong to other lanes). */
-template <int AS>
-struct BOut {
-    typedef __attribute__((address_space(AS))) uint8_t B8;
-    typedef __attribute__((address_space(AS))) uint64_t B64;
-    B8 *b;       /* buffer base (8-aligned) */
-    uint64_t len;/* absolute position in the buffer */
-    uint64_t wbuf;
-    uint32_t lo; /* first byte of the current word that is ours */
-    DGI void init(B8 *base, uint64_t start)
-    {
-        b = base;
-        len = start;
-        wbuf = 0;
-        lo = (uint32_t)(start & 7);
-    }
-    DGI void put_word(uint64_t wi, uint64_t v)
-    {
-        if (lo == 0) {
-            *(B64 *)(b + (wi << 3)) = v;
-        } else {
-            for (uint32_t k = lo; k < 8; k++) b[(wi << 3) + k] = (uint8_t)(v >> (8 * k));
-            lo = 0;
-        }
-    }
-    DGI void wle(uint64_t v, uint32_t n)
-    {
-        const uint32_t used = (uint32_t)(len & 7), sh = used << 3;
-        if (n < 8) v &= (1ull << (n << 3)) - 1;
-        const uint64_t low = (wbuf & ((1ull << sh) - 1)) | (v << sh);
-        const uint64_t high = used ? (v >> (64 - sh)) : 0;
-        const uint64_t wi = len >> 3;
-        len += n;
-        if (used + n >= 8) {
-            put_word(wi, low);
-            wbuf = high;
-        } else {
-            wbuf = low;
-        }
-    }
-    DGI void w8(uint8_t v) { wle(v, 1); }
-    DGI void w16(uint16_t v) { wle(__builtin_bswap16(v), 2); }
-    DGI void w32(uint32_t v) { wle(__builtin_bswap32(v), 4); }
-    DGI void w64(uint64_t v) { wle(__builtin_bswap64(v), 8); }
-    DGI void finish()
-    {
-        const uint32_t e = (uint32_t)(len & 7);
-        const uint64_t wi = len >> 3;
-        for (uint32_t k = lo; k < e; k++) b[(wi << 3) + k] = (uint8_t)(wbuf >> (8 * k));
-    }
-};
-typedef BOut<1> GOut;
-typedef BOut<3> LOut;
 
 /* counts bytes only (string sizes with escapes) */
 struct CountW {
