@@ -23,8 +23,8 @@ def _run(cmd, cwd=None):
     subprocess.run(cmd, cwd=cwd, check=True)
 
 
-UNITS = ("j2t_kern_wave.hip", "j2t_kern_small.hip", "j2t_kern_lds.hip", "j2t_kern_glb.hip", "j2t_host.hip",
-         "j2t_agg.hip", "t2j_kern.hip", "t2j_host.hip", "j2t_kern_flat.hip")
+UNITS = ("j2t_kern_wave.hip", "j2t_kern_wave5.hip", "j2t_kern_small.hip", "j2t_kern_lds.hip", "j2t_kern_glb.hip",
+         "j2t_host.hip", "j2t_agg.hip", "t2j_kern.hip", "t2j_host.hip", "j2t_kern_flat.hip")
 HEADERS = ("j2t_small.h", "j2t_wave.h", "j2t_machine.h", "j2t_device.h", "j2t_fast.h", "dg_tables.h", "host_internal.h",
            "t2j_device.h", "t2j_tables.h", "j2t_flat.h")
 
@@ -44,9 +44,12 @@ def source_hash(extra_flags=()) -> str:
 
 
 COMMON_FLAGS = ("-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wno-unused-result")
-# the flat kernel: machine LICM hoists every constant of the field parser out of
-# the rounds loop into VGPRs (123 -> 103 VGPRs without it)
-DEFAULT_UNIT_FLAGS = {"j2t_kern_flat.hip": ("-mllvm", "-disable-machine-licm")}
+# machine LICM hoists loop-invariant constants into VGPRs: the flat kernel's
+# field parser (123 -> 103 VGPRs without it) and the wave kernel (4 waves/SIMD:
+# 128 VGPRs + 10 spilled -> 115, none spilled; the 5-wave instance needs it to
+# fit 96 VGPRs)
+_NO_LICM = ("-mllvm", "-disable-machine-licm")
+DEFAULT_UNIT_FLAGS = {"j2t_kern_flat.hip": _NO_LICM, "j2t_kern_wave.hip": _NO_LICM, "j2t_kern_wave5.hip": _NO_LICM}
 MARK = b"dgj2t-build:"
 
 

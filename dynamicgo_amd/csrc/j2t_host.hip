@@ -62,7 +62,7 @@ static int scratch_new(dg_ctx *c, hipStream_t owner, Scratch **out)
     if (e == hipSuccess) e = hipMalloc(&x->d_counts, 32);
     if (e == hipSuccess) e = hipMemset(x->d_counts, 0, 32);
     if (e == hipSuccess) e = hipMalloc(&x->ws_deep, DEEP_WS_STRIDE * DEEP_THREADS);
-    if (e == hipSuccess) e = hipMalloc(&x->ws_wave, (size_t)c->n_cu * WV_BLOCKS_PER_CU * WV_WAVES * DCAP);
+    if (e == hipSuccess) e = hipMalloc(&x->ws_wave, (size_t)c->n_cu * std::max(WV_BLOCKS_PER_CU, WV5_BLOCKS_PER_CU) * WV_WAVES * DCAP);
     if (e == hipSuccess) e = hipMalloc(&x->d_sums, (size_t)c->n_cu * 8);
     if (e == hipSuccess) e = hipMalloc(&x->d_frame, FRAME_CAP);
     if (e != hipSuccess) {
@@ -323,6 +323,17 @@ static int enqueue(dg_ctx *c, Scratch *x, const dg_desc *d, uint32_t root, const
     const uint64_t big_max = wm ? strtoull(wm, nullptr, 10) : (uint64_t)WV_MIN_DEFAULT;
     const bool wave = P.fast && !no_wave && d->hdr.total_len <= WV_DESC && d->hdr.total_len <= DESC_LDS_BYTES &&
                       (max_len == 0 || max_len > big_max);
+    /* the wave kernel's instance: 5 waves/SIMD when the caller's max_len
+     * rules out huge messages (their tail grows with a fifth wave per SIMD,
+     * j2t_wave.h), else 4; DG_WAVE_OCC=4|5 forces one */
+    const char *occ_env = getenv("DG_WAVE_OCC");
+    const bool wave5 = occ_env ? atoi(occ_env) == 5 : (max_len != 0 && max_len <= WV_HUGE_MIN);
+    auto wave_launch = [&](hipStream_t st, const Params &Q, const WaveParams &W) {
+        const uint64_t bpc = wave5 ? WV5_BLOCKS_PER_CU : WV_BLOCKS_PER_CU;
+        const uint64_t wblocks = std::min<uint64_t>((n + WV_WAVES - 1) / WV_WAVES, (uint64_t)c->n_cu * bpc);
+        if (wave5) launch_wave_kernel5(dim3((uint32_t)wblocks), st, Q, W);
+        else launch_wave_kernel(dim3((uint32_t)wblocks), st, Q, W);
+    };
     auto lane_launch = [&](dim3 g, const Params &Q) {
         if (d->hdr.total_len <= DESC_LDS_BYTES) launch_lane_kernel_lds(g, s, Q, DP);
         else launch_lane_kernel_glb(g, s, Q, DP);
@@ -375,8 +386,7 @@ static int enqueue(dg_ctx *c, Scratch *x, const dg_desc *d, uint32_t root, const
             W.list_cap = n;
             W.ws = x->ws_wave;
             W.queue = x->d_counts + 2;
-            uint64_t wblocks = std::min<uint64_t>((n + WV_WAVES - 1) / WV_WAVES, (uint64_t)c->n_cu * WV_BLOCKS_PER_CU);
-            launch_wave_kernel(dim3((uint32_t)wblocks), s, P, W);
+            wave_launch(s, P, W);
             HIPCHK(hipGetLastError());
         }
         Params P3 = P;
@@ -413,8 +423,7 @@ static int enqueue(dg_ctx *c, Scratch *x, const dg_desc *d, uint32_t root, const
         W.list_cap = n;
         W.ws = x->ws_wave;
         W.queue = x->d_counts + 2;
-        uint64_t wblocks = std::min<uint64_t>((n + WV_WAVES - 1) / WV_WAVES, (uint64_t)c->n_cu * WV_BLOCKS_PER_CU);
-        launch_wave_kernel(dim3((uint32_t)wblocks), s, P, W);
+        wave_launch(s, P, W);
         HIPCHK(hipGetLastError());
         Params P3 = P;
         P3.list = x->d_bail_list;

@@ -50,7 +50,15 @@ namespace dg {
  * staging, 191 VGPRs) 4.18 ms; 3 waves (168 VGPRs) 3.34 ms; 4 waves (ring
  * 256, 2 KiB staging, 128 VGPRs + 24 spilled, 4 blocks/CU) 2.88 ms. The
  * kernel is latency-bound (dependent ballot/LDS chains), so waves per SIMD
- * beat per-wave efficiency. */
+ * beat per-wave efficiency.
+ *
+ * Two instances are built: this default (4 waves/SIMD, j2t_kern_wave.hip)
+ * and a 5-waves/SIMD one (j2t_kern_wave5.hip: 96 VGPRs, 128 B staging, so
+ * that 5 blocks fit the CU's LDS). With machine LICM off (build.py) the
+ * 5-wave instance runs C3 in 2.14 ms against 2.30 ms, but a message longer
+ * than WV_HUGE_MIN keeps one wave busy for about 1 ms, and sharing its SIMD
+ * with a fifth wave lengthens that tail (C5 5.94 -> 6.14 ms). The host picks
+ * the 5-wave instance when the caller's max_len rules huge messages out. */
 #ifndef DG_WV_RING
 #define DG_WV_RING 256
 #endif
@@ -74,6 +82,7 @@ constexpr uint32_t WV_POSMASK = (1u << 29) - 1;
 constexpr uint32_t WV_MSG = DG_WV_MSG;         /* messages up to this (minus 16) are staged in LDS */
 constexpr uint32_t WV_DESC = 16384;            /* the wave path needs the descriptor in LDS (dynamic, sized to it) */
 constexpr uint32_t WV_BLOCKS_PER_CU = DG_WV_BPC; /* persistent grid: blocks of 4 waves per CU */
+constexpr uint32_t WV5_BLOCKS_PER_CU = 5;      /* the 5-waves/SIMD instance (j2t_kern_wave5.hip) */
 constexpr uint32_t WV_MIN_DEFAULT = 512;       /* messages longer than this go to the wave kernel (DG_WAVE_MIN) */
 constexpr uint64_t WV_HUGE_MIN = 16384;        /* ... and longer than this are queued first */
 constexpr uint32_t WV_REQMASKS = 64;           /* per-struct REQUIRED-field masks kept in LDS */
@@ -1097,7 +1106,7 @@ DGI bool wave_convert(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, L
  * The descriptor is copied to LDS once per block; messages that fit are
  * staged in the wave's LDS buffer. Bailed messages are listed for the exact
  * machine (j2t_lane_kernel in list mode). */
-template <int V> /* instantiated in j2t_kern_wave.hip only */
+template <int V> /* <0> in j2t_kern_wave.hip, <5> in j2t_kern_wave5.hip */
 #ifdef DG_WV_NUMVGPR
 #define DG_WV_VGPR_ATTR __attribute__((amdgpu_num_vgpr(DG_WV_NUMVGPR)))
 #else
@@ -1316,6 +1325,7 @@ void launch_pack_scan_kernel(dim3 grid, hipStream_t s, const uint8_t *out, const
                              const uint32_t *out_len, uint64_t n, uint8_t *dst, uint64_t *dst_off, uint64_t *sums,
                              uint32_t *sync, const MsgFrame &fr);
 void launch_wave_kernel(dim3 grid, hipStream_t s, const Params &P, const WaveParams &W); /* LDS: + the blob */
+void launch_wave_kernel5(dim3 grid, hipStream_t s, const Params &P, const WaveParams &W); /* 5 waves/SIMD */
 void launch_pack_kernel(dim3 grid, hipStream_t s, const uint8_t *out, const uint64_t *out_off, const uint32_t *out_len,
                         uint64_t n, uint8_t *dst, const uint64_t *dst_off);
 
