@@ -618,7 +618,7 @@ DGI bool wave_run(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L
         const bool act = lane < np;
         const uint32_t tp = act ? L.tpos[t & WV_RMASK] : 0;
         const uint32_t kind = act ? tp >> 29 : K_NONE;
-        const int64_t pos = tp & WV_POSMASK;
+        const int32_t pos = (int32_t)(tp & WV_POSMASK);
         const bool op = kind == K_LBRACE || kind == K_LBRACK;
         const bool cl = kind == K_RBRACE || kind == K_RBRACK;
         const uint64_t bo = ballot(op), bc = ballot(cl);
@@ -785,10 +785,10 @@ DGI bool wave_run(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L
         int64_t iv = 0;
         double dv = 0.0;
         uint8_t tt = 0;
-        int64_t ns = -1, nn = 0; /* number text to parse */
+        int32_t ns = -1, nn = 0; /* number text to parse */
         bool slow = false;
         bool whole = true;       /* the number must span all of it */
-        int64_t cs = 0, cn = 0;  /* string body (copy / unquote / base64) */
+        int32_t cs = 0, cn = 0;  /* string body (copy / unquote / base64) */
         uint64_t hv = 0;         /* header bytes (little-endian) and count */
         uint32_t hn = 0;
         if (alive && !skip && keyish) {
