@@ -928,17 +928,19 @@ DGI bool wave_run(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L
             hn = 0;
             ln = 0;
         }
+        /* a number's Thrift bytes become header bytes here, so that the parse
+         * results are dead before the prefix sum (fewer live VGPRs) */
         if (!isnull && ns >= 0 && !skip && hn == 0) ln = num_size(tt);
         WP(4);
         /* part B: closing brackets, once every atomic of the page is in */
         uint64_t reqs = 0;
-        dg_struct csd;
+        uint32_t sidx = 0; /* the closed struct (its dg_struct is reloaded at the emit) */
         if (alive && cl) {
             const uint32_t pf = L.crec[ci].flags;
             if (!(pf & CF_SKIP) && (pf & CF_STRUCT)) {
-                csd = ldrec(&D.S[ldrec(&D.T[L.crec[ci].type]).st]);
+                sidx = ldrec(&D.T[L.crec[ci].type]).st;
+                const dg_struct csd = ldrec(&D.S[sidx]);
                 reqs = (D.R[csd.req_begin] & ~L.crec[ci].seen) | L.crec[ci].nulldr;
-                const uint32_t sidx = ldrec(&D.T[L.crec[ci].type]).st;
                 if (!(flag & (DG_F_WRITE_REQUIRE | DG_F_WRITE_DEFAULT | DG_F_WRITE_OPTIONAL)) && sidx < WV_REQMASKS) {
                     /* nothing is written for unset fields: only a missing
                      * REQUIRED one matters (ERR_NULL_REQUIRED, native/thrift.c:286-290) */
@@ -962,7 +964,7 @@ DGI bool wave_run(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L
         /* output offsets */
         const uint32_t incl = wave_incl_sum(ln, lane);
         const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-        const uint64_t opos = O + incl - ln;
+        const uint32_t opos = (uint32_t)(O + incl - ln); /* slot offsets are 32-bit (outpos, cbd) */
         if (O + tot > cap) return false; /* slot overflow: the exact machine reports it */
         if (alive && op) L.crec[lane].outpos = (uint32_t)opos;
 
@@ -974,7 +976,7 @@ DGI bool wave_run(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L
         {
             WOut w;
             w.init(ob + opos);
-            if (live && cl && hn == 1 && reqs) unset_fields(D, csd, reqs, flag, w); /* before the STOP */
+            if (live && cl && hn == 1 && reqs) unset_fields(D, ldrec(&D.S[sidx]), reqs, flag, w); /* before the STOP */
 #if defined(DG_WV_ABL) && (DG_WV_ABL & 4)
             w.dry = true; /* ablation: no header/number stores */
 #endif
