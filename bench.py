@@ -353,6 +353,7 @@ def bench_t2j(args, rank, world, dev, dist, backend, td, arena, off, meta):
     tl = np.diff(toff).astype(np.int64)
     jslots = np.zeros(n + 1, dtype=np.int64)
     np.cumsum((tl * 3 + 64 + 7) & ~7, out=jslots[1:])  # dg_t2j_slot_bound
+    t_max = int(tl.max()) if n else 0  # the longest Thrift message: picks the kernel's lanes per message
     del d_j2t, d_json
     d_out = torch.empty(int(jslots[-1]) + 64, dtype=torch.uint8, device=dev)
     d_jo = torch.from_numpy(jslots).to(dev)
@@ -361,9 +362,9 @@ def bench_t2j(args, rank, world, dev, dist, backend, td, arena, off, meta):
     opts = 0
 
     def step():
-        _lib.check(L.dg_t2j_batch_device(ctx.h, dh, flat.root_type, d_thrift.data_ptr(), d_toff.data_ptr(), n, opts,
-                                         d_out.data_ptr(), d_jo.data_ptr(), d_jl.data_ptr(), d_jr.data_ptr(),
-                                         stream.cuda_stream))
+        _lib.check(L.dg_t2j_batch_device_ml(ctx.h, dh, flat.root_type, d_thrift.data_ptr(), d_toff.data_ptr(), n,
+                                            opts, d_out.data_ptr(), d_jo.data_ptr(), d_jl.data_ptr(),
+                                            d_jr.data_ptr(), stream.cuda_stream, t_max))
 
     for _ in range(args.warmup):
         step()

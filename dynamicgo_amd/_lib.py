@@ -17,7 +17,7 @@ EXPORTS = ["dg_last_error", "dg_build_info", "dg_ctx_create", "dg_ctx_destroy", 
            "dg_desc_create_device", "dg_desc_destroy", "dg_desc_root", "dg_j2t_batch_device",
            "dg_j2t_batch_device_ml", "dg_j2t_batch_device_iters",
            "dg_slot_bound", "dg_j2t_batch_host", "dg_j2t_do", "dg_pack_device", "dg_pack_device_scan", "dg_pack_device_framed", "dg_agg_create", "dg_agg_do", "dg_agg_stats",
-           "dg_agg_destroy", "dg_bench_device", "dg_desc_attach_t2j", "dg_t2j_slot_bound", "dg_t2j_batch_device",
+           "dg_agg_destroy", "dg_bench_device", "dg_desc_attach_t2j", "dg_t2j_slot_bound", "dg_t2j_batch_device", "dg_t2j_batch_device_ml",
            "dg_t2j_batch_host"]
 
 _lib = None
@@ -72,6 +72,7 @@ def lib() -> C.CDLL:
         "dg_desc_attach_t2j": (i32, [vp, C.c_char_p, sz]),
         "dg_t2j_slot_bound": (u64, [u64]),
         "dg_t2j_batch_device": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, vp, vp, vp, vp]),
+        "dg_t2j_batch_device_ml": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, vp, vp, vp, vp, u64]),
         "dg_t2j_batch_host": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, u64, vp, vp, P64]),
         "dg_bench_device": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, vp, vp, vp, i32, C.POINTER(C.c_float)]),
     }

@@ -49,7 +49,8 @@ COMMON_FLAGS = ("-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wno-unused-
 # 128 VGPRs + 10 spilled -> 115, none spilled; the 5-wave instance needs it to
 # fit 96 VGPRs)
 _NO_LICM = ("-mllvm", "-disable-machine-licm")
-DEFAULT_UNIT_FLAGS = {"j2t_kern_flat.hip": _NO_LICM, "j2t_kern_wave.hip": _NO_LICM, "j2t_kern_wave5.hip": _NO_LICM}
+DEFAULT_UNIT_FLAGS = {"j2t_kern_flat.hip": _NO_LICM, "j2t_kern_wave.hip": _NO_LICM, "j2t_kern_wave5.hip": _NO_LICM,
+                      "t2j_kern.hip": _NO_LICM}  # t2j: 144 -> 105 VGPRs
 MARK = b"dgj2t-build:"
 
 

@@ -12,11 +12,25 @@ using namespace dg;
 
 static const uint64_t T2J_DEEP_WS = (uint64_t)T2J_DEEP_BLOCKS * T2J_BLOCK * T2J_DEEP_DEPTH * sizeof(T2JFrame);
 
+/* lanes per message of the LDS-frame pass (t2j_kern.hip) from the batch's
+ * longest message: short messages want full waves, ~1 KB ones sparse waves;
+ * unknown or huge (a mixed batch) keep the middle. DG_T2J_SPREAD=1|2|4 forces. */
+static uint32_t t2j_spread(uint64_t max_len)
+{
+    const char *e = getenv("DG_T2J_SPREAD");
+    if (e) {
+        const int v = atoi(e);
+        return v == 1 || v == 4 ? (uint32_t)v : 2u;
+    }
+    if (max_len == 0 || max_len > 16384) return 2;
+    return max_len <= 512 ? 1 : 4;
+}
+
 /* one batch on stream s: the LDS-frame pass, the deep pass over what it
  * queued, then the queue counter reset; the scratch's `done` event after */
 static int t2j_launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *src, const uint64_t *in_off,
                       uint64_t n, uint64_t opts, uint8_t *out, const uint64_t *out_off, uint32_t *out_len,
-                      uint64_t *ret, hipStream_t s)
+                      uint64_t *ret, hipStream_t s, uint64_t max_len)
 {
     if (n == 0) return DG_OK;
     if (!d->d_side) return set_err(DG_E_DESC, "descriptor has no t2j side table (dg_desc_attach_t2j)");
@@ -44,7 +58,7 @@ static int t2j_launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
     P.deep_list = x->t2j_list;
     P.deep_count = x->d_counts + 3;
     P.ws = x->ws_t2j;
-    launch_t2j_kernels(n, s, P);
+    launch_t2j_kernels(n, s, P, t2j_spread(max_len));
     hipError_t e = hipGetLastError();
     (void)hipMemsetAsync(x->d_counts + 3, 0, 4, s);
     HIPCHK(hipEventRecord(x->done, s));
@@ -88,15 +102,24 @@ int dg_desc_attach_t2j(dg_desc *d, const void *side, size_t len)
 
 uint64_t dg_t2j_slot_bound(uint64_t len) { return (3 * len + 64 + 7) & ~7ull; }
 
-int dg_t2j_batch_device(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *d_thrift, const uint64_t *d_in_off,
-                        uint64_t n, uint64_t opts, uint8_t *d_out, const uint64_t *d_out_off, uint32_t *d_out_len,
-                        uint64_t *d_ret, void *stream)
+int dg_t2j_batch_device_ml(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *d_thrift,
+                           const uint64_t *d_in_off, uint64_t n, uint64_t opts, uint8_t *d_out,
+                           const uint64_t *d_out_off, uint32_t *d_out_len, uint64_t *d_ret, void *stream,
+                           uint64_t max_len)
 {
     if (!c || !d) return set_err(DG_E_INVALID, "null ctx/desc");
     std::lock_guard<std::mutex> g(c->mu);
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-    return t2j_launch(c, d, root, d_thrift, d_in_off, n, opts, d_out, d_out_off, d_out_len, d_ret, s);
+    return t2j_launch(c, d, root, d_thrift, d_in_off, n, opts, d_out, d_out_off, d_out_len, d_ret, s, max_len);
+}
+
+int dg_t2j_batch_device(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *d_thrift, const uint64_t *d_in_off,
+                        uint64_t n, uint64_t opts, uint8_t *d_out, const uint64_t *d_out_off, uint32_t *d_out_len,
+                        uint64_t *d_ret, void *stream)
+{
+    return dg_t2j_batch_device_ml(c, d, root, d_thrift, d_in_off, n, opts, d_out, d_out_off, d_out_len, d_ret, stream,
+                                  0);
 }
 
 int dg_t2j_batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *thrift, const uint64_t *in_off,
@@ -117,6 +140,8 @@ int dg_t2j_batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
     std::vector<uint64_t> todo(n);
     for (uint64_t i = 0; i < n; i++) todo[i] = i;
     std::vector<uint64_t> slot_of(n, 0); /* stage offset of message i's final bytes */
+    uint64_t max_len = 0;
+    for (uint64_t i = 0; i < n; i++) max_len = std::max<uint64_t>(max_len, in_off[i + 1] - in_off[i]);
     for (int pass = 0; pass < 2 && !todo.empty(); pass++) {
         const uint64_t m = todo.size();
         std::vector<uint64_t> io(m + 1), so(m + 1);
@@ -143,7 +168,7 @@ int dg_t2j_batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
         HIPCHK(hipMemcpyAsync(c->d_in_off, io.data(), (m + 1) * 8, hipMemcpyHostToDevice, s));
         HIPCHK(hipMemcpyAsync(c->d_out_off, so.data(), (m + 1) * 8, hipMemcpyHostToDevice, s));
         if ((rc = t2j_launch(c, d, root, c->d_json, c->d_in_off, m, opts, c->d_out, c->d_out_off, c->d_out_len,
-                             c->d_ret, s)))
+                             c->d_ret, s, max_len)))
             return rc;
         std::vector<uint64_t> r(m);
         std::vector<uint32_t> l(m);

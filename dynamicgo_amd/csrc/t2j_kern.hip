@@ -4,21 +4,20 @@
 namespace dg {
 
 /* one lane per message, frames in LDS; messages that need more frames are
- * queued for t2j_deep_kernel. Every T2J_SPREAD-th lane takes a message: the
- * per-lane walk is a chain of dependent loads, so more (sparser) waves per
- * SIMD hide more of it than full waves would (t2j-c3: 5.41 -> 4.00 ms at 2,
- * 5.68 at 4; t2j-c2 within 2 %). */
-#ifndef DG_T2J_SPREAD
-#define DG_T2J_SPREAD 2
-#endif
-constexpr uint32_t T2J_SPREAD = DG_T2J_SPREAD;
-constexpr uint32_t T2J_MPB = T2J_BLOCK / T2J_SPREAD; /* messages per block */
+ * queued for t2j_deep_kernel. Every SP-th lane takes a message: the per-lane
+ * walk is a chain of dependent loads, so sparser waves, more of them per
+ * SIMD, hide more of it. The best spread depends on the message size
+ * (measured, LICM off): t2j-c2 (~100 B) 0.0705 / 0.0739 / 0.0977 ms at spread
+ * 1 / 2 / 4; t2j-c3 (~1.2 KB) 5.59 / 3.95 / 3.76 ms. The host picks it from
+ * the batch's longest message (t2j_spread). */
+template <uint32_t SP>
 __global__ __launch_bounds__(T2J_BLOCK) void t2j_kernel(T2JParams P)
 {
-    __shared__ __attribute__((aligned(16))) T2JFrame lf[T2J_LDS_DEPTH * T2J_MPB];
-    if (threadIdx.x % T2J_SPREAD) return;
-    const uint32_t slot = threadIdx.x / T2J_SPREAD;
-    const uint64_t i = (uint64_t)blockIdx.x * T2J_MPB + slot;
+    constexpr uint32_t MPB = T2J_BLOCK / SP; /* messages per block */
+    __shared__ __attribute__((aligned(16))) T2JFrame lf[T2J_LDS_DEPTH * MPB];
+    if (threadIdx.x % SP) return;
+    const uint32_t slot = threadIdx.x / SP;
+    const uint64_t i = (uint64_t)blockIdx.x * MPB + slot;
     if (i >= P.n) return;
     const auto D = desc_view<1>((const __attribute__((address_space(1))) uint8_t *)(const void *)P.blob, P.hdr);
     const T2JSide X = t2j_side(P.side);
@@ -28,7 +27,7 @@ __global__ __launch_bounds__(T2J_BLOCK) void t2j_kernel(T2JParams P)
     Out o;
     o.init(P.out + P.out_off[i], P.out_off[i + 1] - P.out_off[i]);
     const uint64_t r = t2j_convert(D, X, s, P.root, P.opts, o,
-                                   (__attribute__((address_space(3))) T2JFrame *)(void *)&lf[slot], T2J_MPB,
+                                   (__attribute__((address_space(3))) T2JFrame *)(void *)&lf[slot], MPB,
                                    T2J_LDS_DEPTH);
     if ((uint8_t)r == DG_ST_DEEP) {
         P.deep_list[atomicAdd(P.deep_count, 1u)] = (uint32_t)i;
@@ -60,10 +59,12 @@ __global__ __launch_bounds__(T2J_BLOCK) void t2j_deep_kernel(T2JParams P)
     }
 }
 
-void launch_t2j_kernels(uint64_t n, hipStream_t s, const T2JParams &P)
+void launch_t2j_kernels(uint64_t n, hipStream_t s, const T2JParams &P, uint32_t spread)
 {
-    const uint32_t blocks = (uint32_t)((n + T2J_MPB - 1) / T2J_MPB);
-    hipLaunchKernelGGL(t2j_kernel, dim3(blocks), dim3(T2J_BLOCK), 0, s, P);
+    const uint32_t mpb = T2J_BLOCK / spread, blocks = (uint32_t)((n + mpb - 1) / mpb);
+    if (spread == 1) hipLaunchKernelGGL(t2j_kernel<1>, dim3(blocks), dim3(T2J_BLOCK), 0, s, P);
+    else if (spread == 4) hipLaunchKernelGGL(t2j_kernel<4>, dim3(blocks), dim3(T2J_BLOCK), 0, s, P);
+    else hipLaunchKernelGGL(t2j_kernel<2>, dim3(blocks), dim3(T2J_BLOCK), 0, s, P);
     hipLaunchKernelGGL(t2j_deep_kernel, dim3(T2J_DEEP_BLOCKS), dim3(T2J_BLOCK), 0, s, P);
 }
 }  // namespace dg

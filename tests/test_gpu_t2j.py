@@ -258,3 +258,59 @@ def test_device_entry_point(chk):
         if er == 0:
             assert out[int(oo[i]):int(oo[i]) + int(ol[i])].tobytes() == eo
     assert over > 0
+
+
+@pytest.mark.parametrize("spread", ["1", "2", "4", "auto"])
+def test_spreads_vs_checker(chk, spread, monkeypatch):
+    """The LDS-frame pass at each lanes-per-message spread (t2j_kern.hip), and
+    the host's own choice from the longest message: random all-types
+    messages (with mutations) and nested C3 Thrift, byte-exact."""
+    if spread != "auto":
+        monkeypatch.setenv("DG_T2J_SPREAD", spread)
+    td = t2jgen.all_types_desc()
+    fl = T.flatten(td)
+    rng = random.Random(77)
+    msgs = [t2jgen.gen_thrift(rng, td) for _ in range(700)]
+    msgs += [t2jgen.mutate(rng, t2jgen.gen_thrift(rng, td)) for _ in range(300)]
+    bad = compare(chk, fl, msgs, 0)
+    assert not bad, bad[:5]
+    ntd = W.nesting_i64_desc()
+    nfl = T.flatten(ntd)
+    thr, rets = conv.BinaryConv(conv.Options()).do_batch(ntd, W.gen_nested_batch(random.Random(43), 300))
+    assert not any(int(r) for r in rets)
+    bad = compare(chk, nfl, thr, 0)
+    assert not bad, bad[:3]
+
+
+def test_device_entry_point_ml(chk):
+    """dg_t2j_batch_device_ml (the longest message given) on C3-sized Thrift:
+    byte-exact through the spread-4 instance."""
+    import torch
+    ntd = W.nesting_i64_desc()
+    fl = T.flatten(ntd)
+    side = T.flatten_t2j(fl)
+    thr, rets = conv.BinaryConv(conv.Options()).do_batch(ntd, W.gen_nested_batch(random.Random(44), 2000))
+    assert not any(int(r) for r in rets)
+    a, off = W.arena(thr)
+    n = len(thr)
+    lens = np.diff(off).astype(np.int64)
+    oo = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum((lens * 3 + 64 + 7) // 8 * 8, out=oo[1:])
+    dev = torch.device("cuda:0")
+    ctx = conv.default_context()
+    dh = ctx.desc_t2j(fl)
+    d_src = torch.from_numpy(a).to(dev)
+    d_in = torch.from_numpy(off.astype(np.int64)).to(dev)
+    d_oo = torch.from_numpy(oo).to(dev)
+    d_out = torch.zeros(int(oo[-1]) + 64, dtype=torch.uint8, device=dev)
+    d_ol = torch.zeros(n, dtype=torch.int32, device=dev)
+    d_ret = torch.zeros(n, dtype=torch.int64, device=dev)
+    _lib.check(_lib.lib().dg_t2j_batch_device_ml(ctx.h, dh, fl.root_type, d_src.data_ptr(), d_in.data_ptr(), n, 0,
+                                                 d_out.data_ptr(), d_oo.data_ptr(), d_ol.data_ptr(),
+                                                 d_ret.data_ptr(), torch.cuda.current_stream().cuda_stream,
+                                                 int(lens.max())))
+    torch.cuda.synchronize()
+    out, ol, ret = d_out.cpu().numpy(), d_ol.cpu().numpy(), d_ret.cpu().numpy()
+    for i, m in enumerate(thr):
+        er, eo = chk.t2j(fl, side, m, 0)
+        assert (int(ret[i]), out[int(oo[i]):int(oo[i]) + int(ol[i])].tobytes()) == (er, eo)
