@@ -93,9 +93,13 @@ def rank_workload(cfg: str, rank: int, world: int, workers: int = 1, c5_n: int =
     size = CONFIGS[cfg][1]
     if cfg == "c5":
         n = c5_n or size
-        a, off = W.gen_mixed_arena(n, 45, workers=workers, large_scale=c5_scale)
+        if world > 1:  # generated once per node (/dev/shm), mapped by every rank
+            a, off = c5_shared_arena(n, 45, c5_scale, gen_workers())
+        else:
+            a, off = W.gen_mixed_arena(n, 45, workers=workers, large_scale=c5_scale)
         lo, hi = shard_ranges(off, world)[rank]
         sa, so = W.arena_slice(a, off, lo, hi)
+        del a
         return W.mixed_desc(), sa, so, {"global_batch": n, "global_json_bytes": int(off[-1]), "shard": [lo, hi]}
     if cfg.startswith("t2j-"):
         cfg = cfg[4:]
@@ -112,6 +116,52 @@ def rank_workload(cfg: str, rank: int, world: int, workers: int = 1, c5_n: int =
         td, msgs = W.simple_desc(), [W.c1_simple_json()] * size
     a, off = W.arena(msgs)
     return td, a, off, {"global_batch": size * world, "global_json_bytes": None, "shard": None}
+
+
+def gen_workers() -> int:
+    """Worker processes for generating the C5 batch: the CPUs this process may
+    use (the ranks of one node wait for the one that generates)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(2, min(n, 32))
+
+
+def _c5_cache_base(n: int, seed: int, scale: float) -> str:
+    job = os.environ.get("MASTER_PORT", "0")
+    return f"/dev/shm/dgj2t_c5_{n}_{seed}_{scale}_{job}"
+
+
+def c5_shared_arena(n: int, seed: int, scale: float, workers: int):
+    """The ONE C5 batch of a multi-rank run: the first rank to take the lock
+    generates it (all its CPUs) into /dev/shm; the others wait for the lock and
+    map the same files read-only. release_c5_cache() unlinks them once every
+    rank has sliced its shard."""
+    import fcntl
+    from dynamicgo_amd import workloads as W
+    base = _c5_cache_base(n, seed, scale)
+    with open(base + ".lock", "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        if not (os.path.exists(base + ".off.npy") and os.path.exists(base + ".arena.npy")):
+            a, off = W.gen_mixed_arena(n, seed, workers=workers, large_scale=scale)
+            for name, arr in (("arena", a), ("off", off)):
+                tmp = f"{base}.{name}.tmp.npy"
+                np.save(tmp, arr)
+                os.replace(tmp, f"{base}.{name}.npy")
+            del a, off
+        fcntl.flock(lk, fcntl.LOCK_UN)
+    return np.load(base + ".arena.npy", mmap_mode="r"), np.load(base + ".off.npy")
+
+
+def release_c5_cache(n: int = None, seed: int = 45, scale: float = 1.0):
+    """Unlink the node's C5 cache (call after a barrier: every rank has its shard)."""
+    base = _c5_cache_base(n or CONFIGS["c5"][1], seed, scale)
+    for suf in (".arena.npy", ".off.npy", ".lock"):
+        try:
+            os.unlink(base + suf)
+        except FileNotFoundError:
+            pass
 
 
 def share_descriptor(flat, rank: int, dev, backend: str):
@@ -136,18 +186,23 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def cpu_baseline(flat, arena, off, flags, budget_s: float = 8.0):
+def cpu_baseline(flat, arena, off, flags, budget_s: float = 6.0):
     """The reference's own native/*.c (oracle/_ref, clang -O3 like the
-    reference's build) on this host: one pinned thread per physical core of
-    this process's CPU share (<= CPU_SHARE), byte-balanced shards, outputs
-    preallocated and first touched by an untimed pass, best of reps; plus the
-    same on one core over a bounded prefix."""
+    reference's build) on this host, outputs preallocated and first touched by
+    an untimed pass, best of reps, byte-balanced shards, threads pinned to
+    distinct physical cores:
+      * value: ALL physical cores this process may use (one
+        thread per physical core);
+      * share: min(CPU_SHARE, physical) cores, the host CPUs the GPU box
+        grants per GPU;
+      * one core over a bounded prefix."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # reported baseline only
     ref = oracle.RefOracle()
     if ref is None:
         return None
     phys, logical = oracle.physical_cpus()
+    cores_all = max(1, len(phys))
     cores = max(1, min(CPU_SHARE, len(phys)))
     n = len(off) - 1
     nbytes = int(off[-1] - off[0])
@@ -157,20 +212,23 @@ def cpu_baseline(flat, arena, off, flags, budget_s: float = 8.0):
         reps = int(max(3, min(200, budget_s / 2 / max(t1, 1e-6))))
         return ref.j2t_timed(flat, a, o, flags, cpus, reps), reps
 
-    t_all, reps_all = timed(arena, off, phys[:cores])
+    t_all, reps_all = timed(arena, off, phys[:cores_all])
+    t_share, reps_share = (t_all, reps_all) if cores == cores_all else timed(arena, off, phys[:cores])
     # one core: a prefix of at most ~64 MB / 65536 messages
     k = int(min(n, 65536, max(1, np.searchsorted(off, off[0] + 64 * 1024 * 1024))))
     a1, o1 = arena[:int(off[k]) + 64], off[:k + 1]
     t_one, reps_one = timed(a1, o1, phys[:1])
     one_bytes = int(o1[-1] - o1[0])
-    return {"value": round(nbytes / t_all / 1e9, 4), "unit": "GB/s", "cores": cores, "kind": "reference",
-            "msgs_per_s": round(n / t_all),
+    return {"value": round(nbytes / t_all / 1e9, 4), "unit": "GB/s", "cores": cores_all, "kind": "reference",
+            "cpu_model": cpu_model(), "msgs_per_s": round(n / t_all),
+            "share": {"cores": cores, "value": round(nbytes / t_share / 1e9, 4), "msgs_per_s": round(n / t_share),
+                      "note": f"the {CPU_SHARE} CPUs per GPU the box grants"},
             "one_core_gbs": round(one_bytes / t_one / 1e9, 4), "one_core_ns_per_msg": round(t_one / k * 1e9, 1),
-            "per_core_gbs": round(nbytes / t_all / 1e9 / cores, 4),
+            "per_core_gbs": round(nbytes / t_all / 1e9 / cores_all, 4),
             "sample": f"all-core: the rank's whole batch ({n} msgs, {nbytes} B), best of {reps_all} passes, "
-                      f"{cores} threads pinned to distinct physical cores of '{cpu_model()}' "
-                      f"(affinity: {logical} logical CPUs = {len(phys)} physical cores; the box grants "
-                      f"{CPU_SHARE} CPUs per GPU); one-core: first {k} msgs ({one_bytes} B), best of {reps_one}; "
+                      f"{cores_all} threads pinned to distinct physical cores of '{cpu_model()}' "
+                      f"(affinity: {logical} logical CPUs = {len(phys)} physical cores); share: {cores} cores, "
+                      f"best of {reps_share}; one-core: first {k} msgs ({one_bytes} B), best of {reps_one}; "
                       f"reference native.c built by oracle/Makefile (clang -O3 -mavx2)"}
 
 
@@ -481,6 +539,10 @@ def main(argv=None):
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         kw = {"device_id": dev} if backend == "nccl" else {}
         torch.distributed.init_process_group(backend, rank=rank, world_size=world, **kw)
+        if args.config == "c5":  # every rank holds its shard: drop the node's shared copy
+            torch.distributed.barrier()
+            if local == 0:
+                release_c5_cache()
 
     if args.config.startswith("t2j-"):
         return bench_t2j(args, rank, world, dev, dist, backend, td, arena, off, meta)

@@ -12,7 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DG_LIB_PATH") or os.path.join(HERE, "libdgj2t.so")
 
 # symbols include/dgj2t.h declares (checked by tests/test_abi.py)
-EXPORTS = ["dg_last_error", "dg_build_info", "dg_ctx_create", "dg_ctx_destroy", "dg_ctx_stream", "dg_ctx_stats", "dg_ctx_counters",
+EXPORTS = ["dg_last_error", "dg_build_info", "dg_ctx_create", "dg_ctx_destroy", "dg_ctx_stream", "dg_ctx_stats", "dg_ctx_counters", "dg_ctx_set_knob", "dg_ctx_get_knob",
            "dg_desc_create",
            "dg_desc_create_device", "dg_desc_destroy", "dg_desc_root", "dg_j2t_batch_device",
            "dg_j2t_batch_device_ml", "dg_j2t_batch_device_iters",
@@ -52,6 +52,8 @@ def lib() -> C.CDLL:
         "dg_ctx_stream": (vp, [vp]),
         "dg_ctx_stats": (i32, [vp, P64, P64, i32]),
         "dg_ctx_counters": (i32, [vp, P64, i32, i32]),
+        "dg_ctx_set_knob": (i32, [vp, C.c_char_p, C.c_int64]),
+        "dg_ctx_get_knob": (i32, [vp, C.c_char_p, C.POINTER(C.c_int64)]),
         "dg_desc_create": (i32, [vp, C.c_char_p, sz, C.POINTER(vp)]),
         "dg_desc_create_device": (i32, [vp, vp, sz, C.POINTER(vp)]),
         "dg_desc_destroy": (None, [vp]),

@@ -197,6 +197,32 @@ class Context:
         _lib.check(_lib.lib().dg_ctx_stats(self.h, C.byref(b), C.byref(d), int(reset)))
         return int(b.value), int(d.value)
 
+    def set_knob(self, name: str, value: int):
+        """A routing knob (dg_ctx_set_knob, include/dgj2t.h): "flat",
+        "wave_min", "wave_occ", "small_mpw", "list_blocks", "t2j_spread"."""
+        _lib.check(_lib.lib().dg_ctx_set_knob(self.h, name.encode(), int(value)))
+
+    def get_knob(self, name: str) -> int:
+        v = C.c_int64(0)
+        _lib.check(_lib.lib().dg_ctx_get_knob(self.h, name.encode(), C.byref(v)))
+        return int(v.value)
+
+    def knobs(self, **kv):
+        """Context manager: set knobs, restore them on exit."""
+        import contextlib
+
+        @contextlib.contextmanager
+        def cm():
+            old = {k: self.get_knob(k) for k in kv}
+            try:
+                for k, v in kv.items():
+                    self.set_knob(k, v)
+                yield self
+            finally:
+                for k, v in old.items():
+                    self.set_knob(k, v)
+        return cm()
+
     def close(self):
         L = _lib.lib()
         for d in self._descs.values():

@@ -30,6 +30,9 @@ __attribute__((visibility("hidden"))) int set_err(int code, const char *fmt, ...
  * launch on another stream waits for its previous launch (hipStreamWaitEvent
  * on `done`), which keeps the ordering rule true in every case. */
 constexpr int DG_MAX_SCRATCH = 8;
+constexpr uint32_t DG_NCOUNTS = 12;
+constexpr uint32_t DG_J2T_COUNTS_BYTES = 6 * 4;
+constexpr uint32_t DG_T2J_DEEP_COUNT = 8;
 struct Scratch {
     hipStream_t owner = nullptr;   /* the stream it was created for */
     hipStream_t last = nullptr;    /* stream of the last launch that used it */
@@ -38,9 +41,14 @@ struct Scratch {
     uint8_t *ws_fast = nullptr;
     uint64_t ws_fast_lanes = 0;
     uint64_t *d_deep_list = nullptr;
-    /* [0] bails, [1] large messages, [2] wave queue, [3] t2j deep count, [4] deep count,
-     * [5] blocks done (deep pass): self-reset by the list-mode launch;
-     * [6] arrivals, [7] departures of dg_pack_device_scan: self-reset */
+    /* DG_NCOUNTS u32 counters, each owned by ONE path:
+     * j2t: [0] bails, [1] large messages, [2] wave queue, [3] huge messages,
+     *      [4] deep count, [5] blocks done (deep pass) -- [0..5] are reset by
+     *      the launch's last kernel (list mode), or by a stream memset of
+     *      DG_J2T_COUNTS_BYTES when an enqueue fails half way;
+     * pack: [6] arrivals, [7] departures of dg_pack_device_scan (self-reset);
+     * t2j: [8] deep-pass queue length (reset by a stream memset after the
+     *      t2j launch). */
     uint32_t *d_counts = nullptr;
     uint32_t *d_bail_list = nullptr;
     uint64_t bail_cap = 0;
@@ -51,16 +59,26 @@ struct Scratch {
     uint64_t *d_sums = nullptr;    /* dg_pack_device_scan: per-block byte totals (n_cu) */
     uint8_t *d_frame = nullptr;    /* dg_pack_device_framed: header + footer bytes */
     std::vector<uint8_t> frame;    /* what d_frame holds */
-    uint8_t *ws_t2j = nullptr;     /* t2j deep pass: T2J_DEEP_DEPTH frames per lane */
-    uint32_t *t2j_list = nullptr;  /* t2j: messages queued for the deep pass ([3] of d_counts counts them) */
+    uint32_t *t2j_list = nullptr;  /* t2j: messages queued for the deep pass ([8] of d_counts counts them) */
     uint64_t t2j_list_cap = 0;
 };
 constexpr uint32_t FRAME_CAP = 4096;
+
+/* routing knobs: env at dg_ctx_create, then dg_ctx_set_knob (include/dgj2t.h) */
+struct Knobs {
+    int64_t flat = -1;
+    int64_t wave_min = 512;
+    int64_t wave_occ = 0;
+    int64_t small_mpw = 64;
+    int64_t list_blocks = 16;
+    int64_t t2j_spread = 0;
+};
 
 struct dg_ctx {
     int device;
     hipStream_t stream;
     int n_cu = 0;
+    Knobs knobs;
     uint32_t *d_pending = nullptr;
     unsigned long long *d_stats = nullptr; /* {bails, deeps} since the last dg_ctx_stats reset */
     std::vector<Scratch *> scratch;
@@ -73,7 +91,30 @@ struct dg_ctx {
     uint64_t *d_out_off = nullptr; uint64_t d_oo_cap = 0;
     uint32_t *d_out_len = nullptr; uint64_t d_ol_cap = 0;
     uint64_t *d_ret = nullptr; uint64_t d_ret_cap = 0;
+    uint8_t *d_pack = nullptr; uint64_t d_pack_cap = 0;      /* packed Thrift (dg_pack_device_scan) */
+    uint64_t *d_pack_off = nullptr; uint64_t d_po_cap = 0;
+    uint8_t *h_up = nullptr; uint64_t h_up_cap = 0;          /* pinned: offsets + JSON, one H2D */
+    uint8_t *h_down = nullptr; uint64_t h_down_cap = 0;      /* pinned: ret + out_len (+ packed bytes) */
+    /* t2j deep pass: T2J_DEEP_DEPTH frames per lane, ONE per context (about
+     * 100 MB, allocated by the first t2j launch), ordered across streams by
+     * ws_t2j_done recorded after each deep pass on ws_t2j_last */
+    uint8_t *ws_t2j = nullptr;
+    hipEvent_t ws_t2j_done = nullptr;
+    hipStream_t ws_t2j_last = nullptr;
 };
+
+/* pinned host staging, grown on demand (hipHostMalloc is slow: keep it) */
+static inline int grow_pinned(uint8_t *&p, uint64_t &cap, uint64_t want)
+{
+    if (cap >= want) return DG_OK;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    uint64_t nc = std::max<uint64_t>(want, cap * 2);
+    nc = std::max<uint64_t>(nc, 1 << 16);
+    HIPCHK(hipHostMalloc((void **)&p, nc, hipHostMallocDefault));
+    cap = nc;
+    return DG_OK;
+}
 
 struct dg_desc {
     dg_ctx *ctx;

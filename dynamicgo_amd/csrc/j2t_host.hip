@@ -48,7 +48,6 @@ static void scratch_free(Scratch *x)
     (void)hipFree(x->ws_deep);
     (void)hipFree(x->d_sums);
     (void)hipFree(x->d_frame);
-    (void)hipFree(x->ws_t2j);
     (void)hipFree(x->t2j_list);
     if (x->done) (void)hipEventDestroy(x->done);
     delete x;
@@ -59,8 +58,8 @@ static int scratch_new(dg_ctx *c, hipStream_t owner, Scratch **out)
     Scratch *x = new Scratch();
     x->owner = owner;
     hipError_t e = hipEventCreateWithFlags(&x->done, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipMalloc(&x->d_counts, 32);
-    if (e == hipSuccess) e = hipMemset(x->d_counts, 0, 32);
+    if (e == hipSuccess) e = hipMalloc(&x->d_counts, DG_NCOUNTS * 4);
+    if (e == hipSuccess) e = hipMemset(x->d_counts, 0, DG_NCOUNTS * 4);
     if (e == hipSuccess) e = hipMalloc(&x->ws_deep, DEEP_WS_STRIDE * DEEP_THREADS);
     if (e == hipSuccess) e = hipMalloc(&x->ws_wave, (size_t)c->n_cu * std::max(WV_BLOCKS_PER_CU, WV5_BLOCKS_PER_CU) * WV_WAVES * DCAP);
     if (e == hipSuccess) e = hipMalloc(&x->d_sums, (size_t)c->n_cu * 8);
@@ -101,6 +100,18 @@ int scratch_for(dg_ctx *c, hipStream_t s, Scratch **out)
  * from (checked by _lib.lib() against the sources next to it) */
 static const char g_build_info[] = "dgj2t-build:" DG_SRC_HASH " arch:gfx950";
 
+static int64_t *knob_ref(dg_ctx *c, const char *name)
+{
+    Knobs &K = c->knobs;
+    if (!strcmp(name, "flat")) return &K.flat;
+    if (!strcmp(name, "wave_min")) return &K.wave_min;
+    if (!strcmp(name, "wave_occ")) return &K.wave_occ;
+    if (!strcmp(name, "small_mpw")) return &K.small_mpw;
+    if (!strcmp(name, "list_blocks")) return &K.list_blocks;
+    if (!strcmp(name, "t2j_spread")) return &K.t2j_spread;
+    return nullptr;
+}
+
 extern "C" {
 
 const char *dg_last_error(void) { return g_err; }
@@ -124,7 +135,35 @@ int dg_ctx_create(int device, dg_ctx **out)
     HIPCHK(hipMalloc(&c->d_stats, 16 * 8));
     HIPCHK(hipMemset(c->d_stats, 0, 16 * 8));
     HIPCHK(hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device));
+    /* routing knobs: the environment is read here, once per context */
+    static const struct { const char *env; const char *name; } envk[] = {
+        {"DG_FLAT", "flat"}, {"DG_WAVE_MIN", "wave_min"}, {"DG_WAVE_OCC", "wave_occ"},
+        {"DG_SMALL_MPW", "small_mpw"}, {"DG_LIST_BLOCKS", "list_blocks"}, {"DG_T2J_SPREAD", "t2j_spread"}};
+    for (const auto &e : envk) {
+        const char *v = getenv(e.env);
+        if (v && *v) *knob_ref(c, e.name) = strtoll(v, nullptr, 10);
+    }
     *out = c;
+    return DG_OK;
+}
+
+int dg_ctx_set_knob(dg_ctx *c, const char *name, int64_t value)
+{
+    if (!c || !name) return set_err(DG_E_INVALID, "null ctx/name");
+    std::lock_guard<std::mutex> g(c->mu);
+    int64_t *k = knob_ref(c, name);
+    if (!k) return set_err(DG_E_INVALID, "unknown knob '%s'", name);
+    *k = value;
+    return DG_OK;
+}
+
+int dg_ctx_get_knob(dg_ctx *c, const char *name, int64_t *value)
+{
+    if (!c || !name || !value) return set_err(DG_E_INVALID, "bad args");
+    std::lock_guard<std::mutex> g(c->mu);
+    int64_t *k = knob_ref(c, name);
+    if (!k) return set_err(DG_E_INVALID, "unknown knob '%s'", name);
+    *value = *k;
     return DG_OK;
 }
 
@@ -143,6 +182,12 @@ void dg_ctx_destroy(dg_ctx *c)
     (void)hipFree(c->d_out_off);
     (void)hipFree(c->d_out_len);
     (void)hipFree(c->d_ret);
+    (void)hipFree(c->d_pack);
+    (void)hipFree(c->d_pack_off);
+    (void)hipHostFree(c->h_up);
+    (void)hipHostFree(c->h_down);
+    (void)hipFree(c->ws_t2j);
+    if (c->ws_t2j_done) (void)hipEventDestroy(c->ws_t2j_done);
     (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -278,10 +323,10 @@ static int enqueue(dg_ctx *c, Scratch *x, const dg_desc *d, uint32_t root, const
     const bool no_wave = (flags & DG_F_NO_WAVE_PATH) != 0;
     /* flat roots go to the field-major flat kernel when the batch's messages
      * fit it (max_len unknown: longer ones are listed for the wave kernel) */
-    const char *fl_env = getenv("DG_FLAT");
-    const bool use_flat = fl_env ? atoi(fl_env) != 0
-                                 : (flags & DG_F_FLAT_PATH) != 0 ||
-                                       (!(flags & DG_F_NO_FLAT_PATH) && (max_len == 0 || max_len <= FL_MAXLEN));
+    const Knobs &K = c->knobs;
+    const bool use_flat = K.flat >= 0 ? K.flat != 0
+                                      : (flags & DG_F_FLAT_PATH) != 0 ||
+                                            (!(flags & DG_F_NO_FLAT_PATH) && (max_len == 0 || max_len <= FL_MAXLEN));
     flags &= ~(DG_F_NO_WAVE_PATH | DG_F_FLAT_PATH | DG_F_NO_FLAT_PATH);
     Params P;
     P.root = root;
@@ -319,15 +364,13 @@ static int enqueue(dg_ctx *c, Scratch *x, const dg_desc *d, uint32_t root, const
     DP.done = x->d_counts + 5;
     DP.blob = d->d_blob;
     DP.hdr = d->hdr;
-    const char *wm = getenv("DG_WAVE_MIN"); /* messages longer than this go to the wave kernel */
-    const uint64_t big_max = wm ? strtoull(wm, nullptr, 10) : (uint64_t)WV_MIN_DEFAULT;
+    const uint64_t big_max = (uint64_t)K.wave_min; /* messages longer than this go to the wave kernel */
     const bool wave = P.fast && !no_wave && d->hdr.total_len <= WV_DESC && d->hdr.total_len <= DESC_LDS_BYTES &&
                       (max_len == 0 || max_len > big_max);
     /* the wave kernel's instance: 5 waves/SIMD when the caller's max_len
      * rules out huge messages (their tail grows with a fifth wave per SIMD,
-     * j2t_wave.h), else 4; DG_WAVE_OCC=4|5 forces one */
-    const char *occ_env = getenv("DG_WAVE_OCC");
-    const bool wave5 = occ_env ? atoi(occ_env) == 5 : (max_len != 0 && max_len <= WV_HUGE_MIN);
+     * j2t_wave.h), else 4; the wave_occ knob (4|5) forces one */
+    const bool wave5 = K.wave_occ ? K.wave_occ == 5 : (max_len != 0 && max_len <= WV_HUGE_MIN);
     auto wave_launch = [&](hipStream_t st, const Params &Q, const WaveParams &W) {
         const uint64_t bpc = wave5 ? WV5_BLOCKS_PER_CU : WV_BLOCKS_PER_CU;
         const uint64_t wblocks = std::min<uint64_t>((n + WV_WAVES - 1) / WV_WAVES, (uint64_t)c->n_cu * bpc);
@@ -338,8 +381,7 @@ static int enqueue(dg_ctx *c, Scratch *x, const dg_desc *d, uint32_t root, const
         if (d->hdr.total_len <= DESC_LDS_BYTES) launch_lane_kernel_lds(g, s, Q, DP);
         else launch_lane_kernel_glb(g, s, Q, DP);
     };
-    const char *sm_env = getenv("DG_SMALL_MPW"); /* 0: lane kernel (in-kernel exact machine) */
-    const int mpw = sm_env ? atoi(sm_env) : 64;
+    const int mpw = (int)K.small_mpw; /* 0: lane kernel (in-kernel exact machine) */
     const bool small = P.fast && !no_wave && mpw > 0 && d->hdr.total_len <= SM_DESC;
     if (small) {
         /* 1. small kernel: lane-per-message fast path; declines -> bail list,
@@ -393,8 +435,7 @@ static int enqueue(dg_ctx *c, Scratch *x, const dg_desc *d, uint32_t root, const
         P3.list = x->d_bail_list;
         P3.list_count = x->d_counts;
         P3.reset2 = x->d_counts + 1; /* P3.fast stays set: the small kernel's declines try the full fast path */
-        const char *lb_env = getenv("DG_LIST_BLOCKS"); /* list-pass grid (default 16) */
-        const uint64_t lb = lb_env ? std::max<uint64_t>(1, strtoull(lb_env, nullptr, 10)) : 16;
+        const uint64_t lb = (uint64_t)std::max<int64_t>(1, K.list_blocks); /* list-pass grid */
         lane_launch(dim3((uint32_t)std::min<uint64_t>(blocks, lb)), P3);
     } else if (!wave) {
         lane_launch(dim3((uint32_t)blocks), P);
@@ -450,7 +491,7 @@ static int launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *jso
     int rc = scratch_for(c, s, &x);
     if (rc) return rc;
     rc = enqueue(c, x, d, root, json, in_off, n, flags, out, out_off, out_len, ret, pending, s, max_len);
-    if (rc) (void)hipMemsetAsync(x->d_counts, 0, 32, s);
+    if (rc) (void)hipMemsetAsync(x->d_counts, 0, DG_J2T_COUNTS_BYTES, s);
     HIPCHK(hipEventRecord(x->done, s));
     x->used = true;
     x->last = s;
@@ -495,6 +536,19 @@ int dg_j2t_batch_device_iters(dg_ctx *c, const dg_desc *d, uint32_t root, const 
     return DG_OK;
 }
 
+/* dg_pack_device_scan / _framed without the context lock (the caller holds it) */
+static int pack_scan_nolock(dg_ctx *c, const uint8_t *d_out, const uint64_t *d_out_off, const uint32_t *d_out_len,
+                            const uint64_t *d_ret, uint64_t n, const uint8_t *hdr, uint32_t hdr_len, const uint8_t *ftr,
+                            uint32_t ftr_len, uint8_t *d_dst, uint64_t *d_dst_off, hipStream_t s);
+
+/* Host batch: ONE pinned upload [in_off | out_off | JSON], the kernels, a
+ * device packing pass (used slot prefixes back to back, failed messages
+ * dropped), then ONE download of [ret | out_len | packed Thrift] when the
+ * batch is small (<= HOST_ONE_TRIP slot bytes), else [ret | out_len] and
+ * then exactly the packed bytes. Slot overflows (rare) are rerun together in
+ * one exact-size launch on the same staging. */
+static const uint64_t HOST_ONE_TRIP = 4ull << 20;
+
 int dg_j2t_batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *json, const uint64_t *in_off,
                       uint64_t n, uint64_t flags, uint8_t *out, uint64_t out_cap, uint64_t *out_off, uint64_t *ret,
                       uint64_t *out_need)
@@ -503,67 +557,99 @@ int dg_j2t_batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
     std::lock_guard<std::mutex> g(c->mu);
     HIPCHK(hipSetDevice(c->device));
     int rc;
-    uint64_t base = in_off[0], bytes = in_off[n] - in_off[0];
-    std::vector<uint64_t> ioff(n + 1), soff(n + 1);
+    hipStream_t s = c->stream;
+    const uint64_t base = in_off[0], bytes = in_off[n] - in_off[0];
+    /* upload: [ioff (n+1) | soff (n+1) | JSON + 64 zero bytes] */
+    const uint64_t up_bytes = 16 * (n + 1) + bytes + 64;
+    if ((rc = grow_pinned(c->h_up, c->h_up_cap, up_bytes))) return rc;
+    uint64_t *ioff = (uint64_t *)(void *)c->h_up, *soff = ioff + n + 1;
+    uint8_t *hj = (uint8_t *)(void *)(soff + n + 1);
+    uint64_t max_len = 1;
     soff[0] = 0;
     for (uint64_t i = 0; i <= n; i++) ioff[i] = in_off[i] - base;
-    for (uint64_t i = 0; i < n; i++) soff[i + 1] = soff[i] + dg_slot_bound(ioff[i + 1] - ioff[i]);
-    if ((rc = grow(c->d_json, c->d_json_cap, bytes + 64))) return rc;
-    if ((rc = grow(c->d_in_off, c->d_in_cap, n + 1))) return rc;
-    if ((rc = grow(c->d_out, c->d_out_cap, soff[n] + 64))) return rc;
-    if ((rc = grow(c->d_out_off, c->d_oo_cap, n + 1))) return rc;
-    if ((rc = grow(c->d_out_len, c->d_ol_cap, n + 1))) return rc;
-    if ((rc = grow(c->d_ret, c->d_ret_cap, n + 1))) return rc;
-    hipStream_t s = c->stream;
-    HIPCHK(hipMemcpyAsync(c->d_json, json + base, bytes, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemsetAsync(c->d_json + bytes, 0, 64, s));
-    HIPCHK(hipMemcpyAsync(c->d_in_off, ioff.data(), (n + 1) * 8, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(c->d_out_off, soff.data(), (n + 1) * 8, hipMemcpyHostToDevice, s));
-    uint64_t max_len = 1;
-    for (uint64_t i = 0; i < n; i++) max_len = std::max<uint64_t>(max_len, ioff[i + 1] - ioff[i]);
-    if ((rc = launch(c, d, root, c->d_json, c->d_in_off, n, flags, c->d_out, c->d_out_off, c->d_out_len, c->d_ret,
-                     nullptr, s, max_len)))
+    for (uint64_t i = 0; i < n; i++) {
+        const uint64_t l = ioff[i + 1] - ioff[i];
+        max_len = std::max<uint64_t>(max_len, l);
+        soff[i + 1] = soff[i] + dg_slot_bound(l);
+    }
+    if (bytes) memcpy(hj, json + base, bytes);
+    memset(hj + bytes, 0, 64);
+    const uint64_t slots = soff[n];
+    /* download: [ret (n u64) | out_len (n u32, padded to 8) | packed] */
+    const uint64_t head = 8 * n + ((4 * n + 7) & ~7ull);
+    const bool one_trip = slots <= HOST_ONE_TRIP;
+    if ((rc = grow(c->d_json, c->d_json_cap, up_bytes))) return rc;
+    if ((rc = grow(c->d_out, c->d_out_cap, slots + 64))) return rc;
+    if ((rc = grow(c->d_pack, c->d_pack_cap, head + slots + 64))) return rc;
+    if ((rc = grow(c->d_pack_off, c->d_po_cap, n + 1))) return rc;
+    if ((rc = grow_pinned(c->h_down, c->h_down_cap, one_trip ? head + slots + 64 : head + 8))) return rc;
+    const uint64_t *d_in = (const uint64_t *)(void *)c->d_json, *d_oo = d_in + n + 1;
+    const uint8_t *d_j = c->d_json + 16 * (n + 1);
+    uint64_t *d_ret = (uint64_t *)(void *)c->d_pack;
+    uint32_t *d_ol = (uint32_t *)(void *)(c->d_pack + 8 * n);
+    uint8_t *d_packed = c->d_pack + head;
+    HIPCHK(hipMemcpyAsync(c->d_json, c->h_up, up_bytes, hipMemcpyHostToDevice, s));
+    if ((rc = launch(c, d, root, d_j, d_in, n, flags, c->d_out, d_oo, d_ol, d_ret, nullptr, s, max_len))) return rc;
+    if ((rc = pack_scan_nolock(c, c->d_out, d_oo, d_ol, d_ret, n, nullptr, 0, nullptr, 0, d_packed, c->d_pack_off, s)))
         return rc;
-    std::vector<uint32_t> olen(n);
-    HIPCHK(hipMemcpyAsync(ret, c->d_ret, n * 8, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(olen.data(), c->d_out_len, n * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(c->h_down, c->d_pack, one_trip ? head + slots : head, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    /* overflowed messages: rerun each with an exact-size slot (GPU) */
+    const uint64_t *hret = (const uint64_t *)(void *)c->h_down;
+    const uint32_t *hol = (const uint32_t *)(void *)(c->h_down + 8 * n);
+    std::vector<uint32_t> olen(hol, hol + n);
+    memcpy(ret, hret, n * 8);
+    /* the packed bytes: failed and overflowed messages hold none */
+    uint64_t packed = 0;
+    for (uint64_t i = 0; i < n; i++)
+        if (ret[i] == 0) packed += olen[i];
+    /* overflowed messages: rerun together, each in a slot of the size it
+     * reported (out_len carries it), on the same device staging (free now) */
     std::vector<uint64_t> redo;
     for (uint64_t i = 0; i < n; i++)
         if ((uint8_t)ret[i] == DG_ST_OUT_OVERFLOW) redo.push_back(i);
-    std::vector<std::vector<uint8_t>> redo_out(redo.size());
-    for (size_t k = 0; k < redo.size(); k++) {
-        uint64_t i = redo[k];
-        uint64_t need = olen[i]; /* DG_ST_OUT_OVERFLOW: out_len carries the bytes needed */
-        uint64_t one_in[2] = {0, ioff[i + 1] - ioff[i]};
-        uint64_t one_out[2] = {0, need + 64};
-        uint8_t *d1;
-        uint64_t *d_io, *d_oo, *d_r;
-        uint32_t *d_ol;
-        HIPCHK(hipMalloc(&d1, one_out[1]));
-        HIPCHK(hipMalloc(&d_io, 16));
-        HIPCHK(hipMalloc(&d_oo, 16));
-        HIPCHK(hipMalloc(&d_r, 8));
-        HIPCHK(hipMalloc(&d_ol, 4));
-        HIPCHK(hipMemcpyAsync(d_io, one_in, 16, hipMemcpyHostToDevice, s));
-        HIPCHK(hipMemcpyAsync(d_oo, one_out, 16, hipMemcpyHostToDevice, s));
-        rc = launch(c, d, root, c->d_json + ioff[i], d_io, 1, flags, d1, d_oo, d_ol, d_r, nullptr, s);
-        if (rc) return rc;
-        uint32_t l1;
-        HIPCHK(hipMemcpyAsync(&ret[i], d_r, 8, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipMemcpyAsync(&l1, d_ol, 4, hipMemcpyDeviceToHost, s));
+    std::vector<uint8_t> main_buf, rdown; /* host copies: main packed bytes (two-trip case), redo results */
+    std::vector<uint64_t> redo_so;
+    uint64_t rhead = 0;
+    if (!redo.empty()) {
+        const uint64_t m = redo.size();
+        uint64_t rb = 0;
+        for (uint64_t i : redo) rb += ioff[i + 1] - ioff[i];
+        std::vector<uint8_t> up(16 * (m + 1) + rb + 64, 0);
+        uint64_t *io = (uint64_t *)(void *)up.data(), *so = io + m + 1;
+        uint8_t *rj = (uint8_t *)(void *)(so + m + 1);
+        io[0] = so[0] = 0;
+        for (uint64_t k = 0; k < m; k++) {
+            const uint64_t i = redo[k], l = ioff[i + 1] - ioff[i];
+            memcpy(rj + io[k], hj + ioff[i], l);
+            io[k + 1] = io[k] + l;
+            so[k + 1] = so[k] + (((uint64_t)olen[i] + 64 + 7) & ~7ull);
+        }
+        if (!one_trip) { /* the main batch's packed bytes, before the staging is reused */
+            main_buf.resize(packed);
+            if (packed) HIPCHK(hipMemcpy(main_buf.data(), d_packed, packed, hipMemcpyDeviceToHost));
+        }
+        rhead = 8 * m + ((4 * m + 7) & ~7ull);
+        if ((rc = grow(c->d_json, c->d_json_cap, up.size()))) return rc;
+        if ((rc = grow(c->d_out, c->d_out_cap, so[m] + 64))) return rc;
+        const uint64_t *r_in = (const uint64_t *)(void *)c->d_json, *r_oo = r_in + m + 1;
+        uint64_t *r_ret = (uint64_t *)(void *)c->d_pack; /* rhead <= head: d_pack is large enough */
+        uint32_t *r_ol = (uint32_t *)(void *)(c->d_pack + 8 * m);
+        HIPCHK(hipMemcpyAsync(c->d_json, up.data(), up.size(), hipMemcpyHostToDevice, s));
+        if ((rc = launch(c, d, root, c->d_json + 16 * (m + 1), r_in, m, flags, c->d_out, r_oo, r_ol, r_ret, nullptr, s,
+                         max_len)))
+            return rc;
+        rdown.resize(rhead + so[m]);
+        HIPCHK(hipMemcpyAsync(rdown.data(), c->d_pack, rhead, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(rdown.data() + rhead, c->d_out, so[m], hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
-        if ((uint8_t)ret[i] == DG_ST_OUT_OVERFLOW)
-            return set_err(DG_E_NOMEM, "message %llu overflowed its exact-size slot", (unsigned long long)i);
-        olen[i] = l1;
-        redo_out[k].resize(l1);
-        if (l1) HIPCHK(hipMemcpy(redo_out[k].data(), d1, l1, hipMemcpyDeviceToHost));
-        (void)hipFree(d1);
-        (void)hipFree(d_io);
-        (void)hipFree(d_oo);
-        (void)hipFree(d_r);
-        (void)hipFree(d_ol);
+        redo_so.assign(so, so + m + 1);
+        for (uint64_t k = 0; k < m; k++) {
+            const uint64_t i = redo[k];
+            memcpy(&ret[i], rdown.data() + 8 * k, 8);
+            memcpy(&olen[i], rdown.data() + 8 * m + 4 * k, 4);
+            if ((uint8_t)ret[i] == DG_ST_OUT_OVERFLOW)
+                return set_err(DG_E_NOMEM, "message %llu overflowed its exact-size slot", (unsigned long long)i);
+        }
     }
     uint64_t total = 0;
     out_off[0] = 0;
@@ -574,15 +660,27 @@ int dg_j2t_batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
     }
     if (out_need) *out_need = total;
     if (total > out_cap || (!out && total)) return set_err(DG_E_NOMEM, "output needs %llu bytes", (unsigned long long)total);
-    /* D2H of each slot's used prefix (contiguous runs merged) */
-    std::vector<uint8_t> stage(soff[n]);
-    HIPCHK(hipMemcpy(stage.data(), c->d_out, soff[n], hipMemcpyDeviceToHost));
+    if (redo.empty()) {
+        /* the packed bytes ARE the output layout */
+        if (one_trip) {
+            if (total) memcpy(out, c->h_down + head, total);
+        } else if (total) {
+            HIPCHK(hipMemcpy(out, d_packed, total, hipMemcpyDeviceToHost));
+        }
+        return DG_OK;
+    }
+    /* interleave: the main batch's packed bytes in order, the redo slots */
+    const uint8_t *mp = one_trip ? c->h_down + head : main_buf.data();
+    uint64_t pp = 0;
     size_t rk = 0;
     for (uint64_t i = 0; i < n; i++) {
-        while (rk < redo.size() && redo[rk] < i) rk++; /* redo is ascending */
-        if (!olen[i]) continue;
-        if (rk < redo.size() && redo[rk] == i) memcpy(out + out_off[i], redo_out[rk].data(), olen[i]);
-        else memcpy(out + out_off[i], stage.data() + soff[i], olen[i]);
+        if (rk < redo.size() && redo[rk] == i) {
+            if (olen[i]) memcpy(out + out_off[i], rdown.data() + rhead + redo_so[rk], olen[i]);
+            rk++;
+        } else if (olen[i]) {
+            memcpy(out + out_off[i], mp + pp, olen[i]);
+            pp += olen[i];
+        }
     }
     return DG_OK;
 }
@@ -612,13 +710,10 @@ int dg_pack_device(dg_ctx *c, const uint8_t *d_out, const uint64_t *d_out_off, c
     return DG_OK;
 }
 
-static int pack_scan(dg_ctx *c, const uint8_t *d_out, const uint64_t *d_out_off, const uint32_t *d_out_len,
-                     const uint64_t *d_ret, uint64_t n, const uint8_t *hdr, uint32_t hdr_len, const uint8_t *ftr,
-                     uint32_t ftr_len, uint8_t *d_dst, uint64_t *d_dst_off, void *stream)
+static int pack_scan_nolock(dg_ctx *c, const uint8_t *d_out, const uint64_t *d_out_off, const uint32_t *d_out_len,
+                            const uint64_t *d_ret, uint64_t n, const uint8_t *hdr, uint32_t hdr_len, const uint8_t *ftr,
+                            uint32_t ftr_len, uint8_t *d_dst, uint64_t *d_dst_off, hipStream_t s)
 {
-    std::lock_guard<std::mutex> g(c->mu);
-    HIPCHK(hipSetDevice(c->device));
-    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     if (n == 0) {
         HIPCHK(hipMemsetAsync(d_dst_off, 0, 8, s));
         return DG_OK;
@@ -627,6 +722,7 @@ static int pack_scan(dg_ctx *c, const uint8_t *d_out, const uint64_t *d_out_off,
     int rc = scratch_for(c, s, &x);
     if (rc) return rc;
     MsgFrame fr{};
+    fr.ret = d_ret; /* failed messages pack as nothing */
     if (hdr) {
         /* header at 0, footer 8-aligned after it; both followed by >= 16 readable bytes */
         const uint32_t fo = (hdr_len + 7) & ~7u;
@@ -644,7 +740,6 @@ static int pack_scan(dg_ctx *c, const uint8_t *d_out, const uint64_t *d_out_off,
         fr.hdr_len = hdr_len;
         fr.ftr = x->d_frame + fo;
         fr.ftr_len = ftr_len;
-        fr.ret = d_ret;
     }
     /* every block must be resident at once (they wait for each other): at
      * most one block per CU */
@@ -658,6 +753,16 @@ static int pack_scan(dg_ctx *c, const uint8_t *d_out, const uint64_t *d_out_off,
     x->last = s;
     if (e != hipSuccess) return set_err(DG_E_HIP, "pack scan launch: %s", hipGetErrorString(e));
     return DG_OK;
+}
+
+static int pack_scan(dg_ctx *c, const uint8_t *d_out, const uint64_t *d_out_off, const uint32_t *d_out_len,
+                     const uint64_t *d_ret, uint64_t n, const uint8_t *hdr, uint32_t hdr_len, const uint8_t *ftr,
+                     uint32_t ftr_len, uint8_t *d_dst, uint64_t *d_dst_off, void *stream)
+{
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    return pack_scan_nolock(c, d_out, d_out_off, d_out_len, d_ret, n, hdr, hdr_len, ftr, ftr_len, d_dst, d_dst_off, s);
 }
 
 int dg_pack_device_scan(dg_ctx *c, const uint8_t *d_out, const uint64_t *d_out_off, const uint32_t *d_out_len,

@@ -1234,8 +1234,9 @@ DGI uint64_t block_sum_u64(uint64_t v, uint64_t *red)
 }
 
 /* Framing (HTTPConv.Do, conv/j2t/http_conv.go:68-94): with fr.hdr set, a
- * message that converted (ret 0) is packed as hdr + body + ftr, one that
- * failed as nothing. */
+ * message that converted (ret 0) is packed as hdr + body + ftr. With fr.ret
+ * set, a message that failed packs as nothing (its out_len may carry the
+ * bytes an overflowed slot needs). */
 struct MsgFrame {
     const uint8_t *hdr; /* device; 16 readable bytes past the end */
     uint32_t hdr_len;
@@ -1258,8 +1259,8 @@ __global__ __launch_bounds__(256) void dg_pack_scan_kernel(const uint8_t *out, c
     const uint64_t hi = lo + per < n ? lo + per : n;
     const uint32_t fx = fr.hdr ? fr.hdr_len + fr.ftr_len : 0u;
     auto msg_len = [&](uint64_t i) -> uint32_t {
-        if (!fr.hdr) return out_len[i];
-        return fr.ret[i] == 0 ? out_len[i] + fx : 0u;
+        if (!fr.ret) return out_len[i];
+        return fr.ret[i] == 0 ? out_len[i] + fx : 0u; /* failed messages pack as nothing */
     };
     uint64_t s = 0;
     for (uint64_t i = lo + tid; i < hi; i += 256) s += msg_len(i);

@@ -810,6 +810,7 @@ DGI void t2j_store(const T2JParams &P, uint64_t i, uint64_t r, Out &o)
 
 constexpr uint32_t T2J_DEEP_BLOCKS = 4; /* 1024 lanes x 96 KiB of frames */
 
-void launch_t2j_kernels(uint64_t n, hipStream_t s, const T2JParams &P, uint32_t spread); /* spread 1, 2 or 4 */
+void launch_t2j_pass(uint64_t n, hipStream_t s, const T2JParams &P, uint32_t spread); /* spread 1, 2 or 4 */
+void launch_t2j_deep(hipStream_t s, const T2JParams &P);
 
 }  // namespace dg

@@ -14,14 +14,11 @@ static const uint64_t T2J_DEEP_WS = (uint64_t)T2J_DEEP_BLOCKS * T2J_BLOCK * T2J_
 
 /* lanes per message of the LDS-frame pass (t2j_kern.hip) from the batch's
  * longest message: short messages want full waves, ~1 KB ones sparse waves;
- * unknown or huge (a mixed batch) keep the middle. DG_T2J_SPREAD=1|2|4 forces. */
-static uint32_t t2j_spread(uint64_t max_len)
+ * unknown or huge (a mixed batch) keep the middle. the t2j_spread knob (1|2|4) forces. */
+static uint32_t t2j_spread(const dg_ctx *c, uint64_t max_len)
 {
-    const char *e = getenv("DG_T2J_SPREAD");
-    if (e) {
-        const int v = atoi(e);
-        return v == 1 || v == 4 ? (uint32_t)v : 2u;
-    }
+    const int64_t v = c->knobs.t2j_spread;
+    if (v) return v == 1 || v == 4 ? (uint32_t)v : 2u;
     if (max_len == 0 || max_len > 16384) return 2;
     return max_len <= 512 ? 1 : 4;
 }
@@ -40,7 +37,10 @@ static int t2j_launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
     int rc = scratch_for(c, s, &x);
     if (rc) return rc;
     if ((rc = grow_x(x, x->t2j_list, x->t2j_list_cap, n))) return rc;
-    if (!x->ws_t2j) HIPCHK(hipMalloc(&x->ws_t2j, T2J_DEEP_WS));
+    if (!c->ws_t2j) {
+        HIPCHK(hipMalloc(&c->ws_t2j, T2J_DEEP_WS));
+        HIPCHK(hipEventCreateWithFlags(&c->ws_t2j_done, hipEventDisableTiming));
+    }
     T2JParams P;
     memset(&P, 0, sizeof P);
     P.root = root;
@@ -56,11 +56,21 @@ static int t2j_launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
     P.hdr = d->hdr;
     P.side = d->d_side;
     P.deep_list = x->t2j_list;
-    P.deep_count = x->d_counts + 3;
-    P.ws = x->ws_t2j;
-    launch_t2j_kernels(n, s, P, t2j_spread(max_len));
+    P.deep_count = x->d_counts + DG_T2J_DEEP_COUNT;
+    P.ws = c->ws_t2j;
+    launch_t2j_pass(n, s, P, t2j_spread(c, max_len));
     hipError_t e = hipGetLastError();
-    (void)hipMemsetAsync(x->d_counts + 3, 0, 4, s);
+    /* the deep workspace is one per context: a deep pass on another stream
+     * than the previous one waits for it (deep messages are rare; the LDS
+     * passes of different streams still overlap) */
+    if (e == hipSuccess && c->ws_t2j_last && c->ws_t2j_last != s) e = hipStreamWaitEvent(s, c->ws_t2j_done, 0);
+    if (e == hipSuccess) {
+        launch_t2j_deep(s, P);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipEventRecord(c->ws_t2j_done, s);
+    if (e == hipSuccess) c->ws_t2j_last = s;
+    (void)hipMemsetAsync(x->d_counts + DG_T2J_DEEP_COUNT, 0, 4, s);
     HIPCHK(hipEventRecord(x->done, s));
     x->used = true;
     x->last = s;

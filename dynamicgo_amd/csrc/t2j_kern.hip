@@ -59,12 +59,16 @@ __global__ __launch_bounds__(T2J_BLOCK) void t2j_deep_kernel(T2JParams P)
     }
 }
 
-void launch_t2j_kernels(uint64_t n, hipStream_t s, const T2JParams &P, uint32_t spread)
+void launch_t2j_pass(uint64_t n, hipStream_t s, const T2JParams &P, uint32_t spread)
 {
     const uint32_t mpb = T2J_BLOCK / spread, blocks = (uint32_t)((n + mpb - 1) / mpb);
     if (spread == 1) hipLaunchKernelGGL(t2j_kernel<1>, dim3(blocks), dim3(T2J_BLOCK), 0, s, P);
     else if (spread == 4) hipLaunchKernelGGL(t2j_kernel<4>, dim3(blocks), dim3(T2J_BLOCK), 0, s, P);
     else hipLaunchKernelGGL(t2j_kernel<2>, dim3(blocks), dim3(T2J_BLOCK), 0, s, P);
+}
+
+void launch_t2j_deep(hipStream_t s, const T2JParams &P)
+{
     hipLaunchKernelGGL(t2j_deep_kernel, dim3(T2J_DEEP_BLOCKS), dim3(T2J_BLOCK), 0, s, P);
 }
 }  // namespace dg

@@ -68,6 +68,19 @@ int dg_ctx_stats(dg_ctx *ctx, uint64_t *bails, uint64_t *deeps, int reset);
  * deep redos, [2..11] wave-kernel phase cycles in a -DDG_WPROF build. */
 int dg_ctx_counters(dg_ctx *ctx, uint64_t *out, int n, int reset);
 
+/* Routing knobs (no reference counterpart; testing and tuning). They are read
+ * from the environment ONCE, by dg_ctx_create, and changed only through these
+ * calls, so routing never changes under a running launch:
+ *   "flat"        DG_FLAT         -1 auto, 0 never, 1 always the flat kernel for flat roots
+ *   "wave_min"    DG_WAVE_MIN     messages longer than this go to the wave kernel (512)
+ *   "wave_occ"    DG_WAVE_OCC     0 auto, 4 or 5: the wave kernel's waves/SIMD instance
+ *   "small_mpw"   DG_SMALL_MPW    small-kernel messages per wave (64); 0 = lane kernel
+ *   "list_blocks" DG_LIST_BLOCKS  grid of the exact-machine list pass (16)
+ *   "t2j_spread"  DG_T2J_SPREAD   0 auto, 1, 2 or 4 lanes per t2j message
+ * Unknown names return DG_E_INVALID. Thread-safe (the context lock). */
+int dg_ctx_set_knob(dg_ctx *ctx, const char *name, int64_t value);
+int dg_ctx_get_knob(dg_ctx *ctx, const char *name, int64_t *value);
+
 /* Upload a dg_desc blob (v1 or v2) (include/dgj2t_desc.h) to the context's device.
  * Replaces reading the Go *thrift.TypeDescriptor graph in place
  * (native/thrift.h:70-137 <-> thrift/descriptor.go:119-267). */

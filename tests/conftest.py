@@ -42,3 +42,21 @@ def gpu_available():
         return torch.cuda.is_available()
     except Exception:
         return False
+
+
+@pytest.fixture
+def knob():
+    """knob(name, value): set a routing knob of the default context
+    (dg_ctx_set_knob); every knob touched is restored after the test."""
+    from dynamicgo_amd import conv
+    ctx = conv.default_context()
+    saved = {}
+
+    def set_(name, value):
+        if name not in saved:
+            saved[name] = ctx.get_knob(name)
+        ctx.set_knob(name, int(value))
+
+    yield set_
+    for k, v in saved.items():
+        ctx.set_knob(k, v)

@@ -49,6 +49,8 @@ def test_c5_generation_is_worker_independent_and_shards_partition():
         a, o = W.gen_mixed_arena(C5_N, 45, large_scale=C5_SCALE)
         assert got == bytes(a[:int(o[-1])])
         assert sum(len(p[2]) - 1 for p in parts) == C5_N
+        bench.release_c5_cache(C5_N, 45, C5_SCALE)
+    assert not [f for f in os.listdir("/dev/shm") if f.startswith("dgj2t_c5_")]
 
 
 def _free_port():
@@ -63,6 +65,9 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         td, a, off, meta = bench.rank_workload("c5", rank, world, c5_n=C5_N, c5_scale=C5_SCALE)
+        dist.barrier()
+        if rank == 0:  # every rank has its shard: the node's shared copy goes
+            bench.release_c5_cache(C5_N, 45, C5_SCALE)
         fl = T.flatten(td)
         blob = bench.share_descriptor(fl if rank == 0 else T.FlatDescriptor(b"", fl.root_type, fl.types), rank,
                                       torch.device("cpu"), "gloo")

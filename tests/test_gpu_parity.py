@@ -60,10 +60,10 @@ def _raw_batch(flat, msgs, flags):
 
 @pytest.mark.parametrize("extra", [0, NO_WAVE, NO_FAST, "wave-all"],
                          ids=["hybrid", "lane-fast+exact", "exact-only", "wave-all"])
-def test_golden_vectors(golden, extra, monkeypatch):
+def test_golden_vectors(golden, extra, knob):
     rows, flats = golden
     if extra == "wave-all":
-        monkeypatch.setenv("DG_WAVE_MIN", "0")
+        knob("wave_min", 0)
         extra = 0
     bad = _run_rows(rows, flats, extra)
     assert not bad, bad[:8]
@@ -94,12 +94,12 @@ def test_fuzz_vs_oracle(which):
 
 
 @pytest.mark.parametrize("cfg", ["c2", "c3", "c3-occ4"])
-def test_full_batch_vs_oracle(cfg, monkeypatch):
+def test_full_batch_vs_oracle(cfg, knob):
     """The bench workloads at full size (65 536 messages), byte-exact, and all
     of them on the fast path (what bench.py measures). C3 runs on the 5-wave
     instance of the wave kernel (max_len <= 16 KiB), c3-occ4 on the other."""
     if cfg == "c3-occ4":
-        monkeypatch.setenv("DG_WAVE_OCC", "4")
+        knob("wave_occ", 4)
         cfg = "c3"
     td, gen, seed = {"c2": (W.simple_desc, W.gen_flat_batch, 42),
                      "c3": (W.nesting_i64_desc, W.gen_nested_batch, 43)}[cfg]
@@ -118,11 +118,11 @@ def test_full_batch_vs_oracle(cfg, monkeypatch):
 
 
 @pytest.mark.parametrize("occ", ["auto", "5"])
-def test_large_messages_vs_oracle(occ, monkeypatch):
+def test_large_messages_vs_oracle(occ, knob):
     """C4-shaped messages (too large to stage in LDS: global-source path), on
     the 4-wave instance (max_len > 16 KiB) and forced onto the 5-wave one."""
     if occ != "auto":
-        monkeypatch.setenv("DG_WAVE_OCC", occ)
+        knob("wave_occ", occ)
     fl = T.flatten(W.large_desc())
     rng = random.Random(44)
     msgs = W.gen_large_batch(rng, 24, blob_bytes=6000, n_values=300) + W.gen_large_batch(rng, 8)

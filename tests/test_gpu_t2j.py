@@ -261,12 +261,12 @@ def test_device_entry_point(chk):
 
 
 @pytest.mark.parametrize("spread", ["1", "2", "4", "auto"])
-def test_spreads_vs_checker(chk, spread, monkeypatch):
+def test_spreads_vs_checker(chk, spread, knob):
     """The LDS-frame pass at each lanes-per-message spread (t2j_kern.hip), and
     the host's own choice from the longest message: random all-types
     messages (with mutations) and nested C3 Thrift, byte-exact."""
     if spread != "auto":
-        monkeypatch.setenv("DG_T2J_SPREAD", spread)
+        knob("t2j_spread", spread)
     td = t2jgen.all_types_desc()
     fl = T.flatten(td)
     rng = random.Random(77)

@@ -19,11 +19,11 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(autouse=True, params=["4", "5"], ids=["occ4", "occ5"])
-def all_messages_on_the_wave_kernel(monkeypatch, request):
+def all_messages_on_the_wave_kernel(knob, request):
     """Route every message (not only those > 512 B) to the wave kernel, once
     through each of its two instances (4 and 5 waves/SIMD, j2t_wave.h)."""
-    monkeypatch.setenv("DG_WAVE_MIN", "0")
-    monkeypatch.setenv("DG_WAVE_OCC", request.param)
+    knob("wave_min", 0)
+    knob("wave_occ", request.param)
 
 
 def _checker():
