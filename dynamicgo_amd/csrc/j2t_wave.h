@@ -76,7 +76,7 @@ constexpr uint32_t WV_RING = DG_WV_RING;       /* token ring per wave (a scan st
 constexpr uint32_t WV_RMASK = WV_RING - 1;
 constexpr uint32_t WV_CHUNK = 256;             /* bytes classified per scan step: 64 lanes x 4 */
 constexpr uint32_t WV_MAXD = 16;               /* container levels handled on the wave path */
-constexpr uint32_t WV_LA = 2;                  /* token lookahead kept unconsumed while scanning */
+constexpr uint32_t WV_FILL = 100;              /* entries scanned ahead before a page is converted */
 constexpr uint32_t WV_NOEND = 0xFFFFFFFFu;     /* string not closed (yet) */
 constexpr uint32_t WV_POSMASK = (1u << 29) - 1;
 constexpr uint32_t WV_MSG = DG_WV_MSG;         /* messages up to this (minus 16) are staged in LDS */
@@ -95,9 +95,6 @@ enum : uint32_t {
 /* byte classes (LDS table); the low 3 bits give a structural byte's kind */
 constexpr uint8_t C_STRUCT = 0x08, C_WS = 0x10, C_QUOTE = 0x20, C_BS = 0x40;
 
-/* trec[] values for keys */
-constexpr uint32_t TR_SKIP = 0xFFFFFFFFu, TR_MAPKEY = 0xFFFFFFFEu;
-
 /* one open container (32 B): in-page openers at crec[lane], earlier pages'
  * openers at crec[64 + level] */
 struct CRec {
@@ -113,8 +110,9 @@ constexpr uint32_t CF_SKIP = 1, CF_OBJ = 2, CF_STRUCT = 4, CF_MAP = 8, CF_LIST =
 struct WaveLds {
     uint32_t tpos[WV_RING]; /* kind << 29 | position */
     uint32_t tend[WV_RING]; /* string: closing quote position; scalar: one past its last byte */
-    uint32_t trec[WV_RING]; /* key: field index / TR_* */
+    uint32_t tsep[WV_RING]; /* separators after the entry: colons (bits 0-7) + commas << 8 */
     uint8_t tbs[WV_RING];   /* string: a backslash inside (set by the scan) */
+    uint8_t pg[64];         /* the page: lane -> entry offset from `consumed` */
     CRec crec[64 + WV_MAXD + 1];
     /* the page's string / base64 bodies as chunk tasks, per token lane */
     uint32_t cinc[64];      /* inclusive prefix of chunk counts */
@@ -451,10 +449,11 @@ __device__ __noinline__ void vnumber_slow(SrcT<const uint64_t> src, int64_t &p, 
 
 /* ---------------- stage 1: structural scan of one chunk ---------------- */
 struct ScanState {
-    uint32_t produced;   /* tokens appended to the ring so far */
+    uint32_t produced;   /* entries appended to the ring so far */
     uint32_t esc_carry;  /* an escape is pending at the chunk boundary */
     uint32_t str_carry;  /* inside a string at the chunk boundary */
     uint32_t scal_carry; /* the chunk's last byte was a scalar byte */
+    uint32_t bad;        /* a separator before the first entry */
 };
 
 /* this lane's 4 bytes of chunk `chunk` (spaces past the end) */
@@ -465,21 +464,27 @@ DGI uint32_t chunk_word(WP wbase, int64_t head, int64_t len, uint32_t chunk, uin
     return wi * 4 - head < len ? wbase[wi] : 0x20202020u;
 }
 
+/* One 256-byte chunk. Entries are the brackets, strings and scalars; the
+ * separators ':' and ',' are NOT entries: each one adds to the separator
+ * word of the entry before it (colon +1, comma +256), so that a string
+ * followed by a colon is a key and grammar is checked on entry pairs.
+ * Returns false, with no side effect, when the chunk's entries would not fit
+ * the ring's free space `room` (the caller converts a page first). */
 template <class LW>
-DGI void scan_chunk(uint32_t x, int64_t head, int64_t len, uint32_t chunk, ScanState &st, LW &L,
-                    const __attribute__((address_space(3))) uint8_t *cls, uint32_t lane, uint64_t lt)
+DGI bool scan_chunk(uint32_t x, int64_t head, int64_t len, uint32_t chunk, ScanState &st, LW &L,
+                    const __attribute__((address_space(3))) uint8_t *cls, uint32_t lane, uint64_t lt, uint32_t room)
 {
     int64_t wi = (int64_t)chunk * 64 + lane;
     int64_t p0 = wi * 4 - head; /* message position of this lane's byte 0 */
     /* string interior without a quote or backslash anywhere in the chunk
-     * (long strings, base64 blobs): no tokens, carries unchanged */
+     * (long strings, base64 blobs): no entries, carries unchanged */
     if (st.str_carry) {
         const uint32_t M = 0x7F7F7F7Fu;
         uint32_t vq = x ^ 0x22222222u, vb = x ^ 0x5C5C5C5Cu;
         uint32_t z = ~(((vq & M) + M) | vq | M) | ~(((vb & M) + M) | vb | M);
         if (!ballot(z != 0)) {
             st.esc_carry = 0;
-            return;
+            return true;
         }
     }
     uint32_t q = 0, bs = 0, sm = 0, ws = 0, knib = 0;
@@ -519,18 +524,30 @@ DGI void scan_chunk(uint32_t x, int64_t head, int64_t len, uint32_t chunk, ScanS
     uint32_t openq = uq & instr, closeq = uq & ~instr & 0xF;
     uint32_t outside = ~(instr | uq) & 0xF;
     uint32_t stm = sm & outside;
+    /* separators: ':' (kind 4) and ',' (kind 5) */
+    uint32_t sepc = 0, sepm = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) {
+        const uint32_t k = (knib >> (3 * j)) & 7;
+        if (k == K_COLON) sepc |= 1u << j;
+        if (k == K_COMMA) sepm |= 1u << j;
+    }
+    sepc &= stm;
+    sepm &= stm;
+    const uint32_t seps = sepc | sepm;
     uint32_t scal = outside & ~ws & ~sm;
     uint64_t sb3 = ballot(scal & 8);
     uint32_t prevs = lane ? (uint32_t)(sb3 >> (lane - 1)) & 1 : st.scal_carry;
     uint32_t sprev = ((scal << 1) | prevs) & 0xF;
     uint32_t sstart = scal & ~sprev;
     uint32_t send = ~scal & sprev & 0xF;
-    uint32_t tok = stm | openq | sstart;
+    uint32_t tok = (stm & ~seps) | openq | sstart;
     uint32_t term = closeq | send;
     uint32_t cnt = (uint32_t)__builtin_popcount(tok);
     uint64_t b0 = ballot(cnt & 1), b1 = ballot(cnt & 2), b2 = ballot(cnt & 4);
-    uint32_t pre = popc(b0 & lt) + 2 * popc(b1 & lt) + 4 * popc(b2 & lt);
     uint32_t total = popc(b0) + 2 * popc(b1) + 4 * popc(b2);
+    if (total > room) return false; /* nothing written: the ring first drains a page */
+    uint32_t pre = popc(b0 & lt) + 2 * popc(b1 & lt) + 4 * popc(b2 & lt);
     uint32_t k = st.produced + pre;
 #pragma unroll
     for (uint32_t j = 0; j < 4; j++) {
@@ -538,12 +555,14 @@ DGI void scan_chunk(uint32_t x, int64_t head, int64_t len, uint32_t chunk, ScanS
             uint32_t kind = ((stm >> j) & 1) ? (knib >> (3 * j)) & 7 : ((openq >> j) & 1) ? K_STRING : K_SCALAR;
             L.tpos[k & WV_RMASK] = (kind << 29) | (uint32_t)(p0 + j);
             L.tend[k & WV_RMASK] = WV_NOEND;
+            L.tsep[k & WV_RMASK] = 0;
             L.tbs[k & WV_RMASK] = 0;
             k++;
         }
     }
-    /* backslashes inside a string mark the open string: the last token
-     * started before them (after every token write of the chunk) */
+    /* backslashes inside a string mark the open string: the last entry
+     * started before them (after every entry write of the chunk; a wave's
+     * LDS operations complete in order) */
     const uint32_t bsi = bs & instr;
     if (bsi) {
 #pragma unroll
@@ -554,19 +573,39 @@ DGI void scan_chunk(uint32_t x, int64_t head, int64_t len, uint32_t chunk, ScanS
             }
         }
     }
-    /* terminators, after every token write of the chunk: the token a
-     * terminator ends is the last token strictly before it */
+    /* terminators and separators: the entry a terminator ends, or a
+     * separator follows, is the last entry strictly before it */
+    bool badsep = false;
 #pragma unroll
     for (uint32_t j = 0; j < 4; j++) {
-        if ((term >> j) & 1) {
-            uint32_t kb = st.produced + pre + (uint32_t)__builtin_popcount(tok & ((1u << j) - 1));
-            L.tend[(kb - 1) & WV_RMASK] = (uint32_t)(p0 + j);
+        const uint32_t kb = st.produced + pre + (uint32_t)__builtin_popcount(tok & ((1u << j) - 1));
+        if ((term >> j) & 1) L.tend[(kb - 1) & WV_RMASK] = (uint32_t)(p0 + j);
+        if ((seps >> j) & 1) {
+            if (kb == 0) badsep = true;
+            else atomicAdd(&L.tsep[(kb - 1) & WV_RMASK], ((sepc >> j) & 1) ? 1u : 256u);
         }
     }
+    if (ballot(badsep)) st.bad = 1;
     st.produced += total;
     st.esc_carry = (uint32_t)__builtin_amdgcn_readlane((int)cout, 63);
     st.str_carry = (st.str_carry + popc(pb)) & 1;
     st.scal_carry = (uint32_t)(sb3 >> 63) & 1;
+    return true;
+}
+
+/* the Thrift bytes of a parsed number (j2t_number's writes,
+ * native/thrift.c:312-365) as a little-endian word of n bytes, for WOut::wle */
+DGI void num_le(uint8_t tt, bool isint, int64_t iv, double dv, uint64_t &v, uint32_t &n)
+{
+    switch (tt) {
+    case DG_T_BYTE: v = isint ? (uint8_t)iv : (uint8_t)cvt32(dv); n = 1; return;
+    case DG_T_I16: v = __builtin_bswap16(isint ? (uint16_t)iv : (uint16_t)cvt32(dv)); n = 2; return;
+    case DG_T_I32: v = __builtin_bswap32(isint ? (uint32_t)iv : (uint32_t)cvt32(dv)); n = 4; return;
+    case DG_T_I64: v = __builtin_bswap64(isint ? (uint64_t)iv : (uint64_t)cvt64(dv)); n = 8; return;
+    case DG_T_DOUBLE: v = __builtin_bswap64((uint64_t)__double_as_longlong(dv)); n = 8; return;
+    }
+    v = 0;
+    n = 0;
 }
 
 /* ---------------- one message ---------------- */
@@ -586,35 +625,62 @@ DGI bool wave_run(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L
     const uint64_t le = lt | (1ull << lane);
 
     WP_DECL
-    ScanState ss{0, 0, 0, 0};
+    ScanState ss{0, 0, 0, 0, 0};
     uint32_t scanned = 0, consumed = 0;
     int32_t depth = 0;
     uint64_t O = 0;
     bool rootdone = false;
 
-    uint32_t xnext = chunk_word(wbase, head, len, 0, lane); /* loads run one chunk ahead */
+    uint32_t xcur = chunk_word(wbase, head, len, 0, lane);
     for (;;) {
-        while (scanned < nchunks && ss.produced - consumed < 64 + WV_LA) {
-            const uint32_t xcur = xnext;
-            if (scanned + 1 < nchunks) xnext = chunk_word(wbase, head, len, scanned + 1, lane);
-            scan_chunk(xcur, head, len, scanned, ss, L, cls, lane, lt);
+        /* scan ahead until WV_FILL entries wait (or the message is scanned):
+         * the live window is [consumed - 2, produced) */
+        while (scanned < nchunks && ss.produced - consumed < WV_FILL) {
+            const uint32_t xnext = scanned + 1 < nchunks ? chunk_word(wbase, head, len, scanned + 1, lane) : 0u;
+            if (!scan_chunk(xcur, head, len, scanned, ss, L, cls, lane, lt, WV_RING - 2 - (ss.produced - consumed)))
+                break;
             scanned++;
+            xcur = xnext;
             if (scanned == nchunks && ss.scal_carry) {
                 if (lane == 0) L.tend[(ss.produced - 1) & WV_RMASK] = (uint32_t)len;
             }
         }
-        /* the live window is [consumed - 2, produced): a token-dense chunk
-         * that overran it (fewer than 2 bytes per token) goes to the exact
-         * machine */
-        if (ss.produced - consumed + 2 > WV_RING) return false;
+        if (ss.bad) return false;
         WP(0);
-        uint32_t avail = ss.produced - consumed;
-        if (scanned < nchunks) avail -= WV_LA;
-        if (avail == 0) break;
-        const uint32_t np = avail < 64 ? avail : 64;
-
-        /* ---------- a page: token t = consumed + lane ---------- */
-        const uint32_t t = consumed + lane;
+        /* entries whose separators and ends are final: all but the last one
+         * while the scan goes on */
+        const uint32_t lim = ss.produced - (scanned < nchunks ? 1u : 0u);
+        if (lim <= consumed) {
+            if (scanned < nchunks) return false; /* a chunk denser than the ring (pathological): exact machine */
+            break;
+        }
+        /* ---------- a page: up to 64 VALUE entries (values and closing
+         * brackets), one per lane; the key before a value (a string followed
+         * by a colon) rides in the value's lane ---------- */
+        uint32_t np, off;
+        {
+            const uint32_t win = lim - consumed < 128u ? lim - consumed : 128u;
+            bool vA = false, vB = false;
+            if (lane < win) {
+                const uint32_t e = (consumed + lane) & WV_RMASK;
+                vA = !((L.tpos[e] >> 29) == K_STRING && (L.tsep[e] & 0xFFu));
+            }
+            if (lane + 64 < win) {
+                const uint32_t e = (consumed + 64 + lane) & WV_RMASK;
+                vB = !((L.tpos[e] >> 29) == K_STRING && (L.tsep[e] & 0xFFu));
+            }
+            const uint64_t bA = ballot(vA), bB = ballot(vB);
+            const uint32_t nA = popc(bA), ntot = nA + popc(bB);
+            np = ntot < 64 ? ntot : 64u;
+            if (np == 0) return false; /* only keys left: truncated input */
+            if (vA) L.pg[popc(bA & lt)] = (uint8_t)lane;
+            const uint32_t iB = nA + popc(bB & lt);
+            if (vB && iB < 64) L.pg[iB] = (uint8_t)(64 + lane);
+            __builtin_amdgcn_wave_barrier();
+            off = lane < np ? (uint32_t)L.pg[lane] : 0u;
+        }
+        const uint32_t lastoff = (uint32_t)__builtin_amdgcn_readlane((int)off, (int)(np - 1));
+        const uint32_t t = consumed + off;
         const bool act = lane < np;
         const uint32_t tp = act ? L.tpos[t & WV_RMASK] : 0;
         const uint32_t kind = act ? tp >> 29 : K_NONE;
@@ -628,7 +694,7 @@ DGI bool wave_run(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L
         const int32_t level = op ? dafter - 1 : dafter;
         const int32_t plev = cl ? level : level - 1; /* level of the parent opener */
         bool bad = alive && level >= (int32_t)WV_MAXD;
-        if (t == 0 && !op) bad = true; /* the root must be an object or array */
+        if (consumed == 0 && lane == 0 && (t != 0 || !op)) bad = true; /* the root: entry 0, an object or array */
         if (ballot(bad)) return false;
 
         WP(1);
@@ -649,37 +715,56 @@ DGI bool wave_run(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L
         bool pobj = false;
         if (alive && plev >= 0) pobj = par >= 0 ? pkind == K_LBRACE : (L.crec[ci].flags & CF_OBJ) != 0;
 
-        /* grammar against the neighbouring tokens */
-        const uint32_t kp = (alive && t >= 1) ? L.tpos[(t - 1) & WV_RMASK] >> 29 : K_NONE;
-        const uint32_t kp2 = (alive && t >= 2) ? L.tpos[(t - 2) & WV_RMASK] >> 29 : K_NONE;
-        const uint32_t tpn = (alive && t + 1 < ss.produced) ? L.tpos[(t + 1) & WV_RMASK] : (K_NONE << 29);
-        const uint32_t kn = tpn >> 29;
-        const bool keyish = kind == K_STRING && pobj && (kp == K_LBRACE || kp == K_COMMA);
-        const bool isval = (kind == K_STRING && !keyish) || kind == K_SCALAR || op;
-        const bool vend = kp == K_SCALAR || kp == K_RBRACE || kp == K_RBRACK ||
-                          (kp == K_STRING && !(pobj && (kp2 == K_LBRACE || kp2 == K_COMMA)));
-        if (alive) {
+        /* my key (the entry before me, when it is a string followed by a
+         * colon) and the entry before me-or-my-key: grammar on entry pairs
+         * and the separator counts between them */
+        bool haskey = false, kesc = false;
+        int32_t kpos = 0;
+        uint32_t kend = 0, ksep = 0, kq = K_NONE, sq = 0;
+        bool qkey = false;
+        if (alive && t >= 1) {
+            const uint32_t a = L.tpos[(t - 1) & WV_RMASK], sa = L.tsep[(t - 1) & WV_RMASK];
+            if ((a >> 29) == K_STRING && (sa & 0xFFu)) {
+                haskey = true;
+                ksep = sa;
+                kpos = (int32_t)(a & WV_POSMASK);
+                kend = L.tend[(t - 1) & WV_RMASK];
+                kesc = L.tbs[(t - 1) & WV_RMASK] != 0;
+                if (t >= 2) {
+                    const uint32_t b = L.tpos[(t - 2) & WV_RMASK];
+                    kq = b >> 29;
+                    sq = L.tsep[(t - 2) & WV_RMASK];
+                    qkey = kq == K_STRING && (sq & 0xFFu);
+                }
+            } else {
+                kq = a >> 29;
+                sq = sa;
+            }
+        }
+        const bool isval = kind == K_STRING || kind == K_SCALAR || op;
+        const uint32_t te = (alive && (kind == K_STRING || kind == K_SCALAR)) ? L.tend[t & WV_RMASK] : 0;
+        if (alive && t != 0) {
+            const bool qvend = kq == K_SCALAR || kq == K_RBRACE || kq == K_RBRACK || (kq == K_STRING && !qkey);
             bool ok;
-            if (t == 0) ok = true;
-            else if (keyish) ok = kn == K_COLON;
-            else if (isval) ok = pobj ? kp == K_COLON : (kp == K_LBRACK || kp == K_COMMA);
-            else if (kind == K_COLON) ok = pobj && kp == K_STRING && (kp2 == K_LBRACE || kp2 == K_COMMA);
-            else if (kind == K_COMMA) ok = vend;
-            else if (kind == K_RBRACE) ok = pobj && (kp == K_LBRACE || vend);
-            else ok = !pobj && (kp == K_LBRACK || vend); /* K_RBRACK */
+            if (isval) {
+                if (pobj) ok = haskey && ksep == 1u && ((kq == K_LBRACE && sq == 0) || (qvend && sq == 256u));
+                else ok = !haskey && ((kq == K_LBRACK && sq == 0) || (qvend && sq == 256u));
+            } else if (kind == K_RBRACE) {
+                ok = pobj && !haskey && ((kq == K_LBRACE && sq == 0) || (qvend && sq == 0));
+            } else { /* K_RBRACK */
+                ok = !pobj && !haskey && ((kq == K_LBRACK && sq == 0) || (qvend && sq == 0));
+            }
             bad |= !ok;
         }
-        const uint32_t te = (alive && (kind == K_STRING || kind == K_SCALAR)) ? L.tend[t & WV_RMASK] : 0;
         if (alive && kind == K_STRING && te == WV_NOEND) bad = true; /* EOF inside a string */
+        if (alive && haskey && kend == WV_NOEND) bad = true;
         if (ballot(bad)) return false;
 
         WP(2);
-        /* key hashes, once (the rounds below only probe) */
+        /* key hashes, once (the level rounds below only probe) */
         uint32_t khash = DG_NAME_HASH_SEED;
-        bool kesc = false;
-        if (alive && keyish) {
-            const int64_t k0 = pos + 1, kl = te - k0;
-            kesc = L.tbs[t & WV_RMASK] != 0;
+        if (alive && haskey) {
+            const int64_t k0 = kpos + 1, kl = (int64_t)kend - k0;
             for (int64_t j = 0; j < kl; j += 8) {
                 uint64_t w = src.get8(k0 + j);
                 const int64_t r = kl - j < 8 ? kl - j : 8;
@@ -688,59 +773,48 @@ DGI bool wave_run(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L
                     if (b < r) khash = DG_NAME_HASH_STEP(khash, (uint8_t)(w >> (8 * b)));
             }
         }
-        /* types, level by level: keys first (they need their struct), then
-         * values (they need their key or container) */
-        uint32_t ty = DG_NONE; /* value: type index; struct key: field index */
+        /* types, level by level (a value needs its container's type; an
+         * opener's record feeds the next level) */
+        uint32_t ty = DG_NONE; /* value type index */
+        uint32_t fi = DG_NONE; /* struct parent: the key's field (global index) */
+        uint32_t fbit = 0;     /* ... and its index within the struct */
+        uint32_t pflags = 0, ptype = 0;
         bool skip = false;
         {
             uint32_t lv = wave_or(alive ? 1u << level : 0u);
             for (lv = uni(lv); lv; lv &= lv - 1) {
                 const int32_t Lv = __builtin_ctz(lv);
                 const bool me = alive && level == Lv;
-                if (me && keyish) {
-                    const uint32_t pf = L.crec[ci].flags, pt = L.crec[ci].type;
-                    uint32_t rec = TR_MAPKEY;
-                    if (pf & CF_SKIP) {
-                        skip = true;
-                        rec = TR_SKIP;
-                    } else if (pf & CF_STRUCT) {
-                        const dg_struct sd = ldrec(&D.S[ldrec(&D.T[pt]).st]);
-                        int32_t fi = kesc ? -2 : wv_lookup(D, sd, src, pos + 1, (uint32_t)(te - pos - 1), khash);
-                        if (fi == -2) {
-                            bad = true; /* escaped key: exact machine */
-                            rec = TR_SKIP;
-                        } else if (fi < 0) {
-                            if ((flag & DG_F_ALLOW_UNKNOWN) == 0) bad = true;
-                            skip = true;
-                            rec = TR_SKIP;
-                        } else {
-                            const dg_field f = ldrec(&D.F[fi]);
-                            if ((flag & DG_F_ENABLE_VM) && f.vm != DG_VM_NONE) bad = true;
-                            if ((f.flags & DG_FF_REQUEST_BASE) && (flag & DG_F_NO_WRITE_BASE)) {
-                                skip = true;
-                                rec = TR_SKIP;
-                            } else {
-                                rec = (uint32_t)fi;
-                                ty = (uint32_t)fi;
-                            }
-                        }
-                    }
-                    L.trec[t & WV_RMASK] = rec;
+                if (me && t != 0 && !cl) { /* a closer's opener may be written in this very round: below */
+                    pflags = L.crec[ci].flags;
+                    ptype = L.crec[ci].type;
                 }
                 if (me && isval) {
                     if (t == 0) {
                         ty = P.root;
-                    } else {
-                        const uint32_t pf = L.crec[ci].flags, pt = L.crec[ci].type;
-                        if (pf & CF_SKIP) {
+                    } else if (pflags & CF_SKIP) {
+                        skip = true;
+                    } else if (pflags & CF_STRUCT) { /* j2t_key native/thrift.c:668-763 */
+                        const dg_struct sd = ldrec(&D.S[ldrec(&D.T[ptype]).st]);
+                        const int32_t f = kesc ? -2 : wv_lookup(D, sd, src, kpos + 1, kend - (uint32_t)kpos - 1, khash);
+                        if (f == -2) {
+                            bad = true; /* escaped key: exact machine */
+                        } else if (f < 0) {
+                            if ((flag & DG_F_ALLOW_UNKNOWN) == 0) bad = true;
                             skip = true;
-                        } else if (pf & CF_STRUCT) {
-                            uint32_t kr = L.trec[(t - 2) & WV_RMASK];
-                            if (kr >= D_nf) skip = true; /* TR_SKIP (never TR_MAPKEY in a struct) */
-                            else ty = ldrec(&D.F[kr]).type;
                         } else {
-                            ty = ldrec(&D.T[pt]).elem;
+                            const dg_field fd = ldrec(&D.F[f]);
+                            if ((flag & DG_F_ENABLE_VM) && fd.vm != DG_VM_NONE) bad = true;
+                            if ((fd.flags & DG_FF_REQUEST_BASE) && (flag & DG_F_NO_WRITE_BASE)) {
+                                skip = true;
+                            } else {
+                                fi = (uint32_t)f;
+                                fbit = (uint32_t)f - sd.field_begin;
+                                ty = fd.type;
+                            }
                         }
+                    } else {
+                        ty = ldrec(&D.T[ptype]).elem; /* list element, map value */
                     }
                     if (op) {
                         CRec c;
@@ -776,169 +850,185 @@ DGI bool wave_run(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L
             }
         }
 
+        if (alive && cl) {
+            pflags = L.crec[ci].flags;
+            ptype = L.crec[ci].type;
+        }
         WP(3);
-        /* lengths, part A: keys and values (with the LDS atomics that count
-         * elements and record struct fields). Every heavy helper has ONE call
-         * site below (I-cache: the kernel must stay small). */
-        uint32_t ln = 0;
-        bool isint = false, isnull = false, esc = false, isbin = false;
-        int64_t iv = 0;
-        double dv = 0.0;
-        uint8_t tt = 0;
-        int32_t ns = -1, nn = 0; /* number text to parse */
-        bool slow = false;
-        bool whole = true;       /* the number must span all of it */
-        int32_t cs = 0, cn = 0;  /* string body (copy / unquote / base64) */
-        uint64_t hv = 0;         /* header bytes (little-endian) and count */
-        uint32_t hn = 0;
-        if (alive && !skip && keyish) {
-            const uint32_t pf = L.crec[ci].flags, pt = L.crec[ci].type;
-            const uint32_t tv = L.tpos[(t + 2) & WV_RMASK];
-            isnull = (tv >> 29) == K_SCALAR && src.at(tv & WV_POSMASK) == 'n';
-            if (pf & CF_STRUCT) { /* native/thrift.c:668-763 + null unwinding 1016-1032 */
-                const dg_field f = ldrec(&D.F[ty]);
-                const dg_struct sd = ldrec(&D.S[ldrec(&D.T[pt]).st]);
-                uint64_t bit = 1ull << (ty - sd.field_begin);
-                uint64_t old = __hip_atomic_fetch_or(&L.crec[ci].seen, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (old & bit) bad = true; /* duplicate key: exact machine keeps the order semantics */
-                if (isnull && f.required != DG_REQ_OPTIONAL)
-                    __hip_atomic_fetch_or(&L.crec[ci].nulldr, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                tt = ldrec(&D.T[f.type]).ttype;
-                hv = (uint32_t)tt | ((uint32_t)__builtin_bswap16(f.id) << 8);
-                hn = 3;
-            } else { /* map key, j2t_map_key native/thrift.c:422-447: parsed even when
-                      * the value turns out null (a bad key errors first) */
-                if (!isnull) atomicAdd(&L.crec[ci].count, 1u);
-                cs = pos + 1;
-                cn = te - cs;
-                tt = ldrec(&D.T[ldrec(&D.T[pt]).key]).ttype;
-                esc = L.tbs[t & WV_RMASK] != 0;
-                if (esc) bad = true;
-                if (tt == DG_T_STRING) {
-                    hv = __builtin_bswap32((uint32_t)cn);
-                    hn = 4;
-                } else {
-                    ns = cs;
-                    nn = cn;
-                    whole = false; /* trailing key text is ignored */
-                    cn = 0;
+        /* lengths, part A: the key part (field header, or map key) and the
+         * value part, with the LDS atomics that count elements and record
+         * struct fields. Every heavy helper has ONE call site below (I-cache:
+         * the kernel must stay small). */
+        bool isnull = alive && kind == K_SCALAR && src.at(pos) == 'n';
+        bool esc = false, isbin = false;
+        uint8_t tt = 0, ktt = 0;
+        uint64_t kb = 0, vb = 0; /* key / value part bytes (little-endian) */
+        uint32_t kbn = 0, vbn = 0;
+        int32_t ks = 0, kn = 0;   /* string map key body */
+        int32_t cs = 0, cn = 0;   /* string value body (copy / unquote / base64) */
+        uint32_t vln = 0;         /* value bytes after vb: string body, or a container's 4-byte count */
+        int32_t kns = -1, knn = 0; /* number map key text (trailing text ignored) */
+        int32_t ns = -1, nn = 0;   /* number value text (all of it) */
+        if (alive && !skip && isval) {
+            tt = ldrec(&D.T[ty]).ttype;
+            if (haskey) {
+                if (pflags & CF_STRUCT) { /* native/thrift.c:668-763 + null unwinding 1016-1032 */
+                    const dg_field f = ldrec(&D.F[fi]);
+                    const uint64_t bit = 1ull << fbit;
+                    const uint64_t old =
+                        __hip_atomic_fetch_or(&L.crec[ci].seen, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (old & bit) bad = true; /* duplicate key: exact machine keeps the order semantics */
+                    if (isnull && f.required != DG_REQ_OPTIONAL)
+                        __hip_atomic_fetch_or(&L.crec[ci].nulldr, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    kb = (uint32_t)tt | ((uint32_t)__builtin_bswap16(f.id) << 8);
+                    kbn = 3;
+                } else { /* map key, j2t_map_key native/thrift.c:422-447: parsed even when the
+                          * value turns out null (a bad key errors first) */
+                    if (!isnull) atomicAdd(&L.crec[ci].count, 1u);
+                    ktt = ldrec(&D.T[ldrec(&D.T[ptype]).key]).ttype;
+                    if (kesc) bad = true;
+                    if (ktt == DG_T_STRING) {
+                        ks = kpos + 1;
+                        kn = (int32_t)kend - ks;
+                        kb = __builtin_bswap32((uint32_t)kn);
+                        kbn = 4;
+                    } else {
+                        kns = kpos + 1;
+                        knn = (int32_t)kend - kns;
+                        if (!num_size(ktt)) bad = true; /* ERR_UNSUPPORT_THRIFT_TYPE */
+                    }
                 }
             }
-        } else if (alive && !skip && isval) {
-            const dg_type vt = ldrec(&D.T[ty]);
-            tt = vt.ttype;
-            const bool inlist = t != 0 && (L.crec[ci].flags & CF_LIST);
             if (kind == K_SCALAR) {
                 ns = pos;
-                nn = te - pos;
+                nn = (int32_t)te - pos;
             } else if (kind == K_STRING) {
                 cs = pos + 1;
-                cn = te - cs;
+                cn = (int32_t)te - cs;
                 if (tt != DG_T_STRING) bad = true;
-                isbin = (flag & DG_F_NO_BASE64) == 0 && (vt.flags & DG_TF_BINARY);
+                isbin = (flag & DG_F_NO_BASE64) == 0 && (ldrec(&D.T[ty]).flags & DG_TF_BINARY);
                 if (!isbin) esc = L.tbs[t & WV_RMASK] != 0; /* a backslash inside (the scan marked it) */
-                hn = 4;
+                vbn = 4;
             } else if (kind == K_LBRACE) {
                 if (L.crec[lane].flags & CF_MAP) {
-                    hv = ldrec(&D.T[vt.key]).ttype | ((uint32_t)ldrec(&D.T[vt.elem]).ttype << 8);
-                    hn = 2;
-                    ln = 4; /* + size, written by the '}' */
+                    const dg_type vt = ldrec(&D.T[ty]);
+                    vb = ldrec(&D.T[vt.key]).ttype | ((uint32_t)ldrec(&D.T[vt.elem]).ttype << 8);
+                    vbn = 2;
+                    vln = 4; /* + size, written by the '}' */
                 }
             } else { /* K_LBRACK */
-                hv = ldrec(&D.T[vt.elem]).ttype;
-                hn = 1;
-                ln = 4;
+                vb = ldrec(&D.T[ldrec(&D.T[ty]).elem]).ttype;
+                vbn = 1;
+                vln = 4;
             }
-            if (inlist) {
-                /* a null element is not counted; checked on the text here */
-                if (!(kind == K_SCALAR && src.at(pos) == 'n')) atomicAdd(&L.crec[ci].count, 1u);
-            }
+            /* a null list element is not counted; checked on the text here */
+            if (t != 0 && (pflags & CF_LIST) && !isnull) atomicAdd(&L.crec[ci].count, 1u);
         } else if (alive && skip && kind == K_SCALAR) {
             ns = pos; /* skip_one validates skipped scalars (native/scanning.c:1134-1330) */
-            nn = te - pos;
+            nn = (int32_t)te - pos;
         }
-        /* scalars: literals inline, numbers through the one parser */
+        /* literals inline */
         if (ns >= 0) {
             const uint8_t c0 = src.at(ns);
-            if (whole && (c0 == 'n' || c0 == 't' || c0 == 'f')) {
+            if (c0 == 'n' || c0 == 't' || c0 == 'f') {
                 const uint32_t w4 = (uint32_t)src.get8(ns + (c0 == 'f'));
                 const uint32_t want = c0 == 'n' ? VS_NULL : c0 == 't' ? VS_TRUE : VS_ALSE;
                 if (nn != 4 + (c0 == 'f') || w4 != want) bad = true;
-                if (c0 == 'n') {
-                    isnull = true;
-                } else if (!skip) {
+                if (c0 != 'n' && !skip) {
                     if (tt != DG_T_BOOL) bad = true;
-                    hv = c0 == 't';
-                    hn = 1;
+                    vb = c0 == 't';
+                    vbn = 1;
                 }
-            } else {
-                int64_t q = 0;
+                ns = -1;
+            } else if (!skip && !num_size(tt)) {
+                bad = true;
+            }
+        }
+        /* numbers: the map key's, then the value's, through ONE parser call
+         * site; each becomes its Thrift bytes at once (fewer live VGPRs) */
+        bool kslow = false, vslow = false;
+        for (uint32_t it = 0; it < 2; it++) {
+            const bool want = it == 0 ? kns >= 0 : ns >= 0;
+            if (!ballot(want)) continue;
+            if (want) {
+                const int32_t s0 = it == 0 ? kns : ns, n0 = it == 0 ? knn : nn;
+                int64_t q = 0, iv = 0;
+                double dv = 0.0;
+                bool isint = false;
 #if defined(DG_WV_ABL) && (DG_WV_ABL & 16)
-                q = nn; iv = nn; isint = true; /* ablation: no number parse */
-                if (0) slow = true;
+                q = n0; iv = n0; isint = true; /* ablation: no number parse */
+                if (0) {
 #else
-                if (nn > RS_MAX) {
-                    slow = true; /* long numbers (big decimals, long map keys): the exact parser */
-                } else {
-                    RSrc ks;
-                    ks.load(src, ns, nn);
-                    if (!fast_vnumber(ks, q, tb, iv, dv, isint)) slow = true;
-                    else if (whole && q != nn) bad = true;
+                bool okn = false;
+                if (n0 <= RS_MAX) {
+                    RSrc rs;
+                    rs.load(src, s0, n0);
+                    okn = fast_vnumber(rs, q, tb, iv, dv, isint);
                 }
+                if (!okn) { /* long numbers (big decimals, long map keys), errors: the exact parser */
 #endif
-                if (!skip && !num_size(tt)) bad = true;
+                    if (it == 0) kslow = true;
+                    else vslow = true;
+                } else if (it == 0) {
+                    num_le(ktt, isint, iv, dv, kb, kbn);
+                } else {
+                    if (q != n0) bad = true;
+                    if (!skip) num_le(tt, isint, iv, dv, vb, vbn);
+                }
             }
         }
         /* numbers the fast parser declines (errors, big-decimal cases): the
          * reference's vnumber (native/scanning.c:958-1083, atof_native
          * native/atof_native.c:418-424), one lane at a time with the wave's
          * 800-byte digit buffer */
-        for (uint64_t sm = ballot(slow && !bad); sm; sm &= sm - 1) {
+        for (uint64_t sm = ballot((kslow || vslow) && !bad); sm; sm &= sm - 1) {
             if (lane == (uint32_t)__builtin_ctzll(sm)) {
-                JState js;
-                int64_t q = 0;
-                vnumber_slow(src.sub(ns, nn), q, js, dbuf);
-                if (js.vt < 0 || (whole && q != nn)) {
-                    bad = true;
-                } else {
-                    isint = js.vt == V_INTEGER;
-                    iv = js.iv;
-                    dv = js.dv;
+                for (uint32_t it = 0; it < 2; it++) {
+                    if (!(it == 0 ? kslow : vslow)) continue;
+                    const int32_t s0 = it == 0 ? kns : ns, n0 = it == 0 ? knn : nn;
+                    JState js;
+                    int64_t q = 0;
+                    vnumber_slow(src.sub(s0, n0), q, js, dbuf);
+                    if (js.vt < 0 || (it == 1 && q != n0)) {
+                        bad = true;
+                    } else if (it == 0) {
+                        num_le(ktt, js.vt == V_INTEGER, js.iv, js.dv, kb, kbn);
+                    } else if (!skip) {
+                        num_le(tt, js.vt == V_INTEGER, js.iv, js.dv, vb, vbn);
+                    }
                 }
             }
         }
         /* strings: length of the body */
-        if (alive && !skip && !isnull && hn == 4 && isval) {
+        if (alive && !skip && kind == K_STRING) {
             if (isbin) {
                 int64_t bl = b64_len(src, cs, cn);
                 if (bl < 0) bad = true;
-                ln = (uint32_t)bl;
+                vln = (uint32_t)bl;
             } else if (esc) {
                 WOut co;
                 co.init_dry();
                 if (!fast_unquote(src, cs, cn, co)) bad = true;
-                ln = (uint32_t)co.len;
+                vln = (uint32_t)co.len;
             } else {
-                ln = (uint32_t)cn;
+                vln = (uint32_t)cn;
             }
-            hv = __builtin_bswap32(ln);
+            vb = __builtin_bswap32(vln);
         }
-        if (keyish && hn == 4) ln = (uint32_t)cn; /* string map key body */
-        if (isnull) {
-            hn = 0;
-            ln = 0;
+        if (isnull) { /* a null value writes nothing, its key included */
+            kbn = 0;
+            kn = 0;
+            vbn = 0;
+            vln = 0;
         }
-        /* a number's Thrift bytes become header bytes here, so that the parse
-         * results are dead before the prefix sum (fewer live VGPRs) */
-        if (!isnull && ns >= 0 && !skip && hn == 0) ln = num_size(tt);
         WP(4);
         /* part B: closing brackets, once every atomic of the page is in */
         uint64_t reqs = 0;
         uint32_t sidx = 0; /* the closed struct (its dg_struct is reloaded at the emit) */
+        uint32_t uln = 0;  /* bytes of the unset fields */
         if (alive && cl) {
-            const uint32_t pf = L.crec[ci].flags;
-            if (!(pf & CF_SKIP) && (pf & CF_STRUCT)) {
-                sidx = ldrec(&D.T[L.crec[ci].type]).st;
+            if (!(pflags & CF_SKIP) && (pflags & CF_STRUCT)) {
+                sidx = ldrec(&D.T[ptype]).st;
                 const dg_struct csd = ldrec(&D.S[sidx]);
                 reqs = (D.R[csd.req_begin] & ~L.crec[ci].seen) | L.crec[ci].nulldr;
                 if (!(flag & (DG_F_WRITE_REQUIRE | DG_F_WRITE_DEFAULT | DG_F_WRITE_OPTIONAL)) && sidx < WV_REQMASKS) {
@@ -951,14 +1041,15 @@ DGI bool wave_run(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L
                     WOut co;
                     co.init_dry();
                     if (!unset_fields(D, csd, reqs, flag, co)) bad = true;
-                    ln = (uint32_t)co.len;
+                    uln = (uint32_t)co.len;
                 }
-                hv = 0; /* STOP after the unset fields */
-                hn = 1;
+                vb = 0; /* STOP after the unset fields */
+                vbn = 1;
             }
         }
         if (ballot(bad)) return false;
-        ln += hn;
+        const uint32_t khead = kbn + (uint32_t)kn; /* bytes before the value part */
+        const uint32_t ln = khead + uln + vbn + vln;
 
         WP(5);
         /* output offsets */
@@ -966,48 +1057,42 @@ DGI bool wave_run(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L
         const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
         const uint32_t opos = (uint32_t)(O + incl - ln); /* slot offsets are 32-bit (outpos, cbd) */
         if (O + tot > cap) return false; /* slot overflow: the exact machine reports it */
-        if (alive && op) L.crec[lane].outpos = (uint32_t)opos;
+        if (alive && op) L.crec[lane].outpos = opos + khead;
 
-        /* emit: header, then the body, through one writer per lane; bodies
-         * without escapes (copies) and base64 bodies go to chunk tasks below */
-        bool deferred = false;
+        /* emit: key part, value header / number / literal, then the body;
+         * string and base64 bodies go to chunk tasks below */
         const bool live = alive && !skip && !isnull;
-        const bool chunked = live && cn > 0 && isval && (isbin || !esc);
+        const bool chunked = live && kind == K_STRING && cn > 0 && (isbin || !esc);
         {
             WOut w;
             w.init(ob + opos);
-            if (live && cl && hn == 1 && reqs) unset_fields(D, ldrec(&D.S[sidx]), reqs, flag, w); /* before the STOP */
 #if defined(DG_WV_ABL) && (DG_WV_ABL & 4)
             w.dry = true; /* ablation: no header/number stores */
 #endif
-            if (live && hn) w.wle(hv, hn);
-            if (live && ns >= 0 && hn == 0) emit_number(w, tt, isint, iv, dv);
-            if (chunked) deferred = true; /* chunk tasks, below */
-            else if (live && esc && isval) {
-                fast_unquote(src, cs, cn, w);
-            } else if (live && cn > 0) {
-                fast_copy(src, cs, cn, w);
-            }
+            if (live && kbn) w.wle(kb, kbn);
+            if (live && kn > 0) fast_copy(src, ks, kn, w); /* string map key (no escapes) */
+            if (live && cl && vbn == 1 && reqs) unset_fields(D, ldrec(&D.S[sidx]), reqs, flag, w); /* before the STOP */
+            if (live && vbn) w.wle(vb, vbn);
+            if (live && !chunked && esc && kind == K_STRING) fast_unquote(src, cs, cn, w);
             w.finish();
-            if (live && !op && !deferred && w.len != ln) bad = true;
+            if (live && !op && !chunked && w.len != ln) bad = true;
         }
         if (alive && cl) {
-            const uint32_t pf = L.crec[ci].flags;
-            if (!(pf & CF_SKIP) && !(pf & CF_STRUCT))
-                put_be32(ob + L.crec[ci].outpos + ((pf & CF_MAP) ? 2 : 1), L.crec[ci].count);
+            if (!(pflags & CF_SKIP) && !(pflags & CF_STRUCT))
+                put_be32(ob + L.crec[ci].outpos + ((pflags & CF_MAP) ? 2 : 1), L.crec[ci].count);
         }
         WP(6);
         /* string / base64 bodies: WV_CH-byte chunk tasks over the 64 lanes
          * (task c belongs to the first lane whose inclusive chunk count
-         * exceeds c), so the page's longest string no longer sets the time */
+         * exceeds c), so the page's longest string does not set the time */
         {
-            const uint32_t nch = deferred ? (uint32_t)((cn + WV_CH - 1) / WV_CH) : 0u;
+            const uint32_t nch = chunked ? (uint32_t)((cn + WV_CH - 1) / WV_CH) : 0u;
             const uint32_t cinc = wave_incl_sum(nch, lane);
             const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)cinc, 63);
             if (T) {
                 L.cinc[lane] = cinc;
                 L.cbs[lane] = (uint32_t)cs;
-                L.cbd[lane] = (uint32_t)(opos + 4);
+                L.cbd[lane] = opos + khead + 4;
                 L.cbn[lane] = (uint32_t)cn | (isbin ? 0x80000000u : 0u);
                 __builtin_amdgcn_wave_barrier();
 #if defined(DG_WV_ABL) && (DG_WV_ABL & 8)
@@ -1058,7 +1143,7 @@ DGI bool wave_run(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L
         }
         WP(8);
         depth = __builtin_amdgcn_readlane(dafter, (int)np - 1);
-        consumed += np;
+        consumed += lastoff + 1;
         if (bend) {
             rootdone = true;
             break;
