@@ -15,8 +15,8 @@ LIB_PATH = os.environ.get("DG_LIB_PATH") or os.path.join(HERE, "libdgj2t.so")
 EXPORTS = ["dg_last_error", "dg_build_info", "dg_ctx_create", "dg_ctx_destroy", "dg_ctx_stream", "dg_ctx_stats", "dg_ctx_counters", "dg_ctx_set_knob", "dg_ctx_get_knob",
            "dg_desc_create",
            "dg_desc_create_device", "dg_desc_destroy", "dg_desc_root", "dg_j2t_batch_device",
-           "dg_j2t_batch_device_ml", "dg_j2t_batch_device_iters",
-           "dg_slot_bound", "dg_j2t_batch_host", "dg_j2t_do", "dg_pack_device", "dg_pack_device_scan", "dg_pack_device_framed", "dg_agg_create", "dg_agg_do", "dg_agg_stats",
+           "dg_j2t_batch_device_ml", "dg_j2t_batch_device_hm", "dg_j2t_batch_device_iters",
+           "dg_slot_bound", "dg_j2t_batch_host", "dg_j2t_batch_host_hm", "dg_j2t_do", "dg_pack_device", "dg_pack_device_scan", "dg_pack_device_framed", "dg_agg_create", "dg_agg_do", "dg_agg_stats",
            "dg_agg_destroy", "dg_bench_device", "dg_desc_attach_t2j", "dg_t2j_slot_bound", "dg_t2j_batch_device", "dg_t2j_batch_device_ml",
            "dg_t2j_batch_host"]
 
@@ -60,6 +60,8 @@ def lib() -> C.CDLL:
         "dg_desc_root": (u32, [vp]),
         "dg_j2t_batch_device": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, vp, vp, vp, vp, vp]),
         "dg_j2t_batch_device_ml": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, vp, vp, vp, vp, vp, u64]),
+        "dg_j2t_batch_device_hm": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, u32, vp, vp, vp, vp, vp, vp, vp, u64]),
+        "dg_j2t_batch_host_hm": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, u32, vp, u64, vp, u64, vp, vp, P64]),
         "dg_j2t_batch_device_iters": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, vp, vp, vp, vp, vp, u64, C.c_int]),
         "dg_slot_bound": (u64, [u64]),
         "dg_j2t_batch_host": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, u64, vp, vp, P64]),

@@ -21,6 +21,7 @@ from typing import List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import _lib
+from . import http as H
 from .thrift import FlatDescriptor, TypeDescriptor, flatten, TYPE_NAMES
 
 # flag bits (native/thrift.h:23-32, internal/types/types.go:81-92)
@@ -41,6 +42,8 @@ F_NO_FLAT_PATH = 1 << 21   # extension: the lane-per-message small kernel even f
 
 DG_ST_OUT_OVERFLOW = 0xF0
 DG_ST_DEEP = 0xF1
+DG_ST_HM_END = 0xF2
+DG_ST_HM_ERR = 0xF3
 
 # internal/types/types.go:107-131 ParsingError messages
 _ERR_MSG = {0: "ok", 1: "eof", 2: "invalid char", 3: "invalid escape char", 4: "invalid unicode escape",
@@ -67,6 +70,8 @@ class Options:
     WriteRequireField: bool = False
     DisallowUnknownField: bool = False
     ReadHttpValueFallback: bool = False
+    TracebackRequredOrRootFields: bool = False
+    MergeBaseFunc: Optional[object] = None  # func(json_base, ctx_base) -> Base (conv/api.go:118-120)
     ValidateUTF8: bool = False  # extension (north_star: "UTF-8 validation"), default off
     # fields only the reverse path (t2j, dynamicgo_amd.t2j) reads
     Int642String: bool = False
@@ -280,27 +285,188 @@ class BinaryConv:
         the Go host serves from the request (conv/j2t/impl_amd64.go:174-198);
         structs without mapped fields convert as usual."""
 
-    def do(self, desc, jbytes: bytes) -> Optional[bytes]:
-        """Do: returns Thrift bytes (None for an empty result) or raises J2TError."""
+    def do(self, desc, jbytes: bytes, req: Optional["H.HTTPRequest"] = None,
+           base: Optional["H.Base"] = None) -> Optional[bytes]:
+        """Do (conv/j2t/conv.go:53-77): returns Thrift bytes (None for an empty
+        result) or raises J2TError / http.ConvError. `req` is the context's
+        conv.CtxKeyHTTPRequest (EnableHttpMapping), `base` its
+        conv.CtxKeyThriftReqBase (EnableThriftBase)."""
+        if req is not None or base is not None:
+            outs, errs = self.do_batch_http(desc, [jbytes], [req], [base])
+            if errs[0] is not None:
+                raise errs[0]
+            return outs[0] or None
         outs, rets = self.do_batch(desc, [jbytes])
         if rets[0] != 0:
             raise J2TError(int(rets[0]), explain_native_error(int(rets[0]), jbytes))
         return outs[0] if outs[0] else None
 
-    def do_into(self, desc, jbytes: bytes, buf: bytearray):
+    def do_into(self, desc, jbytes: bytes, buf: bytearray, req=None, base=None):
         """DoInto: appends to buf."""
-        out = self.do(desc, jbytes)
+        out = self.do(desc, jbytes, req, base)
         if out:
             buf.extend(out)
 
+    def _td(self, desc) -> TypeDescriptor:
+        if isinstance(desc, FlatDescriptor):
+            raise TypeError("the HTTP-mapping path needs the TypeDescriptor (its annotations), not a flat blob")
+        return desc
+
+    def _nested(self, flags: int):
+        """writeStringValue's doImpl recursion (conv/j2t/impl.go:140-145): a
+        JSON-encoded complex value converted as its field's type, top=false,
+        on the GPU."""
+        def conv_nested(f, val: str) -> bytes:
+            src = val.encode("utf-8", "surrogateescape")
+            outs, rets = self.do_batch(f.type, [src], extra_flags=flags & ~to_flags(self.opts))
+            if int(rets[0]) != 0:
+                raise H.ConvError("ErrConvert", "failed to convert value of field '%s'" % f.name,
+                                  J2TError(int(rets[0]), explain_native_error(int(rets[0]), src)))
+            return outs[0]
+        return conv_nested
+
+    def do_batch_http(self, desc, msgs: Sequence[bytes], reqs: Sequence, bases: Optional[Sequence] = None):
+        """BinaryConv.do (conv/j2t/impl.go:38-91) for a batch with the Go-side
+        context: per message the HTTP request (EnableHttpMapping) and the
+        request Base (EnableThriftBase). The host does what the reference's Go
+        callbacks do (dynamicgo_amd.http):
+          * writeRequestBaseToThrift: the Base field first;
+          * handleHttpMappings for every struct with mapped fields, once per
+            message (its bytes depend on the request and the struct only): the
+            HTTP-mapping table the GPU writes from wherever the reference
+            raises ERR_HM (dg_j2t_batch_host_hm, DG_F_HM_SPLIT);
+          * an empty body: everything (impl.go:52-82);
+          * the root's ERR_HM_END (F_TRACE_BACK): handleUnmatchedFields + STOP.
+        Returns (outputs, errors): errors[i] is None, a J2TError (native
+        status) or an http.ConvError."""
+        self._check_opts()
+        o = self.opts
+        td = self._td(desc)
+        n = len(msgs)
+        bases = list(bases) if bases is not None else [None] * n
+        if len(reqs) != n or len(bases) != n:
+            raise ValueError("one request and one base (or None) per message")
+        flags0 = to_flags(o)
+        sd = td.struct if td.type == 12 else None
+        flat = self._flat(td)
+        hx = H.HMContext(o, self._nested(flags0))
+        hm_structs = [x for x in flat.structs if x.hms] if o.EnableHttpMapping else []
+        n_hm = len(hm_structs)
+        outs: List[Optional[bytes]] = [None] * n
+        errs: List[Optional[Exception]] = [None] * n
+        prefix = [b""] * n
+        rows = {}       # message -> its n_hm (off, len, mask) entries
+        hm_err = {}     # (message, slot) -> the host's error for that struct
+        hm_bytes = bytearray()
+        groups = {}     # flag word -> message indices for the GPU
+        rb = None
+        if o.EnableThriftBase and sd is not None:
+            rb = next((f for f in sorted(sd.fields, key=lambda f: f.id) if f.is_request_base), None)
+        for i, src in enumerate(msgs):
+            req = reqs[i]
+            fl = flags0
+            try:
+                if o.EnableHttpMapping and req is None:
+                    raise H.ConvError("ErrInvalidParam", "EnableHttpMapping but no http response in context")
+                pre = b""
+                if rb is not None:
+                    b, no_write = H.write_request_base(bases[i], rb, src, o.MergeBaseFunc)
+                    pre += b
+                    if no_write:
+                        fl |= F_NO_WRITE_BASE
+                if len(src) == 0:
+                    out = pre
+                    if o.EnableHttpMapping and req is not None and sd is not None:
+                        out += hx.empty_body(req, sd)
+                    else:
+                        out += b"\x00"
+                    outs[i] = out
+                    continue
+            except H.ConvError as e:
+                errs[i] = e
+                continue
+            if n_hm:
+                row = []
+                for j, hsd in enumerate(hm_structs):
+                    try:
+                        b, mask, _ = hx.handle_http_mappings(req, hsd, False)
+                        row.append((len(hm_bytes), len(b), mask))
+                        hm_bytes += b
+                    except H.ConvError as e:
+                        row.append((0, 0xFFFFFFFF, 0))  # DG_HM_ERR
+                        hm_err[(i, j)] = e
+                rows[i] = row
+                fl |= F_HM_SPLIT
+            prefix[i] = pre
+            groups.setdefault(fl, []).append(i)
+        ctx = self._ctx()
+        L = _lib.lib()
+        hb = np.frombuffer(bytes(hm_bytes) + b"\0" * 8, dtype=np.uint8)
+        ent = np.dtype([("off", "<u4"), ("len", "<u4"), ("mask", "<u8")])
+        order = sorted(sd.fields, key=lambda f: f.id) if sd is not None else []
+        for fl, idx in groups.items():
+            sub = [msgs[i] for i in idx]
+            m = len(sub)
+            lens = np.fromiter((len(x) for x in sub), dtype=np.uint64, count=m)
+            in_off = np.zeros(m + 1, dtype=np.uint64)
+            np.cumsum(lens, out=in_off[1:])
+            arena = np.frombuffer(b"".join(sub) + b"\0" * 16, dtype=np.uint8)
+            tab = np.zeros(max(1, m * n_hm), dtype=ent)
+            if fl & F_HM_SPLIT:
+                for k, i in enumerate(idx):
+                    for j, e in enumerate(rows[i]):
+                        tab[k * n_hm + j] = e
+            rets = np.zeros(max(m, 1), dtype=np.uint64)
+            out_off = np.zeros(m + 1, dtype=np.uint64)
+            cap = int(lens.sum()) * 4 + 64 * m + len(hm_bytes) * m + 64
+            need = C.c_uint64(0)
+            for _ in range(2):
+                out = np.zeros(cap, dtype=np.uint8)
+                split = bool(fl & F_HM_SPLIT)
+                rc = L.dg_j2t_batch_host_hm(ctx.h, ctx.desc(flat), flat.root_type, arena.ctypes.data,
+                                            in_off.ctypes.data, m, fl, tab.ctypes.data if split else None,
+                                            n_hm if split else 0, hb.ctypes.data, len(hm_bytes) if split else 0,
+                                            out.ctypes.data, cap, out_off.ctypes.data, rets.ctypes.data,
+                                            C.byref(need))
+                if rc == -3 and need.value > cap:
+                    cap = int(need.value) + 64
+                    continue
+                break
+            _lib.check(rc)
+            for k, i in enumerate(idx):
+                r = int(rets[k])
+                body = out[int(out_off[k]):int(out_off[k + 1])].tobytes()
+                if r == 0:
+                    outs[i] = prefix[i] + body
+                elif (r & 0xFF) == DG_ST_HM_END:
+                    # the root's ERR_HM_END: the unmatched fields are the set bits of
+                    # the requires words behind the partial output (field index in id order)
+                    w = r >> 40
+                    part, words = body[:len(body) - 8 * w], body[len(body) - 8 * w:]
+                    ids = []
+                    for j in range(w):
+                        bits = int.from_bytes(words[8 * j:8 * j + 8], "big")
+                        ids += [order[64 * j + b].id for b in range(64)
+                                if (bits >> b) & 1 and 64 * j + b < len(order)]
+                    ids = [x for x in ids if not sd.field_by_id(x).is_request_base]
+                    try:
+                        outs[i] = prefix[i] + part + hx.handle_unmatched_fields(reqs[i], sd, ids, True) + b"\x00"
+                    except H.ConvError as e:
+                        errs[i] = e
+                elif (r & 0xFF) == DG_ST_HM_ERR:
+                    errs[i] = hm_err[(i, r >> 40)]
+                else:
+                    errs[i] = J2TError(r, explain_native_error(r, msgs[i]))
+        return outs, errs
+
     def do_batch_hm_split(self, desc, msgs: Sequence[bytes], prefixes: Sequence[bytes]):
-        """EnableHttpMapping, pre-split on the host: the
-        Go host has run handleHttpMappings (conv/j2t/impl.go:243-292) for the
-        ROOT struct and produced prefixes[i], its mapped fields' Thrift bytes;
-        the GPU converts the bodies with DG_F_HM_SPLIT (mapped keys skipped,
-        mapped fields counted as set) and each result is prefix + body (pass
-        b"" for a root without mapped fields). A nested struct with mapped
-        fields still returns ERR_HM (19)."""
+        """The root-only pre-split (DG_F_HM_SPLIT without a table): the caller
+        has run handleHttpMappings (conv/j2t/impl.go:243-292) for the ROOT
+        struct and passes prefixes[i], its mapped fields' Thrift bytes, every
+        value found; the GPU converts the bodies (mapped keys skipped, mapped
+        fields counted as set) and each result is prefix + body. A nested
+        struct with mapped fields returns ERR_HM (19): do_batch_http serves
+        those."""
         if len(prefixes) != len(msgs):
             raise ValueError("one prefix per message")
         outs, rets = self.do_batch(desc, msgs, extra_flags=F_HTTP_MAPPING | F_HM_SPLIT)
@@ -454,8 +620,10 @@ class HTTPConv:
         return BinaryConv(o, ctx=self.ctx)
 
     def do(self, req, opts: Optional[Options] = None) -> bytes:
-        """HTTPConv.Do: header + body + footer, or J2TError."""
-        body = self._conv(opts).do(self.st, req.get_body()) or b""
+        """HTTPConv.Do: header + body + footer, or J2TError / http.ConvError.
+        The request's mapped values are written by the host half
+        (BinaryConv.do_batch_http)."""
+        body = self._conv(opts).do(self.st, req.get_body(), req=req) or b""
         return self.top + body + self.bottom
 
     def do_into(self, req, buf: bytearray, opts: Optional[Options] = None):
@@ -464,10 +632,21 @@ class HTTPConv:
         buf.extend(out)
 
     def do_batch(self, reqs: Sequence, opts: Optional[Options] = None):
-        """Many requests: converted and framed on the GPU. Returns (framed
-        message per request (b"" where it failed), packed status words)."""
-        import torch
+        """Many requests. A root without HTTP-mapped fields is converted and
+        framed on the GPU (dg_pack_device_framed); one with them goes through
+        the host half (BinaryConv.do_batch_http) and is framed here. Returns
+        (framed message per request (b"" where it failed), errors: None, a
+        J2TError or an http.ConvError)."""
         cv = self._conv(opts)
+        if self.st.struct.hms or cv.opts.EnableThriftBase or any(len(r.get_body()) == 0 for r in reqs):
+            outs, errs = cv.do_batch_http(self.st, [r.get_body() for r in reqs], list(reqs))
+            return [self.top + (o or b"") + self.bottom if e is None else b"" for o, e in zip(outs, errs)], errs
+        outs, rets = self._framed_on_gpu(cv, reqs)
+        return outs, [None if int(r) == 0 else J2TError(int(r), explain_native_error(int(r), q.get_body()))
+                      for r, q in zip(rets, reqs)]
+
+    def _framed_on_gpu(self, cv, reqs: Sequence):
+        import torch
         ctx = cv._ctx()
         flat = cv._flat(self.st)
         bodies = [r.get_body() for r in reqs]
@@ -502,19 +681,14 @@ class HTTPConv:
         outs = [packed[int(doff[i]):int(doff[i + 1])] for i in range(n)]
         for i in pending:  # slot overflow: the exact-size host rerun
             try:
-                outs[i] = self.do(reqs[i], opts)
+                outs[i] = self.do(reqs[i], cv.opts)
                 rets[i] = 0
             except J2TError as e:
                 outs[i], rets[i] = b"", e.ret
         return outs, rets
 
 
-class HTTPRequest:
-    """Minimal http.RequestGetter (http/http.go:63-84): what HTTPConv reads
-    from the request on the GPU path is its body."""
-
-    def __init__(self, body: bytes):
-        self.body = body
-
-    def get_body(self) -> bytes:
-        return self.body
+def HTTPRequest(body: bytes = b"", **kw) -> "H.HTTPRequest":
+    """http.HTTPRequest (dynamicgo_amd.http) with the body first: url,
+    headers, cookies, params, post_form as keyword arguments."""
+    return H.HTTPRequest(body=body, **kw)

@@ -314,9 +314,17 @@ static int ensure_fast_ws(Scratch *x, uint64_t lanes)
     return DG_OK;
 }
 
+/* the HTTP-mapping table of a DG_F_HM_SPLIT batch (dgj2t_defs.h), device pointers */
+struct HMIn {
+    const dg_hm_entry *tab;
+    uint32_t n_hm;
+    const uint8_t *bytes;
+};
+
 static int enqueue(dg_ctx *c, Scratch *x, const dg_desc *d, uint32_t root, const uint8_t *json,
                    const uint64_t *in_off, uint64_t n, uint64_t flags, uint8_t *out, const uint64_t *out_off,
-                   uint32_t *out_len, uint64_t *ret, uint32_t *pending, hipStream_t s, uint64_t max_len)
+                   uint32_t *out_len, uint64_t *ret, uint32_t *pending, hipStream_t s, uint64_t max_len,
+                   const HMIn *hm)
 {
     int rc = ensure_fast_ws(x, n);
     if (rc) return rc;
@@ -342,6 +350,9 @@ static int enqueue(dg_ctx *c, Scratch *x, const dg_desc *d, uint32_t root, const
     P.big_max = 0;
     P.huge_count = nullptr;
     P.huge_min = WV_HUGE_MIN;
+    P.hm_tab = hm ? hm->tab : nullptr;
+    P.hm_bytes = hm ? hm->bytes : nullptr;
+    P.n_hm = hm ? hm->n_hm : 0;
     P.out = out;
     P.out_off = out_off;
     P.out_len = out_len;
@@ -367,10 +378,11 @@ static int enqueue(dg_ctx *c, Scratch *x, const dg_desc *d, uint32_t root, const
     const uint64_t big_max = (uint64_t)K.wave_min; /* messages longer than this go to the wave kernel */
     const bool wave = P.fast && !no_wave && d->hdr.total_len <= WV_DESC && d->hdr.total_len <= DESC_LDS_BYTES &&
                       (max_len == 0 || max_len > big_max);
-    /* the wave kernel's instance: 5 waves/SIMD when the caller's max_len
-     * rules out huge messages (their tail grows with a fifth wave per SIMD,
-     * j2t_wave.h), else 4; the wave_occ knob (4|5) forces one */
-    const bool wave5 = K.wave_occ ? K.wave_occ == 5 : (max_len != 0 && max_len <= WV_HUGE_MIN);
+    /* the wave kernel's instance: 4 waves/SIMD with 2 KiB message staging
+     * (C3 1.46 ms) beats the 5-wave one (96 VGPRs, 98 spilled, 128 B staging:
+     * 1.55 ms) since keys ride in their values' lanes; the wave_occ knob
+     * (4|5) forces one */
+    const bool wave5 = K.wave_occ == 5;
     auto wave_launch = [&](hipStream_t st, const Params &Q, const WaveParams &W) {
         const uint64_t bpc = wave5 ? WV5_BLOCKS_PER_CU : WV_BLOCKS_PER_CU;
         const uint64_t wblocks = std::min<uint64_t>((n + WV_WAVES - 1) / WV_WAVES, (uint64_t)c->n_cu * bpc);
@@ -483,14 +495,15 @@ static int enqueue(dg_ctx *c, Scratch *x, const dg_desc *d, uint32_t root, const
  * this scratch starts clean. */
 static int launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *json, const uint64_t *in_off,
                   uint64_t n, uint64_t flags, uint8_t *out, const uint64_t *out_off, uint32_t *out_len,
-                  uint64_t *ret, uint32_t *pending, hipStream_t s, uint64_t max_len = 0)
+                  uint64_t *ret, uint32_t *pending, hipStream_t s, uint64_t max_len = 0,
+                  const HMIn *hm = nullptr)
 {
     if (n == 0) return DG_OK;
     if (root >= d->hdr.n_types) return set_err(DG_E_INVALID, "root type %u out of range", root);
     Scratch *x;
     int rc = scratch_for(c, s, &x);
     if (rc) return rc;
-    rc = enqueue(c, x, d, root, json, in_off, n, flags, out, out_off, out_len, ret, pending, s, max_len);
+    rc = enqueue(c, x, d, root, json, in_off, n, flags, out, out_off, out_len, ret, pending, s, max_len, hm);
     if (rc) (void)hipMemsetAsync(x->d_counts, 0, DG_J2T_COUNTS_BYTES, s);
     HIPCHK(hipEventRecord(x->done, s));
     x->used = true;
@@ -518,6 +531,20 @@ int dg_j2t_batch_device_ml(dg_ctx *c, const dg_desc *d, uint32_t root, const uin
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     return launch(c, d, root, d_json, d_in_off, n, flags, d_out, d_out_off, d_out_len, d_ret, d_pending, s, max_len);
+}
+
+int dg_j2t_batch_device_hm(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *d_json, const uint64_t *d_in_off,
+                           uint64_t n, uint64_t flags, const dg_hm_entry *d_hm_tab, uint32_t n_hm,
+                           const uint8_t *d_hm_bytes, uint8_t *d_out, const uint64_t *d_out_off, uint32_t *d_out_len,
+                           uint64_t *d_ret, uint32_t *d_pending, void *stream, uint64_t max_len)
+{
+    if (!c || !d || (d_hm_tab && n_hm && !d_hm_bytes)) return set_err(DG_E_INVALID, "bad args");
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    HMIn hm{d_hm_tab, n_hm, d_hm_bytes};
+    return launch(c, d, root, d_json, d_in_off, n, flags, d_out, d_out_off, d_out_len, d_ret, d_pending, s, max_len,
+                  d_hm_tab ? &hm : nullptr);
 }
 
 int dg_j2t_batch_device_iters(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *d_json,
@@ -549,9 +576,9 @@ static int pack_scan_nolock(dg_ctx *c, const uint8_t *d_out, const uint64_t *d_o
  * one exact-size launch on the same staging. */
 static const uint64_t HOST_ONE_TRIP = 4ull << 20;
 
-int dg_j2t_batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *json, const uint64_t *in_off,
-                      uint64_t n, uint64_t flags, uint8_t *out, uint64_t out_cap, uint64_t *out_off, uint64_t *ret,
-                      uint64_t *out_need)
+static int batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *json, const uint64_t *in_off,
+                      uint64_t n, uint64_t flags, const HMIn *hm, uint64_t hm_len, uint8_t *out, uint64_t out_cap,
+                      uint64_t *out_off, uint64_t *ret, uint64_t *out_need)
 {
     if (!c || !d || (!json && n) || !in_off || !out_off || (!ret && n)) return set_err(DG_E_INVALID, "bad args");
     std::lock_guard<std::mutex> g(c->mu);
@@ -559,11 +586,20 @@ int dg_j2t_batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
     int rc;
     hipStream_t s = c->stream;
     const uint64_t base = in_off[0], bytes = in_off[n] - in_off[0];
-    /* upload: [ioff (n+1) | soff (n+1) | JSON + 64 zero bytes] */
-    const uint64_t up_bytes = 16 * (n + 1) + bytes + 64;
+    /* upload: [ioff (n+1) | soff (n+1) | HTTP-mapping table (n x n_hm) and
+     * bytes (optional) | JSON + 64 zero bytes] */
+    const uint64_t nhm = hm ? hm->n_hm : 0;
+    const uint64_t hmb = hm ? (hm_len + 7) & ~7ull : 0;
+    const uint64_t hmw = hm ? 2 * n * nhm + hmb / 8 : 0; /* words */
+    const uint64_t up_bytes = 16 * (n + 1) + 8 * hmw + bytes + 64;
     if ((rc = grow_pinned(c->h_up, c->h_up_cap, up_bytes))) return rc;
     uint64_t *ioff = (uint64_t *)(void *)c->h_up, *soff = ioff + n + 1;
-    uint8_t *hj = (uint8_t *)(void *)(soff + n + 1);
+    uint64_t *hhm = soff + n + 1;
+    uint8_t *hj = (uint8_t *)(void *)(hhm + hmw);
+    if (hm) {
+        if (n * nhm) memcpy(hhm, hm->tab, 16 * n * nhm);
+        if (hm_len) memcpy(hhm + 2 * n * nhm, hm->bytes, hm_len);
+    }
     uint64_t max_len = 1;
     soff[0] = 0;
     for (uint64_t i = 0; i <= n; i++) ioff[i] = in_off[i] - base;
@@ -584,12 +620,19 @@ int dg_j2t_batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
     if ((rc = grow(c->d_pack_off, c->d_po_cap, n + 1))) return rc;
     if ((rc = grow_pinned(c->h_down, c->h_down_cap, one_trip ? head + slots + 64 : head + 8))) return rc;
     const uint64_t *d_in = (const uint64_t *)(void *)c->d_json, *d_oo = d_in + n + 1;
-    const uint8_t *d_j = c->d_json + 16 * (n + 1);
+    HMIn dhm{nullptr, (uint32_t)nhm, nullptr};
+    if (hm) {
+        dhm.tab = (const dg_hm_entry *)(const void *)(d_oo + n + 1);
+        dhm.bytes = (const uint8_t *)(const void *)(d_oo + n + 1 + 2 * n * nhm);
+    }
+    const uint8_t *d_j = c->d_json + 16 * (n + 1) + 8 * hmw;
     uint64_t *d_ret = (uint64_t *)(void *)c->d_pack;
     uint32_t *d_ol = (uint32_t *)(void *)(c->d_pack + 8 * n);
     uint8_t *d_packed = c->d_pack + head;
     HIPCHK(hipMemcpyAsync(c->d_json, c->h_up, up_bytes, hipMemcpyHostToDevice, s));
-    if ((rc = launch(c, d, root, d_j, d_in, n, flags, c->d_out, d_oo, d_ol, d_ret, nullptr, s, max_len))) return rc;
+    if ((rc = launch(c, d, root, d_j, d_in, n, flags, c->d_out, d_oo, d_ol, d_ret, nullptr, s, max_len,
+                     hm ? &dhm : nullptr)))
+        return rc;
     if ((rc = pack_scan_nolock(c, c->d_out, d_oo, d_ol, d_ret, n, nullptr, 0, nullptr, 0, d_packed, c->d_pack_off, s)))
         return rc;
     HIPCHK(hipMemcpyAsync(c->h_down, c->d_pack, one_trip ? head + slots : head, hipMemcpyDeviceToHost, s));
@@ -599,9 +642,10 @@ int dg_j2t_batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
     std::vector<uint32_t> olen(hol, hol + n);
     memcpy(ret, hret, n * 8);
     /* the packed bytes: failed and overflowed messages hold none */
+    auto kept = [&](uint64_t i) { return ret[i] == 0 || (uint8_t)ret[i] == DG_ST_HM_END; };
     uint64_t packed = 0;
     for (uint64_t i = 0; i < n; i++)
-        if (ret[i] == 0) packed += olen[i];
+        if (kept(i)) packed += olen[i];
     /* overflowed messages: rerun together, each in a slot of the size it
      * reported (out_len carries it), on the same device staging (free now) */
     std::vector<uint64_t> redo;
@@ -614,12 +658,15 @@ int dg_j2t_batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
         const uint64_t m = redo.size();
         uint64_t rb = 0;
         for (uint64_t i : redo) rb += ioff[i + 1] - ioff[i];
-        std::vector<uint8_t> up(16 * (m + 1) + rb + 64, 0);
-        uint64_t *io = (uint64_t *)(void *)up.data(), *so = io + m + 1;
-        uint8_t *rj = (uint8_t *)(void *)(so + m + 1);
+        const uint64_t rhw = hm ? 2 * m * nhm + hmb / 8 : 0;
+        std::vector<uint8_t> up(16 * (m + 1) + 8 * rhw + rb + 64, 0);
+        uint64_t *io = (uint64_t *)(void *)up.data(), *so = io + m + 1, *rhm = so + m + 1;
+        uint8_t *rj = (uint8_t *)(void *)(rhm + rhw);
         io[0] = so[0] = 0;
+        if (hm && hm_len) memcpy(rhm + 2 * m * nhm, hm->bytes, hm_len);
         for (uint64_t k = 0; k < m; k++) {
             const uint64_t i = redo[k], l = ioff[i + 1] - ioff[i];
+            if (hm && nhm) memcpy(rhm + 2 * k * nhm, hm->tab + i * nhm, 16 * nhm);
             memcpy(rj + io[k], hj + ioff[i], l);
             io[k + 1] = io[k] + l;
             so[k + 1] = so[k] + (((uint64_t)olen[i] + 64 + 7) & ~7ull);
@@ -635,8 +682,10 @@ int dg_j2t_batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
         uint64_t *r_ret = (uint64_t *)(void *)c->d_pack; /* rhead <= head: d_pack is large enough */
         uint32_t *r_ol = (uint32_t *)(void *)(c->d_pack + 8 * m);
         HIPCHK(hipMemcpyAsync(c->d_json, up.data(), up.size(), hipMemcpyHostToDevice, s));
-        if ((rc = launch(c, d, root, c->d_json + 16 * (m + 1), r_in, m, flags, c->d_out, r_oo, r_ol, r_ret, nullptr, s,
-                         max_len)))
+        HMIn rhmd{(const dg_hm_entry *)(const void *)(r_oo + m + 1), (uint32_t)nhm,
+                  (const uint8_t *)(const void *)(r_oo + m + 1 + 2 * m * nhm)};
+        if ((rc = launch(c, d, root, c->d_json + 16 * (m + 1) + 8 * rhw, r_in, m, flags, c->d_out, r_oo, r_ol, r_ret,
+                         nullptr, s, max_len, hm ? &rhmd : nullptr)))
             return rc;
         rdown.resize(rhead + so[m]);
         HIPCHK(hipMemcpyAsync(rdown.data(), c->d_pack, rhead, hipMemcpyDeviceToHost, s));
@@ -654,7 +703,7 @@ int dg_j2t_batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
     uint64_t total = 0;
     out_off[0] = 0;
     for (uint64_t i = 0; i < n; i++) {
-        if (ret[i] != 0) olen[i] = 0;
+        if (!kept(i)) olen[i] = 0;
         total += olen[i];
         out_off[i + 1] = total;
     }
@@ -683,6 +732,27 @@ int dg_j2t_batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
         }
     }
     return DG_OK;
+}
+
+int dg_j2t_batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *json, const uint64_t *in_off,
+                      uint64_t n, uint64_t flags, uint8_t *out, uint64_t out_cap, uint64_t *out_off, uint64_t *ret,
+                      uint64_t *out_need)
+{
+    return batch_host(c, d, root, json, in_off, n, flags, nullptr, 0, out, out_cap, out_off, ret, out_need);
+}
+
+int dg_j2t_batch_host_hm(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *json, const uint64_t *in_off,
+                         uint64_t n, uint64_t flags, const dg_hm_entry *hm_tab, uint32_t n_hm, const uint8_t *hm_bytes,
+                         uint64_t hm_len, uint8_t *out, uint64_t out_cap, uint64_t *out_off, uint64_t *ret,
+                         uint64_t *out_need)
+{
+    if ((hm_tab && n_hm && n && !hm_tab) || (hm_len && !hm_bytes)) return set_err(DG_E_INVALID, "bad args");
+    for (uint64_t k = 0; hm_tab && k < n * n_hm; k++)
+        if (hm_tab[k].len != DG_HM_ERR && (uint64_t)hm_tab[k].off + hm_tab[k].len > hm_len)
+            return set_err(DG_E_INVALID, "HTTP-mapping entry %llu outside the bytes", (unsigned long long)k);
+    HMIn hm{hm_tab, n_hm, hm_bytes};
+    return batch_host(c, d, root, json, in_off, n, flags, hm_tab ? &hm : nullptr, hm_len, out, out_cap, out_off, ret,
+                      out_need);
 }
 
 int dg_j2t_do(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *json, size_t len, uint64_t flags,

@@ -58,6 +58,10 @@ struct Params {
     uint64_t big_max;
     uint32_t *huge_count;      /* messages longer than huge_min go to the END of big_list (taken first) */
     uint64_t huge_min;
+    const dg_hm_entry *hm_tab; /* DG_F_HM_SPLIT: n_hm entries per message (dgj2t_defs.h), or NULL: the root's
+                                  mapped fields only, all written by the host */
+    const uint8_t *hm_bytes;
+    uint32_t n_hm;
 };
 
 /* List message i (len bytes) for the wave kernel. Huge ones are written from
@@ -112,6 +116,8 @@ struct Machine {
     Workspace ws;
     uint32_t reqlen;
     uint32_t field_cache_len;
+    const dg_hm_entry *hm_row; /* this message's HTTP-mapping entries (Params::hm_tab), or NULL */
+    const uint8_t *hm_bytes;
     JState jt;
     PROF_DECL
 
@@ -210,6 +216,21 @@ struct Machine {
             }
         }
         return 0;
+    }
+
+    /* ERR_HM_END (native/thrift.c:898-903): unset fields went to the Go
+     * handler's field cache. At the root under DG_F_HM_SPLIT the host serves
+     * it (handleUnmatchedFields, conv/j2t/impl_amd64.go:71-115): the output so
+     * far, then the root's remaining requires words (big-endian u64; the
+     * cached fields are their set bits, in field order), status
+     * DG_ST_HM_END with value = the word count. Elsewhere: the reference's
+     * code (a nested struct's callback needs the Go FSM to resume). */
+    template <class FR>
+    DGI uint64_t hm_end(const FR &x, const dg_struct &sd, int64_t p)
+    {
+        if (!(flag & DG_F_HM_SPLIT) || sp != 1) return pack0(E_HM_END, (uint64_t)p);
+        for (uint32_t w = 0; w < sd.req_words; w++) out.w64(sd.req_words == 1 ? x.u : ws.reqarena[(uint32_t)x.u + w]);
+        return pack(DG_ST_HM_END, sd.req_words, (uint64_t)p);
     }
 
     /* j2t_number native/thrift.c:312-365 */
@@ -563,7 +584,7 @@ struct Machine {
                         PROF(6, r = write_unset_fields(x, sd, p - 1));
                         if (r) return r;
                         if (sd.req_words > 1) reqlen -= sd.req_words;
-                        if ((flag & DG_F_ENABLE_HM) && field_cache_len > 0) return pack0(E_HM_END, (uint64_t)p);
+                        if ((flag & DG_F_ENABLE_HM) && field_cache_len > 0) return hm_end(x, sd, p);
                         out.w8(0);
                     } else {
                         out.put32(fbp(x), 0);
@@ -592,7 +613,7 @@ struct Machine {
                         PROF(6, r = write_unset_fields(x, sd, p - 1));
                         if (r) return r;
                         if (sd.req_words > 1) reqlen -= sd.req_words;
-                        if ((flag & DG_F_ENABLE_HM) && field_cache_len != 0) return pack0(E_HM_END, (uint64_t)p);
+                        if ((flag & DG_F_ENABLE_HM) && field_cache_len > 0) return hm_end(x, sd, p);
                         out.w8(0);
                     } else {
                         if (!null_val) set_size(x, fsize(x) + 1);
@@ -707,10 +728,27 @@ struct Machine {
                         /* ERR_HM (native/thrift.c:1119-1123) -> handleHttpMappings; pre-split
                          * (DG_F_HM_SPLIT): the host wrote the root's mapped fields, which
                          * reqs.Set(id, Optional) marks as set (conv/j2t/impl.go:284) */
-                        if (!(flag & DG_F_HM_SPLIT) || sp != 1) return pack0(E_HM, (uint64_t)(p - 1)); /* root: vt[0] */
+                        if (!(flag & DG_F_HM_SPLIT)) return pack0(E_HM, (uint64_t)(p - 1));
+                        uint64_t mask = ~0ull;
+                        if (hm_row) {
+                            /* the host's handleHttpMappings for this struct (the same bytes for
+                             * every instance: they depend on the request and the struct only) */
+                            uint32_t slot = 0;
+                            for (uint32_t s = 0; s < t.st; s++)
+                                if (ldrec(&D.S[s]).flags & DG_SF_HTTP_MAPPING) slot++;
+                            const dg_hm_entry e = hm_row[slot];
+                            if (e.len == DG_HM_ERR) return pack(DG_ST_HM_ERR, slot, (uint64_t)(p - 1));
+                            for (uint32_t b = 0; b < e.len; b++) out.w8(hm_bytes[(uint64_t)e.off + b]);
+                            mask = e.mask;
+                        } else if (sp != 1) {
+                            return pack0(E_HM, (uint64_t)(p - 1)); /* root only: vt[0] */
+                        }
+                        /* a mapped field the host wrote is reqs.Set(id, Optional) (its JSON key is
+                         * skipped); one it did not (ReadHttpValueFallback, not in the request) is
+                         * reqs.Set(id, Required): read from the body (impl.go:276-284) */
                         for (uint32_t k = 0; k < sd.n_fields; k++)
                             if (ldrec(&D.F[sd.field_begin + k]).flags & DG_FF_HTTP_MAPPING)
-                                bm_set_req(nx, sd, k, DG_REQ_OPTIONAL);
+                                bm_set_req(nx, sd, k, k >= 64 || ((mask >> k) & 1) ? DG_REQ_OPTIONAL : DG_REQ_REQUIRED);
                     }
                 } else {
                     out.w8(TY(t.key).ttype);
@@ -774,6 +812,8 @@ DGI uint64_t convert_one(const Params &P, const DV &dv, uint64_t i, const S &src
     m.ws = ws;
     m.reqlen = 0;
     m.field_cache_len = 0;
+    m.hm_row = P.hm_tab ? P.hm_tab + i * P.n_hm : nullptr;
+    m.hm_bytes = P.hm_bytes;
     uint64_t r;
     if (m.src.n == 0) { /* empty body -> STOP (conv/j2t/impl.go:52-82) */
         m.out.w8(0);
@@ -797,15 +837,16 @@ DGI uint64_t convert_one(const Params &P, const DV &dv, uint64_t i, const S &src
         r = m.run(P.root);
 #endif
     }
-    if (r == 0) m.out.finish();
-    if (r == 0 && m.out.len > m.out.cap) {
+    const bool keep = r == 0 || (uint8_t)r == DG_ST_HM_END; /* HM_END: the host completes the output */
+    if (keep) m.out.finish();
+    if (keep && m.out.len > m.out.cap) {
         /* the bytes needed travel in out_len (32 bits); the 24-bit value field
          * of the status word only carries them saturated */
         const uint64_t need = m.out.len;
         olen = need > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)need;
         return pack(DG_ST_OUT_OVERFLOW, need > 0xFFFFFFull ? 0xFFFFFFull : need, 0);
     }
-    olen = r == 0 ? (uint32_t)m.out.len : 0;
+    olen = keep ? (uint32_t)m.out.len : 0;
     return r;
 }
 

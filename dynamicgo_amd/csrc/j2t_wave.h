@@ -1345,7 +1345,10 @@ __global__ __launch_bounds__(256) void dg_pack_scan_kernel(const uint8_t *out, c
     const uint32_t fx = fr.hdr ? fr.hdr_len + fr.ftr_len : 0u;
     auto msg_len = [&](uint64_t i) -> uint32_t {
         if (!fr.ret) return out_len[i];
-        return fr.ret[i] == 0 ? out_len[i] + fx : 0u; /* failed messages pack as nothing */
+        if (fr.ret[i] == 0) return out_len[i] + fx;
+        /* failed messages pack as nothing; an unframed DG_ST_HM_END keeps its
+         * partial output for the host (dgj2t_defs.h) */
+        return !fr.hdr && (uint8_t)fr.ret[i] == DG_ST_HM_END ? out_len[i] : 0u;
     };
     uint64_t s = 0;
     for (uint64_t i = lo + tid; i < hi; i += 256) s += msg_len(i);

@@ -72,7 +72,7 @@ class FieldDescriptor:
     default_value: Optional[bytes] = None  # IDL default as Thrift binary bytes
     is_request_base: bool = False
     is_response_base: bool = False
-    http_mappings: List[str] = _dcfield(default_factory=list)
+    http_mappings: List[Tuple[str, str]] = _dcfield(default_factory=list)  # (annotation key, value), IDL order
 
     def __post_init__(self):
         if self.alias is None:
@@ -346,6 +346,7 @@ def flatten(root: TypeDescriptor) -> FlatDescriptor:
     body[:64] = hdr
     fd = FlatDescriptor(bytes(body), root_idx, types)
     fd.fields = field_objs
+    fd.structs = structs  # StructDescriptors in blob order (the HTTP-mapping table's slots)
     return fd
 
 
@@ -740,7 +741,7 @@ class _Compiler:
                 elif k == "api.js_conv":
                     vm = VM_JSCONV
                 elif k in HTTP_MAPPING_KEYS:
-                    hms.append(k)
+                    hms.append((k, v))
             is_req_base = (self.opts.enable_thrift_base and pf.type.name == "base.Base" and depth == 0)
             is_resp_base = (self.opts.enable_thrift_base and pf.type.name == "base.BaseResp" and depth == 0)
             ftype = self.ptype(ff, pf.type, cache, depth + 1)

@@ -126,6 +126,22 @@ int dg_j2t_batch_device_ml(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type,
                            const uint64_t *d_out_off, uint32_t *d_out_len, uint64_t *d_ret,
                            uint32_t *d_pending, void *stream, uint64_t max_len);
 
+/* dg_j2t_batch_device_ml for DG_F_HM_SPLIT batches (HTTPConv with the host
+ * half of the reference's HTTP-mapping callbacks): d_hm_tab holds n_hm
+ * dg_hm_entry per message (dgj2t_defs.h), the bytes handleHttpMappings
+ * (conv/j2t/impl.go:243-292) wrote for each struct with mapped fields and the
+ * mask of the fields it wrote, into d_hm_bytes. Where the reference returns
+ * ERR_HM to Go, the kernel writes the entry's bytes and resumes. A ROOT whose
+ * unset fields go to the reference's field cache (F_TRACE_BACK) comes back as
+ * DG_ST_HM_END for the host to finish; DG_ST_HM_ERR = the host's entry was an
+ * error. d_hm_tab NULL = the root's mapped fields only, all written by the
+ * host (its bytes put in front by the caller). */
+int dg_j2t_batch_device_hm(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, const uint8_t *d_json,
+                           const uint64_t *d_in_off, uint64_t n, uint64_t flags, const dg_hm_entry *d_hm_tab,
+                           uint32_t n_hm, const uint8_t *d_hm_bytes, uint8_t *d_out, const uint64_t *d_out_off,
+                           uint32_t *d_out_len, uint64_t *d_ret, uint32_t *d_pending, void *stream,
+                           uint64_t max_len);
+
 /* dg_j2t_batch_device_ml enqueued `iters` times back to back in one call
  * (one lock, no host round trip between batches): a host that re-runs the
  * same job -- benchmarks, replays -- keeps the GPU fed. Every iteration is a
@@ -148,6 +164,14 @@ uint64_t dg_slot_bound(uint64_t len);
 int dg_j2t_batch_host(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, const uint8_t *json,
                       const uint64_t *in_off, uint64_t n, uint64_t flags, uint8_t *out, uint64_t out_cap,
                       uint64_t *out_off, uint64_t *ret, uint64_t *out_need);
+
+/* dg_j2t_batch_host with the HTTP-mapping table of dg_j2t_batch_device_hm
+ * (host memory; hm_bytes of hm_len bytes). DG_ST_HM_END messages keep their
+ * partial output (and requires words) in out. */
+int dg_j2t_batch_host_hm(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, const uint8_t *json,
+                         const uint64_t *in_off, uint64_t n, uint64_t flags, const dg_hm_entry *hm_tab, uint32_t n_hm,
+                         const uint8_t *hm_bytes, uint64_t hm_len, uint8_t *out, uint64_t out_cap, uint64_t *out_off,
+                         uint64_t *ret, uint64_t *out_need);
 
 /* One message, BinaryConv.Do semantics (conv/j2t/conv.go:53-77). *out_len is
  * the Thrift length; returns the packed status word through *ret. */

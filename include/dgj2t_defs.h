@@ -22,12 +22,14 @@
 #define DG_F_NO_WAVE_PATH (1ull << 18)  /* extension: skip the wave-per-message kernel, lane kernel only (testing) */
 #define DG_F_FLAT_PATH (1ull << 19)     /* extension: force the field-major flat kernel (j2t_flat.h) for a flat root
                                            struct (the default whenever the batch's messages are <= 256 B) */
-#define DG_F_HM_SPLIT (1ull << 20)      /* extension, with F_ENABLE_HM: the host has already written the ROOT struct's
-                                           HTTP-mapped fields (handleHttpMappings, conv/j2t/impl.go:243-292, every
-                                           value found); the root raises no ERR_HM, its mapped fields count as set
-                                           and their JSON keys are skipped (native/thrift.c:725). The output is the
-                                           body part: the host puts its mapped-field bytes in front. Nested structs
-                                           with mapped fields still return ERR_HM. */
+#define DG_F_HM_SPLIT (1ull << 20)      /* extension, with F_ENABLE_HM: the host has already run handleHttpMappings
+                                           (conv/j2t/impl.go:243-292) for the ROOT struct; the root raises no ERR_HM,
+                                           the mapped fields the host wrote (all of them, or those of the per-message
+                                           mask of dg_j2t_batch_*_hm) count as set and their JSON keys are skipped
+                                           (native/thrift.c:725), the others are read from the body
+                                           (ReadHttpValueFallback). The output is the body part: the host puts its
+                                           mapped-field bytes in front. Nested structs with mapped fields still
+                                           return ERR_HM. */
 #define DG_F_NO_FLAT_PATH (1ull << 21)  /* extension: lane-per-message small kernel even for a flat root (testing) */
 
 /* library-internal per-message statuses (code byte values the reference never
@@ -35,6 +37,28 @@
  * entry point leaves them for the caller and counts them in *d_pending. */
 #define DG_ST_OUT_OVERFLOW 0xF0u /* slot too small; out_len = bytes needed (value bits: same, saturated at 2^24-1) */
 #define DG_ST_DEEP 0xF1u         /* (internal) nesting beyond the fast kernel's stack */
+#define DG_ST_HM_END 0xF2u       /* DG_F_HM_SPLIT + F_TRACE_BACK: the ROOT's ERR_HM_END (native/thrift.c:898-903)
+                                    for the host to serve (handleUnmatchedFields, conv/j2t/impl_amd64.go:71-115):
+                                    out_len covers the output so far followed by the root's remaining requires
+                                    words (big-endian u64, `value` of them); the host appends the cached fields'
+                                    bytes and the STOP */
+#define DG_ST_HM_ERR 0xF3u       /* DG_F_HM_SPLIT: the message opened a struct whose HTTP-mapping entry is an
+                                    error (dg_hm_entry.len == DG_HM_ERR): handleHttpMappings failed for it on the
+                                    host; value = the entry's slot, pos = the struct's '{' */
+
+/* HTTP-mapping table of dg_j2t_batch_*_hm: per message, one entry per struct
+ * of the descriptor with HTTP-mapped fields (slot j = the j-th such struct in
+ * blob order): the bytes the host's handleHttpMappings (conv/j2t/impl.go:
+ * 243-292) writes for that struct, at hm_bytes[off, off + len), and the mask
+ * of its mapped fields it wrote (bit k = the struct's k-th field in id order;
+ * an unset bit = reqs.Set(id, Required), read from the body:
+ * ReadHttpValueFallback). len == DG_HM_ERR: the host failed (DG_ST_HM_ERR). */
+typedef struct dg_hm_entry {
+    uint32_t off;
+    uint32_t len;
+    uint64_t mask;
+} dg_hm_entry;
+#define DG_HM_ERR 0xFFFFFFFFu
 
 /* API error codes */
 #define DG_OK 0

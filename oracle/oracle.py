@@ -101,6 +101,63 @@ class _Base:
             return int(ret), b""
         return 0, out.raw[:ol.value]
 
+    def j2t_hm2(self, flat, json: bytes, flags: int, prefix: bytes, mask: int, root: Optional[int] = None):
+        """j2t_hm with the host's mask of the mapped fields it wrote (bit k =
+        the root's k-th field in id order). Returns (ret, out, field_cache):
+        for the root's ERR_HM_END (code 21) `out` is the output so far and
+        `field_cache` the unmatched field ids (reference harness only)."""
+        f = getattr(self.lib, self.p + "j2t_hm2")
+        f.restype = C.c_uint64
+        f.argtypes = [C.c_void_p, C.c_uint32, C.c_char_p, C.c_size_t, C.c_uint64, C.c_char_p, C.c_size_t,
+                      C.c_uint64, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t), C.c_void_p, C.c_size_t,
+                      C.POINTER(C.c_size_t)]
+        d = self._desc(flat.blob)
+        root = flat.root_type if root is None else root
+        cap = 16 * len(json) + len(prefix) + 65536
+        out = C.create_string_buffer(cap)
+        ol = C.c_size_t(0)
+        fc = (C.c_int32 * 4096)()
+        fl = C.c_size_t(0)
+        ret = f(d, root, json, len(json), flags, prefix, len(prefix), mask & (2**64 - 1), out, cap, C.byref(ol),
+                fc, 4096, C.byref(fl))
+        if ret != 0 and (ret & 0xFF) != 21:
+            return int(ret), b"", []
+        return int(ret), out.raw[:ol.value], [int(fc[k]) for k in range(fl.value)]
+
+    def j2t_hm3(self, flat, json: bytes, flags: int, entries, root: Optional[int] = None):
+        """j2t with ERR_HM served at every depth: entries[struct index] =
+        (bytes, mask) the host wrote for that struct, None = the host failed
+        (the ERR_HM code comes back). Returns (ret, out, field_cache) like
+        j2t_hm2 (reference harness only)."""
+        f = getattr(self.lib, self.p + "j2t_hm3")
+        f.restype = C.c_uint64
+        f.argtypes = [C.c_void_p, C.c_uint32, C.c_char_p, C.c_size_t, C.c_uint64, C.c_char_p, C.c_void_p,
+                      C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t), C.c_void_p, C.c_size_t,
+                      C.POINTER(C.c_size_t)]
+        d = self._desc(flat.blob)
+        root = flat.root_type if root is None else root
+        ns = len(entries)
+        off = (C.c_uint32 * max(ns, 1))()
+        ln = (C.c_uint32 * max(ns, 1))()
+        mk = (C.c_uint64 * max(ns, 1))()
+        buf = b""
+        for k, e in enumerate(entries):
+            if e is None:
+                ln[k] = 0xFFFFFFFF
+                continue
+            off[k], ln[k], mk[k] = len(buf), len(e[0]), e[1] & (2**64 - 1)
+            buf += e[0]
+        cap = 16 * len(json) + 64 * len(buf) + 65536
+        out = C.create_string_buffer(cap)
+        ol = C.c_size_t(0)
+        fc = (C.c_int32 * 4096)()
+        fl = C.c_size_t(0)
+        ret = f(d, root, json, len(json), flags, buf + b"\0", off, ln, mk, out, cap, C.byref(ol), fc, 4096,
+                C.byref(fl))
+        if ret != 0 and (ret & 0xFF) != 21:
+            return int(ret), b"", []
+        return int(ret), out.raw[:ol.value], [int(fc[k]) for k in range(fl.value)]
+
     def j2t_batch(self, flat, msgs: Sequence[bytes], flags: int, nthreads: int = 1,
                   root: Optional[int] = None, slot_factor: int = 4, slot_pad: int = 64):
         """Batch API over an arena: returns (rets u64[n], outs list[bytes])."""

@@ -247,6 +247,20 @@ static void ensure(char **p, size_t *cap, size_t need)
 static const uint8_t *g_hm_prefix;
 static size_t g_hm_len;
 static int g_hm_on;
+/* dgref_j2t_hm2: which mapped fields the host wrote (bit k = the k-th field
+ * of the root in id order; the others are reqs.Set(id, Required),
+ * ReadHttpValueFallback, conv/j2t/impl.go:276-280), and the root's
+ * ERR_HM_END field cache handed back instead of the error */
+static uint64_t g_hm_mask = ~0ull;
+/* dgref_j2t_hm3: per struct index (blob order) the host's bytes and mask,
+ * for an ERR_HM at ANY depth (the bytes handleHttpMappings writes depend on
+ * the request and the struct only) */
+static const uint8_t *g_hm_bytes;
+static const uint32_t *g_hm_off, *g_hm_lens;
+static const uint64_t *g_hm_masks;
+static int32_t *g_fc_out;
+static size_t g_fc_cap, g_fc_len;
+static int g_fc_on;
 
 static uint64_t ref_do(RefCtx *c, RefDesc *d, uint32_t root, const uint8_t *json, size_t n,
                        uint64_t flags, uint8_t *out, size_t out_cap, size_t *out_len)
@@ -359,12 +373,25 @@ static uint64_t ref_do(RefCtx *c, RefDesc *d, uint32_t root, const uint8_t *json
             fsm->vt[fsm->sp - 1].jp = p; /* SetPos */
             continue;
         }
-        if (e == ERR_HM && g_hm_on && fsm->sp == 1) {
-            J2TState *v = &fsm->vt[0];
+        if (e == ERR_HM && g_hm_on && (fsm->sp == 1 || g_hm_off)) {
+            J2TState *v = &fsm->vt[fsm->sp - 1];
             const tStructDesc *st = v->td->st;
-            for (size_t k = 0; k < st->ids.len; k++) {
+            if (g_hm_off) {
+                const size_t si = (size_t)(st - d->structs);
+                if (g_hm_lens[si] == 0xFFFFFFFFu)
+                    return ret; /* the host failed for this struct */
+                g_hm_prefix = g_hm_bytes + g_hm_off[si];
+                g_hm_len = g_hm_lens[si];
+                g_hm_mask = g_hm_masks[si];
+            }
+            for (size_t k = 0, j = 0; k < st->ids.len; k++) {
                 const tFieldDesc *f = ((tFieldDesc **)st->ids.buf)[k];
-                if (f && f->http_mappings.len) bm_set_req(v->ex.es.reqs, f->ID, REQ_OPTIONAL);
+                if (!f)
+                    continue;
+                if (f->http_mappings.len)
+                    bm_set_req(v->ex.es.reqs, f->ID,
+                               j >= 64 || ((g_hm_mask >> j) & 1) ? REQ_OPTIONAL : REQ_REQUIRED);
+                j++;
             }
             if (buf.len + g_hm_len > buf.cap) {
                 size_t nc = (buf.len + g_hm_len) * 2 + 64;
@@ -379,6 +406,17 @@ static uint64_t ref_do(RefCtx *c, RefDesc *d, uint32_t root, const uint8_t *json
             memcpy(buf.buf + buf.len, g_hm_prefix, g_hm_len);
             buf.len += g_hm_len;
             continue;
+        }
+        if (e == ERR_HM_END && g_fc_on && fsm->sp == 1) {
+            /* the root's unmatched fields: the output so far and the cache,
+             * for the caller to serve like handleUnmatchedFields */
+            g_fc_len = fsm->field_cache.len;
+            for (size_t k = 0; k < g_fc_len && k < g_fc_cap; k++)
+                g_fc_out[k] = fsm->field_cache.buf[k];
+            *out_len = buf.len;
+            if (buf.len <= out_cap)
+                memcpy(out, buf.buf, buf.len);
+            return ret;
         }
         break; /* real error or host callback (ERR_HM/HM_END/VM_END) */
     }
@@ -404,6 +442,48 @@ uint64_t dgref_j2t_hm(void *desc, uint32_t root, const uint8_t *json, size_t n, 
     g_hm_on = 1;
     uint64_t r = ref_do(g_ctx, (RefDesc *)desc, root, json, n, flags, out, out_cap, out_len);
     g_hm_on = 0;
+    return r;
+}
+
+/* dgref_j2t_hm with the host's per-message mask of written mapped fields;
+ * a root ERR_HM_END returns its code with *out_len = the output so far and
+ * the field cache in fc[0..*fc_len) */
+uint64_t dgref_j2t_hm2(void *desc, uint32_t root, const uint8_t *json, size_t n, uint64_t flags,
+                       const uint8_t *prefix, size_t plen, uint64_t mask, uint8_t *out, size_t out_cap,
+                       size_t *out_len, int32_t *fc, size_t fc_cap, size_t *fc_len)
+{
+    if (!g_ctx)
+        g_ctx = ctx_new();
+    g_hm_prefix = prefix;
+    g_hm_len = plen;
+    g_hm_on = 1;
+    g_hm_mask = mask;
+    g_fc_out = fc;
+    g_fc_cap = fc_cap;
+    g_fc_len = 0;
+    g_fc_on = 1;
+    uint64_t r = ref_do(g_ctx, (RefDesc *)desc, root, json, n, flags, out, out_cap, out_len);
+    g_hm_on = 0;
+    g_fc_on = 0;
+    g_hm_mask = ~0ull;
+    *fc_len = g_fc_len;
+    return r;
+}
+
+/* dgref_j2t_hm2 with an ERR_HM served at every depth from per-struct
+ * entries (index = struct index in blob order; len 0xFFFFFFFF = the host
+ * failed: the ERR_HM code is returned) */
+uint64_t dgref_j2t_hm3(void *desc, uint32_t root, const uint8_t *json, size_t n, uint64_t flags,
+                       const uint8_t *bytes, const uint32_t *off, const uint32_t *len, const uint64_t *masks,
+                       uint8_t *out, size_t out_cap, size_t *out_len, int32_t *fc, size_t fc_cap, size_t *fc_len)
+{
+    g_hm_bytes = bytes;
+    g_hm_off = off;
+    g_hm_lens = len;
+    g_hm_masks = masks;
+    uint64_t r = dgref_j2t_hm2(desc, root, json, n, flags, NULL, 0, ~0ull, out, out_cap, out_len, fc, fc_cap, fc_len);
+    g_hm_off = NULL;
+    g_hm_lens = NULL;
     return r;
 }
 
