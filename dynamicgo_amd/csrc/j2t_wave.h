@@ -76,7 +76,10 @@ constexpr uint32_t WV_RING = DG_WV_RING;       /* token ring per wave (a scan st
 constexpr uint32_t WV_RMASK = WV_RING - 1;
 constexpr uint32_t WV_CHUNK = 256;             /* bytes classified per scan step: 64 lanes x 4 */
 constexpr uint32_t WV_MAXD = 16;               /* container levels handled on the wave path */
-constexpr uint32_t WV_FILL = 100;              /* entries scanned ahead before a page is converted */
+#ifndef DG_WV_FILL
+#define DG_WV_FILL 120
+#endif
+constexpr uint32_t WV_FILL = DG_WV_FILL;       /* entries scanned ahead before a page is converted */
 constexpr uint32_t WV_NOEND = 0xFFFFFFFFu;     /* string not closed (yet) */
 constexpr uint32_t WV_POSMASK = (1u << 29) - 1;
 constexpr uint32_t WV_MSG = DG_WV_MSG;         /* messages up to this (minus 16) are staged in LDS */

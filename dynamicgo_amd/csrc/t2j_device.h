@@ -31,6 +31,7 @@ namespace dg {
 
 constexpr uint32_t T2J_LDS_DEPTH = 12;   /* frames per lane in LDS */
 constexpr uint32_t T2J_DEEP_DEPTH = 4096; /* frames per lane in the deep rerun */
+constexpr uint32_t T2J_WIDE_WORDS = 1024; /* deep rerun: requires words per lane for structs of > 64 fields */
 constexpr uint32_t T2J_BLOCK = 256;
 constexpr int T2J_SKIP_DEPTH = 1023;     /* MaxSkipDepth, thrift/binary_skip.go:24 */
 
@@ -366,12 +367,60 @@ DGI void emit_side(Out &o, const T2JSide &X, uint32_t off, uint32_t len)
 }
 
 /* one message. FP: frame storage (LDS or device workspace), `cap` frames. */
+/* the Thrift size of a fixed-size scalar, 0 otherwise */
+DGI uint32_t num_bytes(uint8_t tt)
+{
+    switch (tt) {
+    case DG_T_BYTE: return 1;
+    case DG_T_I16: return 2;
+    case DG_T_I32: return 4;
+    case DG_T_I64:
+    case DG_T_DOUBLE: return 8;
+    }
+    return 0;
+}
+
+/* DefaultValue().JSONValue() of a scalar or string IDL constant
+ * (thrift/idl.go:834-955: EncodeInt64 / EncodeFloat64 / EncodeString /
+ * true|false), from its Thrift bytes in the descriptor pool */
+template <class DV>
+DGI void emit_default(Out &o, const DV &D, const dg_field &fd, uint8_t tt)
+{
+    auto byte = [&](uint32_t k) -> uint64_t { return (uint8_t)D.P[fd.dflt_off + k]; };
+    if (tt == DG_T_BOOL) {
+        if (byte(0) == 1) o.wle('t' | ('r' << 8) | ('u' << 16) | ('e' << 24), 4);
+        else o.wle('f' | ('a' << 8) | ('l' << 16) | ('s' << 24) | (0x65ull << 32), 5);
+        return;
+    }
+    if (tt == DG_T_STRING) {
+        const uint32_t n = (uint32_t)((byte(0) << 24) | (byte(1) << 16) | (byte(2) << 8) | byte(3));
+        const uintptr_t a = (uintptr_t)(const void *)&D.P[fd.dflt_off + 4];
+        SrcT<const uint64_t> ps;
+        ps.init((const uint64_t *)(a & ~(uintptr_t)7), (int64_t)(a & 7), (int64_t)n);
+        o.w8('"');
+        emit_quoted(o, ps, 0, n);
+        o.w8('"');
+        return;
+    }
+    const uint32_t nb = num_bytes(tt);
+    uint64_t u = 0;
+    for (uint32_t k = 0; k < nb; k++) u = (u << 8) | byte(k);
+    switch (tt) {
+    case DG_T_BYTE: emit_i64(o, (int8_t)u); break;
+    case DG_T_I16: emit_i64(o, (int16_t)u); break;
+    case DG_T_I32: emit_i64(o, (int32_t)u); break;
+    case DG_T_I64: emit_i64(o, (int64_t)u); break;
+    default: emit_f64(o, __longlong_as_double((long long)u)); break;
+    }
+}
+
 template <class S, class FP, class DV>
 DGI uint64_t t2j_convert(const DV &D, const T2JSide &X, S src, uint32_t root, uint64_t opts, Out &o, FP fr,
-                         uint32_t fstride, uint32_t cap)
+                         uint32_t fstride, uint32_t cap, gu64 *wide = nullptr, uint32_t widecap = 0)
 {
     T2JRd<S> r{src, 0};
     uint32_t sp = 0;
+    uint32_t wlen = 0; /* words of `wide` in use: requires bitmaps of open structs of > 64 fields */
     auto F = [&](uint32_t k) -> auto & { return fr[k * fstride]; };
 
     /* the value of type td at the reader: scalars written, containers opened
@@ -385,21 +434,21 @@ DGI uint64_t t2j_convert(const DV &D, const T2JSide &X, S src, uint32_t root, ui
             else o.wle('f' | ('a' << 8) | ('l' << 16) | ('s' << 24) | (0x65ull << 32), 5);
             return 0;
         case DG_T_BYTE: {
-            if (!r.need(1)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+            if (!r.need(1)) return t2j_err(DG_T2J_E_WRITE, r.p, RD_EOF);
             const uint8_t v = r.u8();
             emit_i64(o, (opts & DG_T2J_BYTE_AS_UINT8) ? (int64_t)v : (int64_t)(int8_t)v);
             return 0;
         }
         case DG_T_I16:
-            if (!r.need(2)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+            if (!r.need(2)) return t2j_err(DG_T2J_E_WRITE, r.p, RD_EOF);
             emit_i64(o, (int16_t)r.be(2));
             return 0;
         case DG_T_I32:
-            if (!r.need(4)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+            if (!r.need(4)) return t2j_err(DG_T2J_E_WRITE, r.p, RD_EOF);
             emit_i64(o, (int32_t)r.be(4));
             return 0;
         case DG_T_I64: {
-            if (!r.need(8)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+            if (!r.need(8)) return t2j_err(DG_T2J_E_WRITE, r.p, RD_EOF);
             const int64_t v = (int64_t)r.be(8);
             if (opts & DG_T2J_INT64_AS_STRING) {
                 o.w8('"');
@@ -411,7 +460,7 @@ DGI uint64_t t2j_convert(const DV &D, const T2JSide &X, S src, uint32_t root, ui
             return 0;
         }
         case DG_T_DOUBLE: {
-            if (!r.need(8)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+            if (!r.need(8)) return t2j_err(DG_T2J_E_WRITE, r.p, RD_EOF);
             const uint64_t u = r.be(8);
             if (((u >> 52) & 0x7FF) == 0x7FF) {
                 if (!(opts & DG_T2J_NULL_FOR_NAN_INF)) return t2j_err(DG_T2J_E_NAN_INF, r.p, 0);
@@ -436,13 +485,22 @@ DGI uint64_t t2j_convert(const DV &D, const T2JSide &X, S src, uint32_t root, ui
         case DG_T_STRUCT: {
             if (sp >= cap) return pack0(DG_ST_DEEP, 0);
             const dg_struct sd = ldrec(&D.S[t.st]);
-            if (sd.req_words != 1) return t2j_err(DG_T2J_E_NEEDS_HOST, r.p, 0); /* > 64 fields */
+            uint64_t u = D.R[sd.req_begin];
+            if (sd.req_words != 1) {
+                /* > 64 fields: the bitmap lives in the deep pass's per-lane
+                 * words (a stack: structs close in reverse order) */
+                if (!wide) return pack0(DG_ST_DEEP, 0);
+                if (wlen + sd.req_words > widecap) return t2j_err(DG_T2J_E_DEPTH, r.p, T2J_DEEP_DEPTH);
+                for (uint32_t w = 0; w < sd.req_words; w++) wide[wlen + w] = D.R[sd.req_begin + w];
+                u = wlen;
+                wlen += sd.req_words;
+            }
             auto &f = F(sp++);
             f.kind = TF_STRUCT;
             f.td = td;
             f.n = 0; /* predicted next field index */
             f.i = 0;
-            f.u = D.R[sd.req_begin];
+            f.u = u;
             o.w8('{');
             return 0;
         }
@@ -576,9 +634,10 @@ DGI uint64_t t2j_convert(const DV &D, const T2JSide &X, S src, uint32_t root, ui
             if (!ttype_valid(t)) return t2j_err(DG_T2J_E_READ, r.p, RD_BAD_TYPE);
             if (t == 0) {
                 /* handleUnsets -> HandleRequires (thrift/utils.go:149-176), ascending id */
-                uint64_t bits = f.u;
+                for (uint32_t w = 0; w < sd.req_words; w++) {
+                uint64_t bits = sd.req_words == 1 ? f.u : (uint64_t)wide[(uint32_t)f.u + w];
                 while (bits) {
-                    const uint32_t k = (uint32_t)__builtin_ctzll(bits);
+                    const uint32_t k = w * 64 + (uint32_t)__builtin_ctzll(bits);
                     bits &= bits - 1;
                     const dg_field fd = ldrec(&D.F[sd.field_begin + k]);
                     if (fd.required == DG_REQ_REQUIRED && !(opts & DG_T2J_WRITE_REQUIRE))
@@ -586,12 +645,21 @@ DGI uint64_t t2j_convert(const DV &D, const T2JSide &X, S src, uint32_t root, ui
                     if ((fd.required == DG_REQ_DEFAULT && !(opts & DG_T2J_WRITE_DEFAULT)) ||
                         (fd.required == DG_REQ_OPTIONAL && !(opts & DG_T2J_WRITE_OPTIONAL) && fd.dflt_len == DG_NONE))
                         continue;
-                    if (fd.dflt_len != DG_NONE) return t2j_err(DG_T2J_E_NEEDS_HOST, r.p, fd.id); /* JSONValue() */
+                    const uint8_t ftt = ldrec(&D.T[fd.type]).ttype;
+                    if (fd.dflt_len != DG_NONE && !(ftt == DG_T_BOOL || num_bytes(ftt) || ftt == DG_T_STRING))
+                        return t2j_err(DG_T2J_E_NEEDS_HOST, r.p, fd.id); /* a container constant's JSONValue() */
                     if (f.i) o.w8(',');
                     f.i = 1;
                     const dg_t2j_field xf = ldrec(&X.X[sd.field_begin + k]);
                     emit_side(o, X, xf.name_off, xf.name_len); /* "name": */
-                    switch (ldrec(&D.T[fd.type]).ttype) { /* writeDefaultOrEmpty conv/t2j/impl.go:440-468 */
+                    if (fd.dflt_len != DG_NONE) {
+                        /* DefaultValue().JSONValue() (thrift/idl.go:834-955): EncodeInt64 /
+                         * EncodeFloat64 / EncodeString / true|false of the IDL constant, here
+                         * from its Thrift bytes in the descriptor pool */
+                        emit_default(o, D, fd, ftt);
+                        continue;
+                    }
+                    switch (ftt) { /* writeDefaultOrEmpty conv/t2j/impl.go:440-468 */
                     case DG_T_BOOL: o.wle('f' | ('a' << 8) | ('l' << 16) | ('s' << 24) | (0x65ull << 32), 5); break;
                     case DG_T_BYTE: case DG_T_I16: case DG_T_I32: case DG_T_I64: case DG_T_DOUBLE: o.w8('0'); break;
                     case DG_T_STRING: o.wle('"' | ('"' << 8), 2); break;
@@ -600,7 +668,9 @@ DGI uint64_t t2j_convert(const DV &D, const T2JSide &X, S src, uint32_t root, ui
                     default: return t2j_err(DG_T2J_E_UNSUPPORTED, r.p, ldrec(&D.T[fd.type]).ttype);
                     }
                 }
+                }
                 o.w8('}');
+                if (sd.req_words != 1) wlen -= sd.req_words;
                 sp--;
                 continue;
             }
@@ -613,7 +683,8 @@ DGI uint64_t t2j_convert(const DV &D, const T2JSide &X, S src, uint32_t root, ui
                 continue;
             }
             const uint32_t k = (uint32_t)fi - sd.field_begin;
-            f.u &= ~(1ull << k);
+            if (sd.req_words == 1) f.u &= ~(1ull << k);
+            else wide[(uint32_t)f.u + (k >> 6)] &= ~(1ull << (k & 63));
             f.n = k + 1;
             if (f.i) o.w8(',');
             f.i = 1;
@@ -704,33 +775,33 @@ DGI uint64_t t2j_convert(const DV &D, const T2JSide &X, S src, uint32_t root, ui
             o.w8('"'); /* buildinTypeToKey (conv/t2j/impl.go:470-530) */
             switch (kt) {
             case DG_T_BYTE: {
-                if (!r.need(1)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+                if (!r.need(1)) return t2j_err(DG_T2J_E_CONVERT, r.p, RD_EOF);
                 const uint8_t v = r.u8();
                 emit_i64(o, (opts & DG_T2J_BYTE_AS_UINT8) ? (int64_t)v : (int64_t)(int8_t)v);
                 break;
             }
             case DG_T_I16:
-                if (!r.need(2)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+                if (!r.need(2)) return t2j_err(DG_T2J_E_CONVERT, r.p, RD_EOF);
                 emit_i64(o, (int16_t)r.be(2));
                 break;
             case DG_T_I32:
-                if (!r.need(4)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+                if (!r.need(4)) return t2j_err(DG_T2J_E_CONVERT, r.p, RD_EOF);
                 emit_i64(o, (int32_t)r.be(4));
                 break;
             case DG_T_I64:
-                if (!r.need(8)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+                if (!r.need(8)) return t2j_err(DG_T2J_E_CONVERT, r.p, RD_EOF);
                 emit_i64(o, (int64_t)r.be(8));
                 break;
             case DG_T_STRING: {
-                if (!r.need(4)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+                if (!r.need(4)) return t2j_err(DG_T2J_E_CONVERT, r.p, RD_EOF);
                 const int32_t sz = (int32_t)r.be(4);
-                if (sz < 0 || !r.need(sz)) return t2j_err(DG_T2J_E_READ, r.p, RD_BAD_SIZE);
+                if (sz < 0 || !r.need(sz)) return t2j_err(DG_T2J_E_CONVERT, r.p, RD_BAD_SIZE);
                 emit_quoted(o, r.src, r.p, sz); /* json.NoQuote */
                 r.p += sz;
                 break;
             }
             default:
-                return t2j_err(DG_T2J_E_UNSUPPORTED, r.p, kt);
+                return t2j_err(DG_T2J_E_CONVERT, r.p, 0x100u | kt); /* wrapped as ErrConvert */
             }
             o.wle('"' | (':' << 8), 2);
             if ((e = value(mt.elem))) return e;

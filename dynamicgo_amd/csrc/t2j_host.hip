@@ -10,7 +10,8 @@
 
 using namespace dg;
 
-static const uint64_t T2J_DEEP_WS = (uint64_t)T2J_DEEP_BLOCKS * T2J_BLOCK * T2J_DEEP_DEPTH * sizeof(T2JFrame);
+static const uint64_t T2J_DEEP_WS =
+    (uint64_t)T2J_DEEP_BLOCKS * T2J_BLOCK * (T2J_DEEP_DEPTH * sizeof(T2JFrame) + (uint64_t)T2J_WIDE_WORDS * 8);
 
 /* lanes per message of the LDS-frame pass (t2j_kern.hip) from the batch's
  * longest message: short messages want full waves, ~1 KB ones sparse waves;

@@ -36,8 +36,9 @@ __global__ __launch_bounds__(T2J_BLOCK) void t2j_kernel(T2JParams P)
     t2j_store(P, i, r, o);
 }
 
-/* the queued deep messages, rerun from the start with T2J_DEEP_DEPTH frames
- * per lane in device memory; a grid-stride loop over the queue (the grid is
+/* the queued deep messages (nested beyond the LDS frames, or holding a
+ * struct of more than 64 fields), rerun from the start with T2J_DEEP_DEPTH
+ * frames and T2J_WIDE_WORDS requires words per lane in device memory; a grid-stride loop over the queue (the grid is
  * small: deep messages are rare) */
 __global__ __launch_bounds__(T2J_BLOCK) void t2j_deep_kernel(T2JParams P)
 {
@@ -46,6 +47,9 @@ __global__ __launch_bounds__(T2J_BLOCK) void t2j_deep_kernel(T2JParams P)
     const auto D = desc_view<1>((const __attribute__((address_space(1))) uint8_t *)(const void *)P.blob, P.hdr);
     const T2JSide X = t2j_side(P.side);
     T2JFrame *fr = (T2JFrame *)(void *)(P.ws + (uint64_t)lane * T2J_DEEP_DEPTH * sizeof(T2JFrame));
+    /* after every lane's frames: the requires words of wide structs */
+    gu64 *wide = (gu64 *)(void *)(P.ws + (uint64_t)T2J_DEEP_BLOCKS * T2J_BLOCK * T2J_DEEP_DEPTH * sizeof(T2JFrame) +
+                                  (uint64_t)lane * T2J_WIDE_WORDS * 8);
     for (uint32_t g = lane; g < cnt; g += gridDim.x * T2J_BLOCK) {
         const uint64_t i = P.deep_list[g];
         const uint64_t a = P.in_off[i], b = P.in_off[i + 1];
@@ -53,7 +57,7 @@ __global__ __launch_bounds__(T2J_BLOCK) void t2j_deep_kernel(T2JParams P)
         s.init((glb_u64 *)(const void *)(P.src + (a & ~7ull)), (int64_t)(a & 7), (int64_t)(b - a));
         Out o;
         o.init(P.out + P.out_off[i], P.out_off[i + 1] - P.out_off[i]);
-        uint64_t r = t2j_convert(D, X, s, P.root, P.opts, o, fr, 1, T2J_DEEP_DEPTH);
+        uint64_t r = t2j_convert(D, X, s, P.root, P.opts, o, fr, 1, T2J_DEEP_DEPTH, wide, T2J_WIDE_WORDS);
         if ((uint8_t)r == DG_ST_DEEP) r = t2j_err(DG_T2J_E_DEPTH, 0, T2J_DEEP_DEPTH);
         t2j_store(P, i, r, o);
     }

@@ -35,13 +35,16 @@ T2J_WRITE_REQUIRE = 1 << 6
 T2J_WRITE_OPTIONAL = 1 << 7
 T2J_ENABLE_VM = 1 << 8
 
-E_READ, E_UNKNOWN_FIELD, E_DISMATCH_TYPE, E_UNSUPPORTED, E_NAN_INF, E_MISS_REQUIRED, E_NEEDS_HOST, E_DEPTH = range(1, 9)
+(E_READ, E_UNKNOWN_FIELD, E_DISMATCH_TYPE, E_UNSUPPORTED, E_NAN_INF, E_MISS_REQUIRED, E_NEEDS_HOST, E_DEPTH, E_WRITE,
+ E_CONVERT) = range(1, 11)
 
 # the meta.ErrCode behaviour the reference wraps each failure in
 # (conv/t2j/impl.go: wrapError call sites; meta/error.go)
 _BEHAVIOR = {E_READ: "ErrRead", E_UNKNOWN_FIELD: "ErrUnknownField", E_DISMATCH_TYPE: "ErrDismatchType",
              E_UNSUPPORTED: "ErrUnsupportedType", E_NAN_INF: "ErrWrite", E_MISS_REQUIRED: "ErrMissRequiredField",
-             E_NEEDS_HOST: "ErrNotImplemented", E_DEPTH: "ErrStackOverflow"}
+             E_NEEDS_HOST: "ErrNotImplemented", E_DEPTH: "ErrStackOverflow",
+             E_WRITE: "ErrWrite",       # truncated BYTE/I16/I32/I64/DOUBLE (conv/t2j/impl.go:200-236)
+             E_CONVERT: "ErrConvert"}   # map key (buildinTypeToKey, conv/t2j/impl.go:355-358)
 _READ_REASON = {1: "EOF", 2: "invalid data type", 3: "invalid data length", 4: "depth limit exceeded"}
 
 
@@ -84,8 +87,11 @@ class T2JError(Exception):
 
     def _detail(self) -> str:
         c, v = self.code, self.value
-        if c == E_READ:
+        if c in (E_READ, E_WRITE):
             return f"{_READ_REASON.get(v, v)} at byte {self.pos}"
+        if c == E_CONVERT:
+            return (f"unsupported descriptor type {v & 0xFF} as MAP key" if v & 0x100 else
+                    f"map key: {_READ_REASON.get(v, v)} at byte {self.pos}")
         if c == E_UNKNOWN_FIELD:
             return f"unknown field {v}"
         if c == E_DISMATCH_TYPE:

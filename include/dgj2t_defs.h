@@ -91,5 +91,10 @@ typedef struct dg_hm_entry {
 #define DG_T2J_E_NEEDS_HOST 7     /* a Go-side feature: IDL default JSON values, HTTP mapping, non-inline value mapping,
                                      structs of more than 64 fields */
 #define DG_T2J_E_DEPTH 8          /* nesting beyond 4096 containers (the GPU's frame budget; Go recurses further) */
+#define DG_T2J_E_WRITE 9          /* ErrWrite: a truncated BYTE/I16/I32/I64/DOUBLE value (doRecurse wraps those reads
+                                     as meta.ErrWrite, conv/t2j/impl.go:200-236); value = RD_EOF (1) */
+#define DG_T2J_E_CONVERT 10       /* ErrConvert: a map key failed (buildinTypeToKey, wrapped as meta.ErrConvert by
+                                     conv/t2j/impl.go:355-358): value = the read reason (RD_*), or 0x100 | type for
+                                     a key type it does not support */
 
 #endif /* DGJ2T_DEFS_H */

@@ -846,8 +846,29 @@ static uint64_t t2j_value(const T2J *c, uint32_t td, TRd *r, JBuf *o);
 /* writeDefaultOrEmpty (conv/t2j/impl.go:440-468) */
 static uint64_t t2j_default_or_empty(const T2J *c, const dg_field *f, size_t pos, JBuf *o)
 {
-    if (f->dflt_len != DG_NONE)
-        return T2J_ERR(DG_T2J_E_NEEDS_HOST, pos, f->id); /* DefaultValue().JSONValue(): Go-side */
+    if (f->dflt_len != DG_NONE) {
+        /* DefaultValue().JSONValue() (thrift/idl.go:834-955) of a scalar or
+         * string constant, from its Thrift bytes; containers stay Go-side */
+        const uint8_t *b = c->blob + c->h->off_pool + f->dflt_off;
+        const uint8_t tt = c->T[f->type].ttype;
+        uint64_t u = 0;
+        int nb = tt == 3 ? 1 : tt == 6 ? 2 : tt == 8 ? 4 : (tt == 10 || tt == 4) ? 8 : 0;
+        for (int k = 0; k < nb; k++) u = (u << 8) | b[k];
+        switch (tt) {
+        case 2: if (b[0] == 1) jb_put(o, "true", 4); else jb_put(o, "false", 5); return 0;
+        case 3: jb_i64(o, (int8_t)u); return 0;
+        case 6: jb_i64(o, (int16_t)u); return 0;
+        case 8: jb_i64(o, (int32_t)u); return 0;
+        case 10: jb_i64(o, (int64_t)u); return 0;
+        case 4: { double d; memcpy(&d, &u, 8); jb_f64(o, d); return 0; }
+        case 11: {
+            uint32_t n = ((uint32_t)b[0] << 24) | ((uint32_t)b[1] << 16) | ((uint32_t)b[2] << 8) | b[3];
+            jb_string(o, b + 4, n);
+            return 0;
+        }
+        }
+        return T2J_ERR(DG_T2J_E_NEEDS_HOST, pos, f->id); /* a container constant: Go-side */
+    }
     switch (c->T[f->type].ttype) {
     case 2: jb_put(o, "false", 5); return 0;
     case 3: case 6: case 8: case 10: jb_i64(o, 0); return 0;
@@ -988,21 +1009,21 @@ static uint64_t t2j_value(const T2J *c, uint32_t td, TRd *r, JBuf *o)
         return 0;
     }
     case 3: {
-        if (!rd_need(r, 1)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_EOF);
+        if (!rd_need(r, 1)) return T2J_ERR(DG_T2J_E_WRITE, r->p, RD_EOF);
         uint8_t v = r->b[r->p++];
         jb_i64(o, (c->opts & DG_T2J_BYTE_AS_UINT8) ? (int64_t)v : (int64_t)(int8_t)v);
         return 0;
     }
     case 6:
-        if (!rd_need(r, 2)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_EOF);
+        if (!rd_need(r, 2)) return T2J_ERR(DG_T2J_E_WRITE, r->p, RD_EOF);
         jb_i64(o, (int16_t)rd_be(r, 2));
         return 0;
     case 8:
-        if (!rd_need(r, 4)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_EOF);
+        if (!rd_need(r, 4)) return T2J_ERR(DG_T2J_E_WRITE, r->p, RD_EOF);
         jb_i64(o, (int32_t)rd_be(r, 4));
         return 0;
     case 10:
-        if (!rd_need(r, 8)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_EOF);
+        if (!rd_need(r, 8)) return T2J_ERR(DG_T2J_E_WRITE, r->p, RD_EOF);
         if (c->opts & DG_T2J_INT64_AS_STRING) {
             jb_c(o, '"');
             jb_i64(o, (int64_t)rd_be(r, 8));
@@ -1012,7 +1033,7 @@ static uint64_t t2j_value(const T2J *c, uint32_t td, TRd *r, JBuf *o)
         }
         return 0;
     case 4: {
-        if (!rd_need(r, 8)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_EOF);
+        if (!rd_need(r, 8)) return T2J_ERR(DG_T2J_E_WRITE, r->p, RD_EOF);
         uint64_t u = rd_be(r, 8);
         if (((u >> 52) & 0x7FF) == 0x7FF) { /* NaN or Inf */
             if (!(c->opts & DG_T2J_NULL_FOR_NAN_INF)) return T2J_ERR(DG_T2J_E_NAN_INF, r->p, 0);
@@ -1067,24 +1088,24 @@ static uint64_t t2j_value(const T2J *c, uint32_t td, TRd *r, JBuf *o)
             jb_c(o, '"'); /* buildinTypeToKey (conv/t2j/impl.go:470-530) */
             switch (K->ttype) {
             case 3: {
-                if (!rd_need(r, 1)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_EOF);
+                if (!rd_need(r, 1)) return T2J_ERR(DG_T2J_E_CONVERT, r->p, RD_EOF);
                 uint8_t v = r->b[r->p++];
                 jb_i64(o, (c->opts & DG_T2J_BYTE_AS_UINT8) ? (int64_t)v : (int64_t)(int8_t)v);
                 break;
             }
-            case 6: if (!rd_need(r, 2)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_EOF); jb_i64(o, (int16_t)rd_be(r, 2)); break;
-            case 8: if (!rd_need(r, 4)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_EOF); jb_i64(o, (int32_t)rd_be(r, 4)); break;
-            case 10: if (!rd_need(r, 8)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_EOF); jb_i64(o, (int64_t)rd_be(r, 8)); break;
+            case 6: if (!rd_need(r, 2)) return T2J_ERR(DG_T2J_E_CONVERT, r->p, RD_EOF); jb_i64(o, (int16_t)rd_be(r, 2)); break;
+            case 8: if (!rd_need(r, 4)) return T2J_ERR(DG_T2J_E_CONVERT, r->p, RD_EOF); jb_i64(o, (int32_t)rd_be(r, 4)); break;
+            case 10: if (!rd_need(r, 8)) return T2J_ERR(DG_T2J_E_CONVERT, r->p, RD_EOF); jb_i64(o, (int64_t)rd_be(r, 8)); break;
             case 11: {
-                if (!rd_need(r, 4)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_EOF);
+                if (!rd_need(r, 4)) return T2J_ERR(DG_T2J_E_CONVERT, r->p, RD_EOF);
                 int32_t sz = (int32_t)rd_be(r, 4);
-                if (sz < 0 || !rd_need(r, (size_t)sz)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_BAD_SIZE);
+                if (sz < 0 || !rd_need(r, (size_t)sz)) return T2J_ERR(DG_T2J_E_CONVERT, r->p, RD_BAD_SIZE);
                 jb_quote(o, r->b + r->p, (size_t)sz);
                 r->p += (size_t)sz;
                 break;
             }
             default:
-                return T2J_ERR(DG_T2J_E_UNSUPPORTED, r->p, K->ttype); /* wrapped as ErrConvert by the caller */
+                return T2J_ERR(DG_T2J_E_CONVERT, r->p, 0x100u | K->ttype); /* conv/t2j/impl.go:355-358 */
             }
             jb_c(o, '"');
             jb_c(o, ':');

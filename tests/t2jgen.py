@@ -60,6 +60,16 @@ def all_types_desc(with_default=False, alias_quirks=True):
     if with_default:
         f.append(T.FieldDescriptor(40, "with_dflt", T.builtin("i32"), T.OPTIONAL,
                                    default_value=T.encode_default(T.builtin("i32"), 7)))
+        f.append(T.FieldDescriptor(41, "d_str", T.builtin("string"), T.DEFAULT,
+                                   default_value=T.encode_default(T.builtin("string"), 'q"\\x\u00e9')))
+        f.append(T.FieldDescriptor(42, "d_dbl", T.builtin("double"), T.OPTIONAL,
+                                   default_value=T.encode_default(T.builtin("double"), -1.25e-7)))
+        f.append(T.FieldDescriptor(43, "d_bool", T.builtin("bool"), T.DEFAULT,
+                                   default_value=T.encode_default(T.builtin("bool"), True)))
+        f.append(T.FieldDescriptor(44, "d_i8", T.builtin("byte"), T.REQUIRED,
+                                   default_value=T.encode_default(T.builtin("byte"), -3)))
+        f.append(T.FieldDescriptor(45, "d_list", T.list_of(T.builtin("i32")), T.OPTIONAL,
+                                   default_value=bytes([8, 0, 0, 0, 1, 0, 0, 0, 4])))  # container: NEEDS_HOST
     return T.struct_type("All", f)
 
 
