@@ -682,14 +682,14 @@ DGI bool is_atof_exact(uint64_t man, int exp, int sgn, double &val)
     return false;
 }
 
-/* atof_eisel_lemire64 native/atof_eisel_lemire.c:74-167 */
-DGI bool eisel_lemire(uint64_t mant, int exp10, int sgn, double &val)
+/* atof_eisel_lemire64 native/atof_eisel_lemire.c:74-167; p_hi = the high
+ * half of the 128-bit power (DG_POW10_M128[exp10 + 348][1]), supplied by the
+ * caller (from the table, or from a window of it a kernel holds in LDS) */
+DGI bool eisel_lemire_p(uint64_t mant, int exp10, int sgn, double &val, uint64_t p_hi)
 {
-    if (exp10 < -348 || exp10 > 347) return false;
     int clz = mant ? __clzll(mant) : 64;
     mant = clz < 64 ? mant << clz : mant;
     uint64_t ret_exp2 = ((uint64_t)(int64_t)((217706 * exp10) >> 16) + 64 + 1023) - (uint64_t)clz;
-    uint64_t p_hi = DG_POW10_M128[exp10 + 348][1];
     uint64_t x_hi = __umul64hi(mant, p_hi), x_lo = mant * p_hi;
     if ((x_hi & 0x1FF) == 0x1FF && (x_lo + mant) < mant) {
         uint64_t p_lo = DG_POW10_M128[exp10 + 348][0];
@@ -715,6 +715,11 @@ DGI bool eisel_lemire(uint64_t mant, int exp10, int sgn, double &val)
     if (sgn == -1) bits |= 1ull << 63;
     val = __longlong_as_double(bits);
     return true;
+}
+DGI bool eisel_lemire(uint64_t mant, int exp10, int sgn, double &val)
+{
+    if (exp10 < -348 || exp10 > 347) return false;
+    return eisel_lemire_p(mant, exp10, sgn, val, DG_POW10_M128[exp10 + 348][1]);
 }
 
 /* ---- atof_native: big-decimal slow path native/atof_native.c:17-424 ---- */

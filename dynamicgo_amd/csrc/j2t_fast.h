@@ -80,10 +80,28 @@ constexpr uint64_t FAST_FLAGS = DG_F_ALLOW_UNKNOWN | DG_F_WRITE_DEFAULT | DG_F_E
                                 DG_F_ENABLE_HM | DG_F_HM_SPLIT;
 
 /* small power tables, copied to LDS by the kernel prologue */
+/* DG_POW10_M128[e + 348][1] for e in [EL_WLO, EL_WLO + EL_WN): the decimal
+ * exponents of ordinary JSON doubles, so Eisel-Lemire reads LDS, not the
+ * 11 KiB table in global memory */
+constexpr int EL_WLO = -40;
+constexpr int EL_WN = 64;
 struct FastTabs {
     const __attribute__((address_space(3))) uint64_t *p10u; /* 10^k, k = 0..19 */
     lds_f64 *p10d;                                          /* 1e0 .. 1e22 */
+    const __attribute__((address_space(3))) uint64_t *pw = nullptr; /* the window above, or none */
 };
+/* fill a FastTabs window (lanes t < EL_WN of the block) */
+DGI void el_window_fill(uint64_t *pw, uint32_t t)
+{
+    if (t < (uint32_t)EL_WN) pw[t] = DG_POW10_M128[EL_WLO + 348 + (int)t][1];
+}
+DGI bool eisel_lemire_t(uint64_t mant, int exp10, int sgn, double &val, const FastTabs &tb)
+{
+    if (exp10 < -348 || exp10 > 347) return false;
+    const uint32_t wi = (uint32_t)(exp10 - EL_WLO);
+    const uint64_t p_hi = tb.pw && wi < (uint32_t)EL_WN ? tb.pw[wi] : DG_POW10_M128[exp10 + 348][1];
+    return eisel_lemire_p(mant, exp10, sgn, val, p_hi);
+}
 
 /* ---- SWAR helpers ---- */
 
@@ -255,10 +273,10 @@ DGI bool fast_vnumber(S &src, SI &p, const FastTabs &tb, int64_t &iv, double &dv
     /* atof_fast native/scanning.c:928-948; atof_native -> bail */
     double val;
     if (!atof_exact_l(man, exp10, sgn, val, tb)) {
-        if (!eisel_lemire(man, exp10, sgn, val)) return false;
+        if (!eisel_lemire_t(man, exp10, sgn, val, tb)) return false;
         if (trunc) {
             double vu;
-            if (!eisel_lemire(man + 1, exp10, sgn, vu) || vu != val) return false;
+            if (!eisel_lemire_t(man + 1, exp10, sgn, vu, tb) || vu != val) return false;
         }
     }
     if ((__double_as_longlong(val) << 1) == 0xFFE0000000000000ull) return false; /* ERR_FLOAT_INF */

@@ -7,23 +7,27 @@
  * and once the top-level commas and colons are known every field converts on
  * its own. The lane-per-message kernel (j2t_small.h) walks a message
  * byte-serially in one lane, so a 64K batch is one wave per SIMD and every
- * latency is exposed. Here a block of 8 waves takes 64 messages:
+ * latency is exposed. Here a block of 4 waves takes 64 messages:
  *
- *  1. structure: 8 lanes per message, each classifies 32 aligned bytes of
- *     the staged message (lane 7 also word 32 when a message reaches it)
- *     into 0x80-per-byte masks (quote, comma, colon, backslash); the
- *     in-string mask is a prefix XOR of the quote bytes carried across the 8
- *     lanes with DPP scans; commas and colons outside strings are recorded
- *     (with the count of quotes before each comma).
- *  2. fields, field-major: wave w converts field fl_slot(w) (+8r) of all 64
+ *  1. structure: 4 lanes per message, each classifies 64 bytes of the
+ *     staged message into bit masks (quote, comma, colon; backslash only
+ *     when the message has one), bit b = byte b; the in-string mask is a
+ *     prefix XOR of the quote bits carried across the 4 lanes with DPP
+ *     scans; commas and colons outside strings are recorded (with the count
+ *     of quotes before each comma).
+ *  2. fields, field-major: wave w converts field w (+4r) of all 64
  *     messages, so the lanes of a wave hold the same field of 64 messages --
  *     the same type, the same code path. Key lookup (the predicted IDL-order
  *     field, else the name table), value parse and Thrift size.
- *  3. every lane reads the sizes of the fields before its own (one barrier),
- *     writes its field into the message's zeroed LDS output stage (shared
- *     edge words OR-ed), leaves string/base64 bodies over 16 B to chunk
- *     tasks that the whole block takes after a barrier, and the 8 lanes of a
- *     message copy the stage to the slot with whole-word stores.
+ *  3. every lane reads the sizes of the fields before its own (one barrier)
+ *     and writes its field straight into the message's slot, byte-exact at
+ *     the partial words it shares with its neighbours; string/base64 bodies
+ *     over 16 B are left to chunk tasks the whole block takes after a
+ *     barrier; a lane per message then checks unset fields and writes STOP.
+ *
+ * No output stage in LDS: ~36 KiB per block with a small descriptor, so 4
+ * blocks (16 waves) fit a CU and a 64K-message batch (1024 blocks) is
+ * resident in one round instead of 1.33.
  *
  * JSON fields are written in input order, exactly as j2t_fsm_exec writes them
  * (native/thrift.c:765-1187: tb_write_field_begin + value per key,
@@ -39,48 +43,55 @@
 
 namespace dg {
 
-constexpr uint32_t FL_G = 8;                     /* lanes per message in the structure phase */
-constexpr uint32_t FL_WAVES = 8;                 /* waves per block = field slots per round */
+constexpr uint32_t FL_G = 4;                     /* lanes per message in the structure phase */
+constexpr uint32_t FL_WAVES = 4;                 /* waves per block */
+#ifndef DG_FL_FPW
+#define DG_FL_FPW 2
+#endif
+constexpr uint32_t FL_FPW = DG_FL_FPW;           /* fields per wave per round (each one more inlined parser) */
+constexpr uint32_t FL_SLOTS = FL_FPW * FL_WAVES; /* fields per round */
 constexpr uint32_t FL_MPB = 64;                  /* messages per block (= lanes of a wave in phase 2) */
-constexpr uint32_t FL_LW = 5;                    /* aligned words a structure lane may read: 4 + word 32 (lane 7) */
+constexpr uint32_t FL_LW = 9;                    /* aligned words a structure lane reads: 64 bytes at any alignment */
 constexpr uint32_t FL_MAXLEN = 256;              /* longest message on this kernel */
 constexpr uint32_t FL_SLOTW = FL_MAXLEN / 8;     /* words per message when the block's span is not staged */
 constexpr uint32_t FL_STAGEW = FL_MPB * FL_SLOTW;/* 16 KiB */
 constexpr uint32_t FL_SLACKW = FL_G * FL_LW + 2; /* reads past the last message stay in the array */
 constexpr uint32_t FL_MAXF = 24;                 /* fields per message (top-level commas + 1) */
-constexpr uint32_t FL_OUTW = 24;                 /* output stage per message (words): 192 B */
 constexpr uint32_t FL_DESC = 16 * 1024;          /* descriptor bytes in LDS (dynamic) */
-constexpr uint32_t FL_INLINE = 16;               /* longer string / base64 bodies are written as chunk tasks */
-constexpr uint32_t FL_CHUNK = 32;                /* input bytes per chunk task */
+#ifndef DG_FL_INLINE
+#define DG_FL_INLINE 16
+#endif
+#ifndef DG_FL_CHUNK
+#define DG_FL_CHUNK 32
+#endif
+constexpr uint32_t FL_INLINE = DG_FL_INLINE;     /* longer string / base64 bodies are written as chunk tasks */
+constexpr uint32_t FL_CHUNK = DG_FL_CHUNK;       /* input bytes per chunk task (a multiple of 8) */
 constexpr uint32_t FL_MAXTASK = 512;             /* chunk tasks per block (more: the message declines) */
 #ifndef DG_FL_WPE
-#define DG_FL_WPE 6 /* waves per SIMD the register budget is cut for: 80 VGPRs, 3 blocks/CU (C2 71 -> 68.5 us/step vs 4) */
+#define DG_FL_WPE 4 /* waves per SIMD the register budget is cut for: 128 VGPRs; LDS allows 4 blocks (16 waves) per CU */
 #endif
 
-/* ---- group (8 lanes, half a DPP row) collectives; converged code only ---- */
+/* ---- group (4 lanes, a DPP quad) collectives; converged code only ---- */
 #define DG_DPP(v, ctrl) ((uint32_t)__builtin_amdgcn_update_dpp(0, (int)(v), (ctrl), 0xF, 0xF, false))
-DGI uint32_t g8_incl_sum(uint32_t v, uint32_t g)
+DGI uint32_t g4_incl_sum(uint32_t v, uint32_t g)
 {
     uint32_t t = DG_DPP(v, 0x111); /* row_shr:1 */
     v += g >= 1 ? t : 0u;
     t = DG_DPP(v, 0x112); /* row_shr:2 */
     v += g >= 2 ? t : 0u;
-    t = DG_DPP(v, 0x114); /* row_shr:4 */
-    v += g >= 4 ? t : 0u;
     return v;
 }
-DGI uint32_t g8_sum(uint32_t v)
+DGI uint32_t g4_sum(uint32_t v)
 {
-    v += DG_DPP(v, 0xB1);  /* quad_perm [1,0,3,2] */
-    v += DG_DPP(v, 0x4E);  /* quad_perm [2,3,0,1] */
-    v += DG_DPP(v, 0x141); /* row_half_mirror: lane i <- 7-i, the other quad */
+    v += DG_DPP(v, 0xB1); /* quad_perm [1,0,3,2] */
+    v += DG_DPP(v, 0x4E); /* quad_perm [2,3,0,1] */
     return v;
 }
 /* the value of the next lane of the group (0 for the last lane) */
-DGI uint32_t g8_next(uint32_t v, uint32_t g)
+DGI uint32_t g4_next(uint32_t v, uint32_t g)
 {
     const uint32_t t = DG_DPP(v, 0x101); /* row_shl:1 */
-    return g < 7 ? t : 0u;
+    return g < 3 ? t : 0u;
 }
 
 /* 0x80 in each byte of w (32-bit half) equal to c */
@@ -389,58 +400,6 @@ DGI uint32_t flat_write(S &src, const FField &F, O &o)
     }
 }
 
-/* An output writer into a message's LDS stage (zeroed beforehand) from an
- * arbitrary byte offset: whole words are stored, the partial words at the two
- * ends of the range -- shared with the neighbouring fields -- are OR-ed in
- * (the bytes outside the range are zero in them). */
-struct LOr {
-    typedef __attribute__((address_space(3))) uint64_t L64;
-    L64 *b;
-    uint32_t len;
-    uint64_t wbuf;
-    bool edge; /* the current word is shared with the field before */
-    DGI void init(L64 *base, uint32_t start)
-    {
-        b = base;
-        len = start;
-        wbuf = 0;
-        edge = (start & 7) != 0;
-    }
-    DGI void put_word(uint32_t wi, uint64_t v)
-    {
-        if (!edge) {
-            b[wi] = v;
-        } else {
-            __hip_atomic_fetch_or((uint64_t *)(void *)&b[wi], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            edge = false;
-        }
-    }
-    DGI void wle(uint64_t v, uint32_t n)
-    {
-        const uint32_t used = len & 7, sh = used << 3;
-        if (n < 8) v &= (1ull << (n << 3)) - 1;
-        const uint64_t low = (wbuf & ((1ull << sh) - 1)) | (v << sh);
-        const uint64_t high = used ? (v >> (64 - sh)) : 0;
-        const uint32_t wi = len >> 3;
-        len += n;
-        if (used + n >= 8) {
-            put_word(wi, low);
-            wbuf = high;
-        } else {
-            wbuf = low;
-        }
-    }
-    DGI void w8(uint8_t v) { wle(v, 1); }
-    DGI void w16(uint16_t v) { wle(__builtin_bswap16(v), 2); }
-    DGI void w32(uint32_t v) { wle(__builtin_bswap32(v), 4); }
-    DGI void w64(uint64_t v) { wle(__builtin_bswap64(v), 8); }
-    DGI void finish()
-    {
-        if (len & 7)
-            __hip_atomic_fetch_or((uint64_t *)(void *)&b[len >> 3], wbuf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-};
-
 struct FlatParams {
     const uint8_t *blob;
     dg_desc_hdr hdr;
@@ -469,15 +428,11 @@ struct FlatParams {
 #define FLP_END()
 #endif
 
-/* the field slot of wave w: waves w and w+4 share a SIMD, so the first
- * fields (often the short scalars) are paired with the last ones */
-DGI uint32_t fl_slot(uint32_t w) { return (w & 3) * 2 + (w >> 2); }
-
 /* per-message state of the block, one array per member (lane = message:
- * consecutive banks) */
+ * consecutive banks). ~36 KiB with a small descriptor: 4 blocks (16 waves)
+ * per CU, so a 64K-message batch (1024 blocks) is resident in one round. */
 struct FlatLds {
     uint64_t in[FL_STAGEW + FL_SLACKW];     /* the staged JSON */
-    uint64_t out[FL_MPB * FL_OUTW];         /* output stages, zeroed */
     uint64_t task[FL_MAXTASK];              /* chunk tasks */
     uint64_t oa[FL_MPB];                    /* output slot */
     uint32_t cap[FL_MPB];
@@ -491,10 +446,11 @@ struct FlatLds {
     uint32_t nbytes[FL_MPB];                /* Thrift bytes before STOP */
     uint32_t sep[FL_MAXF * FL_MPB];         /* [k][m]: comma position | quotes before it << 16 */
     uint16_t col[FL_MAXF * FL_MPB];         /* [k][m]: colon position */
-    uint32_t size[2 * FL_WAVES * FL_MPB];   /* [round & 1][slot][m] */
+    uint16_t size[2 * FL_SLOTS * FL_MPB];   /* [round & 1][slot][m] */
     uint32_t rounds, ntask;
     uint64_t p10u[20];
     double p10d[23];
+    uint64_t pw[EL_WN];                     /* Eisel-Lemire powers window (j2t_fast.h) */
 };
 
 template <int V>
@@ -509,7 +465,7 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
     const uint64_t b1 = b0 + FL_MPB < P.n ? b0 + FL_MPB : P.n;
 
     /* ---- 0. the block's JSON span to LDS (16-byte coalesced), the descriptor,
-     *      per-message offsets; the output stage zeroed ---- */
+     *      per-message offsets ---- */
     const uint64_t lo = P.in_off[b0], hi = P.in_off[b1];
     const uint64_t base = lo & ~15ull;
     const bool staged = hi - base <= (uint64_t)FL_STAGEW * 8;
@@ -524,13 +480,13 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
         uint4 *ld = (uint4 *)s_fdesc;
         for (uint32_t k = tid; k < (S.hdr.total_len + 15) / 16; k += 64 * FL_WAVES) ld[k] = gd[k];
     }
-    for (uint32_t k = tid; k < FL_MPB * FL_OUTW / 2; k += 64 * FL_WAVES) ((uint4 *)L.out)[k] = make_uint4(0, 0, 0, 0);
     if (tid < 20) {
         uint64_t v = 1;
         for (uint32_t k = 0; k < tid; k++) v *= 10;
         L.p10u[tid] = v;
     }
     if (tid < 23) L.p10d[tid] = P10[tid];
+    el_window_fill(L.pw, tid);
     if (tid == 0) {
         L.rounds = 0;
         L.ntask = 0;
@@ -570,7 +526,7 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
         L.nfq[tid] = 0;
     }
     __syncthreads();
-    const uint32_t m1 = tid >> 3, g = tid & 7; /* phases 1 and 4: 8 lanes per message */
+    const uint32_t g = tid & 3, m1 = tid >> 2; /* phase 1: 4 lanes per message */
     if (!staged) {
         /* a span too long for the stage (large messages in between): each
          * message that fits its own 256-byte slot is copied there */
@@ -584,117 +540,118 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
     }
     FLP(0);
     const auto D = desc_view<3>((const __attribute__((address_space(3))) uint8_t *)(void *)s_fdesc, S.hdr);
-    const FastTabs tb{(const __attribute__((address_space(3))) uint64_t *)(void *)L.p10u, (lds_f64 *)(void *)L.p10d};
+    const FastTabs tb{(const __attribute__((address_space(3))) uint64_t *)(void *)L.p10u, (lds_f64 *)(void *)L.p10d,
+                      (const __attribute__((address_space(3))) uint64_t *)(void *)L.pw};
     const dg_type rt = ldrec(&D.T[P.root]);
     const dg_struct sd = ldrec(&D.S[rt.st]);
 
-    /* ---- 1. structure: lane g of a message classifies the aligned words
-     *      [4g, 4g+4) of it, lane 7 also word 32 when the message reaches it
-     *      (bit b of a lane = message byte 32g + b - a7) ---- */
+    /* ---- 1. structure: lane g of a message holds message bytes
+     *      [64g, 64g+64) as 64-bit masks, bit b = byte 64g + b (quotes,
+     *      commas, colons; backslashes only when the message has one) ---- */
     {
         const bool on = L.ok[m1] != 0;
         const uint32_t n = L.n[m1], lwa = L.lw[m1], a7 = lwa & 7, lw = lwa >> 3;
-        const uint32_t nwords = on ? (a7 + n + 7) >> 3 : 0; /* aligned words of the message (<= 33) */
-        /* word 32 (messages of 250-256 B): a wave-uniform extra step */
-        const bool x5 = __builtin_amdgcn_ballot_w64(g == 7 && nwords > 32) != 0;
-        auto word = [&](uint32_t j) -> uint64_t {
-            const uint32_t wi = j < 4 ? 4 * g + j : (g == 7 ? 32u : 0xFFFFu);
-            uint64_t w = 0;
-            if (wi < nwords) {
-                w = L.in[lw + wi];
-                const int32_t wb = (int32_t)(wi * 8) - (int32_t)a7; /* message position of the word's byte 0 */
-                if (wb < 0) w &= ~0ull << ((uint32_t)(-wb) << 3);
-                if (wb + 8 > (int32_t)n) w &= (1ull << ((uint32_t)((int32_t)n - wb) << 3)) - 1;
-            }
-            return w;
-        };
-        uint32_t q80[10], ck[10]; /* per 32-bit half: quotes; commas | colons >> 1 */
-        uint32_t nq = 0, anybs = 0;
-        auto classify = [&](uint32_t j) {
-            const uint64_t w = word(j);
+        const int32_t nv0 = on ? (int32_t)n - 64 * (int32_t)g : 0;
+        const uint32_t nv = nv0 <= 0 ? 0u : nv0 >= 64 ? 64u : (uint32_t)nv0; /* message bytes in this lane */
+        const uint64_t vmask = nv >= 64 ? ~0ull : (1ull << nv) - 1;
+        /* the lane's 64 bytes start a7 bytes into aligned word lw + 8g: nine
+         * words read (the stage has slack past every message), re-aligned
+         * to the message with byte funnel shifts */
+        uint32_t d[18];
 #pragma unroll
-            for (uint32_t h = 0; h < 2; h++) {
-                const uint32_t x = (uint32_t)(w >> (32 * h));
-                q80[2 * j + h] = eq32(x, 0x22222222u);
-                ck[2 * j + h] = eq32(x, 0x2C2C2C2Cu) | (eq32(x, 0x3A3A3A3Au) >> 1);
-                anybs |= eq32(x, 0x5C5C5C5Cu);
-                nq += (uint32_t)__builtin_popcount(q80[2 * j + h]);
-            }
-        };
-#pragma unroll
-        for (uint32_t j = 0; j < 4; j++) classify(j);
-        q80[8] = q80[9] = ck[8] = ck[9] = 0;
-        if (x5) classify(4);
-        /* quote parity: prefix XOR of the quote bytes, carried across halves and the group */
-        const uint32_t qx = g8_incl_sum(nq, g) - nq;
-        uint32_t carry = qx & 1, nc = 0, nk = 0;
-        auto parity = [&](uint32_t h) {
-            uint32_t x = q80[h] >> 7;
-            x ^= x << 8;
-            x ^= x << 16;
-            const uint32_t ins = ((x << 8) - x) ^ (carry ? ~0u : 0u); /* 0xFF: inside a string (opening quote included) */
-            carry ^= (uint32_t)__builtin_popcount(q80[h]) & 1;
-            ck[h] &= ~ins;
-            nc += (uint32_t)__builtin_popcount(ck[h] & 0x80808080u);
-            nk += (uint32_t)__builtin_popcount(ck[h] & 0x40404040u);
-        };
-#pragma unroll
-        for (uint32_t h = 0; h < 8; h++) parity(h);
-        if (x5) {
-            parity(8);
-            parity(9);
+        for (uint32_t j = 0; j < 9; j++) {
+            const uint64_t w = L.in[lw + 8 * g + j];
+            d[2 * j] = (uint32_t)w;
+            d[2 * j + 1] = (uint32_t)(w >> 32);
         }
+        const bool hi4 = a7 >= 4;
+        const uint32_t sh = a7 & 3;
+        uint32_t x[16];
+#pragma unroll
+        for (uint32_t i = 0; i < 16; i++) {
+            const uint32_t lo_ = hi4 ? d[i + 1] : d[i], hi_ = hi4 ? d[i + 2] : d[i + 1];
+            x[i] = __builtin_amdgcn_alignbyte(hi_, lo_, sh);
+        }
+        /* 0x80-per-byte flags of two dwords -> 8 bits (byte i of the pair at bit i) */
+        auto pack8 = [](uint32_t m0, uint32_t m1_) -> uint32_t {
+            return (((m0 >> 7) | (m1_ >> 3)) * 0x01020408u) >> 24;
+        };
+        uint32_t ql = 0, qh = 0, cl = 0, ch = 0, kl = 0, kh = 0, anybs = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++) {
+            const uint32_t x0 = x[2 * j], x1 = x[2 * j + 1];
+            const uint32_t q8 = pack8(eq32(x0, 0x22222222u), eq32(x1, 0x22222222u));
+            const uint32_t c8 = pack8(eq32(x0, 0x2C2C2C2Cu), eq32(x1, 0x2C2C2C2Cu));
+            const uint32_t k8 = pack8(eq32(x0, 0x3A3A3A3Au), eq32(x1, 0x3A3A3A3Au));
+            anybs |= eq32(x0, 0x5C5C5C5Cu) | eq32(x1, 0x5C5C5C5Cu);
+            if (j < 4) {
+                ql |= q8 << (8 * j);
+                cl |= c8 << (8 * j);
+                kl |= k8 << (8 * j);
+            } else {
+                qh |= q8 << (8 * (j - 4));
+                ch |= c8 << (8 * (j - 4));
+                kh |= k8 << (8 * (j - 4));
+            }
+        }
+        uint64_t Q = ((uint64_t)qh << 32 | ql) & vmask, C = ((uint64_t)ch << 32 | cl) & vmask,
+                 K = ((uint64_t)kh << 32 | kl) & vmask;
+        const uint32_t nq = (uint32_t)__builtin_popcountll(Q);
+        const uint32_t qx = g4_incl_sum(nq, g) - nq; /* quotes in the lanes before */
+        /* in-string bytes: inclusive prefix XOR of the quotes (opening quote
+         * inside, closing quote outside), carried across the group */
+        uint64_t S = Q;
+        S ^= S << 1;
+        S ^= S << 2;
+        S ^= S << 4;
+        S ^= S << 8;
+        S ^= S << 16;
+        S ^= S << 32;
+        if (qx & 1) S = ~S;
+        C &= ~S;
+        K &= ~S;
+        const uint32_t nc = (uint32_t)__builtin_popcountll(C), nk = (uint32_t)__builtin_popcountll(K);
         const uint32_t pk = nc | (nk << 10) | (nq << 20);
-        const uint32_t pin = g8_incl_sum(pk, g);
-        const uint32_t ptot = g8_sum(pk);
-        const uint32_t hasbs = g8_sum(anybs ? 1u : 0u);
+        const uint32_t pin = g4_incl_sum(pk, g);
+        const uint32_t ptot = g4_sum(pk);
+        const uint32_t hasbs = g4_sum((anybs & 0x80808080u) && nv ? 1u : 0u);
+        FLP(1);
         uint32_t bad = 0;
         if (hasbs) {
             /* a backslash before '"' or '\\' (an escaped quote or backslash) -> decline,
              * so every quote is a delimiter */
-            uint64_t bw[5], qw[5];
+            uint32_t bl = 0, bh = 0;
 #pragma unroll
-            for (uint32_t j = 0; j < 5; j++) {
-                const uint64_t w = word(j);
-                bw[j] = eqbytes(w, '\\');
-                qw[j] = bw[j] | eqbytes(w, '"');
+            for (uint32_t j = 0; j < 8; j++) {
+                const uint32_t b8 = pack8(eq32(x[2 * j], 0x5C5C5C5Cu), eq32(x[2 * j + 1], 0x5C5C5C5Cu));
+                if (j < 4) bl |= b8 << (8 * j);
+                else bh |= b8 << (8 * (j - 4));
             }
-            const uint32_t nxt = g8_next((uint32_t)(qw[0] & 0x80), g); /* the next lane's first byte */
-            uint64_t bb = 0;
-#pragma unroll
-            for (uint32_t j = 0; j < 4; j++)
-                bb |= bw[j] & ((qw[j] >> 8) | (j < 3 ? qw[j + 1] << 56 : (g == 7 ? qw[4] : (uint64_t)nxt) << 56));
-            bb |= bw[4] & (qw[4] >> 8);
-            bad = g8_sum(bb ? 1u : 0u);
+            const uint64_t B = ((uint64_t)bh << 32 | bl) & vmask, QB = Q | B;
+            const uint32_t nxt = g4_next((uint32_t)(QB & 1), g); /* the next lane's first byte */
+            const uint64_t bb = B & ((QB >> 1) | ((uint64_t)nxt << 63));
+            bad = g4_sum(bb ? 1u : 0u);
         }
         if (on) {
-            uint32_t ci = (pin & 0x3FF) - nc, ki = ((pin >> 10) & 0x3FF) - nk, qc = qx;
-            auto record = [&](uint32_t h) {
-                const uint32_t pos0 = 32 * g + 4 * h - a7; /* message position of the half's byte 0 */
-                uint32_t c = ck[h] & 0x80808080u, k = ck[h] & 0x40404040u;
-                while (c) {
-                    const uint32_t bit = (uint32_t)__builtin_ctz(c);
-                    c &= c - 1;
-                    if (ci < FL_MAXF)
-                        L.sep[ci * FL_MPB + m1] =
-                            (pos0 + (bit >> 3)) | ((qc + (uint32_t)__builtin_popcount(q80[h] & ((1u << bit) - 1))) << 16);
-                    ci++;
-                }
-                while (k) {
-                    const uint32_t bit = (uint32_t)__builtin_ctz(k);
-                    k &= k - 1;
-                    if (ki < FL_MAXF) L.col[ki * FL_MPB + m1] = (uint16_t)(pos0 + (bit >> 3));
-                    ki++;
-                }
-                qc += (uint32_t)__builtin_popcount(q80[h]);
-            };
-#pragma unroll
-            for (uint32_t h = 0; h < 8; h++) record(h);
-            if (x5) {
-                record(8);
-                record(9);
+            uint32_t ci = (pin & 0x3FF) - nc, ki = ((pin >> 10) & 0x3FF) - nk;
+            const uint32_t pos0 = 64 * g;
+            uint64_t c = C, k = K;
+            while (c) {
+                const uint32_t bit = (uint32_t)__builtin_ctzll(c);
+                c &= c - 1;
+                if (ci < FL_MAXF)
+                    L.sep[ci * FL_MPB + m1] =
+                        (pos0 + bit) | ((qx + (uint32_t)__builtin_popcountll(Q & ((1ull << bit) - 1))) << 16);
+                ci++;
+            }
+            while (k) {
+                const uint32_t bit = (uint32_t)__builtin_ctzll(k);
+                k &= k - 1;
+                if (ki < FL_MAXF) L.col[ki * FL_MPB + m1] = (uint16_t)(pos0 + bit);
+                ki++;
             }
         }
+        FLP(2);
         if (g == 0 && on) {
             LSrc src;
             src.init((const __attribute__((address_space(3))) uint64_t *)(void *)&L.in[lw], (int32_t)a7, (int32_t)n);
@@ -710,30 +667,30 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
             L.ok[m1] = ok ? 1u : 0u;
             L.oc[m1] = open | (close << 16);
             L.nfq[m1] = nf | (qtot << 8) | (hasbs ? 1u << 31 : 0u);
-            if (ok) atomicMax(&L.rounds, (nf + FL_WAVES - 1) / FL_WAVES);
+            if (ok) atomicMax(&L.rounds, (nf + FL_SLOTS - 1) / FL_SLOTS);
         }
     }
-    FLP(1);
     __syncthreads();
-    FLP(2);
+    FLP(3);
 #if defined(DG_FL_STOP) && DG_FL_STOP == 1
     return;
 #endif
 
-    /* ---- 2./3. fields, field-major: wave w converts field fl_slot(w) + 8r
-     *      of the block's messages (lane = message) ---- */
+    /* ---- 2./3. fields, field-major: wave w converts field 4r + w of the
+     *      block's messages (lane = message) and writes it
+     *      straight into the slots, byte-exact at the shared edge words ---- */
     {
-        const uint32_t mm = lane, fs = fl_slot(wave);
+        const uint32_t mm = lane;
         const uint32_t ok0 = L.ok[mm], lwa = L.lw[mm], oc = L.oc[mm], nfq = L.nfq[mm];
         const uint32_t nf = nfq & 0xFF, qtot = (nfq >> 8) & 0x3FF;
         const bool hasbs = (nfq >> 31) != 0;
+        const uint32_t cap = L.cap[mm];
+        gu8 *const slot = (gu8 *)(void *)(P.out + L.oa[mm]);
         LSrc src;
         src.init((const __attribute__((address_space(3))) uint64_t *)(void *)&L.in[lwa >> 3], (int32_t)(lwa & 7), (int32_t)L.n[mm]);
         const uint32_t rounds = L.rounds;
         uint32_t nbytes = 0;
-        for (uint32_t r = 0; r < rounds; r++) {
-            const uint32_t k = r * FL_WAVES + fs;
-            FField F;
+        auto parse = [&](uint32_t k, FField &F) {
             F.size = 0;
             F.kind = FV_NONE;
             if (ok0 && k < nf) {
@@ -756,60 +713,82 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
                     else atomicOr(&L.phi[mm], 1u << (bit - 32));
                 }
             }
-            uint32_t *sz = &L.size[(r & 1) * FL_WAVES * FL_MPB];
-            sz[fs * FL_MPB + mm] = F.size;
-            FLP(3);
-            __syncthreads();
+        };
+        /* 0 = error, 1 = written, 2 = the body is left to chunk tasks */
+        auto write = [&](const FField &F, uint32_t off) -> uint32_t {
+            if (!F.size) return 1;
+            if (off + F.size >= cap) return 0; /* the slot holds the field and STOP */
+            WOut o;
+            o.init(slot + off);
+            const uint32_t wr = flat_write(src, F, o);
+            o.finish();
+            return wr;
+        };
+        for (uint32_t r = 0; r < rounds; r++) {
+            FField F[FL_FPW];
+            uint16_t *sz = &L.size[(r & 1) * FL_SLOTS * FL_MPB];
+#pragma unroll
+            for (uint32_t h = 0; h < FL_FPW; h++) {
+                parse(r * FL_SLOTS + wave + h * FL_WAVES, F[h]);
+                sz[(wave + h * FL_WAVES) * FL_MPB + mm] = (uint16_t)F[h].size;
+            }
             FLP(4);
+            __syncthreads();
+            FLP(5);
 #if defined(DG_FL_STOP) && DG_FL_STOP == 2
             continue;
 #endif
-            uint32_t off = nbytes, tot = 0;
+            uint32_t off[FL_FPW], tot = 0;
 #pragma unroll
-            for (uint32_t f = 0; f < FL_WAVES; f++) {
+            for (uint32_t h = 0; h < FL_FPW; h++) off[h] = nbytes;
+#pragma unroll
+            for (uint32_t f = 0; f < FL_SLOTS; f++) {
                 const uint32_t v = sz[f * FL_MPB + mm];
-                off += f < fs ? v : 0u;
+#pragma unroll
+                for (uint32_t h = 0; h < FL_FPW; h++) off[h] += f < wave + h * FL_WAVES ? v : 0u;
                 tot += v;
             }
             nbytes += tot;
-            uint32_t wr = 1;
-            if (F.size) {
-                wr = 0;
-                if (off + F.size <= FL_OUTW * 8) {
-                    LOr o;
-                    o.init((LOr::L64 *)(void *)&L.out[mm * FL_OUTW], off);
-                    wr = flat_write(src, F, o);
-                    o.finish();
-                }
+            uint32_t wr[FL_FPW], nch[FL_FPW], nsum = 0, good = 1;
+#pragma unroll
+            for (uint32_t h = 0; h < FL_FPW; h++) {
+                wr[h] = write(F[h], off[h]);
+                nch[h] = wr[h] == 2 ? (F[h].nb + FL_CHUNK - 1) / FL_CHUNK : 0u;
+                nsum += nch[h];
+                good &= wr[h] != 0;
             }
             {
                 /* bodies left to chunk tasks of FL_CHUNK input bytes: one LDS
                  * atomic per wave (lane 63 reserves the wave's total) */
-                const uint32_t nch = wr == 2 ? (F.nb + FL_CHUNK - 1) / FL_CHUNK : 0u;
-                const uint32_t incl = wave_incl_sum(nch, lane);
-                const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-                if (tot) {
-                    uint32_t base = 0;
-                    if (lane == 63) base = atomicAdd(&L.ntask, tot);
-                    base = (uint32_t)__builtin_amdgcn_readlane((int)base, 63);
-                    const uint32_t t0 = base + incl - nch;
-                    if (nch && t0 + nch <= FL_MAXTASK) {
-                        const bool b64 = F.kind == FV_BIN;
-                        for (uint32_t c = 0; c < nch; c++) {
-                            const uint32_t cs = c * FL_CHUNK, cn = min(FL_CHUNK, F.nb - cs);
-                            const uint32_t dst = off + 7 + (b64 ? c * (FL_CHUNK / 4 * 3) : cs);
-                            L.task[t0 + c] = (uint64_t)mm | ((uint64_t)b64 << 6) | ((uint64_t)(c + 1 == nch) << 7) |
-                                             ((uint64_t)(F.s0 + cs) << 8) | ((uint64_t)cn << 20) | ((uint64_t)dst << 32);
+                const uint32_t incl = wave_incl_sum(nsum, lane);
+                const uint32_t wtot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+                if (wtot) {
+                    uint32_t tb0 = 0;
+                    if (lane == 63) tb0 = atomicAdd(&L.ntask, wtot);
+                    tb0 = (uint32_t)__builtin_amdgcn_readlane((int)tb0, 63);
+                    uint32_t t0 = tb0 + incl - nsum;
+                    if (nsum && t0 + nsum <= FL_MAXTASK) {
+#pragma unroll
+                        for (uint32_t h = 0; h < FL_FPW; h++) {
+                            const bool b64 = F[h].kind == FV_BIN;
+                            for (uint32_t c = 0; c < nch[h]; c++) {
+                                const uint32_t cs = c * FL_CHUNK, cn = min(FL_CHUNK, F[h].nb - cs);
+                                const uint32_t dst = off[h] + 7 + (b64 ? c * (FL_CHUNK / 4 * 3) : cs);
+                                L.task[t0 + c] = (uint64_t)mm | ((uint64_t)b64 << 6) |
+                                                 ((uint64_t)(c + 1 == nch[h]) << 7) | ((uint64_t)(F[h].s0 + cs) << 8) |
+                                                 ((uint64_t)cn << 20) | ((uint64_t)dst << 32);
+                            }
+                            t0 += nch[h];
                         }
-                    } else if (nch) {
-                        wr = 0;
+                    } else if (nsum) {
+                        good = 0;
                     }
                 }
             }
-            if (!wr) L.ok[mm] = 0;
-            FLP(5);
+            if (!good) L.ok[mm] = 0;
+            FLP(6);
         }
-        if (fs == 0) L.nbytes[mm] = nbytes;
+        if (wave == 0) L.nbytes[mm] = nbytes;
     }
     FLP(6);
     __syncthreads();
@@ -822,8 +801,8 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
             const uint32_t lwa = L.lw[m];
             LSrc src;
             src.init((const __attribute__((address_space(3))) uint64_t *)(void *)&L.in[lwa >> 3], (int32_t)(lwa & 7), (int32_t)L.n[m]);
-            LOr o;
-            o.init((LOr::L64 *)(void *)&L.out[m * FL_OUTW], (uint32_t)(tk >> 32));
+            WOut o;
+            o.init((gu8 *)(void *)(P.out + L.oa[m] + (uint32_t)(tk >> 32)));
             bool cok = true;
             if ((tk >> 6) & 1) cok = body_b64(src, s0, cn, ((tk >> 7) & 1) != 0, o);
             else body_copy(src, s0, cn, o);
@@ -834,15 +813,15 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
     __syncthreads();
     FLP(7);
 
-    /* ---- 4. per message (8 lanes): unset fields, then the stage (STOP is
-     *      the zero byte after the fields) to the slot with word stores ---- */
-    {
-        const uint64_t i = b0 + m1;
+    /* ---- 4. per message (a lane): unset fields, then STOP and the result ---- */
+    if (tid < FL_MPB) {
+        const uint32_t m = tid;
+        const uint64_t i = b0 + m;
         if (i < b1) {
-            const uint32_t len = L.nbytes[m1] + 1;
-            bool good = L.ok[m1] && len <= FL_OUTW * 8 && len <= L.cap[m1];
+            const uint32_t len = L.nbytes[m] + 1;
+            bool good = L.ok[m] && len <= L.cap[m];
             if (good) {
-                const uint64_t present = (uint64_t)L.plo[m1] | ((uint64_t)L.phi[m1] << 32);
+                const uint64_t present = (uint64_t)L.plo[m] | ((uint64_t)L.phi[m] << 32);
                 uint64_t bits = D.R[sd.req_begin] & ~present;
                 const uint64_t flag = P.flag;
                 while (bits) { /* unset fields that error or need a default write -> the list pass */
@@ -858,15 +837,10 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
                 }
             }
             if (good) {
-                gu64 *dst = (gu64 *)(void *)(P.out + L.oa[m1]);
-                const __attribute__((address_space(3))) uint64_t *st =
-                    (const __attribute__((address_space(3))) uint64_t *)(void *)&L.out[m1 * FL_OUTW];
-                for (uint32_t w = g; w < (len + 7) / 8; w += FL_G) dst[w] = st[w];
-                if (g == 0) {
-                    P.ret[i] = 0;
-                    P.out_len[i] = len;
-                }
-            } else if (g == 0 && !L.big[m1]) {
+                ((gu8 *)(void *)P.out)[L.oa[m] + len - 1] = 0; /* STOP */
+                P.ret[i] = 0;
+                P.out_len[i] = len;
+            } else if (!L.big[m]) {
                 const uint32_t qq = atomicAdd(S.bail_count, 1u);
                 S.bail_list[qq] = (uint32_t)i;
             }

@@ -40,9 +40,9 @@ reps = 5
 _lib.check(L.dg_bench_device(*args, reps, C.byref(ms)))
 _lib.check(L.dg_ctx_counters(ctx.h, cnt, 16, 1))
 c = list(cnt)[2:10]
-names = ["stage+desc+barrier", "structure", "barrier 1", "parse", "barrier 2", "prefix+write", "tail",
-         "barrier 4"]
-waves = n // 8 // 32  # 8 waves per 64-message block; 1 block in 32 sampled
+names = ["stage+desc+barrier", "classify+scan", "record", "open/close+barrier 1", "parse", "barrier 2", "write+tasks",
+         "chunks+barrier 4"]
+waves = n // 64 // 32 * 4  # 4 waves per 64-message block; 1 block in 32 sampled
 tot = sum(c)
 print(f"{cfg}: {ms.value / reps * 1000:.1f} us/step (instrumented), ok={(d_ret.cpu().numpy() == 0).sum()}")
 for k, nm in enumerate(names):
