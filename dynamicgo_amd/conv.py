@@ -473,8 +473,13 @@ class BinaryConv:
         # a null body converts to nothing: no struct, no mapped fields
         return [p + o if int(r) == 0 and o else b"" for p, o, r in zip(prefixes, outs, rets)], rets
 
-    def do_batch(self, desc, msgs: Sequence[bytes], extra_flags: int = 0) -> Tuple[List[bytes], np.ndarray]:
-        """Batch of independent messages -> (outputs, packed statuses)."""
+    def do_batch(self, desc, msgs: Sequence[bytes], extra_flags: int = 0, chunks: int = 0,
+                 out_cap: Optional[int] = None) -> Tuple[List[bytes], np.ndarray]:
+        """Batch of independent messages -> (outputs, packed statuses).
+        chunks > 0 streams the batch through dg_j2t_pipeline_host in that many
+        overlapped pieces (uploads, kernels and downloads of neighbouring
+        chunks in flight at once); out_cap overrides the first output
+        capacity (the DG_E_NOMEM retry then takes out_need)."""
         self._check_opts()
         flat = self._flat(desc)
         ctx = self._ctx()
@@ -485,20 +490,25 @@ class BinaryConv:
         arena = np.frombuffer(b"".join(msgs) + b"\0" * 16, dtype=np.uint8)
         rets = np.zeros(max(n, 1), dtype=np.uint64)
         out_off = np.zeros(n + 1, dtype=np.uint64)
-        cap = int(lens.sum()) * 4 + 64 * n + 64
-        out = np.zeros(cap, dtype=np.uint8)
+        cap = int(lens.sum()) * 4 + 64 * n + 64 if out_cap is None else out_cap
+        out = np.zeros(max(cap, 1), dtype=np.uint8)
         need = C.c_uint64(0)
         L = _lib.lib()
         flags = to_flags(self.opts) | extra_flags
-        rc = L.dg_j2t_batch_host(ctx.h, ctx.desc(flat), flat.root_type, arena.ctypes.data, in_off.ctypes.data,
-                                 n, flags, out.ctypes.data, cap, out_off.ctypes.data,
-                                 rets.ctypes.data, C.byref(need))
+
+        def call(out, cap):
+            if chunks > 0:
+                return L.dg_j2t_pipeline_host(ctx.h, ctx.desc(flat), flat.root_type, arena.ctypes.data,
+                                              in_off.ctypes.data, n, flags, chunks, out.ctypes.data, cap,
+                                              out_off.ctypes.data, rets.ctypes.data, C.byref(need))
+            return L.dg_j2t_batch_host(ctx.h, ctx.desc(flat), flat.root_type, arena.ctypes.data, in_off.ctypes.data,
+                                       n, flags, out.ctypes.data, cap, out_off.ctypes.data,
+                                       rets.ctypes.data, C.byref(need))
+        rc = call(out, cap)
         if rc == -3 and need.value > cap:
             cap = int(need.value) + 64
             out = np.zeros(cap, dtype=np.uint8)
-            rc = L.dg_j2t_batch_host(ctx.h, ctx.desc(flat), flat.root_type, arena.ctypes.data,
-                                     in_off.ctypes.data, n, flags, out.ctypes.data, cap,
-                                     out_off.ctypes.data, rets.ctypes.data, C.byref(need))
+            rc = call(out, cap)
         _lib.check(rc)
         outs = [out[int(out_off[i]):int(out_off[i + 1])].tobytes() for i in range(n)]
         return outs, rets[:n]
@@ -539,13 +549,18 @@ class Aggregator:
     (conv/j2t/conv_timing_test.go:76-99)."""
 
     def __init__(self, desc, opts: Optional[Options] = None, max_batch: int = 4096, max_wait_us: int = 200,
-                 ctx: Optional[Context] = None):
+                 ctx: Optional[Context] = None, max_bytes: Optional[int] = None):
         self.conv = BinaryConv(opts, ctx=ctx)
         self.flat = self.conv._flat(desc)
         c = self.conv._ctx()
         h = C.c_void_p()
-        _lib.check(_lib.lib().dg_agg_create(c.h, c.desc(self.flat), self.flat.root_type, to_flags(self.conv.opts),
-                                            max_batch, max_wait_us, C.byref(h)))
+        if max_bytes is None:
+            _lib.check(_lib.lib().dg_agg_create(c.h, c.desc(self.flat), self.flat.root_type,
+                                                to_flags(self.conv.opts), max_batch, max_wait_us, C.byref(h)))
+        else:
+            _lib.check(_lib.lib().dg_agg_create2(c.h, c.desc(self.flat), self.flat.root_type,
+                                                 to_flags(self.conv.opts), max_batch, max_bytes, max_wait_us,
+                                                 C.byref(h)))
         self.h = h
 
     def do(self, jbytes: bytes) -> Optional[bytes]:
@@ -565,6 +580,29 @@ class Aggregator:
                 raise J2TError(int(ret.value), explain_native_error(int(ret.value), jbytes))
             return out.raw[:ol.value] or None
         raise J2TError(0, "aggregator: output did not fit")
+
+    def drive(self, msgs: Sequence[bytes], threads: int = 16, window: int = 256):
+        """The reference's b.RunParallel over Do (conv/j2t/conv_timing_test.go:
+        76-99) from C: `threads` OS threads, each with up to `window` calls in
+        flight (dg_agg_drive). Returns (outputs, statuses, latency ns per
+        message, wall seconds); statuses are the packed status words."""
+        n = len(msgs)
+        lens = np.fromiter((len(m) for m in msgs), dtype=np.uint64, count=n)
+        in_off = np.zeros(n + 1, dtype=np.uint64)
+        np.cumsum(lens, out=in_off[1:])
+        arena = np.frombuffer(b"".join(msgs) + b"\0" * 16, dtype=np.uint8)
+        out_off = np.zeros(n + 1, dtype=np.uint64)
+        np.cumsum(lens * 4 + 4096, out=out_off[1:])
+        out = np.zeros(int(out_off[-1]) + 64, dtype=np.uint8)
+        out_len = np.zeros(max(n, 1), dtype=np.uint64)
+        rets = np.zeros(max(n, 1), dtype=np.uint64)
+        lat = np.zeros(max(n, 1), dtype=np.uint32)
+        secs = C.c_double(0)
+        _lib.check(_lib.lib().dg_agg_drive(self.h, arena.ctypes.data, in_off.ctypes.data, n, threads, window,
+                                           out.ctypes.data, out_off.ctypes.data, out_len.ctypes.data,
+                                           rets.ctypes.data, lat.ctypes.data, C.byref(secs)))
+        outs = [out[int(out_off[i]):int(out_off[i]) + int(out_len[i])].tobytes() for i in range(n)]
+        return outs, rets[:n], lat[:n], secs.value
 
     def stats(self) -> Tuple[int, int]:
         """(batches flushed, messages converted)."""

@@ -101,7 +101,15 @@ struct dg_ctx {
     uint8_t *ws_t2j = nullptr;
     hipEvent_t ws_t2j_done = nullptr;
     hipStream_t ws_t2j_last = nullptr;
+    /* dg_j2t_pipeline_host: its per-chunk buffers (j2t_pipe.hip PipeBuf),
+     * kept across calls; pipe_mu serialises pipeline calls */
+    std::mutex pipe_mu;
+    std::vector<void *> pipe;
+    uint64_t pipe_cap_n = 0, pipe_cap_b = 0;
 };
+
+/* frees the context's pipeline buffers (j2t_pipe.hip) */
+__attribute__((visibility("hidden"))) void dg_i_pipe_free(dg_ctx *c);
 
 /* pinned host staging, grown on demand (hipHostMalloc is slow: keep it) */
 static inline int grow_pinned(uint8_t *&p, uint64_t &cap, uint64_t want)
@@ -150,3 +158,11 @@ static inline int grow_x(Scratch *x, T *&p, uint64_t &cap, uint64_t want)
 
 /* the scratch for a launch on stream s (ctx mutex held) */
 __attribute__((visibility("hidden"))) int scratch_for(dg_ctx *c, hipStream_t s, Scratch **out);
+
+/* one batch converted and packed on stream s (takes the ctx mutex): message
+ * i's Thrift at d_packed + d_pack_off[i], d_pack_off[n] = total; failed and
+ * overflowed messages pack as nothing (their d_ret says why) */
+__attribute__((visibility("hidden"))) int dg_i_convert_pack(
+    dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *d_json, const uint64_t *d_in_off, uint64_t n,
+    uint64_t flags, uint8_t *d_out, const uint64_t *d_out_off, uint32_t *d_out_len, uint64_t *d_ret, uint8_t *d_packed,
+    uint64_t *d_pack_off, hipStream_t s, uint64_t max_len);

@@ -172,6 +172,7 @@ void dg_ctx_destroy(dg_ctx *c)
     if (!c) return;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
+    dg_i_pipe_free(c);
     for (Scratch *x : c->scratch) scratch_free(x);
     c->scratch.clear();
     (void)hipFree(c->d_pending);
@@ -834,6 +835,23 @@ static int pack_scan(dg_ctx *c, const uint8_t *d_out, const uint64_t *d_out_off,
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     return pack_scan_nolock(c, d_out, d_out_off, d_out_len, d_ret, n, hdr, hdr_len, ftr, ftr_len, d_dst, d_dst_off, s);
 }
+
+}  // extern "C"
+
+/* conversion + packing of one batch on stream s (failed and overflowed
+ * messages pack as nothing), for the pipelined host paths (j2t_pipe.hip) */
+int dg_i_convert_pack(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *d_json, const uint64_t *d_in_off,
+                      uint64_t n, uint64_t flags, uint8_t *d_out, const uint64_t *d_out_off, uint32_t *d_out_len,
+                      uint64_t *d_ret, uint8_t *d_packed, uint64_t *d_pack_off, hipStream_t s, uint64_t max_len)
+{
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    int rc = launch(c, d, root, d_json, d_in_off, n, flags, d_out, d_out_off, d_out_len, d_ret, nullptr, s, max_len);
+    if (rc) return rc;
+    return pack_scan_nolock(c, d_out, d_out_off, d_out_len, d_ret, n, nullptr, 0, nullptr, 0, d_packed, d_pack_off, s);
+}
+
+extern "C" {
 
 int dg_pack_device_scan(dg_ctx *c, const uint8_t *d_out, const uint64_t *d_out_off, const uint32_t *d_out_len,
                         uint64_t n, uint8_t *d_dst, uint64_t *d_dst_off, void *stream)

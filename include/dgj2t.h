@@ -218,10 +218,54 @@ int dg_agg_create(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, uint64_t
                   uint32_t max_wait_us, dg_agg **out);
 int dg_agg_do(dg_agg *agg, const uint8_t *json, size_t len, uint8_t *out, size_t out_cap, size_t *out_len,
               uint64_t *ret);
+/* dg_agg_create with the JSON capacity of one batch (max_bytes; a message
+ * longer than that is converted alone). dg_agg_create uses
+ * max(1 MiB, 512 B x max_batch). */
+int dg_agg_create2(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, uint64_t flags, uint32_t max_batch,
+                   uint64_t max_bytes, uint32_t max_wait_us, dg_agg **out);
+/* Asynchronous form of dg_agg_do, for a caller with many requests in flight
+ * (an event loop, or a goroutine pool behind one OS thread): dg_agg_submit
+ * copies the JSON into the open batch and returns a ticket; dg_agg_wait
+ * blocks until the ticket's batch is converted and copies its result out
+ * (same results as dg_agg_do). Every ticket must be waited for exactly once,
+ * and `json` must stay valid until then. With nonblock, dg_agg_submit
+ * returns DG_E_AGAIN instead of blocking when no batch is open (a caller
+ * that holds unwaited tickets must use it, and wait for its oldest ticket
+ * before retrying: the next batch opens when the oldest one's callers have
+ * taken their results). */
+typedef struct dg_agg_ticket {
+    void *batch;
+    uint64_t gen;
+    uint32_t idx;
+    const uint8_t *json;
+    size_t len;
+} dg_agg_ticket;
+int dg_agg_submit(dg_agg *agg, const uint8_t *json, size_t len, int nonblock, dg_agg_ticket *t);
+int dg_agg_wait(dg_agg *agg, dg_agg_ticket *t, uint8_t *out, size_t out_cap, size_t *out_len, uint64_t *ret);
 /* batches flushed and messages converted so far */
 int dg_agg_stats(dg_agg *agg, uint64_t *batches, uint64_t *msgs);
-/* converts what is still queued, then stops the flusher */
+/* converts what is still queued, then stops the flusher (every ticket must
+ * have been waited for) */
 void dg_agg_destroy(dg_agg *agg);
+/* Benchmark driver (the reference's b.RunParallel over Do,
+ * conv/j2t/conv_timing_test.go:76-99): `threads` OS threads each convert a
+ * contiguous share of the n messages through the aggregator with up to
+ * `window` requests in flight, message i's result into
+ * out[out_off[i] .. out_off[i+1]) with out_len[i], ret[i], and, if lat_ns,
+ * its submit-to-result latency. *seconds = wall time of the whole run. */
+int dg_agg_drive(dg_agg *agg, const uint8_t *arena, const uint64_t *in_off, uint64_t n, int threads, int window,
+                 uint8_t *out, const uint64_t *out_off, uint64_t *out_len, uint64_t *ret, uint32_t *lat_ns,
+                 double *seconds);
+
+/* dg_j2t_batch_host for large host batches: the batch is streamed in
+ * `chunks` pieces through 3 stream-private buffer sets, so the upload of
+ * chunk k+1, the kernels of chunk k and the download of chunk k-1 overlap,
+ * all issued from C. json, in_off, out, out_off and ret should be pinned
+ * (hipHostMalloc) for the copies to be asynchronous. Same outputs and
+ * DG_E_NOMEM/out_need contract as dg_j2t_batch_host; json needs no padding. */
+int dg_j2t_pipeline_host(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, const uint8_t *json,
+                         const uint64_t *in_off, uint64_t n, uint64_t flags, uint32_t chunks, uint8_t *out,
+                         uint64_t out_cap, uint64_t *out_off, uint64_t *ret, uint64_t *out_need);
 
 /*
  * t2j: Thrift binary -> JSON (the reverse path, conv/t2j). Replaces

@@ -66,6 +66,7 @@ typedef struct dg_hm_entry {
 #define DG_E_HIP (-2)
 #define DG_E_NOMEM (-3)
 #define DG_E_DESC (-4)
+#define DG_E_AGAIN (-5) /* dg_agg_submit(nonblock): no open batch right now */
 
 /* t2j (Thrift binary -> JSON, conv/t2j) option bits: the conv.Options fields
  * conv/t2j/impl.go reads (conv/api.go:52-121) */

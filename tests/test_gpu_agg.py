@@ -51,3 +51,92 @@ def test_aggregator_grows_output_and_drains_on_close():
     chk = oracle.RefOracle() or oracle.PortOracle()
     assert out == chk.j2t(T.flatten(td), b"{}", 0x3)[1]
     agg.close()
+
+
+def _mixed_msgs(n, seed):
+    rng = random.Random(seed)
+    msgs = W.gen_nested_batch(rng, n) + [b"{]", b"", b"null", b'{"I64":"x"}'] * 8
+    rng.shuffle(msgs)
+    return msgs
+
+
+@pytest.mark.parametrize("threads,window,max_batch", [(8, 64, 128), (16, 300, 1024), (3, 1, 64)])
+def test_aggregator_drive_vs_oracle(threads, window, max_batch):
+    """dg_agg_drive: many threads with many calls in flight each (the async
+    submit/wait form); small batches force the ring of in-flight batches to
+    wrap many times and callers to meet sealed batches."""
+    td = W.nesting_i64_desc()
+    msgs = _mixed_msgs(3000, 11)
+    fl = T.flatten(td)
+    chk = oracle.RefOracle() or oracle.PortOracle()
+    want = [chk.j2t(fl, m, 1) for m in msgs]
+    agg = conv.Aggregator(td, conv.Options(), max_batch=max_batch, max_wait_us=500, max_bytes=max_batch * 1200)
+    outs, rets, lat, secs = agg.drive(msgs, threads=threads, window=window)
+    batches, n = agg.stats()
+    agg.close()
+    assert n == len(msgs)
+    assert batches >= len(msgs) // max_batch
+    assert [(int(r), o if int(r) == 0 else b"") for r, o in zip(rets, outs)] == \
+        [(r, o if r == 0 else b"") for r, o in want]
+    assert secs > 0 and int(lat.max()) > 0
+
+
+def test_aggregator_byte_capacity_and_oversize():
+    """A batch sealed by its JSON capacity (not its count), and a message
+    longer than a whole batch (converted alone)."""
+    td = W.nesting_i64_desc()
+    rng = random.Random(5)
+    msgs = W.gen_nested_batch(rng, 400)
+    big = max(msgs, key=len)
+    msgs = msgs + [big]
+    fl = T.flatten(td)
+    chk = oracle.RefOracle() or oracle.PortOracle()
+    want = [chk.j2t(fl, m, 1) for m in msgs]
+    agg = conv.Aggregator(td, conv.Options(), max_batch=4096, max_wait_us=300, max_bytes=len(big) * 3 - 1)
+    outs, rets, _, _ = agg.drive(msgs, threads=4, window=32)
+    agg.close()
+    assert [(int(r), o) for r, o in zip(rets, outs)] == [(r, o) for r, o in want]
+    agg = conv.Aggregator(td, conv.Options(), max_batch=64, max_wait_us=300, max_bytes=len(big) - 1)
+    assert agg.do(big) == want[-1][1]
+    agg.close()
+
+
+@pytest.mark.parametrize("chunks", [1, 3, 7])
+def test_pipeline_host_vs_oracle(chunks):
+    """dg_j2t_pipeline_host: the same outputs as dg_j2t_batch_host and the
+    oracle, for any chunking."""
+    td = W.nesting_i64_desc()
+    msgs = _mixed_msgs(2500, 12)
+    fl = T.flatten(td)
+    chk = oracle.RefOracle() or oracle.PortOracle()
+    want = [chk.j2t(fl, m, 1) for m in msgs]
+    cv = conv.BinaryConv(conv.Options())
+    outs, rets = cv.do_batch(td, msgs, chunks=chunks)
+    assert [(int(r), o if int(r) == 0 else b"") for r, o in zip(rets, outs)] == \
+        [(r, o if r == 0 else b"") for r, o in want]
+
+
+def test_pipeline_host_overflow_splice_and_nomem():
+    """Slot overflows (2 bytes of JSON -> 2190 bytes of Thrift) are rerun and
+    spliced in place, in every chunk; a too-small out_cap gives DG_E_NOMEM
+    with the exact need, and the retry succeeds."""
+    fields = [T.FieldDescriptor(i, "f%d" % i, T.builtin("i64"), T.DEFAULT) for i in range(1, 200)]
+    td = T.struct_type("Wide", fields)
+    rng = random.Random(9)
+    msgs = []
+    for i in range(900):
+        if rng.random() < 0.05:
+            msgs.append(b"{}")
+        else:
+            ks = rng.sample(range(1, 200), 150)
+            msgs.append(("{" + ",".join('"f%d":%d' % (k, rng.randrange(-10**12, 10**12)) for k in ks) + "}").encode())
+    fl = T.flatten(td)
+    chk = oracle.RefOracle() or oracle.PortOracle()
+    opts = conv.Options(WriteDefaultField=True)
+    want = [chk.j2t(fl, m, conv.to_flags(opts)) for m in msgs]
+    cv = conv.BinaryConv(opts)
+    for chunks in (1, 4):
+        outs, rets = cv.do_batch(td, msgs, chunks=chunks)
+        assert [(int(r), o) for r, o in zip(rets, outs)] == [(r, o) for r, o in want]
+    outs, rets = cv.do_batch(td, msgs, chunks=3, out_cap=1000)  # NOMEM first, then the exact need
+    assert [(int(r), o) for r, o in zip(rets, outs)] == [(r, o) for r, o in want]
