@@ -17,7 +17,7 @@ EXPORTS = ["dg_last_error", "dg_build_info", "dg_ctx_create", "dg_ctx_destroy", 
            "dg_desc_create_device", "dg_desc_destroy", "dg_desc_root", "dg_j2t_batch_device",
            "dg_j2t_batch_device_ml", "dg_j2t_batch_device_hm", "dg_j2t_batch_device_iters",
            "dg_slot_bound", "dg_j2t_batch_host", "dg_j2t_batch_host_hm", "dg_j2t_do", "dg_pack_device", "dg_pack_device_scan", "dg_pack_device_framed", "dg_agg_create", "dg_agg_create2", "dg_agg_do",
-           "dg_agg_submit", "dg_agg_wait", "dg_agg_stats", "dg_agg_destroy", "dg_agg_drive", "dg_j2t_pipeline_host", "dg_bench_device", "dg_desc_attach_t2j", "dg_t2j_slot_bound", "dg_t2j_batch_device", "dg_t2j_batch_device_ml",
+           "dg_agg_submit", "dg_agg_wait", "dg_agg_stats", "dg_agg_profile", "dg_agg_destroy", "dg_agg_drive", "dg_j2t_pipeline_host", "dg_bench_device", "dg_desc_attach_t2j", "dg_t2j_slot_bound", "dg_t2j_batch_device", "dg_t2j_batch_device_ml",
            "dg_t2j_batch_host"]
 
 _lib = None
@@ -77,6 +77,7 @@ def lib() -> C.CDLL:
         "dg_agg_drive": (i32, [vp, vp, vp, u64, i32, i32, vp, vp, vp, vp, vp, C.POINTER(C.c_double)]),
         "dg_j2t_pipeline_host": (i32, [vp, vp, u32, vp, vp, u64, u64, u32, vp, u64, vp, vp, P64]),
         "dg_agg_stats": (i32, [vp, P64, P64]),
+        "dg_agg_profile": (i32, [vp, P64, i32]),
         "dg_agg_destroy": (None, [vp]),
         "dg_desc_attach_t2j": (i32, [vp, C.c_char_p, sz]),
         "dg_t2j_slot_bound": (u64, [u64]),

@@ -105,7 +105,9 @@ struct dg_ctx {
      * kept across calls; pipe_mu serialises pipeline calls */
     std::mutex pipe_mu;
     std::vector<void *> pipe;
-    uint64_t pipe_cap_n = 0, pipe_cap_b = 0;
+    uint8_t *h_pipe_out = nullptr; uint64_t h_pipe_out_cap = 0; /* pinned staging when the caller's */
+    uint8_t *h_pipe_aux = nullptr; uint64_t h_pipe_aux_cap = 0; /* buffers are pageable */
+    uint64_t *d_zero = nullptr;                                 /* 8 zero bytes (device) */
 };
 
 /* frees the context's pipeline buffers (j2t_pipe.hip) */
@@ -161,8 +163,13 @@ __attribute__((visibility("hidden"))) int scratch_for(dg_ctx *c, hipStream_t s, 
 
 /* one batch converted and packed on stream s (takes the ctx mutex): message
  * i's Thrift at d_packed + d_pack_off[i], d_pack_off[n] = total; failed and
- * overflowed messages pack as nothing (their d_ret says why) */
+ * overflowed messages pack as nothing (their d_ret says why). Chained form:
+ * positions start at *base_in, bytes past dst_cap are not written (0: no
+ * limit); d_packed / d_pack_off may be pinned host memory; the packing
+ * waits for pack_after (another stream's event) when it is set. base_mod16
+ * = 1 | phase << 1: positions start at (*base_in + phase) & 15 instead. */
 __attribute__((visibility("hidden"))) int dg_i_convert_pack(
     dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *d_json, const uint64_t *d_in_off, uint64_t n,
     uint64_t flags, uint8_t *d_out, const uint64_t *d_out_off, uint32_t *d_out_len, uint64_t *d_ret, uint8_t *d_packed,
-    uint64_t *d_pack_off, hipStream_t s, uint64_t max_len);
+    uint64_t *d_pack_off, hipStream_t s, uint64_t max_len, const uint64_t *base_in = nullptr, uint64_t dst_cap = 0,
+    hipEvent_t pack_after = nullptr, int base_mod16 = 0);

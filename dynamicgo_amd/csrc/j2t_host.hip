@@ -132,6 +132,8 @@ int dg_ctx_create(int device, dg_ctx **out)
      * in order */
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamDefault));
     HIPCHK(hipMalloc(&c->d_pending, 16));
+    HIPCHK(hipMalloc(&c->d_zero, 16));
+    HIPCHK(hipMemset(c->d_zero, 0, 16));
     HIPCHK(hipMalloc(&c->d_stats, 16 * 8));
     HIPCHK(hipMemset(c->d_stats, 0, 16 * 8));
     HIPCHK(hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device));
@@ -176,6 +178,7 @@ void dg_ctx_destroy(dg_ctx *c)
     for (Scratch *x : c->scratch) scratch_free(x);
     c->scratch.clear();
     (void)hipFree(c->d_pending);
+    (void)hipFree(c->d_zero);
     (void)hipFree(c->d_stats);
     (void)hipFree(c->d_json);
     (void)hipFree(c->d_in_off);
@@ -567,7 +570,8 @@ int dg_j2t_batch_device_iters(dg_ctx *c, const dg_desc *d, uint32_t root, const 
 /* dg_pack_device_scan / _framed without the context lock (the caller holds it) */
 static int pack_scan_nolock(dg_ctx *c, const uint8_t *d_out, const uint64_t *d_out_off, const uint32_t *d_out_len,
                             const uint64_t *d_ret, uint64_t n, const uint8_t *hdr, uint32_t hdr_len, const uint8_t *ftr,
-                            uint32_t ftr_len, uint8_t *d_dst, uint64_t *d_dst_off, hipStream_t s);
+                            uint32_t ftr_len, uint8_t *d_dst, uint64_t *d_dst_off, hipStream_t s,
+                            const uint64_t *base_in = nullptr, uint64_t dst_cap = 0, int base_mod16 = 0);
 
 /* Host batch: ONE pinned upload [in_off | out_off | JSON], the kernels, a
  * device packing pass (used slot prefixes back to back, failed messages
@@ -783,10 +787,12 @@ int dg_pack_device(dg_ctx *c, const uint8_t *d_out, const uint64_t *d_out_off, c
 
 static int pack_scan_nolock(dg_ctx *c, const uint8_t *d_out, const uint64_t *d_out_off, const uint32_t *d_out_len,
                             const uint64_t *d_ret, uint64_t n, const uint8_t *hdr, uint32_t hdr_len, const uint8_t *ftr,
-                            uint32_t ftr_len, uint8_t *d_dst, uint64_t *d_dst_off, hipStream_t s)
+                            uint32_t ftr_len, uint8_t *d_dst, uint64_t *d_dst_off, hipStream_t s,
+                            const uint64_t *base_in, uint64_t dst_cap, int base_mod16)
 {
     if (n == 0) {
-        HIPCHK(hipMemsetAsync(d_dst_off, 0, 8, s));
+        if (base_in && !base_mod16) HIPCHK(hipMemcpyAsync(d_dst_off, base_in, 8, hipMemcpyDefault, s));
+        else HIPCHK(hipMemsetAsync(d_dst_off, 0, 8, s));
         return DG_OK;
     }
     Scratch *x;
@@ -794,6 +800,10 @@ static int pack_scan_nolock(dg_ctx *c, const uint8_t *d_out, const uint64_t *d_o
     if (rc) return rc;
     MsgFrame fr{};
     fr.ret = d_ret; /* failed messages pack as nothing */
+    fr.base_in = base_in;
+    fr.dst_cap = dst_cap;
+    fr.base_mod16 = base_mod16 ? 1u : 0u;
+    fr.phase_add = (uint32_t)(base_mod16 >> 1) & 15; /* dg_i_convert_pack: 1 | phase << 1 */
     if (hdr) {
         /* header at 0, footer 8-aligned after it; both followed by >= 16 readable bytes */
         const uint32_t fo = (hdr_len + 7) & ~7u;
@@ -842,13 +852,16 @@ static int pack_scan(dg_ctx *c, const uint8_t *d_out, const uint64_t *d_out_off,
  * messages pack as nothing), for the pipelined host paths (j2t_pipe.hip) */
 int dg_i_convert_pack(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *d_json, const uint64_t *d_in_off,
                       uint64_t n, uint64_t flags, uint8_t *d_out, const uint64_t *d_out_off, uint32_t *d_out_len,
-                      uint64_t *d_ret, uint8_t *d_packed, uint64_t *d_pack_off, hipStream_t s, uint64_t max_len)
+                      uint64_t *d_ret, uint8_t *d_packed, uint64_t *d_pack_off, hipStream_t s, uint64_t max_len,
+                      const uint64_t *base_in, uint64_t dst_cap, hipEvent_t pack_after, int base_mod16)
 {
     std::lock_guard<std::mutex> g(c->mu);
     HIPCHK(hipSetDevice(c->device));
     int rc = launch(c, d, root, d_json, d_in_off, n, flags, d_out, d_out_off, d_out_len, d_ret, nullptr, s, max_len);
     if (rc) return rc;
-    return pack_scan_nolock(c, d_out, d_out_off, d_out_len, d_ret, n, nullptr, 0, nullptr, 0, d_packed, d_pack_off, s);
+    if (pack_after) HIPCHK(hipStreamWaitEvent(s, pack_after, 0));
+    return pack_scan_nolock(c, d_out, d_out_off, d_out_len, d_ret, n, nullptr, 0, nullptr, 0, d_packed, d_pack_off, s,
+                            base_in, dst_cap, base_mod16);
 }
 
 extern "C" {

@@ -1,26 +1,25 @@
 /*
  * j2t_pipe.hip — the host-memory paths around the device batch:
  *
- *  1. the batching aggregator behind BinaryConv.Do.
+ *  1. The batching aggregator behind BinaryConv.Do.
  *     The reference converts ONE message per call, from many goroutines at
  *     once (conv/j2t/conv_timing_test.go:76-99, b.RunParallel over
- *     BinaryConv.Do, conv/j2t/conv.go:53-77). A GPU needs batches, so callers
- *     reserve a place in the open batch with one atomic add, copy their JSON
- *     straight into its pinned upload buffer themselves (in parallel, no lock),
- *     and later copy their Thrift out of its pinned download buffer. A flusher
- *     thread seals a batch when it is full or its first message has waited
- *     max_wait_us, uploads it and launches convert + pack on the batch's own
- *     stream; a completer thread downloads [ret | packed offsets] and then
- *     exactly the packed bytes, and wakes the batch's callers. Up to
- *     AGG_INFLIGHT batches are in flight at once, so uploads, kernels and
- *     downloads of consecutive batches overlap.
+ *     BinaryConv.Do, conv/j2t/conv.go:53-77). A GPU needs batches. Every
+ *     caller thread owns a sub-batch of the open batch (a pinned JSON region
+ *     and its message ends), so a call touches no shared cache line: it
+ *     copies its JSON into its own region and bumps its own count. A flusher
+ *     thread seals the open batch (a seq_cst handshake with a per-thread busy
+ *     flag), uploads every non-empty sub-batch, builds the batch's offsets on
+ *     the device and launches convert + pack on the batch's own stream; a
+ *     completer thread downloads [ret | packed offsets], then exactly the
+ *     packed bytes, and wakes the callers, who copy their results out.
+ *     AGG_INFLIGHT batches rotate, so uploads, kernels and downloads of
+ *     consecutive batches overlap.
  *
  *  2. dg_j2t_pipeline_host: one large host batch (pinned buffers) streamed
- *     through the same per-batch buffers in chunks: H2D, convert, pack, D2H
- *     of chunk k overlap those of chunks k-1 and k+1, all issued from C.
- *
- * Both use PipeBuf: one stream, its events, and the pinned and device
- * buffers of one batch in flight.
+ *     in chunks through PIPE_BUFS stream-private buffer sets: the upload of
+ *     chunk k+1, the kernels of chunk k and the download of chunk k-1
+ *     overlap, all issued from C; slot offsets are computed on the device.
  */
 #include <hip/hip_runtime.h>
 
@@ -42,135 +41,187 @@ namespace {
 
 using Clock = std::chrono::steady_clock;
 
-/* The slot of message i in a batch whose JSON prefix ends at byte e before
- * it: slot_off(e, i) = (4 e + 80 i) & ~7. Slot i is then at least
- * 4 len + 73 >= dg_slot_bound(len) bytes and 8-aligned, and a caller can
- * compute its slot's end from its own reservation alone. */
-static inline uint64_t slot_off(uint64_t e, uint64_t i) { return (4 * e + 80 * i) & ~7ull; }
+/* The slot of message i of a batch whose JSON before it ends at byte e:
+ * slot_off(e, i) = (4 e + 80 i) & ~7. Slot i is then at least
+ * 4 len + 73 >= dg_slot_bound(len) bytes and 8-aligned, and its offset
+ * follows from (start, index) alone. */
+__host__ __device__ inline uint64_t slot_off(uint64_t e, uint64_t i) { return (4 * e + 80 * i) & ~7ull; }
 
-/* one batch in flight: a stream, two events, pinned and device buffers.
- * Upload layout: [in_off (cap_n+1) | out_off (cap_n+1) | JSON (cap_b + 64)];
- * download layout: [ret n | pack_off (n+1) | packed], n = the batch's count */
-struct PipeBuf {
-    int device = 0;
-    hipStream_t s = nullptr;
-    hipEvent_t ev_hdr = nullptr, ev_done = nullptr;
-    uint64_t cap_n = 0, cap_b = 0;
-    uint8_t *h_up = nullptr; uint64_t h_up_cap = 0;
-    uint8_t *h_down = nullptr; uint64_t h_down_cap = 0;
-    uint8_t *d_up = nullptr; uint64_t d_up_cap = 0;
-    uint8_t *d_out = nullptr; uint64_t d_out_cap = 0;
-    uint8_t *d_down = nullptr; uint64_t d_down_cap = 0;
-    uint32_t *d_ol = nullptr; uint64_t d_ol_cap = 0;
+/* ---------------- device: offsets of a batch ---------------- */
 
-    uint64_t up_bytes(uint64_t n, uint64_t b) const { return 16 * (n + 1) + b + 64 + 16; }
-    uint64_t *in_off() { return (uint64_t *)(void *)h_up; }
-    uint64_t *out_off() { return (uint64_t *)(void *)h_up + cap_n + 1; }
-    uint8_t *json() { return h_up + 16 * (cap_n + 1); }
-    uint64_t slot_bytes(uint64_t n, uint64_t b) const { return slot_off(b, n) + 64; }
-    static uint64_t down_head(uint64_t n) { return 16 * n + 8; }
+/* one sub-batch of an aggregator batch: its messages are global indices
+ * [gbase, gbase + n), its JSON bytes [jbase, jbase + bytes) */
+struct SubRef {
+    uint64_t gbase, jbase, n;
+};
 
-    int init(int dev, uint64_t n, uint64_t b)
+/* in_off/out_off of an aggregator batch from its sub-batches' message ends
+ * (loc[i] = end of global message i within its sub-batch's JSON) */
+__global__ __launch_bounds__(256) void agg_offsets_kernel(const SubRef *tab, uint32_t nsub, const uint64_t *loc,
+                                                          uint64_t N, uint64_t *in_off, uint64_t *out_off)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= N) return;
+    uint32_t lo = 0, hi = nsub; /* the last sub-batch with gbase <= i */
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) / 2;
+        if (tab[mid].gbase <= i) lo = mid;
+        else hi = mid;
+    }
+    const SubRef s = tab[lo];
+    const uint64_t start = i == s.gbase ? s.jbase : s.jbase + loc[i - 1];
+    in_off[i] = start;
+    out_off[i] = slot_off(start, i);
+    if (i + 1 == N) {
+        const uint64_t end = s.jbase + loc[i];
+        in_off[N] = end;
+        out_off[N] = slot_off(end, N);
+    }
+}
+
+/* out_off of a chunk [a, a + m) of a host batch, from its raw offsets, and
+ * the 64 zero bytes after its JSON */
+__global__ __launch_bounds__(256) void pipe_slots_kernel(const uint64_t *in_off, uint64_t m, uint64_t *out_off,
+                                                         uint8_t *pad)
+{
+    const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j <= m) out_off[j] = slot_off(in_off[j] - in_off[0], j);
+    if (blockIdx.x == 0 && threadIdx.x < 8) ((uint64_t *)(void *)pad)[threadIdx.x] = 0;
+}
+
+/* A chunk's results into pinned host memory, after the previous chunk's:
+ * base = *base_ptr (0 for the first chunk) is where its bytes start in dst.
+ * The packing laid them out with dst's 16-byte phase at base (src_off[0] =
+ * phase), so the copy is whole aligned 16-byte stores except at both ends,
+ * where bytes of neighbouring chunks share a word (byte stores). Also
+ * dst_off[i] = absolute offsets (dst_off[n] = the next chunk's base) and the
+ * status words; nothing is written at or past dst_cap. */
+__global__ __launch_bounds__(256) void pipe_copy_out_kernel(const uint8_t *src, const uint64_t *src_off, uint64_t n,
+                                                            const uint64_t *ret_src, uint8_t *dst, uint64_t *dst_off,
+                                                            uint64_t *ret_dst, const uint64_t *base_ptr,
+                                                            uint64_t dst_cap)
+{
+    const uint64_t base = base_ptr ? *(volatile const uint64_t *)base_ptr : 0;
+    const uint64_t ph = ((uintptr_t)dst + base) & 15, wb = base - ph; /* src[x] -> dst[wb + x] */
+    const uint64_t tid = (uint64_t)blockIdx.x * 256 + threadIdx.x, nth = (uint64_t)gridDim.x * 256;
+    for (uint64_t i = tid; i <= n; i += nth) {
+        dst_off[i] = wb + src_off[i];
+        if (i < n) ret_dst[i] = ret_src[i];
+    }
+    const uint64_t end = src_off[n];
+    const uint64_t lim = dst_cap > wb ? dst_cap - wb : 0; /* local bytes below dst_cap */
+    const uint64_t stop = end < lim ? end : lim;
+    for (uint64_t w = tid; w * 16 < stop; w += nth) {
+        const uint64_t lo = w * 16, hi = lo + 16;
+        const uint64_t a = lo < ph ? ph : lo, b = hi < stop ? hi : stop;
+        if (a == lo && b == hi) {
+            *(uint4 *)(void *)(dst + wb + lo) = *(const uint4 *)(const void *)(src + lo);
+        } else {
+            for (uint64_t x = a; x < b; x++) dst[wb + x] = src[x];
+        }
+    }
+}
+
+/* device buffers of one batch in flight, grown on demand while idle:
+ * [in_off | out_off] offsets, JSON, slots, out_len, ret */
+struct DevBuf {
+    uint64_t *d_off = nullptr; uint64_t off_cap = 0;   /* in_off (n+1) | out_off (n+1) */
+    uint8_t *d_json = nullptr; uint64_t json_cap = 0;
+    uint8_t *d_out = nullptr; uint64_t out_cap = 0;
+    uint32_t *d_ol = nullptr; uint64_t ol_cap = 0;
+    uint64_t *d_ret = nullptr; uint64_t ret_cap = 0;
+
+    bool fits(uint64_t n, uint64_t b) const
     {
-        device = dev;
-        cap_n = n;
-        cap_b = b;
-        HIPCHK(hipSetDevice(dev));
-        HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-        HIPCHK(hipEventCreateWithFlags(&ev_hdr, hipEventDisableTiming));
-        HIPCHK(hipEventCreateWithFlags(&ev_done, hipEventDisableTiming));
+        return off_cap >= 2 * (n + 1) && json_cap >= b + 64 + 16 && out_cap >= slot_off(b, n) + 64 &&
+               ol_cap >= n + 1 && ret_cap >= n + 1;
+    }
+    /* callers make sure no launch still uses the buffers when they grow */
+    int reserve(uint64_t n, uint64_t b)
+    {
         int rc;
-        if ((rc = grow_pinned(h_up, h_up_cap, up_bytes(n, b)))) return rc;
-        if ((rc = grow_pinned(h_down, h_down_cap, down_head(n) + b + 64))) return rc;
-        if ((rc = grow(d_up, d_up_cap, up_bytes(n, b)))) return rc;
-        if ((rc = grow(d_out, d_out_cap, slot_bytes(n, b)))) return rc;
-        if ((rc = grow(d_down, d_down_cap, down_head(n) + slot_bytes(n, b)))) return rc;
-        if ((rc = grow(d_ol, d_ol_cap, n + 1))) return rc;
-        in_off()[0] = 0;
-        out_off()[0] = 0;
+        if ((rc = grow(d_off, off_cap, 2 * (n + 1)))) return rc;
+        if ((rc = grow(d_json, json_cap, b + 64 + 16))) return rc;
+        if ((rc = grow(d_out, out_cap, slot_off(b, n) + 64))) return rc;
+        if ((rc = grow(d_ol, ol_cap, n + 1))) return rc;
+        if ((rc = grow(d_ret, ret_cap, n + 1))) return rc;
         return DG_OK;
     }
     void release()
     {
-        if (s) (void)hipStreamSynchronize(s);
-        (void)hipHostFree(h_up);
-        (void)hipHostFree(h_down);
-        (void)hipFree(d_up);
+        (void)hipFree(d_off);
+        (void)hipFree(d_json);
         (void)hipFree(d_out);
-        (void)hipFree(d_down);
         (void)hipFree(d_ol);
-        if (ev_hdr) (void)hipEventDestroy(ev_hdr);
-        if (ev_done) (void)hipEventDestroy(ev_done);
-        if (s) (void)hipStreamDestroy(s);
-        s = nullptr;
+        (void)hipFree(d_ret);
+        d_off = d_ret = nullptr;
+        d_json = d_out = nullptr;
+        d_ol = nullptr;
+        off_cap = json_cap = out_cap = ol_cap = ret_cap = 0;
     }
-
-    /* H2D of n messages (b JSON bytes, in h_up or at hjson), convert +
-     * pack, D2H of [ret | pack_off]; ev_hdr follows. Device JSON pointer is
-     * d_up + 16 (cap_n + 1), 16-aligned, with 64 zero bytes after the end. */
-    int enqueue(dg_ctx *c, const dg_desc *d, uint32_t root, uint64_t flags, uint64_t n, uint64_t b, uint64_t max_len,
-                const uint8_t *hjson = nullptr)
+    /* convert + pack n messages whose offsets are at in_off / out_off, JSON
+     * at json. The packing writes straight into pinned host memory: bytes at
+     * h_dst + h_dst_off[i] (positions from *base_in when chained, nothing
+     * past dst_cap), after the event pack_after if set; then ret is
+     * downloaded to h_ret and ev recorded. */
+    int convert(dg_ctx *c, const dg_desc *d, uint32_t root, uint64_t flags, uint64_t n, const uint8_t *json,
+                const uint64_t *in_off, const uint64_t *out_off, uint64_t max_len, hipStream_t s, uint64_t *h_ret,
+                uint8_t *h_dst, uint64_t *h_dst_off, const uint64_t *base_in, uint64_t dst_cap, hipEvent_t pack_after,
+                hipEvent_t ev)
     {
-        HIPCHK(hipSetDevice(device));
-        const uint64_t jo = 16 * (cap_n + 1);
-        HIPCHK(hipMemcpyAsync(d_up, h_up, 8 * (n + 1), hipMemcpyHostToDevice, s));
-        HIPCHK(hipMemcpyAsync(d_up + 8 * (cap_n + 1), h_up + 8 * (cap_n + 1), 8 * (n + 1), hipMemcpyHostToDevice, s));
-        if (hjson) {
-            if (b) HIPCHK(hipMemcpyAsync(d_up + jo, hjson, b, hipMemcpyHostToDevice, s));
-            HIPCHK(hipMemsetAsync(d_up + jo + b, 0, 64, s));
-        } else {
-            HIPCHK(hipMemcpyAsync(d_up + jo, h_up + jo, b + 64, hipMemcpyHostToDevice, s));
-        }
-        uint64_t *d_ret = (uint64_t *)(void *)d_down, *d_po = d_ret + n;
-        int rc = dg_i_convert_pack(c, d, root, d_up + jo, (const uint64_t *)(void *)d_up, n, flags, d_out,
-                                   (const uint64_t *)(void *)(d_up + 8 * (cap_n + 1)), d_ol, d_ret,
-                                   d_down + down_head(n), d_po, s, max_len);
+        int rc = dg_i_convert_pack(c, d, root, json, in_off, n, flags, d_out, out_off, d_ol, d_ret, h_dst, h_dst_off,
+                                   s, max_len, base_in, dst_cap, pack_after);
         if (rc) return rc;
-        HIPCHK(hipMemcpyAsync(h_down, d_down, down_head(n), hipMemcpyDeviceToHost, s));
-        HIPCHK(hipEventRecord(ev_hdr, s));
+        HIPCHK(hipMemcpyAsync(h_ret, d_ret, 8 * n, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipEventRecord(ev, s));
         return DG_OK;
     }
-    /* after ev_hdr: D2H of the packed bytes to dst (pinned), ev_done follows */
-    int download(uint64_t n, uint8_t *dst)
-    {
-        HIPCHK(hipSetDevice(device));
-        const uint64_t total = ((const uint64_t *)(const void *)h_down)[2 * n];
-        if (total) HIPCHK(hipMemcpyAsync(dst, d_down + down_head(n), total, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipEventRecord(ev_done, s));
-        return DG_OK;
-    }
-    const uint64_t *ret() const { return (const uint64_t *)(const void *)h_down; }
-    const uint64_t *pack_off(uint64_t n) const { return ret() + n; }
 };
 
-constexpr uint64_t SEALED = 1ull << 63;
-constexpr int CNT_SHIFT = 40;
-constexpr uint64_t CNT_MASK = (1ull << 23) - 1;
-constexpr uint64_t BYTE_MASK = (1ull << CNT_SHIFT) - 1;
-constexpr int AGG_INFLIGHT = 4;
+/* ---------------- the aggregator ---------------- */
 
-/* one aggregator batch: lives in a ring of AGG_INFLIGHT, reused when its
- * last caller has copied its result out */
+constexpr int AGG_INFLIGHT = 4;
+constexpr int AGG_SLOTS = 256; /* caller threads per aggregator (more convert alone, dg_j2t_do) */
+
+/* one caller thread's part of one batch (its own cache lines) */
+struct alignas(128) Sub {
+    std::atomic<uint32_t> busy{0}; /* 1 while the owner writes a message (the seal handshake) */
+    std::atomic<uint32_t> n{0};    /* messages committed */
+    uint64_t bytes = 0;            /* JSON bytes committed (owner-written) */
+    uint8_t *h = nullptr;          /* pinned: [ends (cap_n u64) | JSON (cap_b + 64)] */
+    uint64_t gbase = 0;            /* set at the seal: its first global index */
+    std::atomic<uint32_t> left{0}; /* results not yet taken */
+    uint64_t *ends() const { return (uint64_t *)(void *)h; }
+};
+
 struct Batch {
-    PipeBuf pb;
-    /* SEALED | count << 40 | bytes: one fetch_add reserves (index, offset) */
-    std::atomic<uint64_t> state{0};
-    /* per reserved index: 0 pending, 1 filled, 2 failed (did not fit) */
-    std::atomic<uint8_t> *status = nullptr;
-    std::atomic<uint64_t> gen{0};        /* generation number of the current fill */
-    std::atomic<int64_t> t_first{0};     /* ns timestamp of reservation 0 */
-    std::atomic<int64_t> k_seal{-1};     /* reservations made before the seal (-1: not sealed yet) */
-    uint32_t k_prev = 0;                 /* k_seal of the previous generation (status entries to clear) */
-    uint32_t n = 0;                      /* messages in the sealed batch */
-    uint64_t bytes = 0;
-    std::atomic<uint32_t> consumed{0};
+    Sub sub[AGG_SLOTS];
+    std::atomic<uint64_t> t_first{0}; /* ns timestamp of its first message (0: none yet) */
+    std::atomic<uint32_t> seal_req{0};
+    std::atomic<uint32_t> parts{0};   /* threads with a message in it (while open) */
+    std::atomic<uint32_t> blocked{0}; /* ... of which wait on it (while open) */
+    std::atomic<uint32_t> active{0};  /* non-empty sub-batches whose results are not all taken */
+    uint64_t g = 0;                   /* generation it holds while open / in flight */
+    uint64_t t_launched = 0;
+    uint64_t n = 0, bytes = 0;
     int rc = DG_OK;
-    uint8_t *h_packed = nullptr; uint64_t h_packed_cap = 0;
+    hipStream_t s = nullptr;
+    hipEvent_t ev_hdr = nullptr, ev_done = nullptr;
+    DevBuf dv;
+    uint8_t *h_hdr = nullptr; uint64_t h_hdr_cap = 0;       /* pinned [ret | pack_off] */
+    uint8_t *h_packed = nullptr; uint64_t h_packed_cap = 0; /* pinned packed Thrift */
+    SubRef *h_tab = nullptr;                                /* pinned sub-batch table */
+    SubRef *d_tab = nullptr;
+    uint64_t *d_loc = nullptr; uint64_t loc_cap = 0;        /* message ends, by global index */
+    std::atomic<uint64_t> done_g{0};  /* last generation whose results are readable */
     std::mutex mu;
     std::condition_variable cv;
-    uint64_t done_gen = 0;               /* under mu: last generation whose results are readable */
-    bool free_ = true;                   /* under the aggregator's mu: every caller is done with it */
+    bool free_ = true;                /* under the aggregator's mu */
+    const uint64_t *ret() const { return (const uint64_t *)(const void *)h_hdr; }
+    const uint64_t *pack_off() const { return ret() + n; }
 };
+
+std::atomic<uint64_t> g_agg_ids{1};
 
 }  // namespace
 
@@ -179,154 +230,200 @@ struct dg_agg {
     const dg_desc *desc;
     uint32_t root;
     uint64_t flags;
-    uint32_t max_batch;
-    uint64_t max_bytes;
+    uint32_t cap_n;   /* per caller thread per batch */
+    uint64_t cap_b;
     std::chrono::nanoseconds max_wait;
-    Batch b[AGG_INFLIGHT];
-    std::atomic<Batch *> cur{nullptr};
-    uint32_t cur_i = 0;
-    std::mutex mu;                       /* cur changes, seal notices, frees, completer queue */
-    std::condition_variable cv_flush;    /* flusher: a seal, a first reservation, a free batch, stop */
-    std::condition_variable cv_cur;      /* callers: cur moved on */
-    std::condition_variable cv_done;     /* completer: a batch in flight */
+    uint64_t id;
+    Batch *b = nullptr;
+    std::atomic<uint64_t> open{0};   /* the open generation; batch b[open % AGG_INFLIGHT] */
+    std::atomic<int> nslots{0};
+    std::atomic<uint8_t> ready[AGG_SLOTS];
+    std::mutex mu;                   /* open changes, frees, flusher wakeups, completer queue */
+    std::condition_variable cv_flush, cv_open, cv_done;
     std::deque<Batch *> inflight;
     bool stop = false;
     std::atomic<uint64_t> batches{0}, msgs{0};
+    /* where the time goes (ns, summed; dg_agg_profile): 0 flusher waiting for
+     * a seal, 1 waiting for a free batch, 2 in launch (uploads + kernel
+     * issue), 3 completer waiting for the header, 4 for the packed bytes,
+     * 5 seal-to-launched, 6 launched-to-done */
+    std::atomic<uint64_t> prof[8] = {};
     std::thread flusher, completer;
 
-    static int64_t now_ns() { return std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now().time_since_epoch()).count(); }
-
-    void seal(Batch *x)
+    static uint64_t now_ns()
     {
-        const uint64_t prev = x->state.fetch_or(SEALED, std::memory_order_acq_rel);
-        if (prev & SEALED) return;
-        {
-            std::lock_guard<std::mutex> g(mu);
-            x->k_seal.store((int64_t)std::min<uint64_t>((prev >> CNT_SHIFT) & CNT_MASK, max_batch),
-                            std::memory_order_release);
-        }
+        return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now().time_since_epoch()).count();
+    }
+    int slot();
+    void wake_flusher()
+    {
+        { std::lock_guard<std::mutex> g(mu); }
         cv_flush.notify_one();
     }
-    /* reserve a place for len bytes: true with (batch, gen, idx, off), or
-     * false when the batch closed first (the caller waits for the next) */
-    bool reserve(Batch *x, uint64_t len, uint64_t &gen, uint32_t &idx, uint64_t &off)
-    {
-        const uint64_t old = x->state.fetch_add((1ull << CNT_SHIFT) | len, std::memory_order_acq_rel);
-        if (old & SEALED) return false;
-        const uint64_t i = (old >> CNT_SHIFT) & CNT_MASK;
-        off = old & BYTE_MASK;
-        if (i < max_batch && off + len <= max_bytes) {
-            idx = (uint32_t)i;
-            gen = x->gen.load(std::memory_order_acquire);
-            if (i == 0) {
-                x->t_first.store(now_ns(), std::memory_order_release);
-                {
-                    std::lock_guard<std::mutex> g(mu); /* the flusher checks t_first under mu */
-                }
-                cv_flush.notify_one();
-            }
-            return true;
-        }
-        if (i < max_batch) x->status[i].store(2, std::memory_order_release);
-        seal(x);
-        return false;
-    }
-    void fill(Batch *x, uint32_t idx, uint64_t off, const uint8_t *json, uint64_t len)
-    {
-        PipeBuf &p = x->pb;
-        if (len) memcpy(p.json() + off, json, len);
-        p.in_off()[idx + 1] = off + len;
-        p.out_off()[idx + 1] = slot_off(off + len, idx + 1);
-        x->status[idx].store(1, std::memory_order_release);
-        if (idx + 1 == max_batch) seal(x);
-    }
-
     void run_flusher();
     void run_completer();
-    void launch_batch(Batch *x);
+    int launch(Batch *x);
 };
 
-void dg_agg::launch_batch(Batch *x)
+/* this thread's slot (sub-batch index), registered on first use: its
+ * pinned regions in every batch of the ring; -1 when all are taken */
+int dg_agg::slot()
 {
-    /* the callers that reserved before the seal are each filling or failing:
-     * wait for every one of them (a failed one writes its status too), so
-     * no caller touches this batch's staging once it is recycled */
-    const uint32_t k = (uint32_t)x->k_seal.load(std::memory_order_acquire);
-    x->k_prev = k;
-    uint32_t n = k;
-    for (uint32_t i = 0; i < k; i++) {
-        uint8_t st;
-        while ((st = x->status[i].load(std::memory_order_acquire)) == 0) std::this_thread::yield();
-        if (st == 2 && i < n) n = i;
+    struct TL {
+        uint64_t id;
+        int slot;
+    };
+    thread_local TL tl[8] = {};
+    thread_local int tl_next = 0;
+    for (const TL &e : tl)
+        if (e.id == id) return e.slot;
+    int s = nslots.fetch_add(1, std::memory_order_seq_cst);
+    if (s >= AGG_SLOTS) {
+        nslots.fetch_sub(1);
+        s = -1;
+    } else {
+        bool ok = true;
+        (void)hipSetDevice(ctx->device);
+        for (int k = 0; k < AGG_INFLIGHT && ok; k++) {
+            uint64_t cap = 0;
+            uint8_t *h = nullptr;
+            ok = grow_pinned(h, cap, 8 * cap_n + cap_b + 64) == DG_OK;
+            b[k].sub[s].h = h;
+        }
+        ready[s].store(ok ? 1 : 2, std::memory_order_release);
+        if (!ok) s = -1;
     }
-    x->n = n;
+    tl[tl_next] = TL{id, s};
+    tl_next = (tl_next + 1) % 8;
+    return s;
+}
+
+int dg_agg::launch(Batch *x)
+{
+    /* the sub-batches: every registered slot, once its owner is not in the
+     * middle of a message (it saw the old generation open before the flip) */
+    const int ns = nslots.load(std::memory_order_seq_cst);
+    uint32_t nsub = 0;
+    uint64_t N = 0, B = 0;
+    for (int s = 0; s < ns; s++) {
+        Sub &u = x->sub[s];
+        while (u.busy.load(std::memory_order_seq_cst)) std::this_thread::yield();
+        const uint32_t k = u.n.load(std::memory_order_acquire);
+        u.left.store(k, std::memory_order_relaxed);
+        if (!k) continue;
+        u.gbase = N;
+        x->h_tab[nsub++] = SubRef{N, B, k};
+        N += k;
+        B += u.bytes;
+    }
+    x->n = N;
+    x->bytes = B;
     x->rc = DG_OK;
-    PipeBuf &p = x->pb;
+    x->active.store(nsub, std::memory_order_release);
+    if (!N) return DG_OK;
+    HIPCHK(hipSetDevice(ctx->device));
+    int rc;
+    if ((rc = x->dv.reserve(N, B))) return rc;
+    if ((rc = grow(x->d_loc, x->loc_cap, N + 1))) return rc;
+    if ((rc = grow_pinned(x->h_hdr, x->h_hdr_cap, 16 * N + 8))) return rc;
+    if ((rc = grow_pinned(x->h_packed, x->h_packed_cap, slot_off(B, N) + 64))) return rc; /* >= any packed size */
+    /* uploads: each sub-batch's JSON and message ends, then the table */
     uint64_t max_len = 1;
-    const uint64_t *io = p.in_off();
-    for (uint32_t i = 0; i < n; i++) max_len = std::max<uint64_t>(max_len, io[i + 1] - io[i]);
-    x->bytes = io[n];
-    memset(p.json() + x->bytes, 0, 64);
-    if (n) x->rc = p.enqueue(ctx, desc, root, flags, n, x->bytes, max_len);
-    batches.fetch_add(n ? 1 : 0, std::memory_order_relaxed);
-    msgs.fetch_add(n, std::memory_order_relaxed);
-    {
-        std::lock_guard<std::mutex> g(mu);
-        inflight.push_back(x);
+    for (uint32_t t = 0, s = 0; t < nsub; s++) {
+        Sub &u = x->sub[s];
+        const uint32_t k = u.n.load(std::memory_order_relaxed);
+        if (!k) continue;
+        const SubRef &r = x->h_tab[t++];
+        const uint64_t *e = u.ends();
+        uint64_t prev = 0;
+        for (uint32_t j = 0; j < k; j++) {
+            max_len = std::max<uint64_t>(max_len, e[j] - prev);
+            prev = e[j];
+        }
+        HIPCHK(hipMemcpyAsync(x->dv.d_json + r.jbase, u.h + 8 * cap_n, u.bytes, hipMemcpyHostToDevice, x->s));
+        HIPCHK(hipMemcpyAsync(x->d_loc + r.gbase, u.h, 8 * k, hipMemcpyHostToDevice, x->s));
     }
-    cv_done.notify_one();
+    HIPCHK(hipMemsetAsync(x->dv.d_json + B, 0, 64, x->s));
+    HIPCHK(hipMemcpyAsync(x->d_tab, x->h_tab, sizeof(SubRef) * nsub, hipMemcpyHostToDevice, x->s));
+    uint64_t *d_in = x->dv.d_off, *d_oo = d_in + N + 1;
+    hipLaunchKernelGGL(agg_offsets_kernel, dim3((uint32_t)((N + 255) / 256)), dim3(256), 0, x->s, x->d_tab, nsub,
+                       x->d_loc, N, d_in, d_oo);
+    HIPCHK(hipGetLastError());
+    uint64_t *h_ret = (uint64_t *)(void *)x->h_hdr;
+    return x->dv.convert(ctx, desc, root, flags, N, x->dv.d_json, d_in, d_oo, max_len, x->s, h_ret, x->h_packed,
+                         h_ret + N, nullptr, 0, nullptr, x->ev_hdr);
 }
 
 void dg_agg::run_flusher()
 {
     for (;;) {
-        Batch *x = cur.load(std::memory_order_acquire);
+        const uint64_t g = open.load(std::memory_order_acquire);
+        Batch *x = &b[g % AGG_INFLIGHT];
+        uint64_t t0 = now_ns();
         {
-            std::unique_lock<std::mutex> g(mu);
+            /* until a caller asks for the seal (its sub-batch is full), the
+             * first message has waited max_wait, or stop */
+            std::unique_lock<std::mutex> lk(mu);
             for (;;) {
-                /* sealed: by a caller that did not fit, by the caller that
-                 * took the last index, or below on the deadline / at stop */
-                if (x->k_seal.load(std::memory_order_acquire) >= 0) break;
-                const uint64_t st = x->state.load(std::memory_order_acquire);
-                const bool any = ((st >> CNT_SHIFT) & CNT_MASK) != 0;
-                if (stop && !any) {
-                    inflight.push_back(nullptr); /* the completer's exit marker */
-                    g.unlock();
-                    cv_done.notify_one();
-                    return;
+                if (x->seal_req.load(std::memory_order_acquire)) break;
+                const uint64_t t0 = x->t_first.load(std::memory_order_acquire);
+                if (stop) {
+                    if (!t0) {
+                        inflight.push_back(nullptr); /* the completer's exit marker */
+                        lk.unlock();
+                        cv_done.notify_one();
+                        return;
+                    }
+                    break;
                 }
-                const int64_t t0 = x->t_first.load(std::memory_order_acquire);
-                if (stop || (t0 && now_ns() - t0 >= max_wait.count())) {
-                    g.unlock();
-                    seal(x);
-                    g.lock();
-                    continue;
+                if (t0) {
+                    const uint64_t now = now_ns();
+                    if (now - t0 >= (uint64_t)max_wait.count()) break;
+                    cv_flush.wait_for(lk, std::chrono::nanoseconds(max_wait.count() - (int64_t)(now - t0)));
+                } else {
+                    cv_flush.wait_for(lk, std::chrono::milliseconds(20));
                 }
-                if (t0) cv_flush.wait_for(g, std::chrono::nanoseconds(max_wait.count() - (now_ns() - t0)));
-                else cv_flush.wait_for(g, std::chrono::milliseconds(5));
             }
         }
-        launch_batch(x);
-        /* the next batch of the ring, once its last caller has copied out */
-        const uint32_t ni = (cur_i + 1) % AGG_INFLIGHT;
-        Batch *y = &b[ni];
+        /* the next batch of the ring, once its callers have taken their results */
+        Batch *y = &b[(g + 1) % AGG_INFLIGHT];
+        uint64_t t1 = now_ns();
+        prof[0].fetch_add(t1 - t0, std::memory_order_relaxed);
         {
-            std::unique_lock<std::mutex> g(mu);
-            cv_flush.wait(g, [&] { return y->free_; });
+            std::unique_lock<std::mutex> lk(mu);
+            cv_flush.wait(lk, [&] { return y->free_; });
             y->free_ = false;
         }
-        y->gen.fetch_add(1, std::memory_order_acq_rel);
-        y->t_first.store(0, std::memory_order_relaxed);
-        y->consumed.store(0, std::memory_order_relaxed);
-        for (uint32_t i = 0; i < y->k_prev; i++) y->status[i].store(0, std::memory_order_relaxed);
-        y->k_seal.store(-1, std::memory_order_relaxed);
-        y->state.store(0, std::memory_order_release);
-        {
-            std::lock_guard<std::mutex> g(mu);
-            cur.store(y, std::memory_order_release);
-            cur_i = ni;
+        const int ns = nslots.load(std::memory_order_acquire);
+        for (int s = 0; s < ns; s++) {
+            y->sub[s].n.store(0, std::memory_order_relaxed);
+            y->sub[s].bytes = 0;
         }
-        cv_cur.notify_all();
+        y->t_first.store(0, std::memory_order_relaxed);
+        y->seal_req.store(0, std::memory_order_relaxed);
+        y->parts.store(0, std::memory_order_relaxed);
+        y->blocked.store(0, std::memory_order_relaxed);
+        y->g = g + 1;
+        /* the flip: callers that still see g finish their message first
+         * (launch() waits for their busy flags) */
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            open.store(g + 1, std::memory_order_seq_cst);
+        }
+        cv_open.notify_all();
+        uint64_t t2 = now_ns();
+        prof[1].fetch_add(t2 - t1, std::memory_order_relaxed);
+        x->rc = launch(x);
+        x->t_launched = now_ns();
+        prof[2].fetch_add(x->t_launched - t2, std::memory_order_relaxed);
+        prof[5].fetch_add(x->t_launched - t1, std::memory_order_relaxed);
+        batches.fetch_add(x->n ? 1 : 0, std::memory_order_relaxed);
+        msgs.fetch_add(x->n, std::memory_order_relaxed);
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            inflight.push_back(x);
+        }
+        cv_done.notify_one();
     }
 }
 
@@ -335,39 +432,77 @@ void dg_agg::run_completer()
     for (;;) {
         Batch *x;
         {
-            std::unique_lock<std::mutex> g(mu);
-            cv_done.wait(g, [&] { return !inflight.empty(); });
+            std::unique_lock<std::mutex> lk(mu);
+            cv_done.wait(lk, [&] { return !inflight.empty(); });
             x = inflight.front();
             inflight.pop_front();
         }
         if (!x) return;
-        PipeBuf &p = x->pb;
+        const uint64_t c0 = now_ns();
+        uint64_t c1 = c0;
         if (x->n && x->rc == DG_OK) {
-            hipError_t e = hipEventSynchronize(p.ev_hdr);
+            /* the packing wrote the bytes and offsets into pinned host
+             * memory; ret followed them */
+            hipError_t e = hipEventSynchronize(x->ev_hdr);
+            c1 = now_ns();
             if (e != hipSuccess) x->rc = set_err(DG_E_HIP, "aggregator batch: %s", hipGetErrorString(e));
         }
-        if (x->n && x->rc == DG_OK) {
-            const uint64_t total = p.pack_off(x->n)[x->n];
-            x->rc = grow_pinned(x->h_packed, x->h_packed_cap, total + 64);
-            if (x->rc == DG_OK) x->rc = p.download(x->n, x->h_packed);
-            if (x->rc == DG_OK) {
-                hipError_t e = hipEventSynchronize(p.ev_done);
-                if (e != hipSuccess) x->rc = set_err(DG_E_HIP, "aggregator download: %s", hipGetErrorString(e));
-            }
-        }
+        /* an empty batch has no caller to free it; a non-empty one is freed
+         * by the caller that takes its last result (x may be reused as soon
+         * as that happens: decide before publishing) */
         const bool empty = x->n == 0;
+        const uint64_t c2 = now_ns();
+        prof[3].fetch_add(c1 - c0, std::memory_order_relaxed);
+        prof[4].fetch_add(c2 - c1, std::memory_order_relaxed);
+        prof[6].fetch_add(c2 - x->t_launched, std::memory_order_relaxed);
         {
-            std::lock_guard<std::mutex> g(x->mu);
-            x->done_gen = x->gen.load(std::memory_order_acquire);
+            std::lock_guard<std::mutex> lk(x->mu);
+            x->done_g.store(x->g, std::memory_order_release);
         }
         x->cv.notify_all();
         if (empty) {
-            std::lock_guard<std::mutex> g(mu);
+            std::lock_guard<std::mutex> lk(mu);
             x->free_ = true;
             cv_flush.notify_one();
         }
     }
 }
+
+/* ---------------- the pipelined host batch ---------------- */
+
+namespace {
+
+constexpr int PIPE_BUFS = 3;
+
+/* one chunk in flight: a stream, events, device buffers, pinned header */
+struct PipeBuf {
+    hipStream_t s = nullptr;
+    hipEvent_t ev_hdr = nullptr, ev_done = nullptr;
+    DevBuf dv;
+    uint8_t *d_packed = nullptr; uint64_t packed_cap = 0; /* [pack_off (n+1) | packed (16-aligned)] */
+    int init(int dev)
+    {
+        HIPCHK(hipSetDevice(dev));
+        HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&ev_hdr, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&ev_done, hipEventDisableTiming));
+        return DG_OK;
+    }
+    void release()
+    {
+        if (s) (void)hipStreamSynchronize(s);
+        dv.release();
+        (void)hipFree(d_packed);
+        d_packed = nullptr;
+        packed_cap = 0;
+        if (ev_hdr) (void)hipEventDestroy(ev_hdr);
+        if (ev_done) (void)hipEventDestroy(ev_done);
+        if (s) (void)hipStreamDestroy(s);
+        s = nullptr;
+    }
+};
+
+}  // namespace
 
 void dg_i_pipe_free(dg_ctx *c)
 {
@@ -376,6 +511,10 @@ void dg_i_pipe_free(dg_ctx *c)
         delete (PipeBuf *)q;
     }
     c->pipe.clear();
+    (void)hipHostFree(c->h_pipe_out);
+    (void)hipHostFree(c->h_pipe_aux);
+    c->h_pipe_out = c->h_pipe_aux = nullptr;
+    c->h_pipe_out_cap = c->h_pipe_aux_cap = 0;
 }
 
 extern "C" {
@@ -383,35 +522,37 @@ extern "C" {
 int dg_agg_create2(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, uint64_t flags, uint32_t max_batch,
                    uint64_t max_bytes, uint32_t max_wait_us, dg_agg **out)
 {
-    if (!ctx || !desc || !out || max_batch == 0 || max_batch > CNT_MASK / 2 || max_bytes == 0 ||
-        max_bytes > (BYTE_MASK >> 2))
-        return set_err(DG_E_INVALID, "bad args");
+    if (!ctx || !desc || !out || max_batch == 0 || max_bytes == 0) return set_err(DG_E_INVALID, "bad args");
     dg_agg *a = new dg_agg();
     a->ctx = ctx;
     a->desc = desc;
     a->root = root_type;
     a->flags = flags;
-    a->max_batch = max_batch;
-    a->max_bytes = max_bytes;
+    a->cap_n = max_batch;
+    a->cap_b = max_bytes;
     a->max_wait = std::chrono::microseconds(max_wait_us);
-    for (Batch &x : a->b) {
-        x.status = new std::atomic<uint8_t>[max_batch];
-        for (uint32_t i = 0; i < max_batch; i++) x.status[i].store(0, std::memory_order_relaxed);
-        int rc = x.pb.init(ctx->device, max_batch, max_bytes);
-        if (rc == DG_OK) rc = grow_pinned(x.h_packed, x.h_packed_cap, max_bytes + 64);
-        if (rc) {
-            for (Batch &y : a->b) {
-                y.pb.release();
-                (void)hipHostFree(y.h_packed);
-                delete[] y.status;
-            }
-            delete a;
-            return rc;
-        }
+    a->id = g_agg_ids.fetch_add(1);
+    for (auto &r : a->ready) r.store(0, std::memory_order_relaxed);
+    a->b = new Batch[AGG_INFLIGHT];
+    int rc = DG_OK;
+    (void)hipSetDevice(ctx->device);
+    for (int k = 0; k < AGG_INFLIGHT && rc == DG_OK; k++) {
+        Batch &x = a->b[k];
+        hipError_t e = hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&x.ev_hdr, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&x.ev_done, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipHostMalloc((void **)&x.h_tab, sizeof(SubRef) * AGG_SLOTS, hipHostMallocDefault);
+        if (e == hipSuccess) e = hipMalloc(&x.d_tab, sizeof(SubRef) * AGG_SLOTS);
+        if (e != hipSuccess) rc = set_err(DG_E_HIP, "aggregator setup: %s", hipGetErrorString(e));
     }
-    a->b[0].free_ = false;
-    a->b[0].gen.store(1);
-    a->cur.store(&a->b[0]);
+    if (rc) {
+        dg_agg_destroy(a);
+        return rc;
+    }
+    /* generations start at 1: done_g == 0 means "nothing converted yet" */
+    a->open.store(1);
+    a->b[1].free_ = false;
+    a->b[1].g = 1;
     a->flusher = std::thread([a] { a->run_flusher(); });
     a->completer = std::thread([a] { a->run_completer(); });
     *out = a;
@@ -421,7 +562,7 @@ int dg_agg_create2(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, uint64_
 int dg_agg_create(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, uint64_t flags, uint32_t max_batch,
                   uint32_t max_wait_us, dg_agg **out)
 {
-    /* room for max_batch messages of 512 B on average (at least 1 MiB) */
+    /* JSON room for max_batch messages of 512 B on average (at least 1 MiB) per thread */
     const uint64_t mb = std::max<uint64_t>(1ull << 20, 512ull * max_batch);
     return dg_agg_create2(ctx, desc, root_type, flags, max_batch, mb, max_wait_us, out);
 }
@@ -432,26 +573,45 @@ int dg_agg_submit(dg_agg *a, const uint8_t *json, size_t len, int nonblock, dg_a
     static const uint8_t empty = 0;
     t->json = len ? json : &empty;
     t->len = len;
-    if (len > a->max_bytes) { /* never fits a batch: converted alone by dg_agg_wait */
-        t->batch = nullptr;
-        return DG_OK;
-    }
+    t->batch = nullptr;
+    const int s = len > a->cap_b ? -1 : a->slot();
+    if (s < 0) return DG_OK; /* converted alone by dg_agg_wait */
     for (;;) {
-        Batch *x = a->cur.load(std::memory_order_acquire);
-        uint64_t gen, off;
-        uint32_t idx;
-        if (a->reserve(x, len, gen, idx, off)) {
-            a->fill(x, idx, off, t->json, len);
-            t->batch = x;
-            t->gen = gen;
-            t->idx = idx;
-            return DG_OK;
+        const uint64_t g = a->open.load(std::memory_order_seq_cst);
+        Batch *x = &a->b[g % AGG_INFLIGHT];
+        Sub &u = x->sub[s];
+        u.busy.store(1, std::memory_order_seq_cst);
+        if (a->open.load(std::memory_order_seq_cst) == g) {
+            const uint32_t j = u.n.load(std::memory_order_relaxed);
+            if (j < a->cap_n && u.bytes + len <= a->cap_b) {
+                if (len) memcpy(u.h + 8 * a->cap_n + u.bytes, t->json, len);
+                u.bytes += len;
+                u.ends()[j] = u.bytes;
+                u.n.store(j + 1, std::memory_order_release);
+                u.busy.store(0, std::memory_order_release);
+                if (j == 0) {
+                    x->parts.fetch_add(1, std::memory_order_acq_rel);
+                    uint64_t z = 0;
+                    if (x->t_first.compare_exchange_strong(z, dg_agg::now_ns(), std::memory_order_acq_rel))
+                        a->wake_flusher();
+                }
+                t->batch = x;
+                t->gen = g;
+                t->idx = ((uint32_t)s << 24) | j; /* slot | index within its sub-batch */
+                return DG_OK;
+            }
+            /* this thread's part of the open batch is full: seal it */
+            u.busy.store(0, std::memory_order_release);
+            if (!x->seal_req.exchange(1, std::memory_order_acq_rel)) a->wake_flusher();
+        } else {
+            u.busy.store(0, std::memory_order_release);
+            continue; /* the batch closed meanwhile: the next one is open */
         }
-        std::unique_lock<std::mutex> g(a->mu);
+        std::unique_lock<std::mutex> lk(a->mu);
         if (a->stop) return set_err(DG_E_INVALID, "aggregator closed");
-        if (a->cur.load(std::memory_order_acquire) != x) continue;
+        if (a->open.load(std::memory_order_acquire) != g) continue;
         if (nonblock) return DG_E_AGAIN; /* the next batch is not free yet */
-        a->cv_cur.wait(g, [&] { return a->cur.load(std::memory_order_acquire) != x || a->stop; });
+        a->cv_open.wait(lk, [&] { return a->open.load(std::memory_order_acquire) != g || a->stop; });
     }
 }
 
@@ -462,26 +622,43 @@ int dg_agg_wait(dg_agg *a, dg_agg_ticket *t, uint8_t *out, size_t out_cap, size_
     bool redo = x == nullptr;
     int rc = DG_OK;
     if (x) {
-        {
-            std::unique_lock<std::mutex> g(x->mu);
-            x->cv.wait(g, [&] { return x->done_gen >= t->gen; });
+        /* waiting on the open batch: once every thread with a message in it
+         * waits on it, nothing more will come from them, so seal it now */
+        if (a->open.load(std::memory_order_acquire) == t->gen &&
+            x->blocked.fetch_add(1, std::memory_order_acq_rel) + 1 >= x->parts.load(std::memory_order_acquire) &&
+            !x->seal_req.exchange(1, std::memory_order_acq_rel))
+            a->wake_flusher();
+        if (x->done_g.load(std::memory_order_acquire) < t->gen) {
+            const uint64_t w0 = dg_agg::now_ns();
+            for (int spin = 0; x->done_g.load(std::memory_order_acquire) < t->gen; spin++) {
+                if (spin < 64) {
+                    std::this_thread::yield();
+                    continue;
+                }
+                std::unique_lock<std::mutex> lk(x->mu);
+                x->cv.wait(lk, [&] { return x->done_g.load(std::memory_order_acquire) >= t->gen; });
+            }
+            a->prof[7].fetch_add(dg_agg::now_ns() - w0, std::memory_order_relaxed);
         }
+        Sub &u = x->sub[t->idx >> 24];
         rc = x->rc;
         if (rc == DG_OK) {
-            const uint64_t r = x->pb.ret()[t->idx];
+            const uint64_t i = u.gbase + (t->idx & 0xFFFFFFu);
+            const uint64_t r = x->ret()[i];
             if ((uint8_t)r == DG_ST_OUT_OVERFLOW) {
                 redo = true; /* its slot was too small: alone, at its exact size */
             } else {
-                const uint64_t *po = x->pb.pack_off(x->n);
-                const uint64_t l = po[t->idx + 1] - po[t->idx];
+                const uint64_t *po = x->pack_off();
+                const uint64_t l = po[i + 1] - po[i];
                 *ret = r;
                 *out_len = l;
                 if (l > out_cap) rc = DG_E_NOMEM; /* the caller retries with out_len bytes */
-                else if (l) memcpy(out, x->h_packed + po[t->idx], l);
+                else if (l) memcpy(out, x->h_packed + po[i], l);
             }
         }
-        if (x->consumed.fetch_add(1, std::memory_order_acq_rel) + 1 == x->n) {
-            std::lock_guard<std::mutex> g(a->mu);
+        if (u.left.fetch_sub(1, std::memory_order_acq_rel) == 1 &&
+            x->active.fetch_sub(1, std::memory_order_acq_rel) == 1) {
+            std::lock_guard<std::mutex> lk(a->mu);
             x->free_ = true;
             a->cv_flush.notify_one();
         }
@@ -511,28 +688,67 @@ int dg_agg_stats(dg_agg *a, uint64_t *batches, uint64_t *msgs)
     return DG_OK;
 }
 
+int dg_agg_profile(dg_agg *a, uint64_t *out, int n)
+{
+    if (!a || !out || n < 0 || n > 8) return set_err(DG_E_INVALID, "bad args");
+    for (int i = 0; i < n; i++) out[i] = a->prof[i].load();
+    return DG_OK;
+}
+
 void dg_agg_destroy(dg_agg *a)
 {
     if (!a) return;
-    {
-        std::lock_guard<std::mutex> g(a->mu);
-        a->stop = true;
+    if (a->flusher.joinable()) {
+        {
+            std::lock_guard<std::mutex> lk(a->mu);
+            a->stop = true;
+        }
+        a->cv_flush.notify_all();
+        a->cv_open.notify_all();
+        a->flusher.join(); /* converts what is in the open batch first */
+        a->completer.join();
     }
-    a->cv_flush.notify_all();
-    a->cv_cur.notify_all();
-    a->flusher.join(); /* converts what is reserved first */
-    a->completer.join();
-    for (Batch &x : a->b) {
-        x.pb.release();
-        (void)hipHostFree(x.h_packed);
-        delete[] x.status;
+    if (a->b) {
+        for (int k = 0; k < AGG_INFLIGHT; k++) {
+            Batch &x = a->b[k];
+            if (x.s) (void)hipStreamSynchronize(x.s);
+            for (Sub &u : x.sub) (void)hipHostFree(u.h);
+            x.dv.release();
+            (void)hipFree(x.d_loc);
+            (void)hipFree(x.d_tab);
+            (void)hipHostFree(x.h_tab);
+            (void)hipHostFree(x.h_hdr);
+            (void)hipHostFree(x.h_packed);
+            if (x.ev_hdr) (void)hipEventDestroy(x.ev_hdr);
+            if (x.ev_done) (void)hipEventDestroy(x.ev_done);
+            if (x.s) (void)hipStreamDestroy(x.s);
+        }
+        delete[] a->b;
     }
     delete a;
 }
 
-/* One host batch streamed through PIPE_BUFS per-chunk buffers on their own
- * streams (see the file comment); the contract of dg_j2t_batch_host. */
-constexpr int PIPE_BUFS = 3;
+/* One host batch streamed through PIPE_BUFS per-chunk buffer sets on their
+ * own streams (see the file comment); the contract of dg_j2t_batch_host.
+ * Chunk k's device JSON pointer is its buffer minus the 16-aligned floor of
+ * its first offset, so the kernels read the caller's offsets unchanged. Its
+ * packing writes straight into the caller's pinned out / out_off (or pinned
+ * staging copied out at the end when they are pageable), starting where
+ * chunk k-1's packing ended: the packings are chained by events, everything
+ * else of neighbouring chunks overlaps, and the host waits once. */
+namespace {
+bool host_pinned(const void *p, void **dev)
+{
+    hipPointerAttribute_t at;
+    if (!p || hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    if (at.type != hipMemoryTypeHost || !at.devicePointer) return false;
+    *dev = at.devicePointer;
+    return true;
+}
+}  // namespace
 
 int dg_j2t_pipeline_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *json, const uint64_t *in_off,
                          uint64_t n, uint64_t flags, uint32_t chunks, uint8_t *out, uint64_t out_cap, uint64_t *out_off,
@@ -547,78 +763,76 @@ int dg_j2t_pipeline_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8
     }
     chunks = (uint32_t)std::min<uint64_t>(chunks, n);
     std::vector<uint64_t> cb(chunks + 1);
-    uint64_t cap_n = 0, cap_b = 0;
     for (uint32_t k = 0; k <= chunks; k++) cb[k] = n * k / chunks;
-    for (uint32_t k = 0; k < chunks; k++) {
-        cap_n = std::max(cap_n, cb[k + 1] - cb[k]);
-        cap_b = std::max(cap_b, in_off[cb[k + 1]] - in_off[cb[k]]);
-    }
-    /* the buffers live in the context, reused across calls (grown on demand) */
     std::lock_guard<std::mutex> pg(c->pipe_mu);
+    HIPCHK(hipSetDevice(c->device));
+    while (c->pipe.size() < (size_t)PIPE_BUFS) {
+        PipeBuf *q = new PipeBuf();
+        c->pipe.push_back(q);
+        int rc = q->init(c->device);
+        if (rc) return rc;
+    }
     const int nb = (int)std::min<uint32_t>(PIPE_BUFS, chunks);
-    if (c->pipe.size() < (size_t)nb || c->pipe_cap_n < cap_n || c->pipe_cap_b < cap_b) {
-        for (void *q : c->pipe) {
-            ((PipeBuf *)q)->release();
-            delete (PipeBuf *)q;
-        }
-        c->pipe.clear();
-        c->pipe_cap_n = std::max(cap_n, c->pipe_cap_n);
-        c->pipe_cap_b = std::max(cap_b, c->pipe_cap_b);
-        for (int i = 0; i < PIPE_BUFS; i++) {
-            PipeBuf *q = new PipeBuf();
-            c->pipe.push_back(q);
-            int rc = q->init(c->device, c->pipe_cap_n, c->pipe_cap_b);
-            if (rc) return rc;
-        }
+    /* where the results go: the caller's buffers if pinned, else staging */
+    void *dv_out = nullptr, *dv_off = nullptr, *dv_ret = nullptr;
+    const bool direct = out_cap > 0 && host_pinned(out, &dv_out) && host_pinned(out_off, &dv_off) &&
+                        host_pinned(ret, &dv_ret);
+    uint8_t *p_out = (uint8_t *)dv_out;
+    uint64_t *p_off = (uint64_t *)dv_off, *p_ret = (uint64_t *)dv_ret;
+    if (!direct) {
+        int rc;
+        if ((rc = grow_pinned(c->h_pipe_out, c->h_pipe_out_cap, out_cap + 64))) return rc;
+        if ((rc = grow_pinned(c->h_pipe_aux, c->h_pipe_aux_cap, 16 * n + 16))) return rc;
+        p_out = c->h_pipe_out;
+        p_off = (uint64_t *)(void *)c->h_pipe_aux;
+        p_ret = p_off + n + 1;
     }
-    uint64_t cursor = 0, need = 0;
-    bool fits = true;
-    std::vector<uint64_t> redo;
-    /* chunk k's results: header read, packed bytes downloaded to out (or
-     * only counted once out_cap is exceeded) */
-    auto drain = [&](uint32_t k) -> int {
-        PipeBuf &p = *(PipeBuf *)c->pipe[k % nb];
-        const uint64_t a = cb[k], m = cb[k + 1] - a;
-        HIPCHK(hipEventSynchronize(p.ev_hdr));
-        const uint64_t *r = p.ret(), *po = p.pack_off(m);
-        const uint64_t total = po[m];
-        memcpy(ret + a, r, 8 * m);
-        for (uint64_t j = 0; j < m; j++) {
-            out_off[a + j] = cursor + po[j];
-            if ((uint8_t)r[j] == DG_ST_OUT_OVERFLOW) redo.push_back(a + j);
-        }
-        if (fits && cursor + total > out_cap) fits = false;
-        if (fits) {
-            int rc = p.download(m, out + cursor);
-            if (rc) return rc;
-        }
-        cursor += total;
-        return DG_OK;
-    };
+    const uint32_t phase = (uint32_t)((uintptr_t)p_out & 15);
     for (uint32_t k = 0; k < chunks; k++) {
-        if (k >= (uint32_t)nb) {
-            int rc = drain(k - nb);
-            if (rc) return rc;
-        }
         PipeBuf &p = *(PipeBuf *)c->pipe[k % nb];
-        if (k >= (uint32_t)nb) HIPCHK(hipEventSynchronize(p.ev_hdr)); /* its staging is free again */
-        const uint64_t a = cb[k], m = cb[k + 1] - a, base = in_off[a];
-        uint64_t *io = p.in_off(), *oo = p.out_off(), max_len = 1;
-        for (uint64_t j = 0; j <= m; j++) {
-            io[j] = in_off[a + j] - base;
-            oo[j] = slot_off(io[j], j);
-        }
-        for (uint64_t j = 0; j < m; j++) max_len = std::max<uint64_t>(max_len, io[j + 1] - io[j]);
-        int rc = p.enqueue(c, d, root, flags, m, io[m], max_len, json + base);
-        if (rc) return rc;
-    }
-    for (uint32_t k = chunks > (uint32_t)nb ? chunks - nb : 0; k < chunks; k++) {
-        int rc = drain(k);
-        if (rc) return rc;
+        const uint64_t a = cb[k], m = cb[k + 1] - a, base = in_off[a], jb = base & ~15ull;
+        uint64_t max_len = 1;
+        for (uint64_t j = a; j < a + m; j++) max_len = std::max<uint64_t>(max_len, in_off[j + 1] - in_off[j]);
+        const uint64_t span = in_off[a + m] - jb;
+        const uint64_t pk = 8 * (m + 1) + 16 + slot_off(span, m) + 64; /* pack_off + phase + packed */
+        int rc;
+        if (!p.dv.fits(m, span) || p.packed_cap < pk) HIPCHK(hipStreamSynchronize(p.s)); /* free to grow */
+        if ((rc = p.dv.reserve(m, span))) return rc;
+        if ((rc = grow(p.d_packed, p.packed_cap, pk))) return rc;
+        uint64_t *d_in = p.dv.d_off, *d_oo = d_in + m + 1;
+        uint64_t *d_po = (uint64_t *)(void *)p.d_packed;
+        uint8_t *d_pk = p.d_packed + ((8 * (m + 1) + 15) & ~15ull);
+        HIPCHK(hipMemcpyAsync(d_in, in_off + a, 8 * (m + 1), hipMemcpyHostToDevice, p.s));
+        if (span) HIPCHK(hipMemcpyAsync(p.dv.d_json, json + jb, span, hipMemcpyHostToDevice, p.s));
+        hipLaunchKernelGGL(pipe_slots_kernel, dim3((uint32_t)((m + 256) / 256)), dim3(256), 0, p.s, d_in, m, d_oo,
+                           p.dv.d_json + span);
+        HIPCHK(hipGetLastError());
+        /* the packing needs the previous chunk's end (written by its copy-out) */
+        PipeBuf *prev = k ? (PipeBuf *)c->pipe[(k - 1) % nb] : nullptr;
+        const uint64_t *base_ptr = k ? p_off + a : nullptr;
+        if ((rc = dg_i_convert_pack(c, d, root, p.dv.d_json - jb, d_in, m, flags, p.dv.d_out, d_oo, p.dv.d_ol,
+                                    p.dv.d_ret, d_pk, d_po, p.s, max_len, base_ptr ? base_ptr : c->d_zero, 0,
+                                    prev ? prev->ev_hdr : nullptr, 1 | (int)(phase << 1))))
+            return rc;
+        const uint32_t cg = (uint32_t)std::min<uint64_t>(std::max<uint64_t>((span / 16 + 255) / 256, (m + 256) / 256),
+                                                         (uint64_t)c->n_cu * 4);
+        hipLaunchKernelGGL(pipe_copy_out_kernel, dim3(cg), dim3(256), 0, p.s, d_pk, d_po, m, p.dv.d_ret, p_out,
+                           p_off + a, p_ret + a, base_ptr, out_cap);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(p.ev_hdr, p.s));
     }
     for (int i = 0; i < nb; i++) HIPCHK(hipStreamSynchronize(((PipeBuf *)c->pipe[i])->s));
-    out_off[n] = cursor;
-    need = cursor;
+    const uint64_t cursor = p_off[n];
+    bool fits = cursor <= out_cap;
+    if (!direct) {
+        memcpy(out_off, p_off, 8 * (n + 1));
+        memcpy(ret, p_ret, 8 * n);
+        if (fits && cursor) memcpy(out, p_out, cursor);
+    }
+    uint64_t need = cursor;
+    std::vector<uint64_t> redo;
+    for (uint64_t i = 0; i < n; i++)
+        if ((uint8_t)ret[i] == DG_ST_OUT_OVERFLOW) redo.push_back(i);
     if (!redo.empty()) {
         /* slot overflows (rare): each alone at its exact size, spliced in
          * place; later messages move up */

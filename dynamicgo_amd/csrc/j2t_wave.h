@@ -1331,6 +1331,18 @@ struct MsgFrame {
     const uint8_t *ftr;
     uint32_t ftr_len;
     const uint64_t *ret;
+    /* chained packing (dg_j2t_pipeline_host): positions start at *base_in
+     * (the previous chunk's end, written by its pack), and bytes that would
+     * end past dst_cap are not written (0: no limit). dst and dst_off may be
+     * pinned host memory: the kernel's stores are then the download. */
+    const uint64_t *base_in;
+    uint64_t dst_cap;
+    /* with base_mod16, positions start at (*base_in) & 15 instead: the
+     * packed bytes keep the 16-byte phase they will have at their final
+     * host address (dst + *base_in, dst & 15 given as phase_add), for an
+     * aligned copy-out (dg_j2t_pipeline_host) */
+    uint32_t base_mod16;
+    uint32_t phase_add; /* base_mod16: added before the mod (the destination's own address phase) */
 };
 
 template <int V>
@@ -1366,6 +1378,11 @@ __global__ __launch_bounds__(256) void dg_pack_scan_kernel(const uint8_t *out, c
     uint64_t base = 0;
     for (uint32_t k = tid; k < b; k += 256) base += __hip_atomic_load(&sums[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     base = block_sum_u64(base, red);
+    if (fr.base_in) {
+        const uint64_t b0 = *(volatile const uint64_t *)fr.base_in;
+        base += fr.base_mod16 ? ((b0 + fr.phase_add) & 15) : b0;
+    }
+    const uint64_t cap = fr.dst_cap ? fr.dst_cap : ~0ull;
     for (uint64_t t0 = lo; t0 < hi; t0 += 256) {
         const uint64_t i = t0 + tid;
         const uint32_t len = i < hi ? msg_len(i) : 0u;
@@ -1384,7 +1401,7 @@ __global__ __launch_bounds__(256) void dg_pack_scan_kernel(const uint8_t *out, c
         const uint32_t nt = hi - t0 < 256 ? (uint32_t)(hi - t0) : 256u;
         for (uint32_t k = w; k < nt; k += 4) {
             uint32_t nb = s_len[k];
-            if (!nb) continue;
+            if (!nb || s_pos[k] + nb > cap) continue;
             gu8 *d = (gu8 *)(void *)(dst + s_pos[k]);
             if (fr.hdr) { /* header, body, footer: byte-exact edges, in program order */
                 SrcT<const uint64_t> h;

@@ -209,18 +209,21 @@ int dg_pack_device_framed(dg_ctx *ctx, const uint8_t *d_out, const uint64_t *d_o
  * batches (the reference's callers run BinaryConv.Do from many goroutines,
  * conv/j2t/conv_timing_test.go:76-99). dg_agg_do blocks the calling thread
  * until its message is converted, with the semantics of dg_j2t_do
- * (BinaryConv.Do, conv/j2t/conv.go:53-77); a flusher thread converts up to
- * max_batch queued messages at once, as soon as max_batch are waiting or the
- * oldest has waited max_wait_us. If out_cap is too small the call returns
+ * (BinaryConv.Do, conv/j2t/conv.go:53-77); see dg_agg_create2 for when a
+ * batch is converted. If out_cap is too small the call returns
  * DG_E_NOMEM with *out_len = the bytes needed. Thread-safe.
  */
 int dg_agg_create(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, uint64_t flags, uint32_t max_batch,
                   uint32_t max_wait_us, dg_agg **out);
 int dg_agg_do(dg_agg *agg, const uint8_t *json, size_t len, uint8_t *out, size_t out_cap, size_t *out_len,
               uint64_t *ret);
-/* dg_agg_create with the JSON capacity of one batch (max_bytes; a message
- * longer than that is converted alone). dg_agg_create uses
- * max(1 MiB, 512 B x max_batch). */
+/* dg_agg_create with an explicit JSON capacity. Capacities are per caller
+ * thread: every thread that calls owns a part of each device batch holding
+ * up to max_batch messages and max_bytes JSON bytes (a message longer than
+ * max_bytes is converted alone); a batch is sealed when one thread's part is
+ * full, when a caller waits on it, or when its first message has waited
+ * max_wait_us. dg_agg_create uses max_bytes = max(1 MiB, 512 B x max_batch).
+ * Up to 256 threads take parts; calls from further threads convert alone. */
 int dg_agg_create2(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, uint64_t flags, uint32_t max_batch,
                    uint64_t max_bytes, uint32_t max_wait_us, dg_agg **out);
 /* Asynchronous form of dg_agg_do, for a caller with many requests in flight
@@ -244,6 +247,11 @@ int dg_agg_submit(dg_agg *agg, const uint8_t *json, size_t len, int nonblock, dg
 int dg_agg_wait(dg_agg *agg, dg_agg_ticket *t, uint8_t *out, size_t out_cap, size_t *out_len, uint64_t *ret);
 /* batches flushed and messages converted so far */
 int dg_agg_stats(dg_agg *agg, uint64_t *batches, uint64_t *msgs);
+/* diagnostics: n <= 8 summed nanosecond counters (flusher waiting for a seal,
+ * for a free batch, issuing a batch; completer waiting for the header, for
+ * the packed bytes; seal to issued; issued to done; callers blocked in
+ * dg_agg_wait) */
+int dg_agg_profile(dg_agg *agg, uint64_t *out, int n);
 /* converts what is still queued, then stops the flusher (every ticket must
  * have been waited for) */
 void dg_agg_destroy(dg_agg *agg);

@@ -15,7 +15,7 @@ tail -2 $O/gputest.log
 timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { cat $O/smoke.log; exit 1; }
 tail -1 $O/smoke.log
 fi
-for c in $CONFIGS; do
+[ -z "$SKIP_BENCH" ] && for c in $CONFIGS; do
   ST=20; [ $c = c5 ] && ST=5
   timeout -k 10 500 python -u bench.py --config $c --steps $ST $BENCH_ARGS > $O/${c}_bench.json 2> $O/${c}_bench.err || { tail -20 $O/${c}_bench.err; exit 1; }
   python -c "import json;d=json.loads(open('$O/${c}_bench.json').read().strip().splitlines()[-1]);print('$c',d['value'],d['unit'],d['ms_per_step'],d['roofline']['frac'],(d.get('cpu_baseline') or {}).get('value'))"
@@ -23,7 +23,7 @@ done
 [ -n "$NO_PROF" ] && exit 0
 ROOT=$(pwd)
 cd /tmp && export TMPDIR=/tmp
-for c in $CONFIGS; do
+[ -z "$SKIP_PROF" ] && for c in $CONFIGS; do
   ST=10; W=3; [ $c = c5 ] && { ST=3; W=1; }
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $ROOT/$O/prof_$c -o $c -- python3 $ROOT/bench.py --config $c --no-cpu-baseline --no-e2e --steps $ST --warmup $W > $ROOT/$O/prof_$c.log 2>&1 || exit 1
   head -4 $ROOT/$O/prof_$c/${c}_kernel_stats.csv
