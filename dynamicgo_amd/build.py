@@ -26,7 +26,7 @@ def _run(cmd, cwd=None):
 UNITS = ("j2t_kern_wave.hip", "j2t_kern_wave5.hip", "j2t_kern_small.hip", "j2t_kern_lds.hip", "j2t_kern_glb.hip",
          "j2t_host.hip", "j2t_pipe.hip", "t2j_kern.hip", "t2j_host.hip", "j2t_kern_flat.hip")
 HEADERS = ("j2t_small.h", "j2t_wave.h", "j2t_machine.h", "j2t_device.h", "j2t_fast.h", "dg_tables.h", "host_internal.h",
-           "t2j_device.h", "t2j_tables.h", "j2t_flat.h")
+           "t2j_device.h", "t2j_tables.h", "j2t_flat.h", "t2j_wave.h")
 
 
 def source_hash(extra_flags=()) -> str:

@@ -47,7 +47,8 @@ struct Scratch {
      *      the launch's last kernel (list mode), or by a stream memset of
      *      DG_J2T_COUNTS_BYTES when an enqueue fails half way;
      * pack: [6] arrivals, [7] departures of dg_pack_device_scan (self-reset);
-     * t2j: [8] deep-pass queue length (reset by a stream memset after the
+     * t2j: [8] deep-pass queue length, [9] long messages, [10] the wave
+     *      kernel's queue, [11] its bails (reset by a stream memset after the
      *      t2j launch). */
     uint32_t *d_counts = nullptr;
     uint32_t *d_bail_list = nullptr;
@@ -61,6 +62,10 @@ struct Scratch {
     std::vector<uint8_t> frame;    /* what d_frame holds */
     uint32_t *t2j_list = nullptr;  /* t2j: messages queued for the deep pass ([8] of d_counts counts them) */
     uint64_t t2j_list_cap = 0;
+    uint32_t *t2j_big = nullptr;   /* t2j: long messages for the wave kernel ([9] counts them, [10] its queue) */
+    uint64_t t2j_big_cap = 0;
+    uint32_t *t2j_bail = nullptr;  /* t2j: the wave kernel's bails ([11] counts them) */
+    uint64_t t2j_bail_cap = 0;
 };
 constexpr uint32_t FRAME_CAP = 4096;
 
@@ -72,6 +77,7 @@ struct Knobs {
     int64_t small_mpw = 64;
     int64_t list_blocks = 16;
     int64_t t2j_spread = 0;
+    int64_t t2j_wave_min = 512; /* t2j messages longer than this take the wave kernel (0: never) */
 };
 
 struct dg_ctx {

@@ -49,6 +49,8 @@ static void scratch_free(Scratch *x)
     (void)hipFree(x->d_sums);
     (void)hipFree(x->d_frame);
     (void)hipFree(x->t2j_list);
+    (void)hipFree(x->t2j_big);
+    (void)hipFree(x->t2j_bail);
     if (x->done) (void)hipEventDestroy(x->done);
     delete x;
 }
@@ -109,6 +111,7 @@ static int64_t *knob_ref(dg_ctx *c, const char *name)
     if (!strcmp(name, "small_mpw")) return &K.small_mpw;
     if (!strcmp(name, "list_blocks")) return &K.list_blocks;
     if (!strcmp(name, "t2j_spread")) return &K.t2j_spread;
+    if (!strcmp(name, "t2j_wave_min")) return &K.t2j_wave_min;
     return nullptr;
 }
 
@@ -140,7 +143,8 @@ int dg_ctx_create(int device, dg_ctx **out)
     /* routing knobs: the environment is read here, once per context */
     static const struct { const char *env; const char *name; } envk[] = {
         {"DG_FLAT", "flat"}, {"DG_WAVE_MIN", "wave_min"}, {"DG_WAVE_OCC", "wave_occ"},
-        {"DG_SMALL_MPW", "small_mpw"}, {"DG_LIST_BLOCKS", "list_blocks"}, {"DG_T2J_SPREAD", "t2j_spread"}};
+        {"DG_SMALL_MPW", "small_mpw"}, {"DG_LIST_BLOCKS", "list_blocks"}, {"DG_T2J_SPREAD", "t2j_spread"},
+        {"DG_T2J_WAVE_MIN", "t2j_wave_min"}};
     for (const auto &e : envk) {
         const char *v = getenv(e.env);
         if (v && *v) *knob_ref(c, e.name) = strtoll(v, nullptr, 10);

@@ -76,13 +76,15 @@ DGI uint32_t ndigits32(uint32_t x)
     return n;
 }
 /* x < 10^8 without leading zeros */
-DGI void emit_small(Out &o, uint32_t x)
+template <class O>
+DGI void emit_small(O &o, uint32_t x)
 {
     const uint32_t nd = ndigits32(x);
     o.wle(dig8(x) >> ((8 - nd) << 3), nd);
 }
 /* u64toa (native/fastint.c:221-231): decimal, no leading zeros */
-DGI void emit_u64(Out &o, uint64_t v)
+template <class O>
+DGI void emit_u64(O &o, uint64_t v)
 {
     if (v < 100000000ull) {
         emit_small(o, (uint32_t)v);
@@ -100,7 +102,8 @@ DGI void emit_u64(Out &o, uint64_t v)
     o.wle(dig8(r), 8);
 }
 /* i64toa (native/fastint.c:212-219) */
-DGI void emit_i64(Out &o, int64_t v)
+template <class O>
+DGI void emit_i64(O &o, int64_t v)
 {
     if (v >= 0) {
         emit_u64(o, (uint64_t)v);
@@ -175,7 +178,8 @@ DGI void sig_digits(uint64_t sig, uint32_t cnt, uint8_t *d)
 /* f64toa (native/fastfloat.c:349-404) for a finite double: the shortest
  * round-trip digits, written as an integer, a decimal, or d.ddde[+-]x when
  * the decimal exponent is < -6 or > 20 (write_dec :241-259) */
-DGI void emit_f64(Out &o, double fp)
+template <class O>
+DGI void emit_f64(O &o, double fp)
 {
     const uint64_t raw = (uint64_t)__double_as_longlong(fp);
     const bool neg = (raw >> 63) != 0;
@@ -251,8 +255,8 @@ DGI void emit_f64(Out &o, double fp)
 
 /* quote (native/parsing.c:487, flags 0) of src[s0, s0+n): 8 bytes per step
  * when none of them needs an escape */
-template <class S>
-DGI void emit_quoted(Out &o, S &src, int64_t s0, int64_t n)
+template <class S, class O>
+DGI void emit_quoted(O &o, S &src, int64_t s0, int64_t n)
 {
     int64_t i = 0;
     while (i < n) {
@@ -293,8 +297,8 @@ DGI uint64_t b64c(uint32_t v) /* one standard-alphabet character */
 }
 /* standard padded base64 of src[s0, s0+n) (base64x.StdEncoding; the
  * reference's b64encode, native/base64.c:173, mode 0) */
-template <class S>
-DGI void emit_base64(Out &o, S &src, int64_t s0, int64_t n)
+template <class S, class O>
+DGI void emit_base64(O &o, S &src, int64_t s0, int64_t n)
 {
     int64_t i = 0;
     for (; i + 3 <= n; i += 3) {
@@ -852,6 +856,15 @@ struct T2JParams {
     uint32_t *deep_list;      /* messages nested beyond the LDS frames */
     uint32_t *deep_count;     /* their number (reset by the host after the deep pass) */
     uint8_t *ws;              /* deep pass: T2J_DEEP_DEPTH frames per lane */
+    /* the wave path (t2j_wave.h): the lane pass lists messages longer than
+     * big_min (when big_list is set) instead of converting them; list mode
+     * (list set): the lane pass converts list[0 .. *list_count) instead of
+     * all n */
+    uint32_t *big_list;
+    uint32_t *big_count;
+    uint64_t big_min;
+    const uint32_t *list;
+    const uint32_t *list_count;
 };
 
 DGI T2JSide t2j_side(const uint8_t *side)
@@ -882,6 +895,18 @@ DGI void t2j_store(const T2JParams &P, uint64_t i, uint64_t r, Out &o)
 constexpr uint32_t T2J_DEEP_BLOCKS = 4; /* 1024 lanes x 96 KiB of frames */
 
 void launch_t2j_pass(uint64_t n, hipStream_t s, const T2JParams &P, uint32_t spread); /* spread 1, 2 or 4 */
+
+/* the wave path (t2j_wave.h) */
+constexpr uint32_t T2W_WAVES = 4; /* waves (messages in flight) per block */
+struct T2WParams {
+    const uint32_t *list;  /* the lane pass's long messages */
+    const uint32_t *count;
+    uint32_t *queue;       /* next list entry to take (zeroed by the host after the launch) */
+    uint32_t *bail_list;   /* messages left to the lane kernel's list mode */
+    uint32_t *bail_count;
+};
+void launch_t2j_list(uint32_t blocks, hipStream_t s, const T2JParams &P); /* list mode, 1 lane per message */
+void launch_t2j_wave(uint32_t blocks, hipStream_t s, const T2JParams &P, const T2WParams &W);
 void launch_t2j_deep(hipStream_t s, const T2JParams &P);
 
 }  // namespace dg

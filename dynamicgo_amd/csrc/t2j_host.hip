@@ -24,8 +24,12 @@ static uint32_t t2j_spread(const dg_ctx *c, uint64_t max_len)
     return max_len <= 512 ? 1 : 4;
 }
 
-/* one batch on stream s: the LDS-frame pass, the deep pass over what it
- * queued, then the queue counter reset; the scratch's `done` event after */
+/* one batch on stream s. With the wave path (a descriptor that fits LDS and
+ * messages that may be long): the lane pass converts the short messages and
+ * lists the long ones, the wave kernel converts those (t2j_wave.h), the lane
+ * pass in list mode converts the wave kernel's bails. Then the deep pass over
+ * what the lane passes queued, and the counter reset; the scratch's `done`
+ * event after. */
 static int t2j_launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *src, const uint64_t *in_off,
                       uint64_t n, uint64_t opts, uint8_t *out, const uint64_t *out_off, uint32_t *out_len,
                       uint64_t *ret, hipStream_t s, uint64_t max_len)
@@ -41,6 +45,13 @@ static int t2j_launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
     if (!c->ws_t2j) {
         HIPCHK(hipMalloc(&c->ws_t2j, T2J_DEEP_WS));
         HIPCHK(hipEventCreateWithFlags(&c->ws_t2j_done, hipEventDisableTiming));
+    }
+    const uint64_t wmin = (uint64_t)c->knobs.t2j_wave_min;
+    const bool wave = wmin > 0 && d->hdr.total_len <= 16384 && d->hdr.n_fields <= 1024 && /* T2W_FX */
+                      (max_len == 0 || max_len > wmin);
+    if (wave) {
+        if ((rc = grow_x(x, x->t2j_big, x->t2j_big_cap, n))) return rc;
+        if ((rc = grow_x(x, x->t2j_bail, x->t2j_bail_cap, n))) return rc;
     }
     T2JParams P;
     memset(&P, 0, sizeof P);
@@ -59,8 +70,35 @@ static int t2j_launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
     P.deep_list = x->t2j_list;
     P.deep_count = x->d_counts + DG_T2J_DEEP_COUNT;
     P.ws = c->ws_t2j;
-    launch_t2j_pass(n, s, P, t2j_spread(c, max_len));
-    hipError_t e = hipGetLastError();
+    hipError_t e = hipSuccess;
+    if (wave) {
+        T2JParams P1 = P;
+        P1.big_list = x->t2j_big;
+        P1.big_count = x->d_counts + DG_T2J_DEEP_COUNT + 1;
+        P1.big_min = wmin;
+        launch_t2j_pass(n, s, P1, 1); /* the short ones: full waves */
+        T2WParams W;
+        W.list = x->t2j_big;
+        W.count = P1.big_count;
+        W.queue = x->d_counts + DG_T2J_DEEP_COUNT + 2;
+        W.bail_list = x->t2j_bail;
+        W.bail_count = x->d_counts + DG_T2J_DEEP_COUNT + 3;
+        if ((e = hipGetLastError()) == hipSuccess) {
+            const uint64_t wblocks = std::min<uint64_t>((n + T2W_WAVES - 1) / T2W_WAVES, (uint64_t)c->n_cu * 4);
+            launch_t2j_wave((uint32_t)wblocks, s, P, W);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) {
+            T2JParams P3 = P;
+            P3.list = x->t2j_bail;
+            P3.list_count = W.bail_count;
+            launch_t2j_list(64, s, P3);
+            e = hipGetLastError();
+        }
+    } else {
+        launch_t2j_pass(n, s, P, t2j_spread(c, max_len));
+        e = hipGetLastError();
+    }
     /* the deep workspace is one per context: a deep pass on another stream
      * than the previous one waits for it (deep messages are rare; the LDS
      * passes of different streams still overlap) */
@@ -71,7 +109,7 @@ static int t2j_launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
     }
     if (e == hipSuccess) e = hipEventRecord(c->ws_t2j_done, s);
     if (e == hipSuccess) c->ws_t2j_last = s;
-    (void)hipMemsetAsync(x->d_counts + DG_T2J_DEEP_COUNT, 0, 4, s);
+    (void)hipMemsetAsync(x->d_counts + DG_T2J_DEEP_COUNT, 0, 16, s);
     HIPCHK(hipEventRecord(x->done, s));
     x->used = true;
     x->last = s;

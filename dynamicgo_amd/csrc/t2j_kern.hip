@@ -1,5 +1,5 @@
 /* t2j kernels (Thrift binary -> JSON): the LDS-frame pass and the deep pass. */
-#include "t2j_device.h"
+#include "t2j_wave.h"
 
 namespace dg {
 
@@ -17,23 +17,86 @@ __global__ __launch_bounds__(T2J_BLOCK) void t2j_kernel(T2JParams P)
     __shared__ __attribute__((aligned(16))) T2JFrame lf[T2J_LDS_DEPTH * MPB];
     if (threadIdx.x % SP) return;
     const uint32_t slot = threadIdx.x / SP;
-    const uint64_t i = (uint64_t)blockIdx.x * MPB + slot;
-    if (i >= P.n) return;
     const auto D = desc_view<1>((const __attribute__((address_space(1))) uint8_t *)(const void *)P.blob, P.hdr);
     const T2JSide X = t2j_side(P.side);
-    const uint64_t a = P.in_off[i], b = P.in_off[i + 1];
-    SrcT<glb_u64> s;
-    s.init((glb_u64 *)(const void *)(P.src + (a & ~7ull)), (int64_t)(a & 7), (int64_t)(b - a));
-    Out o;
-    o.init(P.out + P.out_off[i], P.out_off[i + 1] - P.out_off[i]);
-    const uint64_t r = t2j_convert(D, X, s, P.root, P.opts, o,
-                                   (__attribute__((address_space(3))) T2JFrame *)(void *)&lf[slot], MPB,
-                                   T2J_LDS_DEPTH);
-    if ((uint8_t)r == DG_ST_DEEP) {
-        P.deep_list[atomicAdd(P.deep_count, 1u)] = (uint32_t)i;
-        return;
+    /* all n messages, or (list mode) the wave kernel's bails, grid-strided */
+    const uint64_t cnt = P.list ? (uint64_t)*(volatile const uint32_t *)P.list_count : P.n;
+    for (uint64_t k = (uint64_t)blockIdx.x * MPB + slot; k < cnt; k += (uint64_t)gridDim.x * MPB) {
+        const uint64_t i = P.list ? (uint64_t)P.list[k] : k;
+        const uint64_t a = P.in_off[i], b = P.in_off[i + 1];
+        if (P.big_list && b - a > P.big_min) { /* the wave kernel takes it */
+            P.big_list[atomicAdd(P.big_count, 1u)] = (uint32_t)i;
+            continue;
+        }
+        SrcT<glb_u64> s;
+        s.init((glb_u64 *)(const void *)(P.src + (a & ~7ull)), (int64_t)(a & 7), (int64_t)(b - a));
+        Out o;
+        o.init(P.out + P.out_off[i], P.out_off[i + 1] - P.out_off[i]);
+        const uint64_t r = t2j_convert(D, X, s, P.root, P.opts, o,
+                                       (__attribute__((address_space(3))) T2JFrame *)(void *)&lf[slot], MPB,
+                                       T2J_LDS_DEPTH);
+        if ((uint8_t)r == DG_ST_DEEP) {
+            P.deep_list[atomicAdd(P.deep_count, 1u)] = (uint32_t)i;
+            continue;
+        }
+        t2j_store(P, i, r, o);
     }
-    t2j_store(P, i, r, o);
+}
+
+/* one wavefront per listed message (t2j_wave.h); a persistent grid taking
+ * messages from a queue; bails are listed for the lane kernel's list mode */
+__global__ __launch_bounds__(64 * T2W_WAVES) void t2j_wave_kernel(T2JParams P, T2WParams W)
+{
+    __shared__ __attribute__((aligned(16))) T2WLds wl[T2W_WAVES];
+    __shared__ __attribute__((aligned(16))) uint64_t s_msg[T2W_WAVES][T2W_MSG / 8];
+    extern __shared__ __attribute__((aligned(16))) uint64_t s_desc[]; /* the blob, rounded to 16 B */
+    __shared__ uint64_t s_fx[T2W_FX];
+    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const uint64_t total = *(volatile const uint32_t *)W.count;
+    if ((uint64_t)blockIdx.x * T2W_WAVES >= total) return;
+    {
+        const uint4 *g = (const uint4 *)P.blob;
+        uint4 *l = (uint4 *)s_desc;
+        for (uint32_t k = tid; k < (P.hdr.total_len + 15) / 16; k += 64 * T2W_WAVES) l[k] = g[k];
+    }
+    __syncthreads();
+    const auto dv = desc_view<3>((const __attribute__((address_space(3))) uint8_t *)(void *)s_desc, P.hdr);
+    /* the walker's per-field table: id, ttype, type flags, type index */
+    for (uint32_t f = tid; f < P.hdr.n_fields && f < T2W_FX; f += 64 * T2W_WAVES) {
+        const dg_field fd = ldrec(&dv.F[f]);
+        const dg_type t = ldrec(&dv.T[fd.type]);
+        s_fx[f] = (uint64_t)fd.id | ((uint64_t)t.ttype << 16) |
+                  ((uint64_t)(t.flags | (fd.vm != DG_VM_NONE ? 0x80u : 0u)) << 24) | ((uint64_t)fd.type << 32);
+    }
+    __syncthreads();
+    const __attribute__((address_space(3))) uint64_t *fx = (const __attribute__((address_space(3))) uint64_t *)(void *)s_fx;
+    const T2JSide X = t2j_side(P.side);
+    __attribute__((address_space(3))) uint64_t *mbuf = (__attribute__((address_space(3))) uint64_t *)(void *)s_msg[wave];
+    for (;;) {
+        uint32_t kq = 0;
+        if (lane == 0) kq = __hip_atomic_fetch_add(W.queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t k = (uint32_t)__builtin_amdgcn_readfirstlane((int)kq);
+        if (k >= total) break;
+        const uint64_t m = W.list[k];
+        const uint64_t a = P.in_off[m], b = P.in_off[m + 1];
+        const int64_t len = (int64_t)(b - a), head = (int64_t)(a & 7);
+        const uint64_t words = (uint64_t)(len + head + 7) >> 3;
+        const uint64_t *base;
+        if (words + 2 <= T2W_MSG / 8) {
+            const glb_u64 *g = (const glb_u64 *)(const void *)(P.src + (a & ~7ull));
+            for (uint64_t j = lane; j < words; j += 64) mbuf[j] = g[j];
+            if (lane < 2) mbuf[words + lane] = 0;
+            base = (const uint64_t *)(void *)mbuf;
+        } else {
+            base = (const uint64_t *)(const void *)(P.src + (a & ~7ull));
+        }
+        __builtin_amdgcn_wave_barrier();
+        SrcT<const uint64_t> s;
+        s.init(base, head, len);
+        const bool ok = len > 0 && len <= 0x7FFFFFFF && t2w_run(P, dv, fx, X, m, wl[wave], s, lane);
+        if (!ok && lane == 0) W.bail_list[atomicAdd(W.bail_count, 1u)] = (uint32_t)m;
+        __builtin_amdgcn_wave_barrier();
+    }
 }
 
 /* the queued deep messages (nested beyond the LDS frames, or holding a
@@ -69,6 +132,17 @@ void launch_t2j_pass(uint64_t n, hipStream_t s, const T2JParams &P, uint32_t spr
     if (spread == 1) hipLaunchKernelGGL(t2j_kernel<1>, dim3(blocks), dim3(T2J_BLOCK), 0, s, P);
     else if (spread == 4) hipLaunchKernelGGL(t2j_kernel<4>, dim3(blocks), dim3(T2J_BLOCK), 0, s, P);
     else hipLaunchKernelGGL(t2j_kernel<2>, dim3(blocks), dim3(T2J_BLOCK), 0, s, P);
+}
+
+void launch_t2j_list(uint32_t blocks, hipStream_t s, const T2JParams &P)
+{
+    hipLaunchKernelGGL(t2j_kernel<1>, dim3(blocks), dim3(T2J_BLOCK), 0, s, P);
+}
+
+void launch_t2j_wave(uint32_t blocks, hipStream_t s, const T2JParams &P, const T2WParams &W)
+{
+    const size_t dyn = (P.hdr.total_len + 15) / 16 * 16;
+    hipLaunchKernelGGL(t2j_wave_kernel, dim3(blocks), dim3(64 * T2W_WAVES), dyn, s, P, W);
 }
 
 void launch_t2j_deep(hipStream_t s, const T2JParams &P)

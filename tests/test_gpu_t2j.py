@@ -88,8 +88,12 @@ def test_random_parity(chk, opts):
     assert not bad, bad[:5]
 
 
-def test_numbers_and_strings_exhaustive(chk):
-    """Many doubles (every f64toa format branch), integers and strings."""
+@pytest.mark.parametrize("wmin", ["512", "1", "0"])
+def test_numbers_and_strings_exhaustive(chk, wmin, knob):
+    """Many doubles (every f64toa format branch), integers and strings, on the
+    wave kernel (t2j_wave.h: long messages by default, every message with
+    t2j_wave_min 1) and on the lane kernel alone (0)."""
+    knob("t2j_wave_min", wmin)
     td = T.struct_type("N", [T.FieldDescriptor(1, "d", T.list_of(T.builtin("double")), T.OPTIONAL),
                              T.FieldDescriptor(2, "i", T.list_of(T.builtin("i64")), T.OPTIONAL),
                              T.FieldDescriptor(3, "s", T.list_of(T.builtin("string")), T.OPTIONAL),
@@ -291,6 +295,7 @@ def test_spreads_vs_checker(chk, spread, knob):
     """The LDS-frame pass at each lanes-per-message spread (t2j_kern.hip), and
     the host's own choice from the longest message: random all-types
     messages (with mutations) and nested C3 Thrift, byte-exact."""
+    knob("t2j_wave_min", 0)  # the lane pass for every message
     if spread != "auto":
         knob("t2j_spread", spread)
     td = t2jgen.all_types_desc()
@@ -388,3 +393,55 @@ def test_error_behaviors_match_impl_go(chk):
         assert chk.t2j(fl, side, m, 0)[0] == int(r)
     beh = [t2j.T2JError(int(r)).behavior for r in rets]
     assert beh == ["ErrWrite", "ErrRead", "ErrConvert", "ErrConvert"], beh
+
+
+@pytest.mark.parametrize("opts", OPTS)
+def test_wave_path_random_parity(chk, opts, knob):
+    """Every message through the wave kernel (t2j_wave_min 1): random
+    all-types messages, mutated ones (truncations, bad types: the wave kernel
+    bails them to the lane kernel), under every option set."""
+    knob("t2j_wave_min", 1)
+    td = t2jgen.all_types_desc()
+    fl = T.flatten(td)
+    rng = random.Random(2000 + opts)
+    msgs = [t2jgen.gen_thrift(rng, td) for _ in range(1200)]
+    msgs += [t2jgen.mutate(rng, t2jgen.gen_thrift(rng, td)) for _ in range(600)]
+    bad = compare(chk, fl, msgs, opts)
+    assert not bad, bad[:5]
+
+
+def test_wave_path_nested_and_escapes(chk, knob):
+    """C3-shaped Thrift (lists of structs, maps with i64 / string keys)
+    through the wave kernel, with map keys and values that need escapes at
+    every 8-byte phase, long strings (copy tasks) and long binaries (base64
+    tasks)."""
+    knob("t2j_wave_min", 64)
+    ntd = W.nesting_i64_desc()
+    nfl = T.flatten(ntd)
+    rng = random.Random(44)
+    js = W.gen_nested_batch(rng, 400)
+    thr, rets = conv.BinaryConv(conv.Options()).do_batch(ntd, js)
+    assert not any(int(r) for r in rets)
+    bad = compare(chk, nfl, thr, 0)
+    assert not bad, bad[:3]
+    td = T.struct_type("E", [
+        T.FieldDescriptor(1, "m", T.map_of(T.builtin("string"), T.builtin("string")), T.OPTIONAL),
+        T.FieldDescriptor(2, "b", T.builtin("binary"), T.OPTIONAL),
+        T.FieldDescriptor(3, "s", T.builtin("string"), T.OPTIONAL)])
+    fl = T.flatten(td)
+    msgs = []
+    for k in range(300):
+        kv = []
+        for j in range(rng.randrange(1, 6)):
+            key = bytes(rng.choice(b'ab"\\\n\t\x01\x1fz') for _ in range(rng.randrange(0, 30)))
+            val = bytes(rng.choice(b'xy"\\\r\x02q') for _ in range(rng.randrange(0, 70)))
+            kv.append(struct.pack(">i", len(key)) + key + struct.pack(">i", len(val)) + val)
+        m = b"\x0d\x00\x01\x0b\x0b" + struct.pack(">i", len(kv)) + b"".join(kv)
+        blob = bytes(rng.randrange(256) for _ in range(rng.randrange(0, 200)))
+        m += b"\x0b\x00\x02" + struct.pack(">i", len(blob)) + blob
+        txt = bytes(rng.choice(b"abcdefgh") for _ in range(rng.randrange(0, 300)))
+        m += b"\x0b\x00\x03" + struct.pack(">i", len(txt)) + txt + b"\x00"
+        msgs.append(m)
+    for opts in (0, NOB64):
+        bad = compare(chk, fl, msgs, opts)
+        assert not bad, bad[:3]

@@ -24,8 +24,12 @@ def per_kernel(path, counter):
 
 
 def top_half_mean(v):
-    v = v[len(v) // 2:]
-    return statistics.mean(v) if v else 0.0
+    """mean of the batch launches: dispatches at least half the largest
+    (drops list-mode passes with nothing to do and single-message Do calls)"""
+    if not v:
+        return 0.0
+    big = [x for x in v if x >= v[-1] / 2]
+    return statistics.mean(big)
 
 
 def main():
@@ -40,7 +44,7 @@ def main():
     main_k = kern[ksub]
     res = {"kernel": ksub, **main_k, "all_kernels": kern,
            "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes; KiB x1024; FETCH x2 (gfx950); "
-                     "per kernel: mean of the larger half of its dispatches"}
+                     "per kernel: mean of its dispatches of at least half the largest one's size"}
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res))
 
