@@ -536,12 +536,16 @@ def bench_agg(args, rank, world, dev, dist, backend, td, arena, off, meta):
         b = C.c_uint64(0)
         tot = C.c_uint64(0)
         _lib.check(L.dg_agg_stats(h, C.byref(b), C.byref(tot)))
-        pr = (C.c_uint64 * 8)()
-        _lib.check(L.dg_agg_profile(h, pr, 8))
+        pr = (C.c_uint64 * 12)()
+        _lib.check(L.dg_agg_profile(h, pr, 11))
         nb_ = max(1, b.value)
         prof = {k: round(pr[i] / nb_ / 1e3, 1) for i, k in enumerate(
             ("flusher_wait_seal", "flusher_wait_free", "flusher_issue", "completer_wait_hdr", "completer_wait_data",
              "seal_to_issued", "issued_to_done", "callers_blocked"))}
+        ncalls = max(1, tot.value)
+        prof["ns_per_call_in_submit"] = round(pr[8] / ncalls, 1)
+        prof["ns_per_call_in_wait"] = round(pr[9] / ncalls, 1)
+        prof["submits_without_open_batch"] = int(pr[10])
         L.dg_agg_destroy(h)
         lt = lat[:m].astype(np.float64) / 1e3
         runs.append({"threads": threads, "in_flight_per_thread": window, "per_thread_batch_share": per_thread,

@@ -107,6 +107,11 @@ struct dg_ctx {
     uint8_t *ws_t2j = nullptr;
     hipEvent_t ws_t2j_done = nullptr;
     hipStream_t ws_t2j_last = nullptr;
+    /* the t2j wave kernel's token regions (t2j_wave_ws_bytes, ~200 MB), one
+     * per context, ordered across streams like ws_t2j */
+    uint8_t *ws_t2w = nullptr;
+    hipEvent_t ws_t2w_done = nullptr;
+    hipStream_t ws_t2w_last = nullptr;
     /* dg_j2t_pipeline_host: its per-chunk buffers (j2t_pipe.hip PipeBuf),
      * kept across calls; pipe_mu serialises pipeline calls */
     std::mutex pipe_mu;

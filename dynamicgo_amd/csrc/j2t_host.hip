@@ -196,6 +196,8 @@ void dg_ctx_destroy(dg_ctx *c)
     (void)hipHostFree(c->h_down);
     (void)hipFree(c->ws_t2j);
     if (c->ws_t2j_done) (void)hipEventDestroy(c->ws_t2j_done);
+    (void)hipFree(c->ws_t2w);
+    if (c->ws_t2w_done) (void)hipEventDestroy(c->ws_t2w_done);
     (void)hipStreamDestroy(c->stream);
     delete c;
 }

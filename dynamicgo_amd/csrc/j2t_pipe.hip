@@ -246,8 +246,10 @@ struct dg_agg {
     /* where the time goes (ns, summed; dg_agg_profile): 0 flusher waiting for
      * a seal, 1 waiting for a free batch, 2 in launch (uploads + kernel
      * issue), 3 completer waiting for the header, 4 for the packed bytes,
-     * 5 seal-to-launched, 6 launched-to-done */
-    std::atomic<uint64_t> prof[8] = {};
+     * 5 seal-to-launched, 6 launched-to-done, 7 callers blocked in wait;
+     * dg_agg_drive: 8 in submit, 9 in wait, 10 submits that met no open
+     * batch */
+    std::atomic<uint64_t> prof[12] = {};
     std::thread flusher, completer;
 
     static uint64_t now_ns()
@@ -602,15 +604,16 @@ int dg_agg_submit(dg_agg *a, const uint8_t *json, size_t len, int nonblock, dg_a
             }
             /* this thread's part of the open batch is full: seal it */
             u.busy.store(0, std::memory_order_release);
-            if (!x->seal_req.exchange(1, std::memory_order_acq_rel)) a->wake_flusher();
+            if (!x->seal_req.load(std::memory_order_acquire) && !x->seal_req.exchange(1, std::memory_order_acq_rel))
+                a->wake_flusher();
         } else {
             u.busy.store(0, std::memory_order_release);
             continue; /* the batch closed meanwhile: the next one is open */
         }
+        if (a->open.load(std::memory_order_acquire) != g) continue;
+        if (nonblock) return DG_E_AGAIN; /* the next batch is not open yet (no lock: callers poll this) */
         std::unique_lock<std::mutex> lk(a->mu);
         if (a->stop) return set_err(DG_E_INVALID, "aggregator closed");
-        if (a->open.load(std::memory_order_acquire) != g) continue;
-        if (nonblock) return DG_E_AGAIN; /* the next batch is not free yet */
         a->cv_open.wait(lk, [&] { return a->open.load(std::memory_order_acquire) != g || a->stop; });
     }
 }
@@ -690,7 +693,7 @@ int dg_agg_stats(dg_agg *a, uint64_t *batches, uint64_t *msgs)
 
 int dg_agg_profile(dg_agg *a, uint64_t *out, int n)
 {
-    if (!a || !out || n < 0 || n > 8) return set_err(DG_E_INVALID, "bad args");
+    if (!a || !out || n < 0 || n > 12) return set_err(DG_E_INVALID, "bad args");
     for (int i = 0; i < n; i++) out[i] = a->prof[i].load();
     return DG_OK;
 }
@@ -902,12 +905,16 @@ int dg_agg_drive(dg_agg *a, const uint8_t *arena, const uint64_t *in_off, uint64
             ready.fetch_add(1);
             while (!go.load(std::memory_order_acquire)) std::this_thread::yield();
             uint64_t h = lo;
+            uint64_t ts_sub = 0, ts_wait = 0, n_again = 0;
             auto finish = [&]() {
                 const uint64_t j = h++;
                 const int k = (int)((j - lo) % window);
                 size_t ol = 0;
+                const uint64_t w0 = dg_agg::now_ns();
                 int rc = dg_agg_wait(a, &ring[k], out + out_off[j], out_off[j + 1] - out_off[j], &ol, &ret[j]);
-                if (lat_ns) lat_ns[j] = (uint32_t)std::min<int64_t>(dg_agg::now_ns() - t0[k], 0xffffffffll);
+                const uint64_t w1 = dg_agg::now_ns();
+                ts_wait += w1 - w0;
+                if (lat_ns) lat_ns[j] = (uint32_t)std::min<int64_t>(w1 - t0[k], 0xffffffffll);
                 out_len[j] = ol;
                 if (rc) failed.fetch_add(1);
             };
@@ -916,8 +923,11 @@ int dg_agg_drive(dg_agg *a, const uint8_t *arena, const uint64_t *in_off, uint64
                 const int k = (int)((i - lo) % window);
                 t0[k] = dg_agg::now_ns();
                 for (;;) {
+                    const uint64_t s0 = dg_agg::now_ns();
                     int rc = dg_agg_submit(a, arena + in_off[i], in_off[i + 1] - in_off[i], 1, &ring[k]);
+                    ts_sub += dg_agg::now_ns() - s0;
                     if (rc == DG_OK) break;
+                    n_again++;
                     if (rc != DG_E_AGAIN) {
                         failed.fetch_add(1);
                         ring[k].batch = nullptr;
@@ -930,6 +940,9 @@ int dg_agg_drive(dg_agg *a, const uint8_t *arena, const uint64_t *in_off, uint64
                 }
             }
             while (h < hi) finish();
+            a->prof[8].fetch_add(ts_sub, std::memory_order_relaxed);
+            a->prof[9].fetch_add(ts_wait, std::memory_order_relaxed);
+            a->prof[10].fetch_add(n_again, std::memory_order_relaxed);
         });
     }
     while (ready.load() < threads) std::this_thread::yield();

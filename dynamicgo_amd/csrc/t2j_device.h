@@ -865,6 +865,7 @@ struct T2JParams {
     uint64_t big_min;
     const uint32_t *list;
     const uint32_t *list_count;
+    unsigned long long *stats; /* DG_T2W_PROF builds: phase cycles of the wave kernel (dg_ctx_counters 2..) */
 };
 
 DGI T2JSide t2j_side(const uint8_t *side)
@@ -904,7 +905,11 @@ struct T2WParams {
     uint32_t *queue;       /* next list entry to take (zeroed by the host after the launch) */
     uint32_t *bail_list;   /* messages left to the lane kernel's list mode */
     uint32_t *bail_count;
+    uint8_t *tok;          /* token regions, t2j_wave_ws_bytes(blocks) */
+    uint32_t side_len;     /* the side table's bytes (copied to LDS) */
 };
+uint64_t t2j_wave_ws_bytes(uint32_t blocks);
+constexpr uint32_t T2W_BPC = 4; /* wave-kernel blocks per CU in the grid */
 void launch_t2j_list(uint32_t blocks, hipStream_t s, const T2JParams &P); /* list mode, 1 lane per message */
 void launch_t2j_wave(uint32_t blocks, hipStream_t s, const T2JParams &P, const T2WParams &W);
 void launch_t2j_deep(hipStream_t s, const T2JParams &P);

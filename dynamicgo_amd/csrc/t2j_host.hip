@@ -48,10 +48,14 @@ static int t2j_launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
     }
     const uint64_t wmin = (uint64_t)c->knobs.t2j_wave_min;
     const bool wave = wmin > 0 && d->hdr.total_len <= 16384 && d->hdr.n_fields <= 1024 && /* T2W_FX */
-                      (max_len == 0 || max_len > wmin);
+                      d->side_len <= 12288 /* T2W_SIDE */ && (max_len == 0 || max_len > wmin);
     if (wave) {
         if ((rc = grow_x(x, x->t2j_big, x->t2j_big_cap, n))) return rc;
         if ((rc = grow_x(x, x->t2j_bail, x->t2j_bail_cap, n))) return rc;
+        if (!c->ws_t2w) HIPCHK(hipMalloc(&c->ws_t2w, t2j_wave_ws_bytes((uint32_t)c->n_cu * T2W_BPC)));
+        /* one token workspace per context, like the deep workspace: a wave
+         * pass on another stream waits for the previous one */
+        if (c->ws_t2w_last && c->ws_t2w_last != s) HIPCHK(hipStreamWaitEvent(s, c->ws_t2w_done, 0));
     }
     T2JParams P;
     memset(&P, 0, sizeof P);
@@ -70,6 +74,7 @@ static int t2j_launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
     P.deep_list = x->t2j_list;
     P.deep_count = x->d_counts + DG_T2J_DEEP_COUNT;
     P.ws = c->ws_t2j;
+    P.stats = c->d_stats;
     hipError_t e = hipSuccess;
     if (wave) {
         T2JParams P1 = P;
@@ -83,9 +88,11 @@ static int t2j_launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
         W.queue = x->d_counts + DG_T2J_DEEP_COUNT + 2;
         W.bail_list = x->t2j_bail;
         W.bail_count = x->d_counts + DG_T2J_DEEP_COUNT + 3;
+        const uint32_t wblocks = (uint32_t)c->n_cu * T2W_BPC; /* the token regions are sized for it */
+        W.tok = c->ws_t2w;
+        W.side_len = (uint32_t)d->side_len;
         if ((e = hipGetLastError()) == hipSuccess) {
-            const uint64_t wblocks = std::min<uint64_t>((n + T2W_WAVES - 1) / T2W_WAVES, (uint64_t)c->n_cu * 4);
-            launch_t2j_wave((uint32_t)wblocks, s, P, W);
+            launch_t2j_wave(wblocks, s, P, W);
             e = hipGetLastError();
         }
         if (e == hipSuccess) {
@@ -109,6 +116,11 @@ static int t2j_launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
     }
     if (e == hipSuccess) e = hipEventRecord(c->ws_t2j_done, s);
     if (e == hipSuccess) c->ws_t2j_last = s;
+    if (wave && e == hipSuccess) {
+        if (!c->ws_t2w_done) e = hipEventCreateWithFlags(&c->ws_t2w_done, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventRecord(c->ws_t2w_done, s);
+        if (e == hipSuccess) c->ws_t2w_last = s;
+    }
     (void)hipMemsetAsync(x->d_counts + DG_T2J_DEEP_COUNT, 0, 16, s);
     HIPCHK(hipEventRecord(x->done, s));
     x->used = true;

@@ -43,24 +43,41 @@ __global__ __launch_bounds__(T2J_BLOCK) void t2j_kernel(T2JParams P)
     }
 }
 
-/* one wavefront per listed message (t2j_wave.h); a persistent grid taking
- * messages from a queue; bails are listed for the lane kernel's list mode */
-__global__ __launch_bounds__(64 * T2W_WAVES) void t2j_wave_kernel(T2JParams P, T2WParams W)
+/* the long messages (t2j_wave.h): a persistent grid; each wave takes
+ * T2W_MPT of them at a time, every lane walks one into the wave's token
+ * region, then the wave formats them one by one; bails are listed for the
+ * lane kernel's list mode */
+__global__ __launch_bounds__(64 * T2W_WAVES) __attribute__((amdgpu_waves_per_eu(4))) void t2j_wave_kernel(T2JParams P, T2WParams W)
 {
     __shared__ __attribute__((aligned(16))) T2WLds wl[T2W_WAVES];
+    __shared__ __attribute__((aligned(16))) T2WFrame s_fr[T2W_WAVES][T2W_BD * T2W_MPT];
+    __shared__ uint64_t s_fx[T2W_FX];
     __shared__ __attribute__((aligned(16))) uint64_t s_msg[T2W_WAVES][T2W_MSG / 8];
     extern __shared__ __attribute__((aligned(16))) uint64_t s_desc[]; /* the blob, rounded to 16 B */
-    __shared__ uint64_t s_fx[T2W_FX];
     const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const uint64_t total = *(volatile const uint32_t *)W.count;
-    if ((uint64_t)blockIdx.x * T2W_WAVES >= total) return;
+    if ((uint64_t)blockIdx.x * T2W_WAVES * T2W_MPT >= total) return;
+    /* the descriptor, then the side table (its keys are read 8 bytes at a
+     * time: 16 zero bytes after it) */
+    const uint32_t dlen = (P.hdr.total_len + 15) & ~15u, slen = (W.side_len + 15) & ~15u;
     {
         const uint4 *g = (const uint4 *)P.blob;
         uint4 *l = (uint4 *)s_desc;
-        for (uint32_t k = tid; k < (P.hdr.total_len + 15) / 16; k += 64 * T2W_WAVES) l[k] = g[k];
+        for (uint32_t k = tid; k < dlen / 16; k += 64 * T2W_WAVES) l[k] = g[k];
+        const uint4 *gs = (const uint4 *)P.side;
+        uint4 *ls = (uint4 *)((uint8_t *)s_desc + dlen);
+        for (uint32_t k = tid; k < slen / 16 + 1; k += 64 * T2W_WAVES) ls[k] = k < slen / 16 ? gs[k] : make_uint4(0, 0, 0, 0);
     }
     __syncthreads();
     const auto dv = desc_view<3>((const __attribute__((address_space(3))) uint8_t *)(void *)s_desc, P.hdr);
+    T2WSide X;
+    {
+        const __attribute__((address_space(3))) uint8_t *sb =
+            (const __attribute__((address_space(3))) uint8_t *)(void *)((uint8_t *)s_desc + dlen);
+        const dg_t2j_hdr xh = *(const dg_t2j_hdr *)(const void *)((uint8_t *)s_desc + dlen);
+        X.X = (const __attribute__((address_space(3))) dg_t2j_field *)(sb + xh.off_fields);
+        X.P = sb + xh.off_pool;
+    }
     /* the walker's per-field table: id, ttype, type flags, type index */
     for (uint32_t f = tid; f < P.hdr.n_fields && f < T2W_FX; f += 64 * T2W_WAVES) {
         const dg_field fd = ldrec(&dv.F[f]);
@@ -70,32 +87,18 @@ __global__ __launch_bounds__(64 * T2W_WAVES) void t2j_wave_kernel(T2JParams P, T
     }
     __syncthreads();
     const __attribute__((address_space(3))) uint64_t *fx = (const __attribute__((address_space(3))) uint64_t *)(void *)s_fx;
-    const T2JSide X = t2j_side(P.side);
-    __attribute__((address_space(3))) uint64_t *mbuf = (__attribute__((address_space(3))) uint64_t *)(void *)s_msg[wave];
+    T2WTok *tokw = (T2WTok *)(void *)(W.tok + ((uint64_t)blockIdx.x * T2W_WAVES + wave) * T2W_MPT * T2W_TOKCAP *
+                                                  sizeof(T2WTok));
+    T2WFrame *frs = s_fr[wave];
     for (;;) {
         uint32_t kq = 0;
-        if (lane == 0) kq = __hip_atomic_fetch_add(W.queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint64_t k = (uint32_t)__builtin_amdgcn_readfirstlane((int)kq);
-        if (k >= total) break;
-        const uint64_t m = W.list[k];
-        const uint64_t a = P.in_off[m], b = P.in_off[m + 1];
-        const int64_t len = (int64_t)(b - a), head = (int64_t)(a & 7);
-        const uint64_t words = (uint64_t)(len + head + 7) >> 3;
-        const uint64_t *base;
-        if (words + 2 <= T2W_MSG / 8) {
-            const glb_u64 *g = (const glb_u64 *)(const void *)(P.src + (a & ~7ull));
-            for (uint64_t j = lane; j < words; j += 64) mbuf[j] = g[j];
-            if (lane < 2) mbuf[words + lane] = 0;
-            base = (const uint64_t *)(void *)mbuf;
-        } else {
-            base = (const uint64_t *)(const void *)(P.src + (a & ~7ull));
-        }
-        __builtin_amdgcn_wave_barrier();
-        SrcT<const uint64_t> s;
-        s.init(base, head, len);
-        const bool ok = len > 0 && len <= 0x7FFFFFFF && t2w_run(P, dv, fx, X, m, wl[wave], s, lane);
-        if (!ok && lane == 0) W.bail_list[atomicAdd(W.bail_count, 1u)] = (uint32_t)m;
-        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) kq = __hip_atomic_fetch_add(W.queue, T2W_MPT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t k0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)kq);
+        if (k0 >= total) break;
+        const uint32_t nm = (uint32_t)(total - k0 < T2W_MPT ? total - k0 : T2W_MPT);
+        const uint64_t mine = lane < nm ? (uint64_t)W.list[k0 + lane] : 0ull;
+        t2w_batch(P, W, dv, fx, X, mine, nm, wl[wave], frs, tokw,
+                  (__attribute__((address_space(3))) uint64_t *)(void *)s_msg[wave], lane);
     }
 }
 
@@ -140,10 +143,13 @@ void launch_t2j_list(uint32_t blocks, hipStream_t s, const T2JParams &P)
 }
 
 void launch_t2j_wave(uint32_t blocks, hipStream_t s, const T2JParams &P, const T2WParams &W)
+/* W.tok: blocks * T2W_WAVES * T2W_MPT * T2W_TOKCAP tokens (t2j_wave_ws_bytes) */
 {
-    const size_t dyn = (P.hdr.total_len + 15) / 16 * 16;
+    const size_t dyn = (P.hdr.total_len + 15) / 16 * 16 + (W.side_len + 15) / 16 * 16 + 16;
     hipLaunchKernelGGL(t2j_wave_kernel, dim3(blocks), dim3(64 * T2W_WAVES), dyn, s, P, W);
 }
+
+uint64_t t2j_wave_ws_bytes(uint32_t blocks) { return (uint64_t)blocks * T2W_WAVES * T2W_MPT * T2W_TOKCAP * sizeof(T2WTok); }
 
 void launch_t2j_deep(hipStream_t s, const T2JParams &P)
 {

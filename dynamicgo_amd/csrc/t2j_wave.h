@@ -60,21 +60,23 @@ struct T2WFrame {
 };
 
 struct T2WLds {
-    uint8_t kind[64];   /* TK_* | TKF_* */
-    uint8_t kt[64];     /* map entries: the key's Thrift type */
-    uint32_t pos[64];   /* Thrift position of the value */
-    uint32_t aux[64];   /* TKF_KEYF: field index; TKF_KEYM: Thrift position of the key */
-    uint32_t td[64];    /* value type index */
     uint32_t xk[64];    /* escape bytes the map key string adds (scan tasks) */
     uint32_t xv[64];    /* ... the value string adds */
     uint32_t cinc[64];  /* tasks: inclusive prefix of per-lane task counts */
-    uint32_t ck[64];    /* scan: chunks of the key string (the rest are the value's) */
-    uint32_t cs[64];    /* scan: key string start; write: body source start */
-    uint32_t cn[64];    /* scan: key string length; write: body length | 1 << 31 base64 */
-    uint32_t cvs[64];   /* scan: value string start; write: body output offset in the slot */
-    uint32_t cvn[64];   /* scan: value string length */
-    T2WFrame fr[T2W_MAXD];
+    uint32_t ck[64];    /* tasks: the map key's (the rest are the value's) */
+    uint32_t cs[64];    /* key string source */
+    uint32_t cn[64];    /* scan: key string length; write: key text output offset */
+    uint32_t cvs[64];   /* value string / body source */
+    uint32_t cvn[64];   /* scan: value string length; write: body output offset */
 };
+constexpr uint32_t T2W_MPT = 16; /* messages a wave takes at once (one walker lane each) */
+
+/* the t2j side table (keys) copied to LDS by the wave kernel */
+struct T2WSide {
+    const __attribute__((address_space(3))) dg_t2j_field *X;
+    const __attribute__((address_space(3))) uint8_t *P;
+};
+constexpr uint32_t T2W_SIDE = 12288; /* side tables up to this many bytes take the wave path */
 
 /* up to 32 bytes of output in registers (numbers, literals) */
 struct RegOut {
@@ -90,10 +92,13 @@ struct RegOut {
         if (n < 8) v &= (1ull << (n << 3)) - 1;
         const uint32_t k = len >> 3, sh = (len & 7) << 3;
         const uint64_t lo = v << sh, hi = sh ? v >> (64 - sh) : 0;
-        if (k == 0) { w0 |= lo; w1 |= hi; }
-        else if (k == 1) { w1 |= lo; w2 |= hi; }
-        else if (k == 2) { w2 |= lo; w3 |= hi; }
-        else w3 |= lo;
+        /* masks, not an indexed array: the words stay in registers */
+        const uint64_t m0 = k == 0 ? ~0ull : 0ull, m1 = k == 1 ? ~0ull : 0ull, m2 = k == 2 ? ~0ull : 0ull,
+                       m3 = k == 3 ? ~0ull : 0ull;
+        w0 |= lo & m0;
+        w1 |= (lo & m1) | (hi & m0);
+        w2 |= (lo & m2) | (hi & m1);
+        w3 |= (lo & m3) | (hi & m2);
         len += n;
     }
     DGI void w8(uint8_t c) { wle(c, 1); }
@@ -157,48 +162,62 @@ DGI uint32_t fx_fl(uint64_t v) { return (uint32_t)(v >> 24) & 0xFF; }
 DGI uint32_t fx_td(uint64_t v) { return (uint32_t)(v >> 32); }
 constexpr uint32_t T2W_FX = 1024; /* fields the LDS table holds (descriptors with more take the lane kernel) */
 
-/* the walker's next tokens, up to 64 (lane 0): returns the count, or -1 to
- * bail; `done` when the root struct closed. State across pages: p, the
- * frames (sp of them, the innermost in `cur`), `started`. */
+/* Token sink of the batched walk: this lane's region of the wave's token
+ * buffer (global memory, T2W_TOKCAP tokens of 16 bytes). */
+struct T2WTok {
+    uint32_t pos;  /* Thrift position of the value */
+    uint32_t aux;  /* TKF_KEYF: field index; TKF_KEYM: Thrift position of the key */
+    uint32_t td;   /* value type index */
+    uint32_t kind; /* TK_* | TKF_* | map key ttype << 8 */
+};
+constexpr uint32_t T2W_TOKCAP = 192; /* tokens per message (more: the lane kernel) */
+constexpr uint32_t T2W_BD = 3;       /* frames kept in LDS per lane (the innermost is in registers) */
+
+/* One lane walks its whole message (doRecurse's order, conv/t2j/impl.go:
+ * 189-393) into tokens: returns the count, or -1 to bail. Parent frames
+ * live in LDS at frs[d * T2W_MPT] (d < T2W_BD), the innermost in registers. */
 template <class S, class DV>
-DGI int32_t t2w_walk(const DV &D, const __attribute__((address_space(3))) uint64_t *fx, S &src, int64_t &p,
-                     uint32_t &sp, T2WFrame &cur, T2WLds &L, uint64_t opts, bool &done, bool &started, uint32_t root)
+DGI int32_t t2w_walk(const DV &D, const __attribute__((address_space(3))) uint64_t *fx, S &src,
+                     T2WFrame *frs, T2WTok *tok, uint32_t root, uint64_t opts)
 {
     const int64_t n = src.n;
-    uint32_t nt = 0;
-    auto emit = [&](uint32_t kind, uint32_t pos, uint32_t aux, uint32_t td, uint32_t kt) {
-        L.kind[nt] = (uint8_t)kind;
-        L.kt[nt] = (uint8_t)kt;
-        L.pos[nt] = pos;
-        L.aux[nt] = aux;
-        L.td[nt] = td;
-        nt++;
+    int64_t p = 0;
+    uint32_t sp = 0, nt = 0;
+    T2WFrame cur{};
+    auto emit = [&](uint32_t kind, uint32_t pos, uint32_t aux, uint32_t td, uint32_t kt) -> bool {
+        if (nt >= T2W_TOKCAP) return false;
+        T2WTok t;
+        t.pos = pos;
+        t.aux = aux;
+        t.td = td;
+        t.kind = kind | (kt << 8);
+        tok[nt++] = t;
+        return true;
     };
     /* a value of type td (ttype tt) at p: scalars and strings become one
      * token (p moves past them), containers an open token and a frame */
     auto value = [&](uint32_t td, uint32_t tt, uint32_t flags, uint32_t aux, uint32_t kt) -> bool {
         const uint32_t fs = num_bytes((uint8_t)tt) ? num_bytes((uint8_t)tt) : tt == DG_T_BOOL ? 1u : 0u;
         if (fs) {
-            if (p + fs > n) return false;
-            emit(TK_VAL | flags, (uint32_t)p, aux, td, kt);
+            if (p + fs > n || !emit(TK_VAL | flags, (uint32_t)p, aux, td, kt)) return false;
             p += fs;
             return true;
         }
         if (tt == DG_T_STRING) {
             if (p + 4 > n) return false;
             const int64_t sz = (int32_t)be_at(src, p, 4);
-            if (sz < 0 || p + 4 + sz > n) return false;
-            emit(TK_VAL | flags, (uint32_t)p, aux, td, kt);
+            if (sz < 0 || p + 4 + sz > n || !emit(TK_VAL | flags, (uint32_t)p, aux, td, kt)) return false;
             p += 4 + sz;
             return true;
         }
-        if (sp >= T2W_MAXD) return false;
+        if (sp > T2W_BD) return false;
         const dg_type t = ldrec(&D.T[td]);
         T2WFrame f;
         f.i = 0;
         f.u = 0;
         f.fb = f.nf = f.st = 0;
         f.etd = f.ett = 0;
+        uint32_t ok_kind;
         if (tt == DG_T_STRUCT) {
             const dg_struct sd = ldrec(&D.S[t.st]);
             if (sd.req_words != 1) return false;
@@ -208,7 +227,7 @@ DGI int32_t t2w_walk(const DV &D, const __attribute__((address_space(3))) uint64
             f.nf = sd.n_fields;
             f.st = t.st;
             f.u = D.R[sd.req_begin];
-            emit(TK_OPEN_OBJ | flags, 0, aux, td, kt);
+            ok_kind = TK_OPEN_OBJ;
         } else if (tt == DG_T_LIST || tt == DG_T_SET) {
             if (p + 5 > n) return false;
             const uint64_t w = __builtin_bswap64(src.get8(p)); /* et | count (big-endian) */
@@ -221,7 +240,7 @@ DGI int32_t t2w_walk(const DV &D, const __attribute__((address_space(3))) uint64
             f.n = (uint32_t)cnt;
             f.etd = t.elem;
             f.ett = e.ttype | ((uint32_t)e.flags << 8);
-            emit(TK_OPEN_ARR | flags, 0, aux, td, kt);
+            ok_kind = TK_OPEN_ARR;
         } else if (tt == DG_T_MAP) {
             if (p + 6 > n) return false;
             const uint64_t w = __builtin_bswap64(src.get8(p)); /* kt | vt | count */
@@ -235,28 +254,22 @@ DGI int32_t t2w_walk(const DV &D, const __attribute__((address_space(3))) uint64
             f.n = (uint32_t)cnt;
             f.etd = t.elem;
             f.ett = vd.ttype | ((uint32_t)vd.flags << 8) | ((uint32_t)k << 16);
-            emit(TK_OPEN_OBJ | flags, 0, aux, td, kt);
+            ok_kind = TK_OPEN_OBJ;
         } else {
             return false;
         }
-        if (sp) L.fr[sp - 1] = cur;
+        if (!emit(ok_kind | flags, 0, aux, td, kt)) return false;
+        if (sp) frs[(sp - 1) * T2W_MPT] = cur;
         cur = f;
         sp++;
         return true;
     };
     auto pop = [&]() {
         sp--;
-        if (sp) cur = L.fr[sp - 1];
+        if (sp) cur = frs[(sp - 1) * T2W_MPT];
     };
-    if (!started) { /* the root: a struct (other roots take the lane kernel) */
-        started = true;
-        if (ldrec(&D.T[root]).ttype != DG_T_STRUCT || !value(root, DG_T_STRUCT, 0, 0, 0)) return -1;
-    }
-    while (nt < 64) {
-        if (sp == 0) {
-            done = true;
-            break;
-        }
+    if (ldrec(&D.T[root]).ttype != DG_T_STRUCT || !value(root, DG_T_STRUCT, 0, 0, 0)) return -1;
+    while (sp) {
         if (cur.kind == TF_STRUCT) {
             if (p + 1 > n) return -1;
             const uint64_t w = src.get8(p); /* type, id (big-endian) */
@@ -265,7 +278,7 @@ DGI int32_t t2w_walk(const DV &D, const __attribute__((address_space(3))) uint64
             if (t == 0) { /* STOP: unset fields must write nothing */
                 if (cur.u && !unsets_silent(D, ldrec(&D.S[cur.st]), cur.u, opts)) return -1;
                 p += 1;
-                emit(TK_CLOSE_OBJ, 0, 0, 0, 0);
+                if (!emit(TK_CLOSE_OBJ, 0, 0, 0, 0)) return -1;
                 pop();
                 continue;
             }
@@ -297,65 +310,60 @@ DGI int32_t t2w_walk(const DV &D, const __attribute__((address_space(3))) uint64
             cur.i = 1;
             p += 3;
             if (!value(fx_td(v), t, comma | TKF_KEYF, cur.fb + k, 0)) return -1;
-        } else if (cur.kind == TF_LIST) {
-            if (cur.i == cur.n) {
-                emit(TK_CLOSE_ARR, 0, 0, 0, 0);
-                pop();
-                continue;
-            }
-            const uint32_t comma = cur.i ? TKF_COMMA : 0u;
-            cur.i++;
-            if (!value(cur.etd, cur.ett & 0xFF, comma, 0, 0)) return -1;
         } else {
             if (cur.i == cur.n) {
-                emit(TK_CLOSE_OBJ, 0, 0, 0, 0);
+                if (!emit(cur.kind == TF_LIST ? TK_CLOSE_ARR : TK_CLOSE_OBJ, 0, 0, 0, 0)) return -1;
                 pop();
                 continue;
             }
             const uint32_t comma = cur.i ? TKF_COMMA : 0u;
             cur.i++;
-            const uint8_t kt = (uint8_t)(cur.ett >> 16);
-            const int64_t kp = p;
-            if (kt == DG_T_STRING) {
-                if (p + 4 > n) return -1;
-                const int64_t sz = (int32_t)be_at(src, p, 4);
-                if (sz < 0 || p + 4 + sz > n) return -1;
-                p += 4 + sz;
-            } else {
-                if (p + num_bytes(kt) > n) return -1;
-                p += num_bytes(kt);
+            uint32_t flags = comma, kt = 0;
+            int64_t kp = 0;
+            if (cur.kind == TF_MAP) {
+                kt = (uint8_t)(cur.ett >> 16);
+                kp = p;
+                if (kt == DG_T_STRING) {
+                    if (p + 4 > n) return -1;
+                    const int64_t sz = (int32_t)be_at(src, p, 4);
+                    if (sz < 0 || p + 4 + sz > n) return -1;
+                    p += 4 + sz;
+                } else {
+                    if (p + num_bytes((uint8_t)kt) > n) return -1;
+                    p += num_bytes((uint8_t)kt);
+                }
+                flags |= TKF_KEYM;
             }
-            if (!value(cur.etd, cur.ett & 0xFF, comma | TKF_KEYM, (uint32_t)kp, kt)) return -1;
+            if (!value(cur.etd, cur.ett & 0xFF, flags, (uint32_t)kp, kt)) return -1;
         }
     }
     return (int32_t)nt;
 }
 
-/* the JSON of a number/bool token, into registers; false: bail */
+#ifdef DG_T2W_PROF
+#define T2P_DECL uint64_t t2p_t = __builtin_readcyclecounter(); uint64_t t2p_acc[6] = {0};
+#define T2P(k) do { uint64_t t_ = __builtin_readcyclecounter(); t2p_acc[k] += t_ - t2p_t; t2p_t = t_; } while (0)
+#define T2P_FLUSH() do { if (lane == 0 && P.stats) for (int k_ = 0; k_ < 6; k_++) atomicAdd(&P.stats[2 + k_], (unsigned long long)t2p_acc[k_]); } while (0)
+#else
+#define T2P_DECL
+#define T2P(k)
+#define T2P_FLUSH()
+#endif
+
+/* a number/bool at byte p of Thrift type tt as JSON in registers, through
+ * ONE emit_i64 and ONE emit_f64 call site (the kernel must fit the
+ * instruction cache); false: bail (NaN/Inf without the option) */
 template <class S>
-DGI bool t2w_scalar(S &src, int64_t p, uint8_t tt, uint64_t opts, RegOut &r)
+DGI bool t2w_number(S &src, int64_t p, uint8_t tt, uint64_t opts, bool quote64, RegOut &r)
 {
-    switch (tt) {
-    case DG_T_BOOL:
-        if (be_at(src, p, 1) == 1) r.wle('t' | ('r' << 8) | ('u' << 16) | ('e' << 24), 4);
+    const uint32_t nb = tt == DG_T_BOOL || tt == DG_T_BYTE ? 1u : tt == DG_T_I16 ? 2u : tt == DG_T_I32 ? 4u : 8u;
+    const uint64_t u = be_at(src, p, nb);
+    if (tt == DG_T_BOOL) {
+        if (u == 1) r.wle('t' | ('r' << 8) | ('u' << 16) | ('e' << 24), 4);
         else r.wle('f' | ('a' << 8) | ('l' << 16) | ('s' << 24) | (0x65ull << 32), 5);
         return true;
-    case DG_T_BYTE: {
-        const uint8_t v = (uint8_t)be_at(src, p, 1);
-        emit_i64(r, (opts & DG_T2J_BYTE_AS_UINT8) ? (int64_t)v : (int64_t)(int8_t)v);
-        return true;
     }
-    case DG_T_I16: emit_i64(r, (int16_t)be_at(src, p, 2)); return true;
-    case DG_T_I32: emit_i64(r, (int32_t)be_at(src, p, 4)); return true;
-    case DG_T_I64: {
-        const int64_t v = (int64_t)be_at(src, p, 8);
-        if (opts & DG_T2J_INT64_AS_STRING) r.w8('"');
-        emit_i64(r, v);
-        if (opts & DG_T2J_INT64_AS_STRING) r.w8('"');
-        return true;
-    }
-    case DG_T_DOUBLE: {
-        const uint64_t u = be_at(src, p, 8);
+    if (tt == DG_T_DOUBLE) {
         if (((u >> 52) & 0x7FF) == 0x7FF) {
             if (!(opts & DG_T2J_NULL_FOR_NAN_INF)) return false; /* the error: the lane kernel reports it */
             r.wle('n' | ('u' << 8) | ('l' << 16) | ('l' << 24), 4);
@@ -364,52 +372,31 @@ DGI bool t2w_scalar(S &src, int64_t p, uint8_t tt, uint64_t opts, RegOut &r)
         emit_f64(r, __longlong_as_double((long long)u));
         return true;
     }
-    }
-    return false;
+    /* sign-extend (BYTE as unsigned with ByteAsUint8) */
+    const int64_t v = tt == DG_T_BYTE ? ((opts & DG_T2J_BYTE_AS_UINT8) ? (int64_t)u : (int64_t)(int8_t)u)
+                      : tt == DG_T_I16 ? (int64_t)(int16_t)u
+                      : tt == DG_T_I32 ? (int64_t)(int32_t)u
+                                       : (int64_t)u;
+    if (quote64) r.w8('"');
+    emit_i64(r, v);
+    if (quote64) r.w8('"');
+    return true;
 }
 
-/* a map key that is a number: its digits in registers (buildinTypeToKey) */
-template <class S>
-DGI void t2w_numkey(S &src, int64_t p, uint8_t kt, uint64_t opts, RegOut &r)
-{
-    switch (kt) {
-    case DG_T_BYTE: {
-        const uint8_t v = (uint8_t)be_at(src, p, 1);
-        emit_i64(r, (opts & DG_T2J_BYTE_AS_UINT8) ? (int64_t)v : (int64_t)(int8_t)v);
-        break;
-    }
-    case DG_T_I16: emit_i64(r, (int16_t)be_at(src, p, 2)); break;
-    case DG_T_I32: emit_i64(r, (int32_t)be_at(src, p, 4)); break;
-    default: emit_i64(r, (int64_t)be_at(src, p, 8)); break;
-    }
-}
-
-/* one message (a wave): false = bail */
+/* one page of a message: up to 64 tokens, one per lane (tok = this page's
+ * first token); O = the message's output bytes so far. false: bail. */
 template <class S, class DV>
-DGI bool t2w_run(const T2JParams &P, const DV &D, const __attribute__((address_space(3))) uint64_t *fx,
-                 const T2JSide &X, uint64_t m, T2WLds &L, S src, uint32_t lane)
+DGI bool t2w_page(const T2JParams &P, const DV &D, const T2WSide &X, T2WLds &L, S &src, const T2WTok *tok,
+                  bool act, gu8 *ob, uint64_t cap, uint64_t &O, uint32_t lane)
 {
     const uint64_t opts = P.opts;
-    const uint64_t oa = P.out_off[m], cap = P.out_off[m + 1] - oa;
-    gu8 *ob = (gu8 *)(void *)(P.out + oa);
     const bool b64 = !(opts & DG_T2J_NO_BASE64);
-    int64_t p = 0; /* walker state (lane 0) */
-    uint32_t sp = 0;
-    T2WFrame cur{};
-    bool done = false, started = false;
-    uint64_t O = 0; /* output bytes so far */
-    for (;;) {
-        int32_t nt = 0;
-        if (lane == 0) nt = t2w_walk(D, fx, src, p, sp, cur, L, opts, done, started, P.root);
-        nt = __builtin_amdgcn_readfirstlane(nt);
-        if (nt < 0) return false;
-        const bool fin = __builtin_amdgcn_readfirstlane(done ? 1 : 0) != 0;
-        __builtin_amdgcn_wave_barrier();
-        const bool act = lane < (uint32_t)nt;
-        const uint32_t kd = act ? L.kind[lane] : 0u;
+        T2WTok tk{};
+        if (act) tk = tok[lane];
+        const uint32_t kd = tk.kind & 0xFF;
         const uint32_t kind = kd & 7;
-        const uint32_t pos = act ? L.pos[lane] : 0u, aux = act ? L.aux[lane] : 0u, td = act ? L.td[lane] : 0u;
-        const uint32_t kt = act ? L.kt[lane] : 0u;
+        const uint32_t pos = tk.pos, aux = tk.aux, td = tk.td;
+        const uint32_t kt = tk.kind >> 8;
         const bool keyf = act && (kd & TKF_KEYF), keym = act && (kd & TKF_KEYM), comma = act && (kd & TKF_COMMA);
         const bool isval = act && kind == TK_VAL;
         const dg_type vt = ldrec(&D.T[isval ? td : 0u]);
@@ -452,125 +439,203 @@ DGI bool t2w_run(const T2JParams &P, const DV &D, const __attribute__((address_s
             }
         }
         const uint32_t xk = L.xk[lane], xv = L.xv[lane];
-        /* lengths */
-        RegOut rv, rk;
-        rv.init();
+        /* numbers in registers: the map key's (iteration 0), then the value's,
+         * through one call site */
+        RegOut rk, rv;
         rk.init();
+        rv.init();
         bool bad = false;
-        uint32_t klen = 0, vlen = 0;
-        dg_t2j_field xf{};
+        const bool knum = keym && !kstr, vnum = isval && !isstr;
+#pragma nounroll
+        for (uint32_t it = 0; it < 2; it++) {
+            const bool want = it == 0 ? knum : vnum;
+            if (!ballot(want)) continue;
+            if (want) {
+                RegOut r;
+                r.init();
+                if (it == 0) r.w8('"');
+                if (!t2w_number(src, it == 0 ? aux : pos, it == 0 ? (uint8_t)kt : tt, opts,
+                                it == 1 && tt == DG_T_I64 && (opts & DG_T2J_INT64_AS_STRING), r))
+                    bad = true;
+                if (it == 0) {
+                    r.wle('"' | (':' << 8), 2);
+                    rk = r;
+                } else {
+                    rv = r;
+                }
+            }
+        }
+        if (ballot(bad)) return false;
+        uint32_t klen = 0, koff = 0;
         if (keyf) {
-            xf = ldrec(&X.X[aux]);
+            const dg_t2j_field xf = ldrec(&X.X[aux]);
             klen = xf.key_len;
+            koff = xf.key_off;
         } else if (kstr) {
             klen = kn + xk + 3; /* "key": */
         } else if (keym) {
-            rk.w8('"');
-            t2w_numkey(src, aux, (uint8_t)kt, opts, rk);
-            rk.wle('"' | (':' << 8), 2);
             klen = rk.len;
         }
-        bool chunked = false;
+        uint32_t vlen = 0;
+        bool tasks = false; /* the body goes to copy / base64 tasks */
         if (isstr) {
-            if (isbin) {
-                vlen = 2 + (vn + 2) / 3 * 4;
-                chunked = vn > T2W_B64;
-            } else {
-                vlen = 2 + vn + xv;
-                chunked = xv == 0 && vn > T2W_CH;
-            }
+            vlen = isbin ? 2 + (vn + 2) / 3 * 4 : 2 + vn + xv;
+            tasks = isbin || xv == 0;
         } else if (isval) {
-            if (!t2w_scalar(src, pos, tt, opts, rv)) bad = true;
             vlen = rv.len;
         } else if (act) {
             vlen = 1;
         }
-        if (ballot(bad)) return false;
         const uint32_t ln = (comma ? 1u : 0u) + klen + vlen;
         const uint32_t incl = wave_incl_sum(ln, lane);
         const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
         if (O + tot > cap) return false; /* slot overflow: the lane kernel reports it */
         const uint64_t at = O + incl - ln;
-        /* the token's bytes; a chunked body is left to the tasks below */
+        /* the token's bytes: comma, key, value; string bodies with escapes
+         * (rare) by their lane through ONE emit_quoted call site, the others
+         * skipped here and written by the tasks below */
         {
+            uint64_t wb = at; /* where w was (re)started */
             WOut w;
-            w.init(ob + at);
+            w.init(ob + wb);
             if (comma) w.w8(',');
             if (keyf) {
-                const __attribute__((address_space(1))) uint64_t *kw =
-                    (const __attribute__((address_space(1))) uint64_t *)(X.P + xf.key_off);
+                const __attribute__((address_space(3))) uint64_t *kw =
+                    (const __attribute__((address_space(3))) uint64_t *)(X.P + koff);
                 uint32_t i = 0;
-                for (; i + 8 <= xf.key_len; i += 8) w.wle(kw[i >> 3], 8);
-                if (i < xf.key_len) w.wle(kw[i >> 3], xf.key_len - i);
-            } else if (kstr) {
-                w.w8('"');
-                if (xk) emit_quoted(w, src, (int64_t)aux + 4, kn);
-                else fast_copy(src, (int64_t)aux + 4, (int64_t)kn, w);
-                w.wle('"' | (':' << 8), 2);
-            } else if (keym) {
+                for (; i + 8 <= klen; i += 8) w.wle(kw[i >> 3], 8);
+                if (i < klen) w.wle(kw[i >> 3], klen - i);
+            } else if (knum) {
                 rk.flush(w);
             }
-            if (act && !isval) {
-                w.w8(kind == TK_OPEN_OBJ ? '{' : kind == TK_OPEN_ARR ? '[' : kind == TK_CLOSE_OBJ ? '}' : ']');
-            } else if (isstr) {
-                w.w8('"');
-                if (!chunked) {
-                    if (isbin) emit_base64(w, src, (int64_t)pos + 4, vn);
-                    else if (xv) emit_quoted(w, src, (int64_t)pos + 4, vn);
-                    else fast_copy(src, (int64_t)pos + 4, (int64_t)vn, w);
-                    w.w8('"');
+#pragma nounroll
+            for (uint32_t it = 0; it < 2; it++) {
+                if (it == 1) { /* the value: brackets and numbers first */
+                    if (act && !isval) w.w8(kind == TK_OPEN_OBJ ? '{' : kind == TK_OPEN_ARR ? '[' : kind == TK_CLOSE_OBJ ? '}' : ']');
+                    else if (vnum) rv.flush(w);
                 }
-            } else if (isval) {
-                rv.flush(w);
+                const bool has = it == 0 ? kstr : isstr;
+                if (!ballot(has)) continue;
+                if (has) {
+                    const bool serial = it == 0 ? xk != 0 : !tasks;
+                    const uint32_t n = it == 0 ? kn : vn;
+                    w.w8('"');
+                    if (serial) {
+                        emit_quoted(w, src, (int64_t)(it == 0 ? aux : pos) + 4, n);
+                    } else { /* the tasks write the n body bytes (or their base64) */
+                        const uint64_t skip = it == 1 && isbin ? (uint64_t)(vn + 2) / 3 * 4 : n;
+                        w.finish();
+                        wb += w.len + skip;
+                        w.init(ob + wb);
+                    }
+                    if (it == 0) w.wle('"' | (':' << 8), 2);
+                    else w.w8('"');
+                }
             }
             w.finish();
-            if (chunked) {
-                WOut q; /* the closing quote after the body */
-                q.init(ob + at + ln - 1);
-                q.w8('"');
-                q.finish();
-            }
         }
-        /* chunked bodies: copy / base64 tasks over the wave */
+        /* bodies without escapes -- map key text, string values (copies) --
+         * and binary values (base64): tasks over the wave */
         {
-            const uint32_t nch = !chunked ? 0u : isbin ? (vn + T2W_B64 - 1) / T2W_B64 : (vn + T2W_CH - 1) / T2W_CH;
-            const uint32_t cinc = wave_incl_sum(nch, lane);
+            const uint32_t kcn = kstr && !xk ? (kn + T2W_CH - 1) / T2W_CH : 0u;
+            const uint32_t vcn = !tasks ? 0u : isbin ? (vn + T2W_B64 - 1) / T2W_B64 : (vn + T2W_CH - 1) / T2W_CH;
+            const uint32_t cinc = wave_incl_sum(kcn + vcn, lane);
             const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)cinc, 63);
             if (T) {
                 L.cinc[lane] = cinc;
-                L.cs[lane] = pos + 4;
-                L.cn[lane] = vn | (isbin ? 0x80000000u : 0u);
-                L.cvs[lane] = (uint32_t)(at + ln - vlen + 1); /* after the opening quote */
+                L.ck[lane] = kcn;
+                L.cs[lane] = aux + 4;                                      /* key text source */
+                L.cn[lane] = (uint32_t)(at + (comma ? 1u : 0u) + 1);       /* key text output */
+                L.cvs[lane] = pos + 4;                                     /* value body source */
+                L.cvn[lane] = (uint32_t)(at + ln - vlen + 1);              /* value body output */
+                L.xk[lane] = kn;
+                L.xv[lane] = vn | (isbin ? 0x80000000u : 0u);
                 __builtin_amdgcn_wave_barrier();
                 for (uint32_t c = lane; c < T; c += 64) {
                     uint32_t l = 0;
 #pragma unroll
                     for (uint32_t step = 32; step; step >>= 1)
                         if (L.cinc[l + step - 1] <= c) l += step;
-                    const uint32_t k = c - (l ? L.cinc[l - 1] : 0u);
-                    const uint32_t bn = L.cn[l], blen = bn & 0x7FFFFFFFu;
+                    const uint32_t own = c - (l ? L.cinc[l - 1] : 0u);
+                    const bool iskey = own < L.ck[l];
+                    const uint32_t k = iskey ? own : own - L.ck[l];
+                    const uint32_t bn = iskey ? L.xk[l] : L.xv[l], blen = bn & 0x7FFFFFFFu;
+                    const bool bin = !iskey && (bn >> 31);
+                    const uint32_t step = bin ? T2W_B64 : T2W_CH;
+                    const uint32_t s0 = k * step, n = blen - s0 < step ? blen - s0 : step;
+                    const uint64_t dst = (iskey ? L.cn[l] : L.cvn[l]) + (uint64_t)k * (bin ? T2W_B64 / 3 * 4 : T2W_CH);
+                    const int64_t src0 = (int64_t)(iskey ? L.cs[l] : L.cvs[l]) + s0;
                     WOut w;
-                    if (bn >> 31) {
-                        const uint32_t s0 = k * T2W_B64, n = blen - s0 < T2W_B64 ? blen - s0 : T2W_B64;
-                        w.init(ob + L.cvs[l] + (uint64_t)k * (T2W_B64 / 3 * 4));
-                        emit_base64(w, src, (int64_t)L.cs[l] + s0, (int64_t)n);
-                    } else {
-                        const uint32_t s0 = k * T2W_CH, n = blen - s0 < T2W_CH ? blen - s0 : T2W_CH;
-                        w.init(ob + L.cvs[l] + s0);
-                        fast_copy(src, (int64_t)L.cs[l] + s0, (int64_t)n, w);
-                    }
+                    w.init(ob + dst);
+                    if (bin) emit_base64(w, src, src0, (int64_t)n);
+                    else fast_copy(src, src0, (int64_t)n, w);
                     w.finish();
                 }
             }
         }
         O += tot;
-        if (fin) break;
+        return true;
+}
+
+/* Up to 64 messages (one wave, msgs[0 .. nm)): every lane walks its message
+ * into its token region, then the wave formats the messages one by one, a
+ * page of 64 tokens at a time. Bailed messages are listed for the lane
+ * kernel. */
+template <class DV>
+DGI void t2w_batch(const T2JParams &P, const T2WParams &W, const DV &D,
+                   const __attribute__((address_space(3))) uint64_t *fx, const T2WSide &X, uint64_t mine,
+                   uint32_t nm, T2WLds &L, T2WFrame *frs, T2WTok *tokw,
+                   __attribute__((address_space(3))) uint64_t *mbuf, uint32_t lane)
+{
+    T2P_DECL
+    int32_t ntok = -1;
+    if (lane < nm) {
+        const uint64_t a = P.in_off[mine], b = P.in_off[mine + 1];
+        SrcT<glb_u64> s;
+        s.init((glb_u64 *)(const void *)(P.src + (a & ~7ull)), (int64_t)(a & 7), (int64_t)(b - a));
+        if (b - a > 0 && b - a <= 0x7FFFFFFF) ntok = t2w_walk(D, fx, s, frs + lane, tokw + (uint64_t)lane * T2W_TOKCAP,
+                                                                 P.root, P.opts);
     }
-    if (lane == 0) {
-        P.ret[m] = 0;
-        P.out_len[m] = (uint32_t)O;
+    T2P(0);
+#pragma nounroll
+    for (uint32_t i = 0; i < nm; i++) {
+        const int32_t nti = __builtin_amdgcn_readlane(ntok, (int)i);
+        const uint64_t m = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)mine, (int)i);
+        bool ok = nti >= 0;
+        if (ok) {
+            /* the message staged in the wave's LDS buffer when it fits (the
+             * pages read it at random), else read through L2; one generic
+             * instantiation for both (I-cache) */
+            const uint64_t a = P.in_off[m], b = P.in_off[m + 1];
+            const uint64_t words = (b - a + (a & 7) + 7) >> 3;
+            const uint64_t *base;
+            if (words + 2 <= T2W_MSG / 8) {
+                const glb_u64 *g = (const glb_u64 *)(const void *)(P.src + (a & ~7ull));
+                for (uint64_t j = lane; j < words; j += 64) mbuf[j] = g[j];
+                if (lane < 2) mbuf[words + lane] = 0;
+                base = (const uint64_t *)(void *)mbuf;
+            } else {
+                base = (const uint64_t *)(const void *)(P.src + (a & ~7ull));
+            }
+            __builtin_amdgcn_wave_barrier();
+            SrcT<const uint64_t> src;
+            src.init(base, (int64_t)(a & 7), (int64_t)(b - a));
+            const uint64_t oa = P.out_off[m], cap = P.out_off[m + 1] - oa;
+            gu8 *ob = (gu8 *)(void *)(P.out + oa);
+            uint64_t O = 0;
+            const T2WTok *tk = tokw + (uint64_t)i * T2W_TOKCAP;
+            for (int32_t base = 0; base < nti && ok; base += 64)
+                ok = t2w_page(P, D, X, L, src, tk + base, lane < (uint32_t)(nti - base), ob, cap, O, lane);
+            if (ok && lane == 0) {
+                P.ret[m] = 0;
+                P.out_len[m] = (uint32_t)O;
+            }
+        }
+        if (!ok && lane == 0) W.bail_list[atomicAdd(W.bail_count, 1u)] = (uint32_t)m;
+        __builtin_amdgcn_wave_barrier(); /* mbuf is reused by the next message */
     }
-    return true;
+    T2P(4);
+    T2P_FLUSH();
 }
 
 }  // namespace dg

@@ -247,10 +247,11 @@ int dg_agg_submit(dg_agg *agg, const uint8_t *json, size_t len, int nonblock, dg
 int dg_agg_wait(dg_agg *agg, dg_agg_ticket *t, uint8_t *out, size_t out_cap, size_t *out_len, uint64_t *ret);
 /* batches flushed and messages converted so far */
 int dg_agg_stats(dg_agg *agg, uint64_t *batches, uint64_t *msgs);
-/* diagnostics: n <= 8 summed nanosecond counters (flusher waiting for a seal,
+/* diagnostics: n <= 12 summed counters (ns unless noted) (flusher waiting for a seal,
  * for a free batch, issuing a batch; completer waiting for the header, for
  * the packed bytes; seal to issued; issued to done; callers blocked in
- * dg_agg_wait) */
+ * dg_agg_wait; dg_agg_drive: time in submit, in wait, and the count of
+ * submits that met no open batch) */
 int dg_agg_profile(dg_agg *agg, uint64_t *out, int n);
 /* converts what is still queued, then stops the flusher (every ticket must
  * have been waited for) */

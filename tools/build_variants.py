@@ -10,7 +10,11 @@ for spec in sys.argv[1:]:
     name, flags = spec.split("=", 1)
     fl = tuple(flags.split(","))
     out = os.path.join(b.ROOT, "dynamicgo_amd", f"libdgj2t_{name}.so")
-    units = ("j2t_kern_flat.hip", "j2t_host.hip") if all(f.startswith("-DDG_FL_") for f in fl) else \
-        ("j2t_kern_wave.hip", "j2t_kern_wave5.hip", "j2t_host.hip", "j2t_kern_flat.hip")
+    if all(f.startswith("-DDG_FL_") for f in fl):
+        units = ("j2t_kern_flat.hip", "j2t_host.hip")
+    elif all(f.startswith("-DDG_T2W") for f in fl):
+        units = ("t2j_kern.hip",)
+    else:
+        units = ("j2t_kern_wave.hip", "j2t_kern_wave5.hip", "j2t_host.hip", "j2t_kern_flat.hip")
     b.build_hip(out=out, unit_flags={u: fl for u in units})
     print("built", out, flush=True)
