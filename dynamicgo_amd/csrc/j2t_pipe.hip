@@ -35,9 +35,18 @@
 #include <thread>
 #include <vector>
 
+#include <linux/membarrier.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
 #include "host_internal.h"
 
 namespace {
+
+/* the seal handshake's asymmetric fence: callers pay no StoreLoad fence per
+ * call; the flusher, once per batch, makes every thread of the process
+ * execute one (Linux membarrier, private expedited) */
+int sys_membarrier(int cmd) { return (int)syscall(__NR_membarrier, cmd, 0, 0); }
 
 using Clock = std::chrono::steady_clock;
 
@@ -49,18 +58,64 @@ __host__ __device__ inline uint64_t slot_off(uint64_t e, uint64_t i) { return (4
 
 /* ---------------- device: offsets of a batch ---------------- */
 
+typedef __attribute__((address_space(1))) uint8_t pgu8;
+typedef __attribute__((address_space(1))) uint64_t pgu64;
+
 /* one sub-batch of an aggregator batch: its messages are global indices
  * [gbase, gbase + n), its JSON bytes [jbase, jbase + bytes) */
 struct SubRef {
     uint64_t gbase, jbase, n;
+    const uint8_t *h;   /* the part's pinned host buffer: [ends (cap_n u64) | JSON] */
+    uint64_t bytes;     /* its JSON bytes */
 };
+
+/* Gather of an aggregator batch: block b copies part b's JSON from pinned
+ * host memory (16-byte aligned loads over the link, through LDS) to
+ * d_json + jbase, byte-exact at the words it shares with its neighbours,
+ * and its message ends to loc[gbase ..]; one launch instead of two copies
+ * per part. cap_n: the ends area of every part (u64 entries). */
+__global__ __launch_bounds__(256) void agg_gather_kernel(const SubRef *tab, uint64_t cap_n, uint8_t *d_json,
+                                                         uint64_t *loc)
+{
+    __shared__ __attribute__((aligned(16))) uint64_t st[4096 / 8 + 2];
+    const SubRef r = tab[blockIdx.x];
+    for (uint64_t j = threadIdx.x; j < r.n; j += 256) loc[r.gbase + j] = ((const uint64_t *)(const void *)r.h)[j];
+    const uint8_t *src = r.h + 8 * cap_n; /* 16-aligned (cap_n even, see dg_agg_create2) */
+    for (uint64_t c0 = 0; c0 < r.bytes; c0 += 4096) {
+        const uint64_t cn = r.bytes - c0 < 4096 ? r.bytes - c0 : 4096;
+        __syncthreads();
+        for (uint64_t k = threadIdx.x; k * 16 < cn; k += 256)
+            ((uint4 *)(void *)st)[k] = ((const uint4 *)(const void *)(src + c0))[k];
+        if (threadIdx.x < 2) st[(cn + 7) / 8 + threadIdx.x] = 0;
+        __syncthreads();
+        /* destination words of [jbase + c0, + cn) */
+        const uintptr_t d0 = (uintptr_t)(d_json + r.jbase + c0), wb = d0 & ~(uintptr_t)7;
+        const uint32_t lead = (uint32_t)(d0 - wb);
+        const uint64_t nw = (lead + cn + 7) / 8;
+        for (uint64_t k = threadIdx.x; k < nw; k += 256) {
+            const int64_t off = (int64_t)k * 8 - lead; /* chunk offset of the word's first byte */
+            pgu8 *w = (pgu8 *)(void *)(wb + k * 8);
+            if (off >= 0 && off + 8 <= (int64_t)cn) {
+                const uint32_t b = (uint32_t)off, sh = (b & 7) * 8;
+                const uint64_t lo = st[b >> 3], hi = st[(b >> 3) + 1];
+                *(pgu64 *)w = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+            } else {
+                for (int q = 0; q < 8; q++) {
+                    const int64_t o = off + q;
+                    if (o >= 0 && o < (int64_t)cn) w[q] = ((const uint8_t *)(const void *)st)[o];
+                }
+            }
+        }
+    }
+}
 
 /* in_off/out_off of an aggregator batch from its sub-batches' message ends
  * (loc[i] = end of global message i within its sub-batch's JSON) */
 __global__ __launch_bounds__(256) void agg_offsets_kernel(const SubRef *tab, uint32_t nsub, const uint64_t *loc,
-                                                          uint64_t N, uint64_t *in_off, uint64_t *out_off)
+                                                          uint64_t N, uint64_t *in_off, uint64_t *out_off, uint8_t *pad)
 {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (blockIdx.x == 0 && threadIdx.x < 64) pad[threadIdx.x] = 0; /* 64 zero bytes after the JSON */
     if (i >= N) return;
     uint32_t lo = 0, hi = nsub; /* the last sub-batch with gbase <= i */
     while (hi - lo > 1) {
@@ -188,6 +243,7 @@ struct alignas(128) Sub {
     std::atomic<uint32_t> busy{0}; /* 1 while the owner writes a message (the seal handshake) */
     std::atomic<uint32_t> n{0};    /* messages committed */
     uint64_t bytes = 0;            /* JSON bytes committed (owner-written) */
+    uint64_t maxlen = 0;           /* its longest message (owner-written) */
     uint8_t *h = nullptr;          /* pinned: [ends (cap_n u64) | JSON (cap_b + 64)] */
     uint64_t gbase = 0;            /* set at the seal: its first global index */
     std::atomic<uint32_t> left{0}; /* results not yet taken */
@@ -242,6 +298,7 @@ struct dg_agg {
     std::condition_variable cv_flush, cv_open, cv_done;
     std::deque<Batch *> inflight;
     bool stop = false;
+    bool asym = false; /* membarrier registered: callers use a compiler fence only */
     std::atomic<uint64_t> batches{0}, msgs{0};
     /* where the time goes (ns, summed; dg_agg_profile): 0 flusher waiting for
      * a seal, 1 waiting for a free batch, 2 in launch (uploads + kernel
@@ -314,7 +371,7 @@ int dg_agg::launch(Batch *x)
         u.left.store(k, std::memory_order_relaxed);
         if (!k) continue;
         u.gbase = N;
-        x->h_tab[nsub++] = SubRef{N, B, k};
+        x->h_tab[nsub++] = SubRef{N, B, k, u.h, u.bytes};
         N += k;
         B += u.bytes;
     }
@@ -329,27 +386,18 @@ int dg_agg::launch(Batch *x)
     if ((rc = grow(x->d_loc, x->loc_cap, N + 1))) return rc;
     if ((rc = grow_pinned(x->h_hdr, x->h_hdr_cap, 16 * N + 8))) return rc;
     if ((rc = grow_pinned(x->h_packed, x->h_packed_cap, slot_off(B, N) + 64))) return rc; /* >= any packed size */
-    /* uploads: each sub-batch's JSON and message ends, then the table */
+    /* the parts' longest message (the callers track it) picks the kernels */
     uint64_t max_len = 1;
-    for (uint32_t t = 0, s = 0; t < nsub; s++) {
-        Sub &u = x->sub[s];
-        const uint32_t k = u.n.load(std::memory_order_relaxed);
-        if (!k) continue;
-        const SubRef &r = x->h_tab[t++];
-        const uint64_t *e = u.ends();
-        uint64_t prev = 0;
-        for (uint32_t j = 0; j < k; j++) {
-            max_len = std::max<uint64_t>(max_len, e[j] - prev);
-            prev = e[j];
-        }
-        HIPCHK(hipMemcpyAsync(x->dv.d_json + r.jbase, u.h + 8 * cap_n, u.bytes, hipMemcpyHostToDevice, x->s));
-        HIPCHK(hipMemcpyAsync(x->d_loc + r.gbase, u.h, 8 * k, hipMemcpyHostToDevice, x->s));
-    }
-    HIPCHK(hipMemsetAsync(x->dv.d_json + B, 0, 64, x->s));
-    HIPCHK(hipMemcpyAsync(x->d_tab, x->h_tab, sizeof(SubRef) * nsub, hipMemcpyHostToDevice, x->s));
+    for (int s = 0; s < ns; s++)
+        if (x->sub[s].n.load(std::memory_order_relaxed)) max_len = std::max<uint64_t>(max_len, x->sub[s].maxlen);
+    /* one gather launch reads every part straight from pinned host memory
+     * (the table too), then the offsets */
+    hipLaunchKernelGGL(agg_gather_kernel, dim3(nsub), dim3(256), 0, x->s, x->h_tab, (uint64_t)cap_n, x->dv.d_json,
+                       x->d_loc);
+    HIPCHK(hipGetLastError());
     uint64_t *d_in = x->dv.d_off, *d_oo = d_in + N + 1;
-    hipLaunchKernelGGL(agg_offsets_kernel, dim3((uint32_t)((N + 255) / 256)), dim3(256), 0, x->s, x->d_tab, nsub,
-                       x->d_loc, N, d_in, d_oo);
+    hipLaunchKernelGGL(agg_offsets_kernel, dim3((uint32_t)((N + 255) / 256)), dim3(256), 0, x->s, x->h_tab, nsub,
+                       x->d_loc, N, d_in, d_oo, x->dv.d_json + B);
     HIPCHK(hipGetLastError());
     uint64_t *h_ret = (uint64_t *)(void *)x->h_hdr;
     return x->dv.convert(ctx, desc, root, flags, N, x->dv.d_json, d_in, d_oo, max_len, x->s, h_ret, x->h_packed,
@@ -400,6 +448,7 @@ void dg_agg::run_flusher()
         for (int s = 0; s < ns; s++) {
             y->sub[s].n.store(0, std::memory_order_relaxed);
             y->sub[s].bytes = 0;
+            y->sub[s].maxlen = 0;
         }
         y->t_first.store(0, std::memory_order_relaxed);
         y->seal_req.store(0, std::memory_order_relaxed);
@@ -412,6 +461,9 @@ void dg_agg::run_flusher()
             std::lock_guard<std::mutex> lk(mu);
             open.store(g + 1, std::memory_order_seq_cst);
         }
+        /* every caller either sees g + 1 or has its busy flag visible to
+         * launch() (the other half of the handshake in dg_agg_submit) */
+        if (asym) (void)sys_membarrier(MEMBARRIER_CMD_PRIVATE_EXPEDITED);
         cv_open.notify_all();
         uint64_t t2 = now_ns();
         prof[1].fetch_add(t2 - t1, std::memory_order_relaxed);
@@ -530,10 +582,11 @@ int dg_agg_create2(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, uint64_
     a->desc = desc;
     a->root = root_type;
     a->flags = flags;
-    a->cap_n = max_batch;
+    a->cap_n = (max_batch + 1) & ~1u; /* even: each part's JSON area stays 16-aligned */
     a->cap_b = max_bytes;
     a->max_wait = std::chrono::microseconds(max_wait_us);
     a->id = g_agg_ids.fetch_add(1);
+    a->asym = sys_membarrier(MEMBARRIER_CMD_REGISTER_PRIVATE_EXPEDITED) == 0;
     for (auto &r : a->ready) r.store(0, std::memory_order_relaxed);
     a->b = new Batch[AGG_INFLIGHT];
     int rc = DG_OK;
@@ -582,12 +635,18 @@ int dg_agg_submit(dg_agg *a, const uint8_t *json, size_t len, int nonblock, dg_a
         const uint64_t g = a->open.load(std::memory_order_seq_cst);
         Batch *x = &a->b[g % AGG_INFLIGHT];
         Sub &u = x->sub[s];
-        u.busy.store(1, std::memory_order_seq_cst);
+        if (a->asym) {
+            u.busy.store(1, std::memory_order_relaxed);
+            std::atomic_signal_fence(std::memory_order_seq_cst); /* the flusher's membarrier is the fence */
+        } else {
+            u.busy.store(1, std::memory_order_seq_cst);
+        }
         if (a->open.load(std::memory_order_seq_cst) == g) {
             const uint32_t j = u.n.load(std::memory_order_relaxed);
             if (j < a->cap_n && u.bytes + len <= a->cap_b) {
                 if (len) memcpy(u.h + 8 * a->cap_n + u.bytes, t->json, len);
                 u.bytes += len;
+                if (len > u.maxlen) u.maxlen = len;
                 u.ends()[j] = u.bytes;
                 u.n.store(j + 1, std::memory_order_release);
                 u.busy.store(0, std::memory_order_release);
