@@ -16,6 +16,7 @@ EXPORTS = ["dg_last_error", "dg_build_info", "dg_ctx_create", "dg_ctx_destroy", 
            "dg_desc_create",
            "dg_desc_create_device", "dg_desc_destroy", "dg_desc_root", "dg_j2t_batch_device",
            "dg_j2t_batch_device_ml", "dg_j2t_batch_device_hm", "dg_j2t_batch_device_iters",
+           "dg_j2t_batch_device_inflight",
            "dg_slot_bound", "dg_j2t_batch_host", "dg_j2t_batch_host_hm", "dg_j2t_do", "dg_pack_device", "dg_pack_device_scan", "dg_pack_device_framed", "dg_agg_create", "dg_agg_create2", "dg_agg_do",
            "dg_agg_submit", "dg_agg_wait", "dg_agg_stats", "dg_agg_profile", "dg_agg_destroy", "dg_agg_drive", "dg_j2t_pipeline_host", "dg_bench_device", "dg_desc_attach_t2j", "dg_t2j_slot_bound", "dg_t2j_batch_device", "dg_t2j_batch_device_ml",
            "dg_t2j_batch_host"]
@@ -63,6 +64,7 @@ def lib() -> C.CDLL:
         "dg_j2t_batch_device_hm": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, u32, vp, vp, vp, vp, vp, vp, vp, u64]),
         "dg_j2t_batch_host_hm": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, u32, vp, u64, vp, u64, vp, vp, P64]),
         "dg_j2t_batch_device_iters": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, vp, vp, vp, vp, vp, u64, C.c_int]),
+        "dg_j2t_batch_device_inflight": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, vp, C.c_int, vp, u64, C.c_int]),
         "dg_slot_bound": (u64, [u64]),
         "dg_j2t_batch_host": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, u64, vp, vp, P64]),
         "dg_j2t_do": (i32, [vp, vp, u32, C.c_char_p, sz, u64, vp, sz, C.POINTER(sz), P64]),

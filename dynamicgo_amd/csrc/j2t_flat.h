@@ -44,7 +44,10 @@
 namespace dg {
 
 constexpr uint32_t FL_G = 4;                     /* lanes per message in the structure phase */
-constexpr uint32_t FL_WAVES = 4;                 /* waves per block */
+#ifndef DG_FL_WAVES
+#define DG_FL_WAVES 4
+#endif
+constexpr uint32_t FL_WAVES = DG_FL_WAVES;       /* waves per block (the structure phase uses the first 4) */
 #ifndef DG_FL_FPW
 #define DG_FL_FPW 2
 #endif
@@ -530,7 +533,7 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
     if (!staged) {
         /* a span too long for the stage (large messages in between): each
          * message that fits its own 256-byte slot is copied there */
-        if (L.ok[m1]) {
+        if (tid < FL_G * FL_MPB && L.ok[m1]) {
             const uint64_t a = P.in_off[b0 + m1];
             const uint32_t nw = (uint32_t)(((a & 7) + L.n[m1] + 7) >> 3);
             const glb_u64 *gsrc = (const glb_u64 *)(const void *)P.json + (a >> 3);
@@ -548,7 +551,7 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
     /* ---- 1. structure: lane g of a message holds message bytes
      *      [64g, 64g+64) as 64-bit masks, bit b = byte 64g + b (quotes,
      *      commas, colons; backslashes only when the message has one) ---- */
-    {
+    if (tid < FL_G * FL_MPB) {
         const bool on = L.ok[m1] != 0;
         const uint32_t n = L.n[m1], lwa = L.lw[m1], a7 = lwa & 7, lw = lwa >> 3;
         const int32_t nv0 = on ? (int32_t)n - 64 * (int32_t)g : 0;

@@ -198,6 +198,9 @@ void dg_ctx_destroy(dg_ctx *c)
     if (c->ws_t2j_done) (void)hipEventDestroy(c->ws_t2j_done);
     (void)hipFree(c->ws_t2w);
     if (c->ws_t2w_done) (void)hipEventDestroy(c->ws_t2w_done);
+    for (hipStream_t x : c->side) (void)hipStreamDestroy(x);
+    for (hipEvent_t e : c->side_ev) (void)hipEventDestroy(e);
+    if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
     (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -571,6 +574,42 @@ int dg_j2t_batch_device_iters(dg_ctx *c, const dg_desc *d, uint32_t root, const 
         if (rc) return rc;
     }
     return DG_OK;
+}
+
+int dg_j2t_batch_device_inflight(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *d_json,
+                                 const uint64_t *d_in_off, uint64_t n, uint64_t flags, const uint64_t *d_out_off,
+                                 const dg_out_set *sets, int depth, void *stream, uint64_t max_len, int iters)
+{
+    if (!c || !d || !sets || depth < 1 || depth > 8 || iters < 0) return set_err(DG_E_INVALID, "bad args");
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s0 = stream ? (hipStream_t)stream : c->stream;
+    const int used = std::min(depth, std::max(iters, 1));
+    while ((int)c->side.size() < used - 1) {
+        hipStream_t x;
+        hipEvent_t e;
+        HIPCHK(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        c->side.push_back(x);
+        c->side_ev.push_back(e);
+    }
+    if (!c->fork_ev) HIPCHK(hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
+    if (used > 1) { /* fork: the side streams start after what `stream` holds */
+        HIPCHK(hipEventRecord(c->fork_ev, s0));
+        for (int j = 0; j < used - 1; j++) HIPCHK(hipStreamWaitEvent(c->side[j], c->fork_ev, 0));
+    }
+    int rc = DG_OK;
+    for (int k = 0; k < iters && !rc; k++) {
+        const int j = k % used;
+        const dg_out_set &o = sets[j];
+        rc = launch(c, d, root, d_json, d_in_off, n, flags, o.d_out, d_out_off, o.d_out_len, o.d_ret, o.d_pending,
+                    j ? c->side[j - 1] : s0, max_len);
+    }
+    for (int j = 0; j < used - 1; j++) { /* join, also after an error */
+        HIPCHK(hipEventRecord(c->side_ev[j], c->side[j]));
+        HIPCHK(hipStreamWaitEvent(s0, c->side_ev[j], 0));
+    }
+    return rc;
 }
 
 /* dg_pack_device_scan / _framed without the context lock (the caller holds it) */

@@ -344,10 +344,14 @@ DGI int32_t t2w_walk(const DV &D, const __attribute__((address_space(3))) uint64
 #define T2P_DECL uint64_t t2p_t = __builtin_readcyclecounter(); uint64_t t2p_acc[6] = {0};
 #define T2P(k) do { uint64_t t_ = __builtin_readcyclecounter(); t2p_acc[k] += t_ - t2p_t; t2p_t = t_; } while (0)
 #define T2P_FLUSH() do { if (lane == 0 && P.stats) for (int k_ = 0; k_ < 6; k_++) atomicAdd(&P.stats[2 + k_], (unsigned long long)t2p_acc[k_]); } while (0)
+#define T2P_ARG , uint64_t &t2p_t, uint64_t *t2p_acc
+#define T2P_PASS , t2p_t, t2p_acc
 #else
 #define T2P_DECL
 #define T2P(k)
 #define T2P_FLUSH()
+#define T2P_ARG
+#define T2P_PASS
 #endif
 
 /* a number/bool at byte p of Thrift type tt as JSON in registers, through
@@ -387,7 +391,7 @@ DGI bool t2w_number(S &src, int64_t p, uint8_t tt, uint64_t opts, bool quote64, 
  * first token); O = the message's output bytes so far. false: bail. */
 template <class S, class DV>
 DGI bool t2w_page(const T2JParams &P, const DV &D, const T2WSide &X, T2WLds &L, S &src, const T2WTok *tok,
-                  bool act, gu8 *ob, uint64_t cap, uint64_t &O, uint32_t lane)
+                  bool act, gu8 *ob, uint64_t cap, uint64_t &O, uint32_t lane T2P_ARG)
 {
     const uint64_t opts = P.opts;
     const bool b64 = !(opts & DG_T2J_NO_BASE64);
@@ -439,6 +443,7 @@ DGI bool t2w_page(const T2JParams &P, const DV &D, const T2WSide &X, T2WLds &L, 
             }
         }
         const uint32_t xk = L.xk[lane], xv = L.xv[lane];
+        T2P(1);
         /* numbers in registers: the map key's (iteration 0), then the value's,
          * through one call site */
         RegOut rk, rv;
@@ -466,6 +471,7 @@ DGI bool t2w_page(const T2JParams &P, const DV &D, const T2WSide &X, T2WLds &L, 
             }
         }
         if (ballot(bad)) return false;
+        T2P(2);
         uint32_t klen = 0, koff = 0;
         if (keyf) {
             const dg_t2j_field xf = ldrec(&X.X[aux]);
@@ -534,6 +540,7 @@ DGI bool t2w_page(const T2JParams &P, const DV &D, const T2WSide &X, T2WLds &L, 
             }
             w.finish();
         }
+        T2P(3);
         /* bodies without escapes -- map key text, string values (copies) --
          * and binary values (base64): tasks over the wave */
         {
@@ -574,6 +581,7 @@ DGI bool t2w_page(const T2JParams &P, const DV &D, const T2WSide &X, T2WLds &L, 
             }
         }
         O += tot;
+        T2P(5);
         return true;
 }
 
@@ -625,7 +633,7 @@ DGI void t2w_batch(const T2JParams &P, const T2WParams &W, const DV &D,
             uint64_t O = 0;
             const T2WTok *tk = tokw + (uint64_t)i * T2W_TOKCAP;
             for (int32_t base = 0; base < nti && ok; base += 64)
-                ok = t2w_page(P, D, X, L, src, tk + base, lane < (uint32_t)(nti - base), ob, cap, O, lane);
+                ok = t2w_page(P, D, X, L, src, tk + base, lane < (uint32_t)(nti - base), ob, cap, O, lane T2P_PASS);
             if (ok && lane == 0) {
                 P.ret[m] = 0;
                 P.out_len[m] = (uint32_t)O;

@@ -151,6 +151,26 @@ int dg_j2t_batch_device_iters(dg_ctx *ctx, const dg_desc *desc, uint32_t root_ty
                               const uint64_t *d_out_off, uint32_t *d_out_len, uint64_t *d_ret,
                               uint32_t *d_pending, void *stream, uint64_t max_len, int iters);
 
+/* One in-flight batch's outputs (dg_j2t_batch_device_inflight). */
+typedef struct dg_out_set {
+    uint8_t *d_out;      /* slot arena, laid out by the shared d_out_off */
+    uint32_t *d_out_len;
+    uint64_t *d_ret;
+    uint32_t *d_pending;
+} dg_out_set;
+
+/* `iters` complete conversions of the batch with up to `depth` (1..8) of them
+ * in flight at once: conversion k writes sets[k % depth] on the context's
+ * k % depth-th stream (stream 0 = `stream`; the others are the context's own,
+ * forked from `stream` at the call and joined back into it before return, so
+ * work enqueued on `stream` afterwards sees every conversion done). Batch k+1's
+ * kernels fill the CUs batch k's tail and list pass leave idle -- what a
+ * gateway with several batches from its aggregator in flight runs. depth 1 is
+ * dg_j2t_batch_device_iters. */
+int dg_j2t_batch_device_inflight(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, const uint8_t *d_json,
+                                 const uint64_t *d_in_off, uint64_t n, uint64_t flags, const uint64_t *d_out_off,
+                                 const dg_out_set *sets, int depth, void *stream, uint64_t max_len, int iters);
+
 /* Output-slot size the device path uses by default for a message of len bytes. */
 uint64_t dg_slot_bound(uint64_t len);
 

@@ -239,3 +239,42 @@ def test_batch_device_iters_vs_oracle(cfg):
             b.out_off.data_ptr(), b.out_len.data_ptr(), b.ret.data_ptr(), None, st, ml, 3))
         torch.cuda.synchronize()
         assert b.results() == _oracle_all(fl, msgs)
+
+
+@pytest.mark.parametrize("cfg", ["c2", "c5mix"])
+@pytest.mark.parametrize("depth", [2, 3])
+def test_batch_device_inflight_vs_oracle(cfg, depth):
+    """dg_j2t_batch_device_inflight (the bench's timed steps): `depth`
+    conversions in flight on the context's streams, each into its own output
+    set; every set holds exactly the oracle's output, and work enqueued on the
+    caller's stream afterwards sees all of them done (the join)."""
+    import torch
+    rng = random.Random(78)
+    if cfg == "c2":
+        td, msgs = W.simple_desc(), W.gen_flat_batch(rng, 3000)
+    else:
+        td, msgs = W.mixed_desc(), W.gen_mixed_batch(rng, 1500, large_scale=0.05)
+    fl = T.flatten(td)
+    ctx = conv.default_context()
+    dh = ctx.desc(fl)
+    bs = [DevBatch(msgs) for _ in range(depth)]
+    pend = [torch.zeros(4, dtype=torch.int32, device="cuda:0") for _ in range(depth)]
+    for b in bs:
+        b.out.zero_()
+        b.ret.fill_(-1)
+    sets = (C.c_void_p * (4 * depth))(*[p for b, pd in zip(bs, pend)
+                                          for p in (b.out.data_ptr(), b.out_len.data_ptr(), b.ret.data_ptr(),
+                                                    pd.data_ptr())])
+    s = torch.cuda.Stream()
+    _lib.check(_lib.lib().dg_j2t_batch_device_inflight(
+        ctx.h, dh, fl.root_type, bs[0].json.data_ptr(), bs[0].in_off.data_ptr(), bs[0].n, 1,
+        bs[0].out_off.data_ptr(), sets, depth, s.cuda_stream, bs[0].max_len, 2 * depth + 1))
+    # the join: copies enqueued on the caller's stream see every set finished
+    with torch.cuda.stream(s):
+        got = [(b.out.clone(), b.out_len.clone(), b.ret.clone()) for b in bs]
+    s.synchronize()
+    exp = _oracle_all(fl, msgs)
+    for b, (o, ol, r) in zip(bs, got):
+        b.out, b.out_len, b.ret = o, ol, r
+        assert b.results() == exp
+    assert all(int(p.sum().item()) == 0 for p in pend)

@@ -39,7 +39,7 @@ for it in range(3):
     torch.cuda.synchronize()
 _lib.check(L.dg_ctx_counters(ctx.h, cnt, 16, 1))
 c = list(cnt)
-names = ["walk (all lanes)", "-", "-", "-", "format", "-"]
+names = ["walk (all lanes)", "tok+esc scan", "numbers", "len+prefix+write", "stage+other", "copy tasks"]
 tot = sum(c[2:8])
 print(f"ok={(d_jr.cpu().numpy() == 0).sum()} of {n}")
 for k, nm in enumerate(names):
