@@ -69,18 +69,15 @@ DGI uint64_t dig8(uint32_t x)
     const uint32_t a = x / 10000, b = x - a * 10000;
     return (uint64_t)dig4(a) | ((uint64_t)dig4(b) << 32);
 }
-DGI uint32_t ndigits32(uint32_t x)
-{
-    uint32_t n = 1;
-    for (uint32_t p = 10; n < 10 && x >= p; p *= 10) n++;
-    return n;
-}
-/* x < 10^8 without leading zeros */
+/* x < 10^8 without leading zeros: the 8 digits with leading zeros, shifted
+ * past the leading '0' bytes (at least one digit stays) */
 template <class O>
 DGI void emit_small(O &o, uint32_t x)
 {
-    const uint32_t nd = ndigits32(x);
-    o.wle(dig8(x) >> ((8 - nd) << 3), nd);
+    const uint64_t d = dig8(x);
+    const uint64_t z = d ^ 0x3030303030303030ull; /* nonzero bytes: digits 1-9 */
+    const uint32_t lead = z ? ((uint32_t)__builtin_ctzll(z) >> 3) : 7u;
+    o.wle(d >> (lead << 3), 8 - lead);
 }
 /* u64toa (native/fastint.c:221-231): decimal, no leading zeros */
 template <class O>
@@ -111,14 +108,6 @@ DGI void emit_i64(O &o, int64_t v)
         o.w8('-');
         emit_u64(o, 0ull - (uint64_t)v);
     }
-}
-
-/* decimal digits of v (1..17; the reference's misnamed ctz10) */
-DGI uint32_t ndigits64(uint64_t v)
-{
-    uint32_t n = 1;
-    for (uint64_t p = 10; n < 20 && v >= p; p *= 10) n++;
-    return n;
 }
 
 /* Schubfach: the shortest decimal sig * 10^exp in the rounding interval of
@@ -165,14 +154,52 @@ DGI void f64_to_dec(uint64_t rsig, int32_t rexp, uint64_t c, int32_t q, uint64_t
     dexp = k;
 }
 
-/* the digits of sig (cnt of them, <= 17) into d[0..cnt) */
-DGI void sig_digits(uint64_t sig, uint32_t cnt, uint8_t *d)
-{
-    for (int32_t i = (int32_t)cnt - 1; i >= 0; i--) {
-        const uint64_t q = sig / 10;
-        d[i] = (uint8_t)('0' + (sig - q * 10));
-        sig = q;
+/* the decimal digits of sig (< 10^17) as a 24-byte ASCII string with
+ * leading zeros, held in three words (byte i of the string = byte i & 7 of
+ * word i >> 3), and the positions of its first and last nonzero digits */
+struct Dig24 {
+    uint64_t w0, w1, w2;
+    uint32_t first, last;
+    DGI void init(uint64_t sig)
+    {
+        const uint64_t a = sig / 100000000ull;
+        const uint32_t b = (uint32_t)(sig - a * 100000000ull);
+        const uint32_t a1 = (uint32_t)(a / 100000000ull), a0 = (uint32_t)(a - (uint64_t)a1 * 100000000ull);
+        w0 = dig8(a1);
+        w1 = dig8(a0);
+        w2 = dig8(b);
+        const uint64_t z0 = w0 ^ 0x3030303030303030ull, z1 = w1 ^ 0x3030303030303030ull,
+                       z2 = w2 ^ 0x3030303030303030ull;
+        first = z0 ? (uint32_t)__builtin_ctzll(z0) >> 3
+                   : z1 ? 8 + ((uint32_t)__builtin_ctzll(z1) >> 3) : 16 + ((uint32_t)__builtin_ctzll(z2 | (1ull << 63)) >> 3);
+        last = z2 ? 16 + ((63 - (uint32_t)__builtin_clzll(z2)) >> 3)
+                  : z1 ? 8 + ((63 - (uint32_t)__builtin_clzll(z1)) >> 3) : ((63 - (uint32_t)__builtin_clzll(z0 | 1)) >> 3);
     }
+    /* string bytes [from, from + len) (from + len <= 24): the string shifted
+     * by `from` bytes, straight-line (no indexed words: they would live in
+     * scratch), then up to three writes */
+    template <class O>
+    DGI void put(O &o, uint32_t from, uint32_t len) const
+    {
+        const uint32_t k = from >> 3, b = (from & 7) << 3;
+        const uint64_t x0 = k == 0 ? w0 : k == 1 ? w1 : w2, x1 = k == 0 ? w1 : k == 1 ? w2 : 0ull,
+                       x2 = k == 0 ? w2 : 0ull;
+        const uint64_t s0 = b ? (x0 >> b) | (x1 << (64 - b)) : x0, s1 = b ? (x1 >> b) | (x2 << (64 - b)) : x1,
+                       s2 = b ? x2 >> b : x2;
+        if (len) o.wle(s0, len < 8 ? len : 8u);
+        if (len > 8) o.wle(s1, len - 8 < 8 ? len - 8 : 8u);
+        if (len > 16) o.wle(s2, len - 16);
+    }
+};
+
+/* k <= 24 ASCII zeros */
+template <class O>
+DGI void put_zeros(O &o, uint32_t k)
+{
+    const uint64_t z = 0x3030303030303030ull;
+    if (k) o.wle(z, k < 8 ? k : 8u);
+    if (k > 8) o.wle(z, k - 8 < 8 ? k - 8 : 8u);
+    if (k > 16) o.wle(z, k - 16);
 }
 
 /* f64toa (native/fastfloat.c:349-404) for a finite double: the shortest
@@ -206,51 +233,48 @@ DGI void emit_f64(O &o, double fp)
     uint64_t sig;
     int32_t exp;
     f64_to_dec(rsig, rexp, c, q, sig, exp);
-    const uint32_t cnt = ndigits64(sig);
+    /* the digits as words: d[i] = string byte D.first + i */
+    Dig24 D;
+    D.init(sig);
+    const uint32_t cnt = 24 - D.first;
     const int32_t dot = (int32_t)cnt + exp;
     const int32_t sci = dot - 1;
-    uint8_t d[20];
-    sig_digits(sig, cnt, d);
-    uint32_t nd = cnt; /* digits without trailing zeros */
+    const uint32_t nd = D.last - D.first + 1; /* digits without trailing zeros */
     if (sci < -6 || sci > 20) { /* format_exponent :168-203 */
-        while (nd > 1 && d[nd - 1] == '0') nd--;
-        o.w8(d[0]);
+        D.put(o, D.first, 1);
         if (nd > 1) {
             o.w8('.');
-            for (uint32_t i = 1; i < nd; i++) o.w8(d[i]);
+            D.put(o, D.first + 1, nd - 1);
         }
-        o.w8('e');
         int32_t e = exp + (int32_t)cnt - 1;
         if (e < 0) {
-            o.w8('-');
+            o.wle('e' | ('-' << 8), 2);
             e = -e;
         } else {
-            o.w8('+');
+            o.wle('e' | ('+' << 8), 2);
         }
         emit_small(o, (uint32_t)e);
         return;
     }
     if (dot < (int32_t)cnt) { /* format_decimal :205-239 */
-        while (nd > 1 && d[nd - 1] == '0') nd--;
         if (dot <= 0) {
-            o.w8('0');
-            o.w8('.');
-            for (int32_t i = 0; i < -dot; i++) o.w8('0');
-            for (uint32_t i = 0; i < nd; i++) o.w8(d[i]);
+            o.wle('0' | ('.' << 8), 2);
+            put_zeros(o, (uint32_t)-dot);
+            D.put(o, D.first, nd);
             return;
         }
         if ((int32_t)nd > dot) {
-            for (int32_t i = 0; i < dot; i++) o.w8(d[i]);
+            D.put(o, D.first, (uint32_t)dot);
             o.w8('.');
-            for (uint32_t i = (uint32_t)dot; i < nd; i++) o.w8(d[i]);
+            D.put(o, D.first + (uint32_t)dot, nd - (uint32_t)dot);
         } else {
-            for (uint32_t i = 0; i < nd; i++) o.w8(d[i]);
-            for (int32_t i = (int32_t)nd; i < dot; i++) o.w8('0');
+            D.put(o, D.first, nd);
+            put_zeros(o, (uint32_t)dot - nd);
         }
         return;
     }
-    for (uint32_t i = 0; i < cnt; i++) o.w8(d[i]); /* integer digits, then zeros up to the point */
-    for (int32_t i = (int32_t)cnt; i < dot; i++) o.w8('0');
+    D.put(o, D.first, cnt); /* integer digits, then zeros up to the point */
+    put_zeros(o, (uint32_t)(dot - (int32_t)cnt));
 }
 
 /* quote (native/parsing.c:487, flags 0) of src[s0, s0+n): 8 bytes per step

@@ -171,14 +171,22 @@ struct T2WTok {
     uint32_t kind; /* TK_* | TKF_* | map key ttype << 8 */
 };
 constexpr uint32_t T2W_TOKCAP = 192; /* tokens per message (more: the lane kernel) */
+constexpr uint32_t T2W_RING = 8;     /* tokens a walker keeps in LDS before writing them out together */
 constexpr uint32_t T2W_BD = 3;       /* frames kept in LDS per lane (the innermost is in registers) */
 
 /* One lane walks its whole message (doRecurse's order, conv/t2j/impl.go:
  * 189-393) into tokens: returns the count, or -1 to bail. Parent frames
- * live in LDS at frs[d * T2W_MPT] (d < T2W_BD), the innermost in registers. */
+ * live in LDS at frs[d * T2W_MPT] (d < T2W_BD), the innermost in registers.
+ * Tokens collect in the lane's LDS ring (ring[j * T2W_MPT], j < T2W_RING)
+ * and go to global memory T2W_RING at a time: a global store ahead of the
+ * walk's next (dependent) load would make that load wait for the store's
+ * acknowledgement too (one vmcnt counts both). */
+typedef uint32_t tok_v4 __attribute__((ext_vector_type(4))); /* a token as one 16-byte LDS word */
+typedef __attribute__((address_space(3))) tok_v4 lds_tok;
+static_assert(T2W_RING * T2W_MPT * sizeof(T2WTok) <= T2W_MSG && T2W_TOKCAP % T2W_RING == 0, "ring in the stage");
 template <class S, class DV>
 DGI int32_t t2w_walk(const DV &D, const __attribute__((address_space(3))) uint64_t *fx, S &src,
-                     T2WFrame *frs, T2WTok *tok, uint32_t root, uint64_t opts)
+                     T2WFrame *frs, T2WTok *tok, lds_tok *ring, uint32_t root, uint64_t opts)
 {
     const int64_t n = src.n;
     int64_t p = 0;
@@ -186,12 +194,17 @@ DGI int32_t t2w_walk(const DV &D, const __attribute__((address_space(3))) uint64
     T2WFrame cur{};
     auto emit = [&](uint32_t kind, uint32_t pos, uint32_t aux, uint32_t td, uint32_t kt) -> bool {
         if (nt >= T2W_TOKCAP) return false;
-        T2WTok t;
-        t.pos = pos;
-        t.aux = aux;
-        t.td = td;
-        t.kind = kind | (kt << 8);
-        tok[nt++] = t;
+        tok_v4 t;
+        t.x = pos;
+        t.y = aux;
+        t.z = td;
+        t.w = kind | (kt << 8);
+        ring[(nt % T2W_RING) * T2W_MPT] = t;
+        nt++;
+        if (nt % T2W_RING == 0) {
+#pragma unroll
+            for (uint32_t j = 0; j < T2W_RING; j++) ((tok_v4 *)(void *)tok)[nt - T2W_RING + j] = ring[j * T2W_MPT];
+        }
         return true;
     };
     /* a value of type td (ttype tt) at p: scalars and strings become one
@@ -337,6 +350,7 @@ DGI int32_t t2w_walk(const DV &D, const __attribute__((address_space(3))) uint64
             if (!value(cur.etd, cur.ett & 0xFF, flags, (uint32_t)kp, kt)) return -1;
         }
     }
+    for (uint32_t j = nt & ~(T2W_RING - 1); j < nt; j++) ((tok_v4 *)(void *)tok)[j] = ring[(j % T2W_RING) * T2W_MPT];
     return (int32_t)nt;
 }
 
@@ -601,9 +615,11 @@ DGI void t2w_batch(const T2JParams &P, const T2WParams &W, const DV &D,
         const uint64_t a = P.in_off[mine], b = P.in_off[mine + 1];
         SrcT<glb_u64> s;
         s.init((glb_u64 *)(const void *)(P.src + (a & ~7ull)), (int64_t)(a & 7), (int64_t)(b - a));
+        /* the walk's token rings live in the message stage (unused until the formatting) */
         if (b - a > 0 && b - a <= 0x7FFFFFFF) ntok = t2w_walk(D, fx, s, frs + lane, tokw + (uint64_t)lane * T2W_TOKCAP,
-                                                                 P.root, P.opts);
+                                                                 (lds_tok *)(void *)mbuf + lane, P.root, P.opts);
     }
+    __builtin_amdgcn_wave_barrier();
     T2P(0);
 #pragma nounroll
     for (uint32_t i = 0; i < nm; i++) {
