@@ -184,11 +184,26 @@ constexpr uint32_t T2W_BD = 3;       /* frames kept in LDS per lane (the innermo
 typedef uint32_t tok_v4 __attribute__((ext_vector_type(4))); /* a token as one 16-byte LDS word */
 typedef __attribute__((address_space(3))) tok_v4 lds_tok;
 static_assert(T2W_RING * T2W_MPT * sizeof(T2WTok) <= T2W_MSG && T2W_TOKCAP % T2W_RING == 0, "ring in the stage");
+/* bytes [p, p + 16) of the message as two little-endian words: three
+ * aligned words read at once (the third only when it lies within the 16
+ * readable bytes past the message, wmax) */
+template <class S>
+DGI void t2w_win(const S &src, int64_t p, int64_t wmax, uint64_t &lo, uint64_t &hi)
+{
+    const int64_t b = src.off0 + p, k = b >> 3;
+    const uint32_t sh = (uint32_t)(b & 7) << 3;
+    const uint64_t a0 = src.w8[k], a1 = src.w8[k + 1], a2r = src.w8[k + 2 <= wmax ? k + 2 : wmax];
+    const uint64_t a2 = k + 2 <= wmax ? a2r : 0ull;
+    lo = sh ? (a0 >> sh) | (a1 << (64 - sh)) : a0;
+    hi = sh ? (a1 >> sh) | (a2 << (64 - sh)) : a1;
+}
+
 template <class S, class DV>
 DGI int32_t t2w_walk(const DV &D, const __attribute__((address_space(3))) uint64_t *fx, S &src,
                      T2WFrame *frs, T2WTok *tok, lds_tok *ring, uint32_t root, uint64_t opts)
 {
     const int64_t n = src.n;
+    const int64_t wmax = (src.off0 + n + 8) >> 3; /* the last word inside the 16 readable bytes past the end */
     int64_t p = 0;
     uint32_t sp = 0, nt = 0;
     T2WFrame cur{};
@@ -207,9 +222,10 @@ DGI int32_t t2w_walk(const DV &D, const __attribute__((address_space(3))) uint64
         }
         return true;
     };
-    /* a value of type td (ttype tt) at p: scalars and strings become one
-     * token (p moves past them), containers an open token and a frame */
-    auto value = [&](uint32_t td, uint32_t tt, uint32_t flags, uint32_t aux, uint32_t kt) -> bool {
+    /* a value of type td (ttype tt) at p, whose first 8 bytes are w: scalars
+     * and strings become one token (p moves past them), containers an open
+     * token and a frame */
+    auto value = [&](uint32_t td, uint32_t tt, uint32_t flags, uint32_t aux, uint32_t kt, uint64_t w) -> bool {
         const uint32_t fs = num_bytes((uint8_t)tt) ? num_bytes((uint8_t)tt) : tt == DG_T_BOOL ? 1u : 0u;
         if (fs) {
             if (p + fs > n || !emit(TK_VAL | flags, (uint32_t)p, aux, td, kt)) return false;
@@ -218,7 +234,7 @@ DGI int32_t t2w_walk(const DV &D, const __attribute__((address_space(3))) uint64
         }
         if (tt == DG_T_STRING) {
             if (p + 4 > n) return false;
-            const int64_t sz = (int32_t)be_at(src, p, 4);
+            const int64_t sz = (int32_t)__builtin_bswap32((uint32_t)w);
             if (sz < 0 || p + 4 + sz > n || !emit(TK_VAL | flags, (uint32_t)p, aux, td, kt)) return false;
             p += 4 + sz;
             return true;
@@ -243,9 +259,9 @@ DGI int32_t t2w_walk(const DV &D, const __attribute__((address_space(3))) uint64
             ok_kind = TK_OPEN_OBJ;
         } else if (tt == DG_T_LIST || tt == DG_T_SET) {
             if (p + 5 > n) return false;
-            const uint64_t w = __builtin_bswap64(src.get8(p)); /* et | count (big-endian) */
-            const uint8_t et = (uint8_t)(w >> 56);
-            const int64_t cnt = (int32_t)(uint32_t)(w >> 24);
+            const uint64_t wb = __builtin_bswap64(w); /* et | count (big-endian) */
+            const uint8_t et = (uint8_t)(wb >> 56);
+            const int64_t cnt = (int32_t)(uint32_t)(wb >> 24);
             const dg_type e = ldrec(&D.T[t.elem]);
             if (cnt < 0 || et != e.ttype) return false;
             p += 5;
@@ -256,9 +272,9 @@ DGI int32_t t2w_walk(const DV &D, const __attribute__((address_space(3))) uint64
             ok_kind = TK_OPEN_ARR;
         } else if (tt == DG_T_MAP) {
             if (p + 6 > n) return false;
-            const uint64_t w = __builtin_bswap64(src.get8(p)); /* kt | vt | count */
-            const uint8_t k = (uint8_t)(w >> 56), v = (uint8_t)(w >> 48);
-            const int64_t cnt = (int32_t)(uint32_t)(w >> 16);
+            const uint64_t wb = __builtin_bswap64(w); /* kt | vt | count */
+            const uint8_t k = (uint8_t)(wb >> 56), v = (uint8_t)(wb >> 48);
+            const int64_t cnt = (int32_t)(uint32_t)(wb >> 16);
             const dg_type kd = ldrec(&D.T[t.key]), vd = ldrec(&D.T[t.elem]);
             if (cnt < 0 || k != kd.ttype || v != vd.ttype) return false;
             if (!(k == DG_T_STRING || num_bytes(k)) || k == DG_T_DOUBLE) return false; /* buildinTypeToKey's */
@@ -281,13 +297,17 @@ DGI int32_t t2w_walk(const DV &D, const __attribute__((address_space(3))) uint64
         sp--;
         if (sp) cur = frs[(sp - 1) * T2W_MPT];
     };
-    if (ldrec(&D.T[root]).ttype != DG_T_STRUCT || !value(root, DG_T_STRUCT, 0, 0, 0)) return -1;
+    if (ldrec(&D.T[root]).ttype != DG_T_STRUCT || !value(root, DG_T_STRUCT, 0, 0, 0, 0)) return -1;
+    /* one window read per step, whatever kind of step it is: the lanes of a
+     * wave are at different kinds of steps, and a read inside each branch
+     * would be waited for once per branch */
     while (sp) {
+        uint64_t lo, hi;
+        t2w_win(src, p, wmax, lo, hi);
         if (cur.kind == TF_STRUCT) {
             if (p + 1 > n) return -1;
-            const uint64_t w = src.get8(p); /* type, id (big-endian) */
             const uint64_t h = cur.n < cur.nf ? fx[cur.fb + cur.n] : 0ull; /* the predicted field */
-            const uint8_t t = (uint8_t)w;
+            const uint8_t t = (uint8_t)lo;             /* type, id (big-endian) */
             if (t == 0) { /* STOP: unset fields must write nothing */
                 if (cur.u && !unsets_silent(D, ldrec(&D.S[cur.st]), cur.u, opts)) return -1;
                 p += 1;
@@ -296,22 +316,22 @@ DGI int32_t t2w_walk(const DV &D, const __attribute__((address_space(3))) uint64
                 continue;
             }
             if (p + 3 > n) return -1;
-            const uint32_t id = (uint32_t)(((w >> 8) & 0xFF) << 8 | ((w >> 16) & 0xFF));
+            const uint32_t id = (uint32_t)(((lo >> 8) & 0xFF) << 8 | ((lo >> 16) & 0xFF));
             uint32_t k = cur.n;
             uint64_t v = h;
             if (cur.n >= cur.nf || fx_id(h) != id) { /* fields are sorted by id */
-                uint32_t lo = 0, hi = cur.nf;
+                uint32_t lo_ = 0, hi_ = cur.nf;
                 k = 0xFFFFFFFFu;
-                while (lo < hi) {
-                    const uint32_t mid = (lo + hi) >> 1;
+                while (lo_ < hi_) {
+                    const uint32_t mid = (lo_ + hi_) >> 1;
                     const uint64_t x = fx[cur.fb + mid];
                     if (fx_id(x) == id) {
                         k = mid;
                         v = x;
                         break;
                     }
-                    if (fx_id(x) < id) lo = mid + 1;
-                    else hi = mid;
+                    if (fx_id(x) < id) lo_ = mid + 1;
+                    else hi_ = mid;
                 }
                 if (k == 0xFFFFFFFFu) return -1; /* unknown field (skip or error): the lane kernel */
             }
@@ -322,7 +342,7 @@ DGI int32_t t2w_walk(const DV &D, const __attribute__((address_space(3))) uint64
             const uint32_t comma = cur.i ? TKF_COMMA : 0u;
             cur.i = 1;
             p += 3;
-            if (!value(fx_td(v), t, comma | TKF_KEYF, cur.fb + k, 0)) return -1;
+            if (!value(fx_td(v), t, comma | TKF_KEYF, cur.fb + k, 0, (lo >> 24) | (hi << 40))) return -1;
         } else {
             if (cur.i == cur.n) {
                 if (!emit(cur.kind == TF_LIST ? TK_CLOSE_ARR : TK_CLOSE_OBJ, 0, 0, 0, 0)) return -1;
@@ -333,21 +353,26 @@ DGI int32_t t2w_walk(const DV &D, const __attribute__((address_space(3))) uint64
             cur.i++;
             uint32_t flags = comma, kt = 0;
             int64_t kp = 0;
+            uint64_t vw = lo;
             if (cur.kind == TF_MAP) {
                 kt = (uint8_t)(cur.ett >> 16);
                 kp = p;
                 if (kt == DG_T_STRING) {
                     if (p + 4 > n) return -1;
-                    const int64_t sz = (int32_t)be_at(src, p, 4);
+                    const int64_t sz = (int32_t)__builtin_bswap32((uint32_t)lo);
                     if (sz < 0 || p + 4 + sz > n) return -1;
                     p += 4 + sz;
+                    uint64_t h2;
+                    t2w_win(src, p, wmax, vw, h2); /* the value after the key's body */
                 } else {
-                    if (p + num_bytes((uint8_t)kt) > n) return -1;
-                    p += num_bytes((uint8_t)kt);
+                    const uint32_t nb = num_bytes((uint8_t)kt);
+                    if (p + nb > n) return -1;
+                    p += nb;
+                    vw = nb >= 8 ? hi : (lo >> (8 * nb)) | (hi << (64 - 8 * nb));
                 }
                 flags |= TKF_KEYM;
             }
-            if (!value(cur.etd, cur.ett & 0xFF, flags, (uint32_t)kp, kt)) return -1;
+            if (!value(cur.etd, cur.ett & 0xFF, flags, (uint32_t)kp, kt, vw)) return -1;
         }
     }
     for (uint32_t j = nt & ~(T2W_RING - 1); j < nt; j++) ((tok_v4 *)(void *)tok)[j] = ring[(j % T2W_RING) * T2W_MPT];
