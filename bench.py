@@ -64,6 +64,7 @@ CONFIGS = {
 }
 AGG_METRIC = "conv/j2t BinaryConv.Do calls/s through the batching aggregator (host memory in/out), 16 threads"
 T2J_METRIC = "conv/t2j GB/s Thrift in + msgs/s, 64K-batch device-resident"
+DEFAULT_INFLIGHT = {"c5": 1}  # batches in flight in the timed steps (j2t configs)
 FLAGS = {"c2x": 0x7}  # default: conv.Options{} -> F_ALLOW_UNKNOWN (conv/j2t/conv.go:102-104)
 
 
@@ -99,7 +100,9 @@ def rank_workload(cfg: str, rank: int, world: int, workers: int = 1, c5_n: int =
     size = CONFIGS[cfg][1]
     if cfg == "c5":
         n = c5_n or size
-        if world > 1:  # generated once per node (/dev/shm), mapped by every rank
+        # generated once per node (/dev/shm), mapped by every rank; DG_C5_CACHE=1
+        # also at one rank (a profiler run: no generator pool under the tool)
+        if world > 1 or os.environ.get("DG_C5_CACHE"):
             a, off = c5_shared_arena(n, 45, c5_scale, gen_workers())
         else:
             a, off = W.gen_mixed_arena(n, 45, workers=workers, large_scale=c5_scale)
@@ -624,9 +627,9 @@ def main(argv=None):
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory end-to-end measurement")
-    ap.add_argument("--inflight", type=int, default=2,
-                    help="j2t configs: batches in flight in the timed steps (dg_j2t_batch_device_inflight); "
-                         "the serial (1) rate is reported beside it")
+    ap.add_argument("--inflight", type=int, default=None,
+                    help="j2t configs: batches in flight in the timed steps (dg_j2t_batch_device_inflight; default "
+                         "2, C5's 1M batch 1); the serial (1) rate is reported beside it")
     args = ap.parse_args(argv)
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -692,7 +695,10 @@ def main(argv=None):
     d_pend = torch.zeros(4, dtype=torch.int32, device=dev)
     stream = torch.cuda.Stream(dev)  # the kernels and the timing events share it
     torch.cuda.set_stream(stream)
-    depth = max(1, min(8, args.inflight))
+    # a 64K batch leaves CUs idle in its tail and list pass that the next
+    # batch fills; C5's 1M-message batch does not (measured: 2 in flight 4.73
+    # vs 4.45 ms per step)
+    depth = max(1, min(8, args.inflight if args.inflight is not None else DEFAULT_INFLIGHT.get(args.config, 2)))
     # one output set per batch in flight (set 0 = the serial leg's buffers)
     osets = [(d_out, d_ol, d_ret, d_pend)] + [
         (torch.empty_like(d_out), torch.zeros_like(d_ol), torch.zeros_like(d_ret), torch.zeros_like(d_pend))
