@@ -74,6 +74,16 @@ constexpr uint32_t FL_MAXTASK = 512;             /* chunk tasks per block (more:
 #define DG_FL_WPE 4 /* waves per SIMD the register budget is cut for: 128 VGPRs; LDS allows 4 blocks (16 waves) per CU */
 #endif
 
+#ifndef DG_FL_PERM
+#define DG_FL_PERM 0
+#endif
+/* the field (within a round) wave w converts as its h-th: w + 4h, or with
+ * DG_FL_PERM 1 a snake (w, then 7 - w) that pairs early with late fields */
+DGI uint32_t fl_slot(uint32_t w, uint32_t h)
+{
+    return DG_FL_PERM == 1 ? (h & 1 ? (h + 1) * FL_WAVES - 1 - w : h * FL_WAVES + w) : w + h * FL_WAVES;
+}
+
 /* ---- group (4 lanes, a DPP quad) collectives; converged code only ---- */
 #define DG_DPP(v, ctrl) ((uint32_t)__builtin_amdgcn_update_dpp(0, (int)(v), (ctrl), 0xF, 0xF, false))
 DGI uint32_t g4_incl_sum(uint32_t v, uint32_t g)
@@ -732,8 +742,8 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
             uint16_t *sz = &L.size[(r & 1) * FL_SLOTS * FL_MPB];
 #pragma unroll
             for (uint32_t h = 0; h < FL_FPW; h++) {
-                parse(r * FL_SLOTS + wave + h * FL_WAVES, F[h]);
-                sz[(wave + h * FL_WAVES) * FL_MPB + mm] = (uint16_t)F[h].size;
+                parse(r * FL_SLOTS + fl_slot(wave, h), F[h]);
+                sz[fl_slot(wave, h) * FL_MPB + mm] = (uint16_t)F[h].size;
             }
             FLP(4);
             __syncthreads();
@@ -748,7 +758,7 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
             for (uint32_t f = 0; f < FL_SLOTS; f++) {
                 const uint32_t v = sz[f * FL_MPB + mm];
 #pragma unroll
-                for (uint32_t h = 0; h < FL_FPW; h++) off[h] += f < wave + h * FL_WAVES ? v : 0u;
+                for (uint32_t h = 0; h < FL_FPW; h++) off[h] += f < fl_slot(wave, h) ? v : 0u;
                 tot += v;
             }
             nbytes += tot;

@@ -222,142 +222,94 @@ DGI int32_t t2w_walk(const DV &D, const __attribute__((address_space(3))) uint64
         }
         return true;
     };
-    /* a value of type td (ttype tt) at p, whose first 8 bytes are w: scalars
-     * and strings become one token (p moves past them), containers an open
-     * token and a frame */
-    auto value = [&](uint32_t td, uint32_t tt, uint32_t flags, uint32_t aux, uint32_t kt, uint64_t w) -> bool {
-        const uint32_t fs = num_bytes((uint8_t)tt) ? num_bytes((uint8_t)tt) : tt == DG_T_BOOL ? 1u : 0u;
-        if (fs) {
-            if (p + fs > n || !emit(TK_VAL | flags, (uint32_t)p, aux, td, kt)) return false;
-            p += fs;
-            return true;
-        }
-        if (tt == DG_T_STRING) {
-            if (p + 4 > n) return false;
-            const int64_t sz = (int32_t)__builtin_bswap32((uint32_t)w);
-            if (sz < 0 || p + 4 + sz > n || !emit(TK_VAL | flags, (uint32_t)p, aux, td, kt)) return false;
-            p += 4 + sz;
-            return true;
-        }
-        if (sp > T2W_BD) return false;
-        const dg_type t = ldrec(&D.T[td]);
-        T2WFrame f;
-        f.i = 0;
-        f.u = 0;
-        f.fb = f.nf = f.st = 0;
-        f.etd = f.ett = 0;
-        uint32_t ok_kind;
-        if (tt == DG_T_STRUCT) {
-            const dg_struct sd = ldrec(&D.S[t.st]);
-            if (sd.req_words != 1) return false;
-            f.kind = TF_STRUCT;
-            f.n = 0;
-            f.fb = sd.field_begin;
-            f.nf = sd.n_fields;
-            f.st = t.st;
-            f.u = D.R[sd.req_begin];
-            ok_kind = TK_OPEN_OBJ;
-        } else if (tt == DG_T_LIST || tt == DG_T_SET) {
-            if (p + 5 > n) return false;
-            const uint64_t wb = __builtin_bswap64(w); /* et | count (big-endian) */
-            const uint8_t et = (uint8_t)(wb >> 56);
-            const int64_t cnt = (int32_t)(uint32_t)(wb >> 24);
-            const dg_type e = ldrec(&D.T[t.elem]);
-            if (cnt < 0 || et != e.ttype) return false;
-            p += 5;
-            f.kind = TF_LIST;
-            f.n = (uint32_t)cnt;
-            f.etd = t.elem;
-            f.ett = e.ttype | ((uint32_t)e.flags << 8);
-            ok_kind = TK_OPEN_ARR;
-        } else if (tt == DG_T_MAP) {
-            if (p + 6 > n) return false;
-            const uint64_t wb = __builtin_bswap64(w); /* kt | vt | count */
-            const uint8_t k = (uint8_t)(wb >> 56), v = (uint8_t)(wb >> 48);
-            const int64_t cnt = (int32_t)(uint32_t)(wb >> 16);
-            const dg_type kd = ldrec(&D.T[t.key]), vd = ldrec(&D.T[t.elem]);
-            if (cnt < 0 || k != kd.ttype || v != vd.ttype) return false;
-            if (!(k == DG_T_STRING || num_bytes(k)) || k == DG_T_DOUBLE) return false; /* buildinTypeToKey's */
-            p += 6;
-            f.kind = TF_MAP;
-            f.n = (uint32_t)cnt;
-            f.etd = t.elem;
-            f.ett = vd.ttype | ((uint32_t)vd.flags << 8) | ((uint32_t)k << 16);
-            ok_kind = TK_OPEN_OBJ;
-        } else {
-            return false;
-        }
-        if (!emit(ok_kind | flags, 0, aux, td, kt)) return false;
+    auto push = [&](const T2WFrame &f) {
         if (sp) frs[(sp - 1) * T2W_MPT] = cur;
         cur = f;
         sp++;
-        return true;
     };
     auto pop = [&]() {
         sp--;
         if (sp) cur = frs[(sp - 1) * T2W_MPT];
     };
-    if (ldrec(&D.T[root]).ttype != DG_T_STRUCT || !value(root, DG_T_STRUCT, 0, 0, 0, 0)) return -1;
-    /* one window read per step, whatever kind of step it is: the lanes of a
-     * wave are at different kinds of steps, and a read inside each branch
-     * would be waited for once per branch */
+    /* the root struct */
+    {
+        const dg_type rt = ldrec(&D.T[root]);
+        if (rt.ttype != DG_T_STRUCT) return -1;
+        const dg_struct sd = ldrec(&D.S[rt.st]);
+        if (sd.req_words != 1 || !emit(TK_OPEN_OBJ, 0, 0, root, 0)) return -1;
+        T2WFrame f{};
+        f.kind = TF_STRUCT;
+        f.fb = sd.field_begin;
+        f.nf = sd.n_fields;
+        f.st = rt.st;
+        f.u = D.R[sd.req_begin];
+        push(f);
+    }
+    /* One step per token, with ONE window read, ONE value decoder and ONE
+     * emit: the 16 walkers of a wave sit at different kinds of steps, and the
+     * wave runs the union of their paths, so every duplicated site (a read,
+     * the token ring's flush) would be paid once per kind. */
     while (sp) {
         uint64_t lo, hi;
         t2w_win(src, p, wmax, lo, hi);
+        uint32_t ek = 0, eaux = 0, ekt = 0; /* the token: kind | flags, key, map key type */
+        uint32_t act = 0;                   /* 1: a closer (pop), 2: an opener (push) */
+        bool isv = false;                   /* a value follows at p: type vtd / vtt, first 8 bytes vw */
+        uint32_t vtd = 0, vtt = 0;
+        uint64_t vw = lo;
         if (cur.kind == TF_STRUCT) {
             if (p + 1 > n) return -1;
-            const uint64_t h = cur.n < cur.nf ? fx[cur.fb + cur.n] : 0ull; /* the predicted field */
-            const uint8_t t = (uint8_t)lo;             /* type, id (big-endian) */
-            if (t == 0) { /* STOP: unset fields must write nothing */
+            const uint8_t t = (uint8_t)lo; /* type, id (big-endian) */
+            if (t == 0) {                  /* STOP: unset fields must write nothing */
                 if (cur.u && !unsets_silent(D, ldrec(&D.S[cur.st]), cur.u, opts)) return -1;
                 p += 1;
-                if (!emit(TK_CLOSE_OBJ, 0, 0, 0, 0)) return -1;
-                pop();
-                continue;
-            }
-            if (p + 3 > n) return -1;
-            const uint32_t id = (uint32_t)(((lo >> 8) & 0xFF) << 8 | ((lo >> 16) & 0xFF));
-            uint32_t k = cur.n;
-            uint64_t v = h;
-            if (cur.n >= cur.nf || fx_id(h) != id) { /* fields are sorted by id */
-                uint32_t lo_ = 0, hi_ = cur.nf;
-                k = 0xFFFFFFFFu;
-                while (lo_ < hi_) {
-                    const uint32_t mid = (lo_ + hi_) >> 1;
-                    const uint64_t x = fx[cur.fb + mid];
-                    if (fx_id(x) == id) {
-                        k = mid;
-                        v = x;
-                        break;
+                ek = TK_CLOSE_OBJ;
+                act = 1;
+            } else {
+                if (p + 3 > n) return -1;
+                const uint64_t h = cur.n < cur.nf ? fx[cur.fb + cur.n] : 0ull; /* the predicted field */
+                const uint32_t id = (uint32_t)(((lo >> 8) & 0xFF) << 8 | ((lo >> 16) & 0xFF));
+                uint32_t k = cur.n;
+                uint64_t v = h;
+                if (cur.n >= cur.nf || fx_id(h) != id) { /* fields are sorted by id */
+                    uint32_t lo_ = 0, hi_ = cur.nf;
+                    k = 0xFFFFFFFFu;
+                    while (lo_ < hi_) {
+                        const uint32_t mid = (lo_ + hi_) >> 1;
+                        const uint64_t x = fx[cur.fb + mid];
+                        if (fx_id(x) == id) {
+                            k = mid;
+                            v = x;
+                            break;
+                        }
+                        if (fx_id(x) < id) lo_ = mid + 1;
+                        else hi_ = mid;
                     }
-                    if (fx_id(x) < id) lo_ = mid + 1;
-                    else hi_ = mid;
+                    if (k == 0xFFFFFFFFu) return -1; /* unknown field (skip or error): the lane kernel */
                 }
-                if (k == 0xFFFFFFFFu) return -1; /* unknown field (skip or error): the lane kernel */
+                if (fx_tt(v) != t) return -1;
+                if ((opts & DG_T2J_ENABLE_VM) && (fx_fl(v) & 0x80)) return -1;
+                cur.u &= ~(1ull << k);
+                cur.n = k + 1;
+                ek = (cur.i ? TKF_COMMA : 0u) | TKF_KEYF;
+                cur.i = 1;
+                p += 3;
+                eaux = cur.fb + k;
+                isv = true;
+                vtd = fx_td(v);
+                vtt = t;
+                vw = (lo >> 24) | (hi << 40);
             }
-            if (fx_tt(v) != t) return -1;
-            if ((opts & DG_T2J_ENABLE_VM) && (fx_fl(v) & 0x80)) return -1;
-            cur.u &= ~(1ull << k);
-            cur.n = k + 1;
-            const uint32_t comma = cur.i ? TKF_COMMA : 0u;
-            cur.i = 1;
-            p += 3;
-            if (!value(fx_td(v), t, comma | TKF_KEYF, cur.fb + k, 0, (lo >> 24) | (hi << 40))) return -1;
+        } else if (cur.i == cur.n) {
+            ek = cur.kind == TF_LIST ? TK_CLOSE_ARR : TK_CLOSE_OBJ;
+            act = 1;
         } else {
-            if (cur.i == cur.n) {
-                if (!emit(cur.kind == TF_LIST ? TK_CLOSE_ARR : TK_CLOSE_OBJ, 0, 0, 0, 0)) return -1;
-                pop();
-                continue;
-            }
-            const uint32_t comma = cur.i ? TKF_COMMA : 0u;
+            ek = cur.i ? TKF_COMMA : 0u;
             cur.i++;
-            uint32_t flags = comma, kt = 0;
-            int64_t kp = 0;
-            uint64_t vw = lo;
             if (cur.kind == TF_MAP) {
-                kt = (uint8_t)(cur.ett >> 16);
-                kp = p;
-                if (kt == DG_T_STRING) {
+                ekt = (uint8_t)(cur.ett >> 16);
+                eaux = (uint32_t)p;
+                if (ekt == DG_T_STRING) {
                     if (p + 4 > n) return -1;
                     const int64_t sz = (int32_t)__builtin_bswap32((uint32_t)lo);
                     if (sz < 0 || p + 4 + sz > n) return -1;
@@ -365,15 +317,87 @@ DGI int32_t t2w_walk(const DV &D, const __attribute__((address_space(3))) uint64
                     uint64_t h2;
                     t2w_win(src, p, wmax, vw, h2); /* the value after the key's body */
                 } else {
-                    const uint32_t nb = num_bytes((uint8_t)kt);
+                    const uint32_t nb = num_bytes((uint8_t)ekt);
                     if (p + nb > n) return -1;
                     p += nb;
                     vw = nb >= 8 ? hi : (lo >> (8 * nb)) | (hi << (64 - 8 * nb));
                 }
-                flags |= TKF_KEYM;
+                ek |= TKF_KEYM;
             }
-            if (!value(cur.etd, cur.ett & 0xFF, flags, (uint32_t)kp, kt, vw)) return -1;
+            isv = true;
+            vtd = cur.etd;
+            vtt = cur.ett & 0xFF;
         }
+        /* the value: scalars and strings are one token (p moves past them),
+         * containers an open token and a frame */
+        uint32_t epos = 0, etd = 0;
+        T2WFrame f;
+        if (isv) {
+            etd = vtd;
+            const uint32_t fs = num_bytes((uint8_t)vtt) ? num_bytes((uint8_t)vtt) : vtt == DG_T_BOOL ? 1u : 0u;
+            if (fs) {
+                if (p + fs > n) return -1;
+                epos = (uint32_t)p;
+                p += fs;
+            } else if (vtt == DG_T_STRING) {
+                if (p + 4 > n) return -1;
+                const int64_t sz = (int32_t)__builtin_bswap32((uint32_t)vw);
+                if (sz < 0 || p + 4 + sz > n) return -1;
+                epos = (uint32_t)p;
+                p += 4 + sz;
+            } else {
+                if (sp > T2W_BD) return -1;
+                const dg_type t = ldrec(&D.T[vtd]);
+                f.i = 0;
+                f.u = 0;
+                f.fb = f.nf = f.st = 0;
+                f.etd = f.ett = 0;
+                if (vtt == DG_T_STRUCT) {
+                    const dg_struct sd = ldrec(&D.S[t.st]);
+                    if (sd.req_words != 1) return -1;
+                    f.kind = TF_STRUCT;
+                    f.n = 0;
+                    f.fb = sd.field_begin;
+                    f.nf = sd.n_fields;
+                    f.st = t.st;
+                    f.u = D.R[sd.req_begin];
+                    ek |= TK_OPEN_OBJ;
+                } else if (vtt == DG_T_LIST || vtt == DG_T_SET) {
+                    if (p + 5 > n) return -1;
+                    const uint64_t wb = __builtin_bswap64(vw); /* et | count (big-endian) */
+                    const uint8_t et = (uint8_t)(wb >> 56);
+                    const int64_t cnt = (int32_t)(uint32_t)(wb >> 24);
+                    const dg_type e = ldrec(&D.T[t.elem]);
+                    if (cnt < 0 || et != e.ttype) return -1;
+                    p += 5;
+                    f.kind = TF_LIST;
+                    f.n = (uint32_t)cnt;
+                    f.etd = t.elem;
+                    f.ett = e.ttype | ((uint32_t)e.flags << 8);
+                    ek |= TK_OPEN_ARR;
+                } else if (vtt == DG_T_MAP) {
+                    if (p + 6 > n) return -1;
+                    const uint64_t wb = __builtin_bswap64(vw); /* kt | vt | count */
+                    const uint8_t k = (uint8_t)(wb >> 56), v = (uint8_t)(wb >> 48);
+                    const int64_t cnt = (int32_t)(uint32_t)(wb >> 16);
+                    const dg_type kd = ldrec(&D.T[t.key]), vd = ldrec(&D.T[t.elem]);
+                    if (cnt < 0 || k != kd.ttype || v != vd.ttype) return -1;
+                    if (!(k == DG_T_STRING || num_bytes(k)) || k == DG_T_DOUBLE) return -1; /* buildinTypeToKey's */
+                    p += 6;
+                    f.kind = TF_MAP;
+                    f.n = (uint32_t)cnt;
+                    f.etd = t.elem;
+                    f.ett = vd.ttype | ((uint32_t)vd.flags << 8) | ((uint32_t)k << 16);
+                    ek |= TK_OPEN_OBJ;
+                } else {
+                    return -1;
+                }
+                act = 2;
+            }
+        }
+        if (!emit(ek, epos, eaux, etd, ekt)) return -1;
+        if (act == 1) pop();
+        else if (act == 2) push(f);
     }
     for (uint32_t j = nt & ~(T2W_RING - 1); j < nt; j++) ((tok_v4 *)(void *)tok)[j] = ring[(j % T2W_RING) * T2W_MPT];
     return (int32_t)nt;
