@@ -79,24 +79,63 @@ DGI void emit_small(O &o, uint32_t x)
     const uint32_t lead = z ? ((uint32_t)__builtin_ctzll(z) >> 3) : 7u;
     o.wle(d >> (lead << 3), 8 - lead);
 }
-/* u64toa (native/fastint.c:221-231): decimal, no leading zeros */
+/* the decimal digits of sig (< 10^24) as a 24-byte ASCII string with
+ * leading zeros, held in three words (byte i of the string = byte i & 7 of
+ * word i >> 3), and the positions of its first and last nonzero digits */
+struct Dig24 {
+    uint64_t w0, w1, w2;
+    uint32_t first, last;
+    DGI void init(uint64_t sig)
+    {
+        const uint64_t a = sig / 100000000ull;
+        const uint32_t b = (uint32_t)(sig - a * 100000000ull);
+        const uint32_t a1 = (uint32_t)(a / 100000000ull), a0 = (uint32_t)(a - (uint64_t)a1 * 100000000ull);
+        w0 = dig8(a1);
+        w1 = dig8(a0);
+        w2 = dig8(b);
+        const uint64_t z0 = w0 ^ 0x3030303030303030ull, z1 = w1 ^ 0x3030303030303030ull,
+                       z2 = w2 ^ 0x3030303030303030ull;
+        first = z0 ? (uint32_t)__builtin_ctzll(z0) >> 3
+                   : z1 ? 8 + ((uint32_t)__builtin_ctzll(z1) >> 3) : 16 + ((uint32_t)__builtin_ctzll(z2 | (1ull << 63)) >> 3);
+        last = z2 ? 16 + ((63 - (uint32_t)__builtin_clzll(z2)) >> 3)
+                  : z1 ? 8 + ((63 - (uint32_t)__builtin_clzll(z1)) >> 3) : ((63 - (uint32_t)__builtin_clzll(z0 | 1)) >> 3);
+    }
+    /* string bytes [from, from + len) (from + len <= 24): the string shifted
+     * by `from` bytes, straight-line (no indexed words: they would live in
+     * scratch), then up to three writes */
+    template <class O>
+    DGI void put(O &o, uint32_t from, uint32_t len) const
+    {
+        const uint32_t k = from >> 3, b = (from & 7) << 3;
+        const uint64_t x0 = k == 0 ? w0 : k == 1 ? w1 : w2, x1 = k == 0 ? w1 : k == 1 ? w2 : 0ull,
+                       x2 = k == 0 ? w2 : 0ull;
+        const uint64_t s0 = b ? (x0 >> b) | (x1 << (64 - b)) : x0, s1 = b ? (x1 >> b) | (x2 << (64 - b)) : x1,
+                       s2 = b ? x2 >> b : x2;
+        if (len) o.wle(s0, len < 8 ? len : 8u);
+        if (len > 8) o.wle(s1, len - 8 < 8 ? len - 8 : 8u);
+        if (len > 16) o.wle(s2, len - 16);
+    }
+};
+
+/* k <= 24 ASCII zeros */
+template <class O>
+DGI void put_zeros(O &o, uint32_t k)
+{
+    const uint64_t z = 0x3030303030303030ull;
+    if (k) o.wle(z, k < 8 ? k : 8u);
+    if (k > 8) o.wle(z, k - 8 < 8 ? k - 8 : 8u);
+    if (k > 16) o.wle(z, k - 16);
+}
+
+/* u64toa (native/fastint.c:221-231): decimal, no leading zeros. Straight
+ * line (the 24-digit string, then its digits from the first nonzero one):
+ * lanes formatting numbers of different lengths take the same path. */
 template <class O>
 DGI void emit_u64(O &o, uint64_t v)
 {
-    if (v < 100000000ull) {
-        emit_small(o, (uint32_t)v);
-        return;
-    }
-    const uint64_t q = v / 100000000ull;
-    const uint32_t r = (uint32_t)(v - q * 100000000ull);
-    if (q < 100000000ull) {
-        emit_small(o, (uint32_t)q);
-    } else {
-        const uint64_t q2 = q / 100000000ull;
-        emit_small(o, (uint32_t)q2);
-        o.wle(dig8((uint32_t)(q - q2 * 100000000ull)), 8);
-    }
-    o.wle(dig8(r), 8);
+    Dig24 D;
+    D.init(v); /* v == 0: first = 23, the last '0' */
+    D.put(o, D.first, 24 - D.first);
 }
 /* i64toa (native/fastint.c:212-219) */
 template <class O>
@@ -152,54 +191,6 @@ DGI void f64_to_dec(uint64_t rsig, int32_t rexp, uint64_t c, int32_t q, uint64_t
     const bool up = vb > mid || (vb == mid && (s & 1) != 0);
     sig = s + (up ? 1 : 0);
     dexp = k;
-}
-
-/* the decimal digits of sig (< 10^17) as a 24-byte ASCII string with
- * leading zeros, held in three words (byte i of the string = byte i & 7 of
- * word i >> 3), and the positions of its first and last nonzero digits */
-struct Dig24 {
-    uint64_t w0, w1, w2;
-    uint32_t first, last;
-    DGI void init(uint64_t sig)
-    {
-        const uint64_t a = sig / 100000000ull;
-        const uint32_t b = (uint32_t)(sig - a * 100000000ull);
-        const uint32_t a1 = (uint32_t)(a / 100000000ull), a0 = (uint32_t)(a - (uint64_t)a1 * 100000000ull);
-        w0 = dig8(a1);
-        w1 = dig8(a0);
-        w2 = dig8(b);
-        const uint64_t z0 = w0 ^ 0x3030303030303030ull, z1 = w1 ^ 0x3030303030303030ull,
-                       z2 = w2 ^ 0x3030303030303030ull;
-        first = z0 ? (uint32_t)__builtin_ctzll(z0) >> 3
-                   : z1 ? 8 + ((uint32_t)__builtin_ctzll(z1) >> 3) : 16 + ((uint32_t)__builtin_ctzll(z2 | (1ull << 63)) >> 3);
-        last = z2 ? 16 + ((63 - (uint32_t)__builtin_clzll(z2)) >> 3)
-                  : z1 ? 8 + ((63 - (uint32_t)__builtin_clzll(z1)) >> 3) : ((63 - (uint32_t)__builtin_clzll(z0 | 1)) >> 3);
-    }
-    /* string bytes [from, from + len) (from + len <= 24): the string shifted
-     * by `from` bytes, straight-line (no indexed words: they would live in
-     * scratch), then up to three writes */
-    template <class O>
-    DGI void put(O &o, uint32_t from, uint32_t len) const
-    {
-        const uint32_t k = from >> 3, b = (from & 7) << 3;
-        const uint64_t x0 = k == 0 ? w0 : k == 1 ? w1 : w2, x1 = k == 0 ? w1 : k == 1 ? w2 : 0ull,
-                       x2 = k == 0 ? w2 : 0ull;
-        const uint64_t s0 = b ? (x0 >> b) | (x1 << (64 - b)) : x0, s1 = b ? (x1 >> b) | (x2 << (64 - b)) : x1,
-                       s2 = b ? x2 >> b : x2;
-        if (len) o.wle(s0, len < 8 ? len : 8u);
-        if (len > 8) o.wle(s1, len - 8 < 8 ? len - 8 : 8u);
-        if (len > 16) o.wle(s2, len - 16);
-    }
-};
-
-/* k <= 24 ASCII zeros */
-template <class O>
-DGI void put_zeros(O &o, uint32_t k)
-{
-    const uint64_t z = 0x3030303030303030ull;
-    if (k) o.wle(z, k < 8 ? k : 8u);
-    if (k > 8) o.wle(z, k - 8 < 8 ? k - 8 : 8u);
-    if (k > 16) o.wle(z, k - 16);
 }
 
 /* f64toa (native/fastfloat.c:349-404) for a finite double: the shortest

@@ -39,8 +39,14 @@ namespace dg {
 constexpr uint32_t T2W_MSG = 2048;  /* messages up to this (minus 16) are staged in LDS */
 constexpr uint32_t T2W_MAXD = 16;   /* nesting the walker handles */
 constexpr uint32_t T2W_MIN = 512;   /* messages longer than this take the wave kernel */
-constexpr uint32_t T2W_CH = 16;     /* string body bytes per copy task */
-constexpr uint32_t T2W_B64 = 24;    /* base64 input bytes per task (32 characters) */
+#ifndef DG_T2W_CH
+#define DG_T2W_CH 8
+#endif
+#ifndef DG_T2W_B64
+#define DG_T2W_B64 12
+#endif
+constexpr uint32_t T2W_CH = DG_T2W_CH;   /* string body bytes per copy task (8/12: t2j-c3 1.67 -> 1.59 ms vs 16/24; 4/6 no better) */
+constexpr uint32_t T2W_B64 = DG_T2W_B64; /* base64 input bytes per task (4/3 as many characters) */
 
 enum : uint32_t { TK_VAL = 0, TK_OPEN_OBJ = 1, TK_OPEN_ARR = 2, TK_CLOSE_OBJ = 3, TK_CLOSE_ARR = 4 };
 enum : uint32_t { TKF_COMMA = 8, TKF_KEYF = 16, TKF_KEYM = 32 };
