@@ -794,7 +794,11 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
                             t0 += nch[h];
                         }
                     } else if (nsum) {
+                        /* past the cap: the message declines, and its slots
+                         * below the cap are marked empty (the task pass reads
+                         * every slot up to min(ntask, cap)) */
                         good = 0;
+                        for (uint32_t c = t0; c < t0 + nsum && c < FL_MAXTASK; c++) L.task[c] = ~0ull;
                     }
                 }
             }
@@ -810,6 +814,7 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
         const uint32_t nt = min(L.ntask, FL_MAXTASK);
         for (uint32_t t = tid; t < nt; t += 64 * FL_WAVES) {
             const uint64_t tk = L.task[t];
+            if (tk == ~0ull) continue; /* a declined message's slot */
             const uint32_t m = (uint32_t)tk & 63, s0 = (uint32_t)(tk >> 8) & 0xFFF, cn = (uint32_t)(tk >> 20) & 0xFFF;
             const uint32_t lwa = L.lw[m];
             LSrc src;
