@@ -193,41 +193,13 @@ DGI void f64_to_dec(uint64_t rsig, int32_t rexp, uint64_t c, int32_t q, uint64_t
     dexp = k;
 }
 
-/* f64toa (native/fastfloat.c:349-404) for a finite double: the shortest
- * round-trip digits, written as an integer, a decimal, or d.ddde[+-]x when
+/* the shortest digits sig * 10^exp (sig's digits in D) in f64toa's layout
+ * (native/fastfloat.c:349-404): an integer, a decimal, or d.ddde[+-]x when
  * the decimal exponent is < -6 or > 20 (write_dec :241-259) */
 template <class O>
-DGI void emit_f64(O &o, double fp)
+DGI void f64_write_dec(O &o, const Dig24 &D, int32_t exp)
 {
-    const uint64_t raw = (uint64_t)__double_as_longlong(fp);
-    const bool neg = (raw >> 63) != 0;
-    const uint64_t rsig = raw & 0x000FFFFFFFFFFFFFull;
-    const int32_t rexp = (int32_t)((raw >> 52) & 0x7FF);
-    if (neg) o.w8('-');
-    if ((raw << 1) == 0) {
-        o.w8('0');
-        return;
-    }
-    uint64_t c;
-    int32_t q;
-    if (rexp != 0) {
-        c = rsig | 0x0010000000000000ull;
-        q = rexp - 1075;
-        if (q <= 0 && q >= -52 && (c & ((1ull << -q) - 1)) == 0) { /* an integer */
-            emit_u64(o, c >> -q);
-            return;
-        }
-    } else {
-        c = rsig;
-        q = -1074;
-    }
-    uint64_t sig;
-    int32_t exp;
-    f64_to_dec(rsig, rexp, c, q, sig, exp);
-    /* the digits as words: d[i] = string byte D.first + i */
-    Dig24 D;
-    D.init(sig);
-    const uint32_t cnt = 24 - D.first;
+    const uint32_t cnt = 24 - D.first; /* d[i] = string byte D.first + i */
     const int32_t dot = (int32_t)cnt + exp;
     const int32_t sci = dot - 1;
     const uint32_t nd = D.last - D.first + 1; /* digits without trailing zeros */
@@ -266,6 +238,42 @@ DGI void emit_f64(O &o, double fp)
     }
     D.put(o, D.first, cnt); /* integer digits, then zeros up to the point */
     put_zeros(o, (uint32_t)(dot - (int32_t)cnt));
+}
+
+/* f64toa (native/fastfloat.c:349-404) for a finite double: the shortest
+ * round-trip digits, written as an integer, a decimal, or d.ddde[+-]x when
+ * the decimal exponent is < -6 or > 20 (write_dec :241-259) */
+template <class O>
+DGI void emit_f64(O &o, double fp)
+{
+    const uint64_t raw = (uint64_t)__double_as_longlong(fp);
+    const bool neg = (raw >> 63) != 0;
+    const uint64_t rsig = raw & 0x000FFFFFFFFFFFFFull;
+    const int32_t rexp = (int32_t)((raw >> 52) & 0x7FF);
+    if (neg) o.w8('-');
+    if ((raw << 1) == 0) {
+        o.w8('0');
+        return;
+    }
+    uint64_t c;
+    int32_t q;
+    if (rexp != 0) {
+        c = rsig | 0x0010000000000000ull;
+        q = rexp - 1075;
+        if (q <= 0 && q >= -52 && (c & ((1ull << -q) - 1)) == 0) { /* an integer */
+            emit_u64(o, c >> -q);
+            return;
+        }
+    } else {
+        c = rsig;
+        q = -1074;
+    }
+    uint64_t sig;
+    int32_t exp;
+    f64_to_dec(rsig, rexp, c, q, sig, exp);
+    Dig24 D;
+    D.init(sig);
+    f64_write_dec(o, D, exp);
 }
 
 /* quote (native/parsing.c:487, flags 0) of src[s0, s0+n): 8 bytes per step

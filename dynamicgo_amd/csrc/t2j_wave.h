@@ -423,9 +423,12 @@ DGI int32_t t2w_walk(const DV &D, const __attribute__((address_space(3))) uint64
 #define T2P_PASS
 #endif
 
-/* a number/bool at byte p of Thrift type tt as JSON in registers, through
- * ONE emit_i64 and ONE emit_f64 call site (the kernel must fit the
- * instruction cache); false: bail (NaN/Inf without the option) */
+/* a number/bool at byte p of Thrift type tt as JSON in registers. Integers
+ * and doubles share ONE 24-digit conversion (Dig24) and its writes: the
+ * lanes of a page format both kinds at once, so separate i64toa and f64toa
+ * paths would each be paid by the whole wave (f64toa, native/fastfloat.c:
+ * 349-404; i64toa, native/fastint.c:212-231). false: bail (NaN/Inf without
+ * the option) */
 template <class S>
 DGI bool t2w_number(S &src, int64_t p, uint8_t tt, uint64_t opts, bool quote64, RegOut &r)
 {
@@ -436,22 +439,43 @@ DGI bool t2w_number(S &src, int64_t p, uint8_t tt, uint64_t opts, bool quote64, 
         else r.wle('f' | ('a' << 8) | ('l' << 16) | ('s' << 24) | (0x65ull << 32), 5);
         return true;
     }
+    bool neg, dec = false;
+    uint64_t mag;
+    int32_t exp = 0;
     if (tt == DG_T_DOUBLE) {
-        if (((u >> 52) & 0x7FF) == 0x7FF) {
+        const uint64_t rsig = u & 0x000FFFFFFFFFFFFFull;
+        const int32_t rexp = (int32_t)((u >> 52) & 0x7FF);
+        if (rexp == 0x7FF) {
             if (!(opts & DG_T2J_NULL_FOR_NAN_INF)) return false; /* the error: the lane kernel reports it */
             r.wle('n' | ('u' << 8) | ('l' << 16) | ('l' << 24), 4);
             return true;
         }
-        emit_f64(r, __longlong_as_double((long long)u));
-        return true;
+        neg = (u >> 63) != 0;
+        const uint64_t c = rexp ? rsig | 0x0010000000000000ull : rsig;
+        const int32_t q = rexp ? rexp - 1075 : -1074;
+        if ((u << 1) == 0) {
+            mag = 0; /* "0" / "-0" */
+        } else if (rexp && q <= 0 && q >= -52 && (c & ((1ull << -q) - 1)) == 0) {
+            mag = c >> -q; /* an integer */
+        } else {
+            f64_to_dec(rsig, rexp, c, q, mag, exp);
+            dec = true;
+        }
+    } else {
+        /* sign-extend (BYTE as unsigned with ByteAsUint8) */
+        const int64_t v = tt == DG_T_BYTE ? ((opts & DG_T2J_BYTE_AS_UINT8) ? (int64_t)u : (int64_t)(int8_t)u)
+                          : tt == DG_T_I16 ? (int64_t)(int16_t)u
+                          : tt == DG_T_I32 ? (int64_t)(int32_t)u
+                                           : (int64_t)u;
+        neg = v < 0;
+        mag = neg ? 0ull - (uint64_t)v : (uint64_t)v;
     }
-    /* sign-extend (BYTE as unsigned with ByteAsUint8) */
-    const int64_t v = tt == DG_T_BYTE ? ((opts & DG_T2J_BYTE_AS_UINT8) ? (int64_t)u : (int64_t)(int8_t)u)
-                      : tt == DG_T_I16 ? (int64_t)(int16_t)u
-                      : tt == DG_T_I32 ? (int64_t)(int32_t)u
-                                       : (int64_t)u;
     if (quote64) r.w8('"');
-    emit_i64(r, v);
+    if (neg) r.w8('-');
+    Dig24 D;
+    D.init(mag); /* mag == 0: first = 23, the last '0' */
+    if (dec) f64_write_dec(r, D, exp);
+    else D.put(r, D.first, 24 - D.first);
     if (quote64) r.w8('"');
     return true;
 }

@@ -1,6 +1,6 @@
 # t2j: word-wise f64toa digits + walker token ring -- tests, phase profile, bench
 set -o pipefail
-O=gpurun_out/r3ab
+O=gpurun_out/r3ag
 mkdir -p $O
 timeout -k 10 500 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_t2j.py > $O/t2j_tests.log 2>&1 || { tail -30 $O/t2j_tests.log; exit 1; }
 tail -2 $O/t2j_tests.log
