@@ -74,6 +74,9 @@ constexpr uint32_t FL_MAXTASK = 512;             /* chunk tasks per block (more:
 #define DG_FL_WPE 4 /* waves per SIMD the register budget is cut for: 128 VGPRs; LDS allows 4 blocks (16 waves) per CU */
 #endif
 
+#ifndef DG_FL_DEFER_NUM
+#define DG_FL_DEFER_NUM 0 /* 1: numbers of known fields parsed in the write phase */
+#endif
 #ifndef DG_FL_PERM
 #define DG_FL_PERM 0
 #endif
@@ -165,6 +168,7 @@ struct FField {
     uint8_t tt;       /* field type */
     uint16_t id;
     bool i16q;        /* js_conv i16 quirk: i16 then i8 */
+    bool defer;       /* FV_NUM: the text [s0, s0+nb) is parsed by flat_write */
 };
 
 template <class S>
@@ -240,6 +244,7 @@ DGI bool fl_field(const DV &D, const dg_struct &sd, S &src, uint32_t sk, uint32_
         if (fi >= 0) f = ldrec(&D.F[fi]);
     }
     /* the value, [v0, ve) */
+    F.defer = false;
     uint32_t vk;
     uint32_t vs0 = 0, vnb = 0;
     bool vesc = false, isint = false, bv = false;
@@ -252,8 +257,17 @@ DGI bool fl_field(const DV &D, const dg_struct &sd, S &src, uint32_t sk, uint32_
         vesc = hasbs && has_byte(src, vs0, vnb, '\\');
         vk = FV_STR;
     } else if (c == '-' || (uint8_t)(c - '0') <= 9) {
-        SI qq = (SI)v0;
-        if (!fast_vnumber(src, qq, tb, iv, dv, isint) || (uint32_t)qq != ve) return false;
+        /* a known field without a value mapping: a number's Thrift size
+         * follows from the field type alone, so its text is parsed by
+         * flat_write after the size barrier (the wave holding a double no
+         * longer holds the others back); skipped and mapped fields parse it
+         * here, as the reference validates them before anything else */
+        const bool later = DG_FL_DEFER_NUM && fi >= 0 && !((flag & DG_F_ENABLE_VM) && f.vm != DG_VM_NONE);
+        if (!later) {
+            SI qq = (SI)v0;
+            if (!fast_vnumber(src, qq, tb, iv, dv, isint) || (uint32_t)qq != ve) return false;
+        }
+        F.defer = later;
         vs0 = v0;
         vnb = ve - v0;
         vk = FV_NUM;
@@ -385,20 +399,27 @@ DGI bool body_b64(S &src, uint32_t s0, uint32_t n, bool last, O &o)
  * 2 = header and length written, the body (> FL_INLINE bytes of a string
  * without escapes or of canonical base64) is left to chunk tasks. */
 template <class S, class O>
-DGI uint32_t flat_write(S &src, const FField &F, O &o)
+DGI uint32_t flat_write(S &src, const FField &F, const FastTabs &tb, O &o)
 {
     typedef typename S::idx SI;
     if (F.kind == FV_NONE) return 1;
+    bool isint = F.isint;
+    int64_t iv = F.iv;
+    double dv = F.dv;
+    if (F.kind == FV_NUM && F.defer) { /* the number's text, parsed now (native/scanning.c vnumber) */
+        SI qq = (SI)F.s0;
+        if (!fast_vnumber(src, qq, tb, iv, dv, isint) || (uint32_t)qq != F.s0 + F.nb) return 0;
+    }
     o.wle((uint32_t)F.tt | ((uint32_t)__builtin_bswap16(F.id) << 8), 3);
     switch (F.kind) {
-    case FV_BOOL: o.w8((uint8_t)F.iv); return 1;
+    case FV_BOOL: o.w8((uint8_t)iv); return 1;
     case FV_NUM:
         if (F.i16q) {
-            emit_number(o, DG_T_I16, F.isint, F.iv, F.dv);
-            emit_number(o, DG_T_BYTE, F.isint, F.iv, F.dv);
+            emit_number(o, DG_T_I16, isint, iv, dv);
+            emit_number(o, DG_T_BYTE, isint, iv, dv);
             return 1;
         }
-        return emit_number(o, F.tt, F.isint, F.iv, F.dv) ? 1u : 0u;
+        return emit_number(o, F.tt, isint, iv, dv) ? 1u : 0u;
     case FV_NUMSTR:
     case FV_STR:
         o.w32(F.kind == FV_NUMSTR ? F.nb : F.size - 7);
@@ -733,7 +754,7 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
             if (off + F.size >= cap) return 0; /* the slot holds the field and STOP */
             WOut o;
             o.init(slot + off);
-            const uint32_t wr = flat_write(src, F, o);
+            const uint32_t wr = flat_write(src, F, tb, o);
             o.finish();
             return wr;
         };
