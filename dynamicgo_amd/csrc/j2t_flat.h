@@ -75,7 +75,7 @@ constexpr uint32_t FL_MAXTASK = 512;             /* chunk tasks per block (more:
 #endif
 
 #ifndef DG_FL_DEFER_NUM
-#define DG_FL_DEFER_NUM 0 /* 1: numbers of known fields parsed in the write phase */
+#define DG_FL_DEFER_NUM 0 /* 1: numbers of known fields parsed in the write phase (measured 51.6 vs 50.2 us/step: off) */
 #endif
 #ifndef DG_FL_PERM
 #define DG_FL_PERM 0
