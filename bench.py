@@ -64,7 +64,10 @@ CONFIGS = {
 }
 AGG_METRIC = "conv/j2t BinaryConv.Do calls/s through the batching aggregator (host memory in/out), 16 threads"
 T2J_METRIC = "conv/t2j GB/s Thrift in + msgs/s, 64K-batch device-resident"
-DEFAULT_INFLIGHT = {"c5": 1, "t2j-c2": 1, "t2j-c3": 1}  # batches in flight in the timed steps (t2j: 1 until measured)
+# batches in flight in the timed steps (default 2). Measured one at a time
+# faster or equal: C5's 1M batch (4.45 vs 4.73 ms), t2j-c3 (1.48 vs 1.50 ms;
+# its wave kernel's workspace is ordered across streams)
+DEFAULT_INFLIGHT = {"c5": 1, "t2j-c3": 1}
 FLAGS = {"c2x": 0x7}  # default: conv.Options{} -> F_ALLOW_UNKNOWN (conv/j2t/conv.go:102-104)
 
 
