@@ -15,9 +15,9 @@ LIB_PATH = os.environ.get("DG_LIB_PATH") or os.path.join(HERE, "libdgj2t.so")
 EXPORTS = ["dg_last_error", "dg_build_info", "dg_ctx_create", "dg_ctx_destroy", "dg_ctx_stream", "dg_ctx_stats", "dg_ctx_counters", "dg_ctx_set_knob", "dg_ctx_get_knob",
            "dg_desc_create",
            "dg_desc_create_device", "dg_desc_destroy", "dg_desc_root", "dg_j2t_batch_device",
-           "dg_j2t_batch_device_ml", "dg_j2t_batch_device_hm", "dg_j2t_batch_device_iters",
+           "dg_j2t_batch_device_ml", "dg_j2t_batch_device_hm", "dg_j2t_batch_device_cb", "dg_j2t_batch_device_iters",
            "dg_j2t_batch_device_inflight",
-           "dg_slot_bound", "dg_j2t_batch_host", "dg_j2t_batch_host_hm", "dg_j2t_do", "dg_pack_device", "dg_pack_device_scan", "dg_pack_device_framed", "dg_agg_create", "dg_agg_create2", "dg_agg_do",
+           "dg_slot_bound", "dg_j2t_batch_host", "dg_j2t_batch_host_hm", "dg_j2t_batch_host_cb", "dg_j2t_do", "dg_pack_device", "dg_pack_device_scan", "dg_pack_device_framed", "dg_agg_create", "dg_agg_create2", "dg_agg_do",
            "dg_agg_submit", "dg_agg_wait", "dg_agg_stats", "dg_agg_profile", "dg_agg_destroy", "dg_agg_drive", "dg_j2t_pipeline_host", "dg_bench_device", "dg_desc_attach_t2j", "dg_t2j_slot_bound", "dg_t2j_batch_device", "dg_t2j_batch_device_ml",
            "dg_t2j_batch_host"]
 
@@ -63,6 +63,8 @@ def lib() -> C.CDLL:
         "dg_j2t_batch_device_ml": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, vp, vp, vp, vp, vp, u64]),
         "dg_j2t_batch_device_hm": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, u32, vp, vp, vp, vp, vp, vp, vp, u64]),
         "dg_j2t_batch_host_hm": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, u32, vp, u64, vp, u64, vp, vp, P64]),
+        "dg_j2t_batch_device_cb": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, vp, vp, vp, vp, vp, vp, u64]),
+        "dg_j2t_batch_host_cb": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, vp, u64, vp, vp, P64]),
         "dg_j2t_batch_device_iters": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, vp, vp, vp, vp, vp, u64, C.c_int]),
         "dg_j2t_batch_device_inflight": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, vp, C.c_int, vp, u64, C.c_int]),
         "dg_slot_bound": (u64, [u64]),
@@ -117,6 +119,22 @@ def _check_provenance(L):
     if os.environ.get("DG_LOG_LIB"):
         import sys
         print(f"[dynamicgo_amd] loaded {LIB_PATH} ({BUILD_INFO})", file=sys.stderr, flush=True)
+
+
+class HMEntry(C.Structure):
+    """dg_hm_entry (include/dgj2t_defs.h)"""
+    _fields_ = [("off", C.c_uint32), ("len", C.c_uint32), ("mask", C.c_uint64)]
+
+
+class VMEntry(C.Structure):
+    """dg_cb_entry (include/dgj2t_defs.h)"""
+    _fields_ = [("off", C.c_uint32), ("count", C.c_uint32)]
+
+
+class CBTables(C.Structure):
+    """dg_cb_tables (include/dgj2t_defs.h)"""
+    _fields_ = [("hm_tab", C.c_void_p), ("n_hm", C.c_uint32), ("ans_tab", C.c_void_p),
+                ("bytes", C.c_void_p), ("len", C.c_uint64)]
 
 
 def check(rc: int):

@@ -15,6 +15,7 @@ Every call runs the HIP kernels in libdgj2t.so; there is no CPU fallback.
 from __future__ import annotations
 
 import ctypes as C
+import struct as _st
 from dataclasses import dataclass
 from typing import List, Optional, Sequence, Tuple
 
@@ -22,7 +23,7 @@ import numpy as np
 
 from . import _lib
 from . import http as H
-from .thrift import FlatDescriptor, TypeDescriptor, flatten, TYPE_NAMES
+from .thrift import FlatDescriptor, TypeDescriptor, flatten, TYPE_NAMES, ValueMappingError
 
 # flag bits (native/thrift.h:23-32, internal/types/types.go:81-92)
 F_ALLOW_UNKNOWN = 1
@@ -44,6 +45,8 @@ DG_ST_OUT_OVERFLOW = 0xF0
 DG_ST_DEEP = 0xF1
 DG_ST_HM_END = 0xF2
 DG_ST_HM_ERR = 0xF3
+DG_ST_HM_END_AT = 0xF4
+E_VM_END = 24  # ERR_VM_END (native/native.h:70): a non-inline value mapping for the host
 
 # internal/types/types.go:107-131 ParsingError messages
 _ERR_MSG = {0: "ok", 1: "eof", 2: "invalid char", 3: "invalid escape char", 4: "invalid unicode escape",
@@ -296,9 +299,9 @@ class BinaryConv:
             if errs[0] is not None:
                 raise errs[0]
             return outs[0] or None
-        outs, rets = self.do_batch(desc, [jbytes])
-        if rets[0] != 0:
-            raise J2TError(int(rets[0]), explain_native_error(int(rets[0]), jbytes))
+        outs, errs = self.do_batch_errors(desc, [jbytes])
+        if errs[0] is not None:
+            raise errs[0]
         return outs[0] if outs[0] else None
 
     def do_into(self, desc, jbytes: bytes, buf: bytearray, req=None, base=None):
@@ -324,6 +327,141 @@ class BinaryConv:
                                   J2TError(int(rets[0]), explain_native_error(int(rets[0]), src)))
             return outs[0]
         return conv_nested
+
+    def _host_cb(self, flat: FlatDescriptor, msgs: Sequence[bytes], flags: int, hm_rows=None, n_hm: int = 0,
+                 hm_bytes: bytes = b"", vm_answers=None):
+        """dg_j2t_batch_host_cb over `msgs` with the host's callback answers:
+        hm_rows[k] = message k's n_hm (off, len, mask) HTTP-mapping entries
+        into hm_bytes, vm_answers[k] = the Thrift bytes of its first
+        value-mapping answers (dgj2t_defs.h dg_cb_tables). Returns
+        (outputs, packed statuses); an output holds the partial output and
+        requires words for DG_ST_HM_END, the 16-byte record for ERR_VM_END."""
+        ctx = self._ctx()
+        L = _lib.lib()
+        m = len(msgs)
+        lens = np.fromiter((len(x) for x in msgs), dtype=np.uint64, count=m)
+        in_off = np.zeros(m + 1, dtype=np.uint64)
+        np.cumsum(lens, out=in_off[1:])
+        arena = np.frombuffer(b"".join(msgs) + b"\0" * 16, dtype=np.uint8)
+        pool = bytearray(hm_bytes)
+        cb = None
+        keep = []
+        extra = 0  # output the host's answers add per message (first capacity)
+        if hm_rows is not None or vm_answers is not None:
+            cb = _lib.CBTables()
+            if hm_rows is not None and n_hm:
+                tab = (_lib.HMEntry * (m * n_hm))()
+                for k, row in enumerate(hm_rows):
+                    for j, (off, ln, mask) in enumerate(row):
+                        tab[k * n_hm + j] = _lib.HMEntry(off, ln, mask & (2**64 - 1))
+                cb.hm_tab, cb.n_hm = C.cast(tab, C.c_void_p), n_hm
+                keep.append(tab)
+            if vm_answers is not None:
+                vt = (_lib.VMEntry * max(m, 1))()
+                for k, ans in enumerate(vm_answers):
+                    vt[k] = _lib.VMEntry(len(pool), len(ans))
+                    for a in ans:
+                        pool += len(a).to_bytes(4, "little") + a
+                cb.ans_tab = C.cast(vt, C.c_void_p)
+                keep.append(vt)
+            pb = (C.c_uint8 * (len(pool) + 8)).from_buffer_copy(bytes(pool) + b"\0" * 8)
+            keep.append(pb)
+            cb.bytes, cb.len = C.cast(pb, C.c_void_p), len(pool)
+            extra = len(pool) + 64 * m
+        rets = np.zeros(max(m, 1), dtype=np.uint64)
+        out_off = np.zeros(m + 1, dtype=np.uint64)
+        cap = int(lens.sum()) * 4 + 64 * m + 64 + extra
+        need = C.c_uint64(0)
+        for _ in range(2):
+            out = np.zeros(cap, dtype=np.uint8)
+            rc = L.dg_j2t_batch_host_cb(ctx.h, ctx.desc(flat), flat.root_type, arena.ctypes.data, in_off.ctypes.data,
+                                        m, flags, C.byref(cb) if cb is not None else None, out.ctypes.data, cap,
+                                        out_off.ctypes.data, rets.ctypes.data, C.byref(need))
+            if rc == -3 and need.value > cap:  # DG_E_NOMEM: once more with the size it needs
+                cap = int(need.value) + 64
+                continue
+            break
+        _lib.check(rc)
+        return [out[int(out_off[k]):int(out_off[k + 1])].tobytes() for k in range(m)], rets[:m]
+
+    def _serve_callbacks(self, flat: FlatDescriptor, msgs: Sequence[bytes], flags: int, outs, rets, errs,
+                         hm_rows=None, n_hm: int = 0, hm_bytes: bytes = b"", hm_end=None):
+        """The reference's mid-message Go callbacks (handleError,
+        conv/j2t/impl_amd64.go:169-247), served and resumed: each message the
+        device stopped at a callback gets the host's answer appended to its
+        answers (dg_cb_entry) and is converted again, until it finishes.
+          * ERR_VM_END (native/thrift.c:641-665) -> handleValueMapping
+            (impl_amd64.go:117-155): the field header, then the field's
+            ValueMapping.write on the value's JSON text;
+          * DG_ST_HM_END_AT, a nested struct's ERR_HM_END -> hm_end(i, struct,
+            field ids): handleUnmatchedFields' bytes (impl_amd64.go:71-115).
+        In place on outs / rets / errs; a failing callback leaves the message
+        its stop status and its error in errs."""
+        answers = {}
+        todo = [i for i in range(len(msgs)) if (int(rets[i]) & 0xFF) in (E_VM_END, DG_ST_HM_END_AT)
+                and errs[i] is None]
+        while todo:
+            live = []
+            for i in todo:
+                src, rec, r = msgs[i], outs[i], int(rets[i])
+                outs[i] = b""
+                if (r & 0xFF) == DG_ST_HM_END_AT:
+                    si = _st.unpack(">Q", rec[:8])[0]
+                    sd = flat.structs[si]
+                    order = sorted(sd.fields, key=lambda f: f.id)
+                    ids = []
+                    for w in range(r >> 40):
+                        bits = _st.unpack(">Q", rec[8 + 8 * w:16 + 8 * w])[0]
+                        ids += [order[64 * w + b].id for b in range(64) if (bits >> b) & 1 and 64 * w + b < len(order)]
+                    try:
+                        if hm_end is None:
+                            raise H.ConvError("ErrInvalidParam", "http request is nil")
+                        ans = hm_end(i, sd, ids)
+                    except H.ConvError as e:
+                        errs[i] = e
+                        continue
+                    answers.setdefault(i, []).append(ans)
+                    live.append(i)
+                    continue
+                end = r >> 8
+                start, fidx = _st.unpack(">QQ", rec[:16])
+                f = flat.fields[fidx] if fidx < len(getattr(flat, "fields", [])) else None
+                if f is None:
+                    errs[i] = H.ConvError("ErrConvert", "unknown field id for value-mapping")
+                    continue
+                if end >= len(src) or start > end:  # impl_amd64.go:132-134
+                    errs[i] = H.ConvError("ErrConvert", "invalid value-mapping position")
+                    continue
+                try:
+                    if f.value_mapping is None:
+                        raise ValueMappingError("no value mapping registered for type %d" % f.vm)
+                    val = f.value_mapping.write(f, bytes(src[start:end]))
+                except Exception as e:  # any Write error (impl_amd64.go:137-139)
+                    errs[i] = H.ConvError("ErrConvert", "failed to convert field '%s' value" % f.name, e)
+                    continue
+                answers.setdefault(i, []).append(bytes([f.type.type]) + _st.pack(">h", f.id) + bytes(val))
+                live.append(i)
+            if not live:
+                break
+            o2, r2 = self._host_cb(flat, [msgs[i] for i in live], flags,
+                                   [hm_rows[i] for i in live] if hm_rows is not None else None, n_hm, hm_bytes,
+                                   [answers[i] for i in live])
+            for k, i in enumerate(live):
+                outs[i], rets[i] = o2[k], r2[k]
+            todo = [i for i in live if (int(rets[i]) & 0xFF) in (E_VM_END, DG_ST_HM_END_AT)]
+
+    def do_batch_errors(self, desc, msgs: Sequence[bytes], extra_flags: int = 0):
+        """BinaryConv.Do over a batch (conv/j2t/conv.go:53-77): (outputs,
+        errors), errors[i] None, a J2TError (the native status) or an
+        http.ConvError (a value-mapping callback that failed)."""
+        outs, rets, vm_errs = self._do_batch(desc, msgs, extra_flags)
+        errs = [None] * len(msgs)
+        for i, r in enumerate(rets):
+            if i in vm_errs:
+                errs[i] = vm_errs[i]
+            elif int(r) != 0:
+                errs[i] = J2TError(int(r), explain_native_error(int(r), msgs[i]))
+        return outs, errs
 
     def do_batch_http(self, desc, msgs: Sequence[bytes], reqs: Sequence, bases: Optional[Sequence] = None):
         """BinaryConv.do (conv/j2t/impl.go:38-91) for a batch with the Go-side
@@ -399,43 +537,24 @@ class BinaryConv:
                 fl |= F_HM_SPLIT
             prefix[i] = pre
             groups.setdefault(fl, []).append(i)
-        ctx = self._ctx()
-        L = _lib.lib()
-        hb = np.frombuffer(bytes(hm_bytes) + b"\0" * 8, dtype=np.uint8)
-        ent = np.dtype([("off", "<u4"), ("len", "<u4"), ("mask", "<u8")])
         order = sorted(sd.fields, key=lambda f: f.id) if sd is not None else []
         for fl, idx in groups.items():
             sub = [msgs[i] for i in idx]
-            m = len(sub)
-            lens = np.fromiter((len(x) for x in sub), dtype=np.uint64, count=m)
-            in_off = np.zeros(m + 1, dtype=np.uint64)
-            np.cumsum(lens, out=in_off[1:])
-            arena = np.frombuffer(b"".join(sub) + b"\0" * 16, dtype=np.uint8)
-            tab = np.zeros(max(1, m * n_hm), dtype=ent)
-            if fl & F_HM_SPLIT:
-                for k, i in enumerate(idx):
-                    for j, e in enumerate(rows[i]):
-                        tab[k * n_hm + j] = e
-            rets = np.zeros(max(m, 1), dtype=np.uint64)
-            out_off = np.zeros(m + 1, dtype=np.uint64)
-            cap = int(lens.sum()) * 4 + 64 * m + len(hm_bytes) * m + 64
-            need = C.c_uint64(0)
-            for _ in range(2):
-                out = np.zeros(cap, dtype=np.uint8)
-                split = bool(fl & F_HM_SPLIT)
-                rc = L.dg_j2t_batch_host_hm(ctx.h, ctx.desc(flat), flat.root_type, arena.ctypes.data,
-                                            in_off.ctypes.data, m, fl, tab.ctypes.data if split else None,
-                                            n_hm if split else 0, hb.ctypes.data, len(hm_bytes) if split else 0,
-                                            out.ctypes.data, cap, out_off.ctypes.data, rets.ctypes.data,
-                                            C.byref(need))
-                if rc == -3 and need.value > cap:
-                    cap = int(need.value) + 64
-                    continue
-                break
-            _lib.check(rc)
+            split = bool(fl & F_HM_SPLIT)
+            sub_rows = [rows[i] for i in idx] if split else None
+            out_k, rets = self._host_cb(flat, sub, fl, sub_rows, n_hm if split else 0, bytes(hm_bytes) if split else b"")
+            sub_errs = [None] * len(idx)
+            if fl & (F_VALUE_MAPPING | F_HM_SPLIT):
+                def hm_end(k, hsd, ids, idx=idx):  # a nested struct's ERR_HM_END (top = true)
+                    return hx.handle_unmatched_fields(reqs[idx[k]], hsd, ids, True) + b"\x00"
+                self._serve_callbacks(flat, sub, fl, out_k, rets, sub_errs, sub_rows, n_hm if split else 0,
+                                      bytes(hm_bytes) if split else b"", hm_end)
             for k, i in enumerate(idx):
+                if sub_errs[k] is not None:
+                    errs[i] = sub_errs[k]
+                    continue
                 r = int(rets[k])
-                body = out[int(out_off[k]):int(out_off[k + 1])].tobytes()
+                body = out_k[k]
                 if r == 0:
                     outs[i] = prefix[i] + body
                 elif (r & 0xFF) == DG_ST_HM_END:
@@ -479,7 +598,14 @@ class BinaryConv:
         chunks > 0 streams the batch through dg_j2t_pipeline_host in that many
         overlapped pieces (uploads, kernels and downloads of neighbouring
         chunks in flight at once); out_cap overrides the first output
-        capacity (the DG_E_NOMEM retry then takes out_need)."""
+        capacity (the DG_E_NOMEM retry then takes out_need). Non-inline
+        value mappings are served (ERR_VM_END); one whose callback failed
+        keeps status ERR_VM_END (do_batch_errors returns its error)."""
+        outs, rets, _ = self._do_batch(desc, msgs, extra_flags, chunks, out_cap)
+        return outs, rets
+
+    def _do_batch(self, desc, msgs: Sequence[bytes], extra_flags: int = 0, chunks: int = 0,
+                  out_cap: Optional[int] = None):
         self._check_opts()
         flat = self._flat(desc)
         ctx = self._ctx()
@@ -511,7 +637,16 @@ class BinaryConv:
             rc = call(out, cap)
         _lib.check(rc)
         outs = [out[int(out_off[i]):int(out_off[i + 1])].tobytes() for i in range(n)]
-        return outs, rets[:n]
+        rets = rets[:n]
+        vm_errs = {}
+        if flags & F_VALUE_MAPPING and any((int(r) & 0xFF) == E_VM_END for r in rets):
+            errs = [None] * n
+            self._serve_callbacks(flat, msgs, flags, outs, rets, errs)
+            vm_errs = {i: e for i, e in enumerate(errs) if e is not None}
+        for i in range(n):
+            if int(rets[i]) != 0:
+                outs[i] = b""
+        return outs, rets, vm_errs
 
     def do_device(self, desc, json, in_off, out, out_off, out_len, ret, pending=None, stream=None):
         """Device-resident batch over torch CUDA tensors (uint8/int64/int32).

@@ -327,11 +327,14 @@ static int ensure_fast_ws(Scratch *x, uint64_t lanes)
     return DG_OK;
 }
 
-/* the HTTP-mapping table of a DG_F_HM_SPLIT batch (dgj2t_defs.h), device pointers */
+/* the host's callback answers of a batch (dg_cb_tables, dgj2t_defs.h):
+ * HTTP-mapping entries (DG_F_HM_SPLIT) and value-mapping entries, device
+ * pointers */
 struct HMIn {
     const dg_hm_entry *tab;
     uint32_t n_hm;
     const uint8_t *bytes;
+    const dg_cb_entry *vm = nullptr;
 };
 
 static int enqueue(dg_ctx *c, Scratch *x, const dg_desc *d, uint32_t root, const uint8_t *json,
@@ -366,6 +369,7 @@ static int enqueue(dg_ctx *c, Scratch *x, const dg_desc *d, uint32_t root, const
     P.hm_tab = hm ? hm->tab : nullptr;
     P.hm_bytes = hm ? hm->bytes : nullptr;
     P.n_hm = hm ? hm->n_hm : 0;
+    P.ans_tab = hm ? hm->vm : nullptr;
     P.out = out;
     P.out_off = out_off;
     P.out_len = out_len;
@@ -560,6 +564,19 @@ int dg_j2t_batch_device_hm(dg_ctx *c, const dg_desc *d, uint32_t root, const uin
                   d_hm_tab ? &hm : nullptr);
 }
 
+int dg_j2t_batch_device_cb(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *d_json, const uint64_t *d_in_off,
+                           uint64_t n, uint64_t flags, const dg_cb_tables *cb, uint8_t *d_out, const uint64_t *d_out_off,
+                           uint32_t *d_out_len, uint64_t *d_ret, uint32_t *d_pending, void *stream, uint64_t max_len)
+{
+    if (!c || !d || (cb && (cb->hm_tab || cb->ans_tab) && !cb->bytes)) return set_err(DG_E_INVALID, "bad args");
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    HMIn hm{cb ? cb->hm_tab : nullptr, cb ? cb->n_hm : 0u, cb ? cb->bytes : nullptr, cb ? cb->ans_tab : nullptr};
+    return launch(c, d, root, d_json, d_in_off, n, flags, d_out, d_out_off, d_out_len, d_ret, d_pending, s, max_len,
+                  cb ? &hm : nullptr);
+}
+
 int dg_j2t_batch_device_iters(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *d_json,
                               const uint64_t *d_in_off, uint64_t n, uint64_t flags, uint8_t *d_out,
                               const uint64_t *d_out_off, uint32_t *d_out_len, uint64_t *d_ret, uint32_t *d_pending,
@@ -629,6 +646,7 @@ static const uint64_t HOST_ONE_TRIP = 4ull << 20;
 static int batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *json, const uint64_t *in_off,
                       uint64_t n, uint64_t flags, const HMIn *hm, uint64_t hm_len, uint8_t *out, uint64_t out_cap,
                       uint64_t *out_off, uint64_t *ret, uint64_t *out_need)
+/* hm: host pointers (tab may be NULL with vm set, and the reverse) */
 {
     if (!c || !d || (!json && n) || !in_off || !out_off || (!ret && n)) return set_err(DG_E_INVALID, "bad args");
     std::lock_guard<std::mutex> g(c->mu);
@@ -636,11 +654,12 @@ static int batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
     int rc;
     hipStream_t s = c->stream;
     const uint64_t base = in_off[0], bytes = in_off[n] - in_off[0];
-    /* upload: [ioff (n+1) | soff (n+1) | HTTP-mapping table (n x n_hm) and
-     * bytes (optional) | JSON + 64 zero bytes] */
-    const uint64_t nhm = hm ? hm->n_hm : 0;
+    /* upload: [ioff (n+1) | soff (n+1) | HTTP-mapping table (n x n_hm),
+     * value-mapping table (n), answer bytes (optional) | JSON + 64 zero bytes] */
+    const uint64_t nhm = hm && hm->tab ? hm->n_hm : 0;
+    const uint64_t nvm = hm && hm->vm ? 1 : 0;
     const uint64_t hmb = hm ? (hm_len + 7) & ~7ull : 0;
-    const uint64_t hmw = hm ? 2 * n * nhm + hmb / 8 : 0; /* words */
+    const uint64_t hmw = hm ? 2 * n * nhm + n * nvm + hmb / 8 : 0; /* words */
     const uint64_t up_bytes = 16 * (n + 1) + 8 * hmw + bytes + 64;
     if ((rc = grow_pinned(c->h_up, c->h_up_cap, up_bytes))) return rc;
     uint64_t *ioff = (uint64_t *)(void *)c->h_up, *soff = ioff + n + 1;
@@ -648,7 +667,8 @@ static int batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
     uint8_t *hj = (uint8_t *)(void *)(hhm + hmw);
     if (hm) {
         if (n * nhm) memcpy(hhm, hm->tab, 16 * n * nhm);
-        if (hm_len) memcpy(hhm + 2 * n * nhm, hm->bytes, hm_len);
+        if (n * nvm) memcpy(hhm + 2 * n * nhm, hm->vm, 8 * n);
+        if (hm_len) memcpy(hhm + 2 * n * nhm + n * nvm, hm->bytes, hm_len);
     }
     uint64_t max_len = 1;
     soff[0] = 0;
@@ -672,8 +692,9 @@ static int batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
     const uint64_t *d_in = (const uint64_t *)(void *)c->d_json, *d_oo = d_in + n + 1;
     HMIn dhm{nullptr, (uint32_t)nhm, nullptr};
     if (hm) {
-        dhm.tab = (const dg_hm_entry *)(const void *)(d_oo + n + 1);
-        dhm.bytes = (const uint8_t *)(const void *)(d_oo + n + 1 + 2 * n * nhm);
+        dhm.tab = nhm ? (const dg_hm_entry *)(const void *)(d_oo + n + 1) : nullptr;
+        dhm.vm = nvm ? (const dg_cb_entry *)(const void *)(d_oo + n + 1 + 2 * n * nhm) : nullptr;
+        dhm.bytes = (const uint8_t *)(const void *)(d_oo + n + 1 + 2 * n * nhm + n * nvm);
     }
     const uint8_t *d_j = c->d_json + 16 * (n + 1) + 8 * hmw;
     uint64_t *d_ret = (uint64_t *)(void *)c->d_pack;
@@ -692,7 +713,10 @@ static int batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
     std::vector<uint32_t> olen(hol, hol + n);
     memcpy(ret, hret, n * 8);
     /* the packed bytes: failed and overflowed messages hold none */
-    auto kept = [&](uint64_t i) { return ret[i] == 0 || (uint8_t)ret[i] == DG_ST_HM_END; };
+    auto kept = [&](uint64_t i) {
+        return ret[i] == 0 || (uint8_t)ret[i] == DG_ST_HM_END || (uint8_t)ret[i] == 24 /* ERR_VM_END's record */ ||
+               (uint8_t)ret[i] == DG_ST_HM_END_AT;
+    };
     uint64_t packed = 0;
     for (uint64_t i = 0; i < n; i++)
         if (kept(i)) packed += olen[i];
@@ -708,15 +732,16 @@ static int batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
         const uint64_t m = redo.size();
         uint64_t rb = 0;
         for (uint64_t i : redo) rb += ioff[i + 1] - ioff[i];
-        const uint64_t rhw = hm ? 2 * m * nhm + hmb / 8 : 0;
+        const uint64_t rhw = hm ? 2 * m * nhm + m * nvm + hmb / 8 : 0;
         std::vector<uint8_t> up(16 * (m + 1) + 8 * rhw + rb + 64, 0);
         uint64_t *io = (uint64_t *)(void *)up.data(), *so = io + m + 1, *rhm = so + m + 1;
         uint8_t *rj = (uint8_t *)(void *)(rhm + rhw);
         io[0] = so[0] = 0;
-        if (hm && hm_len) memcpy(rhm + 2 * m * nhm, hm->bytes, hm_len);
+        if (hm && hm_len) memcpy(rhm + 2 * m * nhm + m * nvm, hm->bytes, hm_len);
         for (uint64_t k = 0; k < m; k++) {
             const uint64_t i = redo[k], l = ioff[i + 1] - ioff[i];
             if (hm && nhm) memcpy(rhm + 2 * k * nhm, hm->tab + i * nhm, 16 * nhm);
+            if (hm && nvm) memcpy(rhm + 2 * m * nhm + k, hm->vm + i, 8);
             memcpy(rj + io[k], hj + ioff[i], l);
             io[k + 1] = io[k] + l;
             so[k + 1] = so[k] + (((uint64_t)olen[i] + 64 + 7) & ~7ull);
@@ -732,8 +757,9 @@ static int batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
         uint64_t *r_ret = (uint64_t *)(void *)c->d_pack; /* rhead <= head: d_pack is large enough */
         uint32_t *r_ol = (uint32_t *)(void *)(c->d_pack + 8 * m);
         HIPCHK(hipMemcpyAsync(c->d_json, up.data(), up.size(), hipMemcpyHostToDevice, s));
-        HMIn rhmd{(const dg_hm_entry *)(const void *)(r_oo + m + 1), (uint32_t)nhm,
-                  (const uint8_t *)(const void *)(r_oo + m + 1 + 2 * m * nhm)};
+        HMIn rhmd{nhm ? (const dg_hm_entry *)(const void *)(r_oo + m + 1) : nullptr, (uint32_t)nhm,
+                  (const uint8_t *)(const void *)(r_oo + m + 1 + 2 * m * nhm + m * nvm),
+                  nvm ? (const dg_cb_entry *)(const void *)(r_oo + m + 1 + 2 * m * nhm) : nullptr};
         if ((rc = launch(c, d, root, c->d_json + 16 * (m + 1) + 8 * rhw, r_in, m, flags, c->d_out, r_oo, r_ol, r_ret,
                          nullptr, s, max_len, hm ? &rhmd : nullptr)))
             return rc;
@@ -803,6 +829,31 @@ int dg_j2t_batch_host_hm(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8
     HMIn hm{hm_tab, n_hm, hm_bytes};
     return batch_host(c, d, root, json, in_off, n, flags, hm_tab ? &hm : nullptr, hm_len, out, out_cap, out_off, ret,
                       out_need);
+}
+
+int dg_j2t_batch_host_cb(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *json, const uint64_t *in_off,
+                         uint64_t n, uint64_t flags, const dg_cb_tables *cb, uint8_t *out, uint64_t out_cap,
+                         uint64_t *out_off, uint64_t *ret, uint64_t *out_need)
+{
+    if (!cb) return batch_host(c, d, root, json, in_off, n, flags, nullptr, 0, out, out_cap, out_off, ret, out_need);
+    if ((cb->len && !cb->bytes) || (cb->hm_tab && cb->n_hm && !n)) return set_err(DG_E_INVALID, "bad args");
+    for (uint64_t k = 0; cb->hm_tab && k < n * cb->n_hm; k++)
+        if (cb->hm_tab[k].len != DG_HM_ERR && (uint64_t)cb->hm_tab[k].off + cb->hm_tab[k].len > cb->len)
+            return set_err(DG_E_INVALID, "HTTP-mapping entry %llu outside the bytes", (unsigned long long)k);
+    for (uint64_t i = 0; cb->ans_tab && i < n; i++) {
+        /* the answers must lie inside the bytes (the kernel walks them unchecked) */
+        uint64_t at = cb->ans_tab[i].off;
+        for (uint32_t k = 0; k < cb->ans_tab[i].count; k++) {
+            if (at + 4 > cb->len) return set_err(DG_E_INVALID, "value-mapping entry %llu outside the bytes", (unsigned long long)i);
+            uint32_t l;
+            memcpy(&l, cb->bytes + at, 4);
+            at += 4 + (uint64_t)l;
+            if (at > cb->len) return set_err(DG_E_INVALID, "value-mapping entry %llu outside the bytes", (unsigned long long)i);
+        }
+    }
+    HMIn hm{cb->hm_tab, cb->hm_tab ? cb->n_hm : 0u, cb->bytes, cb->ans_tab};
+    return batch_host(c, d, root, json, in_off, n, flags, (cb->hm_tab || cb->ans_tab) ? &hm : nullptr, cb->len, out,
+                      out_cap, out_off, ret, out_need);
 }
 
 int dg_j2t_do(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *json, size_t len, uint64_t flags,

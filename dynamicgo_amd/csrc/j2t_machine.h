@@ -60,8 +60,9 @@ struct Params {
     uint64_t huge_min;
     const dg_hm_entry *hm_tab; /* DG_F_HM_SPLIT: n_hm entries per message (dgj2t_defs.h), or NULL: the root's
                                   mapped fields only, all written by the host */
-    const uint8_t *hm_bytes;
+    const uint8_t *hm_bytes;   /* the host's callback answers (dg_cb_tables.bytes) */
     uint32_t n_hm;
+    const dg_cb_entry *ans_tab; /* non-inline value mapping: one entry per message (dgj2t_defs.h), or NULL */
 };
 
 /* List message i (len bytes) for the wave kernel. Huge ones are written from
@@ -118,6 +119,9 @@ struct Machine {
     uint32_t field_cache_len;
     const dg_hm_entry *hm_row; /* this message's HTTP-mapping entries (Params::hm_tab), or NULL */
     const uint8_t *hm_bytes;
+    const dg_cb_entry *ans_row; /* this message's value-mapping answers (Params::ans_tab), or NULL */
+    uint32_t ans_seen;          /* non-inline value-mapping values met so far */
+    uint64_t ans_at;            /* hm_bytes offset of the next answer */
     JState jt;
     PROF_DECL
 
@@ -226,11 +230,42 @@ struct Machine {
      * DG_ST_HM_END with value = the word count. Elsewhere: the reference's
      * code (a nested struct's callback needs the Go FSM to resume). */
     template <class FR>
-    DGI uint64_t hm_end(const FR &x, const dg_struct &sd, int64_t p)
+    DGI uint64_t hm_end(const FR &x, const dg_struct &sd, uint32_t si, int64_t p)
     {
-        if (!(flag & DG_F_HM_SPLIT) || sp != 1) return pack0(E_HM_END, (uint64_t)p);
-        for (uint32_t w = 0; w < sd.req_words; w++) out.w64(sd.req_words == 1 ? x.u : ws.reqarena[(uint32_t)x.u + w]);
-        return pack(DG_ST_HM_END, sd.req_words, (uint64_t)p);
+        if (!(flag & DG_F_HM_SPLIT)) return pack0(E_HM_END, (uint64_t)p);
+        if (sp == 1) {
+            for (uint32_t w = 0; w < sd.req_words; w++) out.w64(sd.req_words == 1 ? x.u : ws.reqarena[(uint32_t)x.u + w]);
+            return pack(DG_ST_HM_END, sd.req_words, (uint64_t)p);
+        }
+        /* nested: the host's handleUnmatchedFields answer (fields + STOP), or
+         * stop for it (dgj2t_defs.h dg_cb_entry) */
+        field_cache_len = 0;
+        if (take_answer()) return 0;
+        out.set_len(0);
+        out.w64(si);
+        for (uint32_t w = 0; w < sd.req_words; w++) {
+            uint64_t bits = sd.req_words == 1 ? x.u : ws.reqarena[(uint32_t)x.u + w], m = 0;
+            while (bits) { /* the fields write_unset_fields cached (native/thrift.c:281-294) */
+                const uint32_t b = __builtin_ctzll(bits);
+                bits &= bits - 1;
+                const dg_field f = ldrec(&D.F[sd.field_begin + w * 64 + b]);
+                if (!(f.flags & DG_FF_REQUEST_BASE) && f.required == DG_REQ_REQUIRED) m |= 1ull << b;
+            }
+            out.w64(m);
+        }
+        return pack(DG_ST_HM_END_AT, sd.req_words, (uint64_t)p);
+    }
+
+    /* the host's next callback answer (dg_cb_entry), if it has one: written */
+    DGI bool take_answer()
+    {
+        if (!ans_row || ans_seen >= ans_row->count) return false;
+        const uint32_t n = (uint32_t)hm_bytes[ans_at] | ((uint32_t)hm_bytes[ans_at + 1] << 8) |
+                           ((uint32_t)hm_bytes[ans_at + 2] << 16) | ((uint32_t)hm_bytes[ans_at + 3] << 24);
+        for (uint32_t b = 0; b < n; b++) out.w8(hm_bytes[ans_at + 4 + b]);
+        ans_at += 4 + (uint64_t)n;
+        ans_seen++;
+        return true;
     }
 
     /* j2t_number native/thrift.c:312-365 */
@@ -516,13 +551,29 @@ struct Machine {
             }
             return 0;
         }
-        /* non-inline value mapping: host callback (ERR_VM_END) */
+        /* non-inline value mapping: skip the value, then the Go host's
+         * handleValueMapping (conv/j2t/impl_amd64.go:117-155) on its text */
         p -= 1;
         int64_t s0 = p;
         SkipRes sr = skip_one(src, p, skipbits, skipcap);
         p = sr.p;
         if (sr.r == SKIP_DEEP) return pack0(DG_ST_DEEP, 0);
         if (sr.r < 0) return pack((uint32_t)-sr.r, (uint64_t)s0, (uint64_t)p);
+        /* agw.body_dynamic on a STRING field: field header, then the raw value
+         * text as a binary (thrift/annotation/value_mapping.go:101-106); the
+         * host rejects a value that ends the input (impl_amd64.go:132) */
+        if (f.vm == DG_VM_BODY_DYNAMIC && ft == DG_T_STRING && p < src.n) {
+            out.w8(ft);
+            out.w16(f.id);
+            out.w32((uint32_t)(p - s0));
+            copy_src(s0, p - s0);
+            return 0;
+        }
+        if (take_answer()) return 0; /* the host's answer for this value (dg_cb_entry) */
+        /* ERR_VM_END for the host: the value's start and the field, in the slot */
+        out.set_len(0);
+        out.w64((uint64_t)s0);
+        out.w64((uint64_t)fidx);
         return pack0(E_VM_END, (uint64_t)p);
     }
 
@@ -584,8 +635,12 @@ struct Machine {
                         PROF(6, r = write_unset_fields(x, sd, p - 1));
                         if (r) return r;
                         if (sd.req_words > 1) reqlen -= sd.req_words;
-                        if ((flag & DG_F_ENABLE_HM) && field_cache_len > 0) return hm_end(x, sd, p);
-                        out.w8(0);
+                        if ((flag & DG_F_ENABLE_HM) && field_cache_len > 0) {
+                            uint64_t r2 = hm_end(x, sd, t.st, p);
+                            if (r2) return r2;
+                        } else {
+                            out.w8(0);
+                        }
                     } else {
                         out.put32(fbp(x), 0);
                     }
@@ -613,8 +668,12 @@ struct Machine {
                         PROF(6, r = write_unset_fields(x, sd, p - 1));
                         if (r) return r;
                         if (sd.req_words > 1) reqlen -= sd.req_words;
-                        if ((flag & DG_F_ENABLE_HM) && field_cache_len > 0) return hm_end(x, sd, p);
-                        out.w8(0);
+                        if ((flag & DG_F_ENABLE_HM) && field_cache_len > 0) {
+                            uint64_t r2 = hm_end(x, sd, t.st, p);
+                            if (r2) return r2;
+                        } else {
+                            out.w8(0);
+                        }
                     } else {
                         if (!null_val) set_size(x, fsize(x) + 1);
                         else {
@@ -814,6 +873,9 @@ DGI uint64_t convert_one(const Params &P, const DV &dv, uint64_t i, const S &src
     m.field_cache_len = 0;
     m.hm_row = P.hm_tab ? P.hm_tab + i * P.n_hm : nullptr;
     m.hm_bytes = P.hm_bytes;
+    m.ans_row = P.ans_tab ? P.ans_tab + i : nullptr;
+    m.ans_seen = 0;
+    m.ans_at = m.ans_row ? m.ans_row->off : 0;
     uint64_t r;
     if (m.src.n == 0) { /* empty body -> STOP (conv/j2t/impl.go:52-82) */
         m.out.w8(0);
@@ -837,7 +899,8 @@ DGI uint64_t convert_one(const Params &P, const DV &dv, uint64_t i, const S &src
         r = m.run(P.root);
 #endif
     }
-    const bool keep = r == 0 || (uint8_t)r == DG_ST_HM_END; /* HM_END: the host completes the output */
+    /* HM_END: the host completes the output; VM_END / HM_END_AT: the callback's record */
+    const bool keep = r == 0 || (uint8_t)r == DG_ST_HM_END || (uint8_t)r == E_VM_END || (uint8_t)r == DG_ST_HM_END_AT;
     if (keep) m.out.finish();
     if (keep && m.out.len > m.out.cap) {
         /* the bytes needed travel in out_len (32 bits); the 24-bit value field

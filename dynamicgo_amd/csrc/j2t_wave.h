@@ -1362,8 +1362,9 @@ __global__ __launch_bounds__(256) void dg_pack_scan_kernel(const uint8_t *out, c
         if (!fr.ret) return out_len[i];
         if (fr.ret[i] == 0) return out_len[i] + fx;
         /* failed messages pack as nothing; an unframed DG_ST_HM_END keeps its
-         * partial output for the host (dgj2t_defs.h) */
-        return !fr.hdr && (uint8_t)fr.ret[i] == DG_ST_HM_END ? out_len[i] : 0u;
+         * partial output and an ERR_VM_END its record for the host (dgj2t_defs.h) */
+        const uint8_t c = (uint8_t)fr.ret[i];
+        return !fr.hdr && (c == DG_ST_HM_END || c == 24u || c == DG_ST_HM_END_AT) ? out_len[i] : 0u;
     };
     uint64_t s = 0;
     for (uint64_t i = lo + tid; i < hi; i += 256) s += msg_len(i);

@@ -12,7 +12,8 @@ Mirrors the reference's descriptor model:
 This is host-side descriptor construction (init-time), not the
 hot path. The IDL front end covers the subset the reference's testdata uses:
 include, namespace, typedef, enum, const, struct/union/exception, service;
-annotations go.tag json, api.key, api.js_conv and the api.* HTTP mappings.
+annotations go.tag json, api.key, api.js_conv, the api.* HTTP mappings, the
+agw.* ones of InitAGWAnnos and registered value mappings.
 """
 from __future__ import annotations
 
@@ -34,6 +35,7 @@ OPTIONAL, DEFAULT, REQUIRED = 0, 1, 2
 
 VM_NONE = 0
 VM_JSCONV = 101  # internal/types/types.go:445
+VM_BODY_DYNAMIC = 257  # thrift/annotation/value_mapping.go:51
 
 HTTP_MAPPING_KEYS = ("api.query", "api.path", "api.header", "api.cookie", "api.body",
                      "api.http_code", "api.raw_body", "api.form", "api.raw_uri",
@@ -73,10 +75,70 @@ class FieldDescriptor:
     is_request_base: bool = False
     is_response_base: bool = False
     http_mappings: List[Tuple[str, str]] = _dcfield(default_factory=list)  # (annotation key, value), IDL order
+    value_mapping: Optional["ValueMapping"] = None  # FieldDescriptor.ValueMapping() (thrift/descriptor.go:318-321)
 
     def __post_init__(self):
         if self.alias is None:
             self.alias = self.name
+
+
+class ValueMappingError(Exception):
+    """An error a ValueMapping.write returns (wrapped by the caller as
+    meta.ErrConvert "failed to convert field '<name>' value")."""
+
+
+class ValueMapping:
+    """thrift.ValueMapping (thrift/annotation.go): the non-inline value
+    mappings the Go host runs on ERR_VM_END (handleValueMapping,
+    conv/j2t/impl_amd64.go:117-155). ``write`` gets the field and the value's
+    raw JSON text and returns the Thrift bytes BinaryProtocol would append
+    after the field header (raise ValueMappingError to fail the message)."""
+
+    def write(self, field: "FieldDescriptor", src: bytes) -> bytes:
+        raise NotImplementedError
+
+
+class AgwBodyDynamic(ValueMapping):
+    """agwBodyDynamic.Write (thrift/annotation/value_mapping.go:101-106): the
+    value's JSON text as a Thrift binary. The GPU serves it inline for STRING
+    fields; this host copy only runs for the cases it refuses."""
+
+    def write(self, field, src: bytes) -> bytes:
+        if field.type.type != STRING:
+            raise ValueMappingError("body_dynamic only support STRING type")
+        return _st.pack(">I", len(src)) + bytes(src)
+
+
+class _InlineJSConv(ValueMapping):
+    """api.js_conv: inline on the device (native/thrift.c:514-634); never
+    called back."""
+
+    def write(self, field, src: bytes) -> bytes:  # pragma: no cover - inline
+        raise ValueMappingError("api.js_conv is inline")
+
+
+# annotation key -> (value-mapping type, ValueMapping) (thrift/annotation/register.go:42)
+_VALUE_MAPPINGS: Dict[str, Tuple[int, ValueMapping]] = {"api.js_conv": (VM_JSCONV, _InlineJSConv())}
+# key-mapping annotations (register.go:45): the field's JSON alias
+_KEY_MAPPINGS = {"api.key"}
+
+
+def register_value_mapping(key: str, vm_type: int, mapping: ValueMapping):
+    """thrift.RegisterAnnotation of a value-mapping annotation
+    (thrift/annotation.go, e.g. value_mapping_test.go:46-48): fields annotated
+    with `key` get value-mapping type `vm_type` (> 255: served by the host
+    through `mapping` on ERR_VM_END)."""
+    if not 0 < vm_type < 65536:
+        raise ValueError("value-mapping type out of range")
+    _VALUE_MAPPINGS[key] = (vm_type, mapping)
+
+
+def init_agw_annos():
+    """annotation.InitAGWAnnos (thrift/annotation/register.go:56-66), the
+    parts j2t reads: agw.js_conv, agw.body_dynamic and agw.key."""
+    _VALUE_MAPPINGS["agw.js_conv"] = (VM_JSCONV, _InlineJSConv())
+    _VALUE_MAPPINGS["agw.body_dynamic"] = (VM_BODY_DYNAMIC, AgwBodyDynamic())
+    _KEY_MAPPINGS.add("agw.key")
 
 
 class StructDescriptor:
@@ -730,16 +792,17 @@ class _Compiler:
         for pf in ff.structs[name]:
             alias = pf.name
             vm = VM_NONE
+            vmap = None
             hms = []
             for k, v in pf.annos:
                 if k == "go.tag":
                     m = re.search(r'json:"([^"]*)"', v) or re.search(r"json:\\\"([^\\]*)\\\"", v)
                     if m:
                         alias = m.group(1).split(",")[0] or alias
-                elif k == "api.key":
+                elif k in _KEY_MAPPINGS:
                     alias = v
-                elif k == "api.js_conv":
-                    vm = VM_JSCONV
+                elif k in _VALUE_MAPPINGS:
+                    vm, vmap = _VALUE_MAPPINGS[k]
                 elif k in HTTP_MAPPING_KEYS:
                     hms.append((k, v))
             is_req_base = (self.opts.enable_thrift_base and pf.type.name == "base.Base" and depth == 0)
@@ -748,7 +811,7 @@ class _Compiler:
             dflt = self.const_default(ff, ftype, pf.default) if self.opts.use_default_value else None
             req = {"default": DEFAULT, "optional": OPTIONAL, "required": REQUIRED}[pf.req]
             sd.add_field(FieldDescriptor(pf.id, pf.name, ftype, req, alias, vm, dflt,
-                                         is_req_base, is_resp_base, hms),
+                                         is_req_base, is_resp_base, hms, vmap),
                          set_optional_bitmap=self.opts.set_optional_bitmap,
                          map_field_way=self.opts.map_field_way)
         return td

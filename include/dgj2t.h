@@ -142,6 +142,15 @@ int dg_j2t_batch_device_hm(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type,
                            uint32_t *d_out_len, uint64_t *d_ret, uint32_t *d_pending, void *stream,
                            uint64_t max_len);
 
+/* dg_j2t_batch_device_ml with the host's answers to the reference's Go
+ * callbacks (dg_cb_tables, dgj2t_defs.h; device pointers): the HTTP-mapping
+ * table of dg_j2t_batch_device_hm and the value-mapping answers (ERR_VM_END,
+ * handleValueMapping conv/j2t/impl_amd64.go:117-155). cb NULL = none. */
+int dg_j2t_batch_device_cb(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, const uint8_t *d_json,
+                           const uint64_t *d_in_off, uint64_t n, uint64_t flags, const dg_cb_tables *cb,
+                           uint8_t *d_out, const uint64_t *d_out_off, uint32_t *d_out_len, uint64_t *d_ret,
+                           uint32_t *d_pending, void *stream, uint64_t max_len);
+
 /* dg_j2t_batch_device_ml enqueued `iters` times back to back in one call
  * (one lock, no host round trip between batches): a host that re-runs the
  * same job -- benchmarks, replays -- keeps the GPU fed. Every iteration is a
@@ -192,6 +201,13 @@ int dg_j2t_batch_host_hm(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, c
                          const uint64_t *in_off, uint64_t n, uint64_t flags, const dg_hm_entry *hm_tab, uint32_t n_hm,
                          const uint8_t *hm_bytes, uint64_t hm_len, uint8_t *out, uint64_t out_cap, uint64_t *out_off,
                          uint64_t *ret, uint64_t *out_need);
+
+/* dg_j2t_batch_host with the host's callback answers (dg_cb_tables, host
+ * memory): DG_ST_HM_END messages keep their partial output (and requires
+ * words) in out, ERR_VM_END messages (code 24) their 16-byte record. */
+int dg_j2t_batch_host_cb(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, const uint8_t *json,
+                         const uint64_t *in_off, uint64_t n, uint64_t flags, const dg_cb_tables *cb, uint8_t *out,
+                         uint64_t out_cap, uint64_t *out_off, uint64_t *ret, uint64_t *out_need);
 
 /* One message, BinaryConv.Do semantics (conv/j2t/conv.go:53-77). *out_len is
  * the Thrift length; returns the packed status word through *ret. */

@@ -42,6 +42,7 @@
                                     out_len covers the output so far followed by the root's remaining requires
                                     words (big-endian u64, `value` of them); the host appends the cached fields'
                                     bytes and the STOP */
+#define DG_ST_HM_END_AT 0xF4u    /* a nested struct's ERR_HM_END for the host (dg_cb_entry) */
 #define DG_ST_HM_ERR 0xF3u       /* DG_F_HM_SPLIT: the message opened a struct whose HTTP-mapping entry is an
                                     error (dg_hm_entry.len == DG_HM_ERR): handleHttpMappings failed for it on the
                                     host; value = the entry's slot, pos = the struct's '{' */
@@ -59,6 +60,45 @@ typedef struct dg_hm_entry {
     uint64_t mask;
 } dg_hm_entry;
 #define DG_HM_ERR 0xFFFFFFFFu
+
+/* Callbacks the reference returns to its Go host mid-message and resumes
+ * after (handleError, conv/j2t/impl_amd64.go:169-247), served here by
+ * converting the message again with the host's answers:
+ *  - ERR_VM_END (native/thrift.c:641-665): a non-inline value mapping (a
+ *    value-mapping type above DG_VM_INLINE_MAX under F_ENABLE_VM; the device
+ *    serves DG_VM_BODY_DYNAMIC on a STRING field itself). The host writes the
+ *    field header and runs the annotation's ValueMapping.Write on the value's
+ *    JSON text (handleValueMapping, impl_amd64.go:117-155).
+ *  - ERR_HM_END (native/thrift.c:898-903,952-957) of a NESTED struct under
+ *    DG_F_HM_SPLIT + F_TRACE_BACK (the root's is DG_ST_HM_END): the host
+ *    writes the cached fields from the request, then STOP
+ *    (handleUnmatchedFields, impl_amd64.go:71-115).
+ * Per message one dg_cb_entry: `count` answers at bytes[off..], in the order
+ * the message meets the callbacks, each a u32 little-endian length and that
+ * many bytes. The (count+1)-th callback stops the message:
+ *  - ERR_VM_END: status code 24, pos = the value's end (as the reference packs
+ *    it); out_len 16: the value's start and the field's descriptor index, two
+ *    big-endian u64.
+ *  - nested ERR_HM_END: status DG_ST_HM_END_AT (below), value = w, pos = the
+ *    position after the '}'; out_len 8 + 8w: the struct's descriptor index,
+ *    then w big-endian u64 words whose set bits are the cached fields (bit k =
+ *    the struct's k-th field in id order). */
+typedef struct dg_cb_entry {
+    uint32_t off;
+    uint32_t count;
+} dg_cb_entry;
+
+/* The host's answers to the reference's Go callbacks for one batch
+ * (dg_j2t_batch_*_cb): HTTP-mapping entries (n_hm per message, see
+ * dg_hm_entry; hm_tab NULL: none) and callback answers (one dg_cb_entry per
+ * message; ans_tab NULL: none), both pointing into `bytes` (len bytes). */
+typedef struct dg_cb_tables {
+    const dg_hm_entry *hm_tab;
+    uint32_t n_hm;
+    const dg_cb_entry *ans_tab;
+    const uint8_t *bytes;
+    uint64_t len;
+} dg_cb_tables;
 
 /* API error codes */
 #define DG_OK 0

@@ -74,6 +74,8 @@
 #define DG_VM_NONE 0
 #define DG_VM_JSCONV 101
 #define DG_VM_INLINE_MAX 255
+#define DG_VM_BODY_DYNAMIC 257 /* agw.body_dynamic (thrift/annotation/value_mapping.go:49-51,101-106): the
+                                  value's raw JSON text as a Thrift binary; served on the device */
 
 /* dg_struct.flags */
 #define DG_SF_HTTP_MAPPING 1u /* len(StructDescriptor.hms) != 0 */

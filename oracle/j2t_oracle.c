@@ -13,7 +13,8 @@
  *    the end in check_leading_zero; the harness pads with NUL);
  *  - output buffers never run out (the reference's OOM re-entry is a
  *    transparent retry in Go, conv/j2t/impl_amd64.go:199-226);
- *  - host callbacks (ERR_HM, ERR_HM_END, ERR_VM_END) are returned as codes.
+ *  - host callbacks ERR_HM and ERR_HM_END are returned as codes; ERR_VM_END
+ *    is served like the Go host does for the test mappings (vm_host.h).
  */
 #include <math.h>
 #include <stdbool.h>
@@ -50,6 +51,8 @@ enum { J_VAL = 0, J_ARR = 1, J_OBJ = 2, J_KEY = 3, J_ELEM = 4, J_ARR_0 = 5, J_OB
 #define MAX_RECURSE 4096
 
 /* WRAP_ERR_POS / WRAP_ERR0 native/thrift.h:226-242 (v, p already cast by caller) */
+#include "vm_host.h"
+
 #define PACK(e, v, p) ((((uint64_t)(v)) << 40) | (((uint64_t)(p)) << 8) | (uint8_t)(e))
 #define PACK0(e, v) ((((uint64_t)(v)) << 8) | (uint8_t)(e))
 /* WRAP_ERR2's value: ((uint32_t)(vh) << 8 | (uint8_t)(vl)) */
@@ -1578,13 +1581,22 @@ static uint64_t j2t_field_vm(M *m, int64_t *p, Frame *vt)
         }
         return 0;
     }
-    /* non-inline value mapping: host callback (ERR_VM_END) */
+    /* non-inline value mapping: host callback (ERR_VM_END), served here the
+     * way the Go host does and resumed (oracle/vm_host.h); a failing callback
+     * returns the ERR_VM_END word */
     *p -= 1;
     int64_t s = *p;
     int64_t r = skip_one(src, p, m->skipstk);
     if (r < 0)
         return PACK(-r, (uint64_t)s, (uint64_t)*p);
-    return PACK0(E_VM_END, (uint64_t)*p);
+    if (*p >= src->n) /* "invalid value-mapping position" (conv/j2t/impl_amd64.go:132-134) */
+        return PACK0(E_VM_END, (uint64_t)*p);
+    bgrow(b, b->len + (size_t)(*p - r) + 16);
+    long k = vmh_write(f->vm, ft, f->id, src->s + r, (size_t)(*p - r), b->b + b->len);
+    if (k < 0)
+        return PACK0(E_VM_END, (uint64_t)*p);
+    b->len += (size_t)k;
+    return 0;
 }
 
 /* j2t_fsm_exec native/thrift.c:765-1187 */

@@ -158,6 +158,25 @@ class _Base:
             return int(ret), b"", []
         return int(ret), out.raw[:ol.value], [int(fc[k]) for k in range(fl.value)]
 
+    def set_hm_end_cb(self, fn):
+        """A nested struct's ERR_HM_END served by `fn(struct_index, field_ids)
+        -> bytes or None` (the test's host, handleUnmatchedFields + STOP);
+        None = the host failed. fn None clears it (reference harness only)."""
+        proto = C.CFUNCTYPE(C.c_long, C.c_uint32, C.POINTER(C.c_int32), C.c_size_t, C.POINTER(C.c_uint8), C.c_size_t)
+        if fn is None:
+            self._hm_end_keep = None
+            self.lib.dgref_set_hm_end_cb(proto())
+            return
+
+        def tramp(si, ids, n, dst, cap):
+            b = fn(int(si), [int(ids[k]) for k in range(n)])
+            if b is None or len(b) > cap:
+                return -1
+            C.memmove(dst, bytes(b), len(b))
+            return len(b)
+        self._hm_end_keep = proto(tramp)
+        self.lib.dgref_set_hm_end_cb(self._hm_end_keep)
+
     def j2t_batch(self, flat, msgs: Sequence[bytes], flags: int, nthreads: int = 1,
                   root: Optional[int] = None, slot_factor: int = 4, slot_pad: int = 64):
         """Batch API over an arena: returns (rets u64[n], outs list[bytes])."""

@@ -33,6 +33,7 @@
 
 #include "../include/dgj2t_desc.h"
 #include "../include/dgj2t_defs.h"
+#include "vm_host.h"
 
 typedef struct {
     tTypeDesc *types;
@@ -258,6 +259,13 @@ static uint64_t g_hm_mask = ~0ull;
 static const uint8_t *g_hm_bytes;
 static const uint32_t *g_hm_off, *g_hm_lens;
 static const uint64_t *g_hm_masks;
+/* a NESTED struct's ERR_HM_END: the test's host (the Python restatement of
+ * handleUnmatchedFields) writes the cached fields + STOP through this
+ * callback: (struct index in blob order, field ids, count, dst, cap) ->
+ * bytes written, or -1 = the host failed (the ERR_HM_END word is returned) */
+typedef long (*dgref_hm_end_fn)(uint32_t, const int32_t *, size_t, uint8_t *, size_t);
+static dgref_hm_end_fn g_hm_end_cb;
+void dgref_set_hm_end_cb(dgref_hm_end_fn f) { g_hm_end_cb = f; }
 static int32_t *g_fc_out;
 static size_t g_fc_cap, g_fc_len;
 static int g_fc_on;
@@ -418,7 +426,75 @@ static uint64_t ref_do(RefCtx *c, RefDesc *d, uint32_t root, const uint8_t *json
                 memcpy(out, buf.buf, buf.len);
             return ret;
         }
-        break; /* real error or host callback (ERR_HM/HM_END/VM_END) */
+        if (e == ERR_HM_END && g_hm_end_cb && fsm->sp > 1) {
+            /* handleError -> handleUnmatchedFields (conv/j2t/impl_amd64.go:71-115,
+             * 185-198): the struct on top (At(SP-1)), the field cache, then
+             * FieldCache[:0], SP-- and SetPos(pos) */
+            const J2TState *sv = &fsm->vt[fsm->sp - 1];
+            if (!sv->td || sv->td->type != TTYPE_STRUCT || fsm->field_cache.len == 0)
+                break;
+            const size_t si = (size_t)(sv->td->st - d->structs);
+            uint8_t tmp[1 << 16];
+            long k = g_hm_end_cb((uint32_t)si, fsm->field_cache.buf, fsm->field_cache.len, tmp, sizeof tmp);
+            if (k < 0)
+                break;
+            if (buf.len + (size_t)k > buf.cap) {
+                size_t nc = (buf.len + (size_t)k) * 2 + 64;
+                char *nb = (char *)malloc(nc + 64);
+                memcpy(nb, buf.buf, buf.len);
+                free(c->buf);
+                c->buf = nb;
+                c->buf_cap = nc + 64;
+                buf.buf = nb;
+                buf.cap = nc;
+            }
+            memcpy(buf.buf + buf.len, tmp, (size_t)k);
+            buf.len += (size_t)k;
+            fsm->field_cache.len = 0;
+            fsm->sp--;
+            fsm->vt[fsm->sp - 1].jp = (long)p;
+            continue;
+        }
+        if (e == ERR_VM_END) {
+            /* handleError -> handleValueMapping (conv/j2t/impl_amd64.go:117-155,
+             * 233-243): the struct at SP-2, the field by id, the value's span from
+             * FieldValueCache, field header + ValueMapping.Write, then SP-- and
+             * SetPos(pos) (vm_host.h); a failing callback returns the word */
+            if (fsm->sp < 2)
+                break;
+            const J2TState *sv = &fsm->vt[fsm->sp - 2];
+            if (!sv->td || sv->td->type != TTYPE_STRUCT)
+                break;
+            const tStructDesc *st = sv->td->st;
+            const FieldVal *fv = &fsm->fval_cache;
+            const tFieldDesc *f = (size_t)fv->id < st->ids.len ? ((tFieldDesc **)st->ids.buf)[fv->id] : NULL;
+            if (!f || (size_t)fv->end >= slen || fv->start < 0)
+                break;
+            const size_t vn = (size_t)(fv->end - fv->start);
+            if (buf.len + vn + 16 > buf.cap) {
+                size_t nc = (buf.len + vn + 16) * 2 + 64;
+                char *nb = (char *)malloc(nc + 64);
+                memcpy(nb, buf.buf, buf.len);
+                free(c->buf);
+                c->buf = nb;
+                c->buf_cap = nc + 64;
+                buf.buf = nb;
+                buf.cap = nc;
+            }
+            long k = vmh_write(f->vm, f->type->type, (uint16_t)f->ID, (const uint8_t *)c->src + fv->start, vn,
+                               (uint8_t *)buf.buf + buf.len);
+            if (k < 0)
+                break;
+            buf.len += (size_t)k;
+            fsm->sp--;
+            if (fsm->sp > 0) {
+                fsm->vt[fsm->sp - 1].jp = (long)p;
+                continue;
+            }
+            ret = 0;
+            break;
+        }
+        break; /* real error or host callback (ERR_HM/HM_END) */
     }
     if (ret != 0)
         return ret;

@@ -53,7 +53,17 @@ def _expected(td, body, req, opts):
         except H.ConvError as e:
             return "err", e.behavior
     ents = _entries(flat, hx, req)
-    r, out, fc = REF.j2t_hm3(flat, body, conv.to_flags(opts), ents)
+
+    def nested_end(si, ids):  # a nested struct's ERR_HM_END: handleUnmatchedFields (top = true) + STOP
+        try:
+            return hx.handle_unmatched_fields(req, flat.structs[si], ids, True) + b"\x00"
+        except H.ConvError:
+            return None
+    REF.set_hm_end_cb(nested_end)
+    try:
+        r, out, fc = REF.j2t_hm3(flat, body, conv.to_flags(opts), ents)
+    finally:
+        REF.set_hm_end_cb(None)
     if r == 0:
         return "ok", out
     if r & 0xFF == 21:  # the root's ERR_HM_END: handleUnmatchedFields + STOP
