@@ -164,7 +164,9 @@ __global__ __launch_bounds__(256) void pipe_copy_out_kernel(const uint8_t *src, 
         if (i < n) ret_dst[i] = ret_src[i];
     }
     const uint64_t end = src_off[n];
-    const uint64_t lim = dst_cap > wb ? dst_cap - wb : 0; /* local bytes below dst_cap */
+    /* local bytes below dst_cap: dst_cap - wb without the wrap of wb = base - ph
+     * when base < ph (the first chunk into a destination not 16-aligned) */
+    const uint64_t lim = dst_cap + ph > base ? dst_cap + ph - base : 0;
     const uint64_t stop = end < lim ? end : lim;
     for (uint64_t w = tid; w * 16 < stop; w += nth) {
         const uint64_t lo = w * 16, hi = lo + 16;
@@ -884,7 +886,9 @@ int dg_j2t_pipeline_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8
         HIPCHK(hipEventRecord(p.ev_hdr, p.s));
     }
     for (int i = 0; i < nb; i++) HIPCHK(hipStreamSynchronize(((PipeBuf *)c->pipe[i])->s));
-    const uint64_t cursor = p_off[n];
+    /* the host's view of the offsets (a hipHostRegister'd buffer's device
+     * alias need not equal its host address) */
+    const uint64_t cursor = direct ? out_off[n] : p_off[n];
     bool fits = cursor <= out_cap;
     if (!direct) {
         memcpy(out_off, p_off, 8 * (n + 1));

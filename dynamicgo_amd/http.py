@@ -217,9 +217,48 @@ def mapping_request(kind: str, value: str, req: HTTPRequest, field: T.FieldDescr
         return req.get_body().decode("utf-8", "surrogateescape")
     elif kind == "api.raw_uri":
         return req.get_uri()
-    else:  # api.http_code: response only; api.no_body_struct: not restated here
+    elif kind == "api.no_body_struct":
+        return no_body_struct(req, field)
+    else:  # api.http_code: response only
         return None
     return v if v != "" else None
+
+
+def mapping_encoding(kind: str) -> int:
+    """HttpMapping.Encoding(): Thrift binary for api.no_body_struct
+    (http_mapping.go:350-352), JSON for the request-side others."""
+    return ENCODING_THRIFT_BINARY if kind == "api.no_body_struct" else ENCODING_JSON
+
+
+def no_body_struct(req: HTTPRequest, field: T.FieldDescriptor) -> Optional[str]:
+    """apiNoBodyStruct.Request (thrift/annotation/http_mapping.go:299-344): the
+    STRUCT field's value built from the request alone -- each of its mapped
+    fields (HttpMappingFields order) with its first value found, or its
+    default / empty value, then STOP -- as Thrift binary (returned as a str
+    whose surrogateescape encoding is the bytes). The conv options come from
+    the context in Go; none here: the zero Options (base64 on, unknown fields
+    allowed). A value WriteStringWithDesc rejects leaves only its header
+    (the Go code drops that error)."""
+    if field.type.type != T.STRUCT:
+        return None  # "apiNoBodyStruct only support STRUCT type"
+    out = b""
+    for f in field.type.struct.hms:
+        val = None
+        for kind, value in f.http_mappings:
+            v = mapping_request(kind, value, req, f)
+            if v is not None:
+                val = v
+                break
+        out += field_begin(f)
+        if val is None or val == "":
+            out += write_default_or_empty(f)
+        else:
+            try:
+                out += decode_text(val, f.type, False, True)
+            except (ValueError, ConvError):
+                pass
+    out += b"\x00"
+    return out.decode("utf-8", "surrogateescape")
 
 
 def try_get_value_from_http(req: Optional[HTTPRequest], key: str) -> Tuple[str, bool, int]:
@@ -416,7 +455,7 @@ class HMContext:
             for kind, value in f.http_mappings:
                 v = mapping_request(kind, value, req, f)
                 if v is not None:
-                    enc, ok, val = ENCODING_JSON, True, v
+                    enc, ok, val = mapping_encoding(kind), True, v
                     break
             if not ok:
                 if nobody:

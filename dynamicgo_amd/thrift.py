@@ -121,6 +121,12 @@ class _InlineJSConv(ValueMapping):
 _VALUE_MAPPINGS: Dict[str, Tuple[int, ValueMapping]] = {"api.js_conv": (VM_JSCONV, _InlineJSConv())}
 # key-mapping annotations (register.go:45): the field's JSON alias
 _KEY_MAPPINGS = {"api.key"}
+# agw.source / janus.source (sourceMapper, thrift/annotation/anno_mapping.go:
+# 92-136), registered by init_agw_annos: source value -> HTTP mapping kind
+_SOURCE_KEYS: set = set()
+_SOURCE_KINDS = {"query": "api.query", "header": "api.header", "body": "api.body", "cookie": "api.cookie",
+                 "post": "api.form", "path": "api.path", "raw_uri": "api.raw_uri", "raw_body": "api.raw_body",
+                 "not_body_struct": "api.no_body_struct"}
 
 
 def register_value_mapping(key: str, vm_type: int, mapping: ValueMapping):
@@ -139,6 +145,7 @@ def init_agw_annos():
     _VALUE_MAPPINGS["agw.js_conv"] = (VM_JSCONV, _InlineJSConv())
     _VALUE_MAPPINGS["agw.body_dynamic"] = (VM_BODY_DYNAMIC, AgwBodyDynamic())
     _KEY_MAPPINGS.add("agw.key")
+    _SOURCE_KEYS.update(("agw.source", "janus.source"))
 
 
 class StructDescriptor:
@@ -794,6 +801,7 @@ class _Compiler:
             vm = VM_NONE
             vmap = None
             hms = []
+            sources = []
             for k, v in pf.annos:
                 if k == "go.tag":
                     m = re.search(r'json:"([^"]*)"', v) or re.search(r"json:\\\"([^\\]*)\\\"", v)
@@ -805,6 +813,16 @@ class _Compiler:
                     vm, vmap = _VALUE_MAPPINGS[k]
                 elif k in HTTP_MAPPING_KEYS:
                     hms.append((k, v))
+                elif k in _SOURCE_KEYS:
+                    sources.append(v)
+            if sources:
+                # decideNameCase (anno_mapping.go:138-163): api.key / agw.key, else
+                # the field name (the agw.to_snake-style name cases are not restated)
+                name = next((v for k, v in pf.annos if k in ("api.key", "agw.key") and v), pf.name)
+                for v in sources:
+                    kind = _SOURCE_KINDS.get(v.lower())
+                    if kind is not None:
+                        hms.append((kind, name))
             is_req_base = (self.opts.enable_thrift_base and pf.type.name == "base.Base" and depth == 0)
             is_resp_base = (self.opts.enable_thrift_base and pf.type.name == "base.BaseResp" and depth == 0)
             ftype = self.ptype(ff, pf.type, cache, depth + 1)

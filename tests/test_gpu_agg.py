@@ -144,11 +144,13 @@ def test_pipeline_host_overflow_splice_and_nomem():
     assert [(int(r), o) for r, o in zip(rets, outs)] == [(r, o) for r, o in want]
 
 
-@pytest.mark.parametrize("chunks", [1, 5])
-def test_pipeline_host_pinned_direct(chunks):
+@pytest.mark.parametrize("chunks,shift", [(1, 0), (5, 0), (1, 3), (4, 11)])
+def test_pipeline_host_pinned_direct(chunks, shift):
     """With pinned host buffers the chained packing writes the caller's
     out / out_off straight from the GPU; a too-small out_cap writes nothing
-    past it and reports the exact need."""
+    past it and reports the exact need. shift: `out` starts that many bytes
+    into a pinned allocation (not 16-aligned: the first chunk's copy-out
+    must not drop its bytes)."""
     import ctypes as C
     import numpy as np
     import torch
@@ -167,7 +169,8 @@ def test_pipeline_host_pinned_direct(chunks):
     L = _lib.lib()
     need = C.c_uint64(0)
     for cap in (1000, int(off[-1]) * 4 + 80 * n + 64):
-        h_out = torch.full((cap + 64,), 0xAB, dtype=torch.uint8).pin_memory()
+        h_buf = torch.full((cap + 64 + shift,), 0xAB, dtype=torch.uint8).pin_memory()
+        h_out = h_buf[shift:]
         h_oo = torch.zeros(n + 1, dtype=torch.int64).pin_memory()
         h_ret = torch.zeros(n, dtype=torch.int64).pin_memory()
         rc = L.dg_j2t_pipeline_host(ctx.h, ctx.desc(fl), fl.root_type, h_json.data_ptr(), h_in.data_ptr(), n, 1,

@@ -213,3 +213,13 @@ def test_thrift_request_base():
     out3 = conv.BinaryConv(opts3).do(td, json.dumps(d3).encode(), base=H.Base(LogID="1", Extra={"a": "1", "b": "1"}))
     got = decode(out3)["Base"]
     assert got["LogID"] == "1" and got["Client"] == "" and got["Extra"] == {"a": "1", "b": "1", "c": "2"}
+
+
+def test_no_body_struct():
+    """TestNoBodyStruct (conv/j2t/conv_test.go:1191-1212): the whole Do."""
+    from test_http_host import NO_BODY_EXPECTED, _no_body_struct_desc
+    td = _no_body_struct_desc()
+    req = conv.HTTPRequest(b"{}", url="http://localhost?b=1")
+    out = conv.BinaryConv(conv.Options(EnableHttpMapping=True)).do(td, b"{}", req=req)
+    assert out == NO_BODY_EXPECTED + b"\x00"
+    assert _check(td, [b"{}", b'{"NoBodyStruct":{"A":5}}'], [req, req], conv.Options(EnableHttpMapping=True)) == 2

@@ -100,3 +100,27 @@ def test_base_writer():
     assert nw and merged == ["2"] and out[:3] == bytes([12]) + struct.pack(">h", 255)
     out2, nw2 = H.write_request_base(b, f, b'{"Base":{"LogID":"2"}}', None)
     assert not nw2 and out2 == out
+
+
+def _no_body_struct_desc():
+    T.init_agw_annos()  # agw.source = "not_body_struct" -> api.no_body_struct (anno_mapping.go:125-126)
+    svc = T.new_descriptor_from_path(os.path.join(IDL, "example3.thrift"), T.Options(use_default_value=True))
+    return svc.functions()["NoBodyStructMethod"].request().struct.fields[0].type
+
+
+NO_BODY_EXPECTED = (b"\x0c\x00\x01" + b"\x08\x00\x02" + struct.pack(">i", 1) +
+                    b"\x08\x00\x03" + struct.pack(">i", 1) + b"\x00")
+
+
+def test_no_body_struct_mapping():
+    """apiNoBodyStruct.Request (http_mapping.go:299-344) as TestNoBodyStruct
+    (conv/j2t/conv_test.go:1191-1212) drives it: B from the query, C (not in
+    the request) its IDL default, A (unmapped) absent, then STOP, written as
+    Thrift binary (Encoding ThriftBinary) after the field header."""
+    td = _no_body_struct_desc()
+    f = td.struct.field_by_id(1)
+    assert f.http_mappings == [("api.no_body_struct", "NoBodyStruct")]
+    req = conv.HTTPRequest(b"{}", url="http://localhost?b=1")
+    hx = H.HMContext(conv.Options(EnableHttpMapping=True))
+    b, mask, again = hx.handle_http_mappings(req, td.struct, False)
+    assert b == NO_BODY_EXPECTED and mask == 1 and not again
