@@ -636,7 +636,7 @@ def bench_agg(args, rank, world, dev, dist, backend, td, arena, off, meta):
             "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
             "config": {"workload": CONFIGS[args.config][0], "global_batch": meta["global_batch"], "msgs_per_rank": n,
                        "avg_json_bytes": round(json_bytes / max(n, 1), 1), "flags": flags,
-                       "per_thread_batch_share": max_batch, "max_wait_us": max_wait_us, "batches_in_flight": 4,
+                       "per_thread_batch_share": max_batch, "max_wait_us": max_wait_us, "batches_in_flight": int(os.environ.get("DG_AGG_RING", "8")),
                        "gbs_json_in": main["gbs_json_in"], "lat_us_p50": main["lat_us_p50"],
                        "lat_us_p99": main["lat_us_p99"], "runs": runs, "checked_vs_oracle": n,
                        "reference_per_core_ns_per_op": (cpu or {}).get("one_core_ns_per_msg"),

@@ -207,7 +207,8 @@ class Context:
 
     def set_knob(self, name: str, value: int):
         """A routing knob (dg_ctx_set_knob, include/dgj2t.h): "flat",
-        "wave_min", "wave_occ", "small_mpw", "list_blocks", "t2j_spread"."""
+        "wave_min", "wave_occ", "small_mpw", "list_blocks", "t2j_spread",
+        "t2j_wave_min", "flat_wrap"."""
         _lib.check(_lib.lib().dg_ctx_set_knob(self.h, name.encode(), int(value)))
 
     def get_knob(self, name: str) -> int:

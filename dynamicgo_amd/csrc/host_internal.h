@@ -78,6 +78,7 @@ struct Knobs {
     int64_t list_blocks = 16;
     int64_t t2j_spread = 0;
     int64_t t2j_wave_min = 512; /* t2j messages longer than this take the wave kernel (0: never) */
+    int64_t flat_wrap = -1;     /* the flat kernel's wrapped mode for roots that wrap a flat struct (0: off) */
 };
 
 struct dg_ctx {

@@ -190,6 +190,28 @@ DGI bool has_byte(S &src, uint32_t s0, uint32_t nb, uint8_t ch)
     return false;
 }
 
+/* the name table of struct sd (native/thrift.c:449-468 j2t_find_field_key):
+ * the global field index of key src[k0, k0+kn), or -1 */
+template <class S, class DV>
+DGI int32_t fl_lookup(const DV &D, const dg_struct &sd, S &src, uint32_t k0, uint32_t kn)
+{
+    typedef typename S::idx SI;
+    uint32_t h = DG_NAME_HASH_SEED;
+    for (uint32_t j = 0; j < kn; j += 8) {
+        const uint64_t w = src.get8((SI)(k0 + j));
+        const uint32_t r = kn - j < 8 ? kn - j : 8u;
+#pragma unroll
+        for (uint32_t bb = 0; bb < 8; bb++)
+            if (bb < r) h = DG_NAME_HASH_STEP(h, (uint8_t)(w >> (8 * bb)));
+    }
+    for (uint32_t s = h & sd.name_mask;; s = (s + 1) & sd.name_mask) {
+        const dg_name nm = ldrec(&D.N[sd.name_begin + s]);
+        if (nm.field == DG_NONE) return -1;
+        if (nm.hash == h && nm.key_len == kn && key_eq(src, (SI)k0, kn, (decltype(&D.R[0]))(&D.P[nm.key_off])))
+            return (int32_t)nm.field;
+    }
+}
+
 /* Field k: bytes (sk, ek) between its separators, its colon at ck, nq quotes
  * inside. Key lookup, value parse and Thrift size; false = decline the
  * message. Every quote of the message is a delimiter (phase 1 declined \" and
@@ -225,22 +247,7 @@ DGI bool fl_field(const DV &D, const dg_struct &sd, S &src, uint32_t sk, uint32_
             fi = (int32_t)(sd.field_begin + k);
     }
     if (fi < 0) {
-        uint32_t h = DG_NAME_HASH_SEED;
-        for (uint32_t j = 0; j < kn; j += 8) {
-            const uint64_t w = src.get8((SI)(k0 + j));
-            const uint32_t r = kn - j < 8 ? kn - j : 8u;
-#pragma unroll
-            for (uint32_t bb = 0; bb < 8; bb++)
-                if (bb < r) h = DG_NAME_HASH_STEP(h, (uint8_t)(w >> (8 * bb)));
-        }
-        for (uint32_t s = h & sd.name_mask;; s = (s + 1) & sd.name_mask) {
-            const dg_name nm = ldrec(&D.N[sd.name_begin + s]);
-            if (nm.field == DG_NONE) break;
-            if (nm.hash == h && nm.key_len == kn && key_eq(src, (SI)k0, kn, (decltype(&D.R[0]))(&D.P[nm.key_off]))) {
-                fi = (int32_t)nm.field;
-                break;
-            }
-        }
+        fi = fl_lookup(D, sd, src, k0, kn);
         if (fi >= 0) f = ldrec(&D.F[fi]);
     }
     /* the value, [v0, ve) */
@@ -439,6 +446,17 @@ struct FlatParams {
     dg_desc_hdr hdr;
     uint32_t *bail_count;
     uint32_t *bail_list;
+    /* wrapped mode: the batch root R (P.root) is not flat, but a message
+     * {"key":{...}} whose one member is a field of R with the flat struct
+     * type wrap_inner converts as that field's header, the inner object on
+     * this kernel, STOP, STOP. wrap_ok: the fields of R (bit = index in R)
+     * allowed as that member: type wrap_inner, no value mapping or base
+     * skip in play, and R's other fields need nothing at '}' under the
+     * batch's flags (j2t_write_unset_fields, native/thrift.c:258-310).
+     * Anything else declines to the list pass. */
+    uint32_t wrap;
+    uint32_t wrap_inner;
+    uint64_t wrap_ok;
 };
 
 /* -DDG_FLPROF: cycles per wave by phase (s_memtime at the marks, summed
@@ -478,6 +496,7 @@ struct FlatLds {
     uint32_t plo[FL_MPB], phi[FL_MPB];      /* present fields (struct field-index bits) */
     uint32_t big[FL_MPB];                   /* listed for the wave kernel */
     uint32_t nbytes[FL_MPB];                /* Thrift bytes before STOP */
+    uint32_t wid[FL_MPB];                   /* wrapped mode: 0x10000 | the outer field's id, 0 = not wrapped */
     uint32_t sep[FL_MAXF * FL_MPB];         /* [k][m]: comma position | quotes before it << 16 */
     uint16_t col[FL_MAXF * FL_MPB];         /* [k][m]: colon position */
     uint16_t size[2 * FL_SLOTS * FL_MPB];   /* [round & 1][slot][m] */
@@ -576,8 +595,60 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
     const auto D = desc_view<3>((const __attribute__((address_space(3))) uint8_t *)(void *)s_fdesc, S.hdr);
     const FastTabs tb{(const __attribute__((address_space(3))) uint64_t *)(void *)L.p10u, (lds_f64 *)(void *)L.p10d,
                       (const __attribute__((address_space(3))) uint64_t *)(void *)L.pw};
-    const dg_type rt = ldrec(&D.T[P.root]);
+    const dg_type rt = ldrec(&D.T[S.wrap ? S.wrap_inner : P.root]);
     const dg_struct sd = ldrec(&D.S[rt.st]);
+    if (S.wrap) {
+        /* ---- 0b. wrapped mode: ws '{' ws "key" ws ':' ws {inner} ws '}' ws
+         *      with the key a wrap_ok field of R: the inner object becomes
+         *      the message (its bytes, slot +3 for the outer header) ---- */
+        if (tid < FL_MPB) {
+            uint32_t wid = 0;
+            if (L.ok[tid]) {
+                const uint32_t n = L.n[tid], lwa = L.lw[tid];
+                LSrc src;
+                src.init((const __attribute__((address_space(3))) uint64_t *)(void *)&L.in[lwa >> 3], (int32_t)(lwa & 7),
+                         (int32_t)n);
+                uint32_t p = skip_ws(src, 0);
+                bool ok = p < n && src.raw((int32_t)p) == '{';
+                p = ok ? skip_ws(src, p + 1) : p;
+                ok = ok && p < n && src.raw((int32_t)p) == '"';
+                const uint32_t k0 = p + 1;
+                uint32_t q = k0;
+                while (ok && q < n && src.raw((int32_t)q) != '"') {
+                    if (src.raw((int32_t)q) == '\\') ok = false; /* an escaped key: the list pass unquotes it */
+                    q++;
+                }
+                ok = ok && q < n;
+                const uint32_t kn = q - k0;
+                p = ok ? skip_ws(src, q + 1) : p;
+                ok = ok && p < n && src.raw((int32_t)p) == ':';
+                p = ok ? skip_ws(src, p + 1) : p;
+                ok = ok && p < n && src.raw((int32_t)p) == '{';
+                uint32_t e = n;
+                while (ok && e > p && isspace_(src.raw((int32_t)(e - 1)))) e--;
+                ok = ok && e > p + 1 && src.raw((int32_t)(e - 1)) == '}';
+                uint32_t ic = e - 1;
+                while (ok && ic > p && isspace_(src.raw((int32_t)(ic - 1)))) ic--;
+                ok = ok && ic > p + 1 && src.raw((int32_t)(ic - 1)) == '}';
+                if (ok) {
+                    const dg_struct rs = ldrec(&D.S[ldrec(&D.T[P.root]).st]);
+                    const int32_t fi = fl_lookup(D, rs, src, k0, kn);
+                    const uint32_t k = (uint32_t)fi - rs.field_begin;
+                    ok = fi >= 0 && k < 64 && ((S.wrap_ok >> k) & 1);
+                    if (ok) {
+                        wid = 0x10000u | ldrec(&D.F[fi]).id;
+                        L.lw[tid] = lwa + p;
+                        L.n[tid] = ic - p;
+                        L.oa[tid] += 3;
+                        L.cap[tid] = L.cap[tid] > 4 ? L.cap[tid] - 4 : 0u;
+                    }
+                }
+                if (!ok) L.ok[tid] = 0;
+            }
+            L.wid[tid] = wid;
+        }
+        __syncthreads();
+    }
 
     /* ---- 1. structure: lane g of a message holds message bytes
      *      [64g, 64g+64) as 64-bit masks, bit b = byte 64g + b (quotes,
@@ -858,6 +929,7 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
         const uint64_t i = b0 + m;
         if (i < b1) {
             const uint32_t len = L.nbytes[m] + 1;
+            const uint32_t wid = S.wrap ? L.wid[m] : 0u;
             bool good = L.ok[m] && len <= L.cap[m];
             if (good) {
                 const uint64_t present = (uint64_t)L.plo[m] | ((uint64_t)L.phi[m] << 32);
@@ -875,7 +947,17 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
                     }
                 }
             }
-            if (good) {
+            if (good && wid) {
+                /* the outer field header, the inner STOP, the outer STOP */
+                gu8 *o = (gu8 *)(void *)P.out + L.oa[m];
+                o[-3] = DG_T_STRUCT;
+                o[-2] = (uint8_t)(wid >> 8);
+                o[-1] = (uint8_t)wid;
+                o[len - 1] = 0;
+                o[len] = 0;
+                P.ret[i] = 0;
+                P.out_len[i] = len + 4;
+            } else if (good) {
                 ((gu8 *)(void *)P.out)[L.oa[m] + len - 1] = 0; /* STOP */
                 P.ret[i] = 0;
                 P.out_len[i] = len;

@@ -112,6 +112,7 @@ static int64_t *knob_ref(dg_ctx *c, const char *name)
     if (!strcmp(name, "list_blocks")) return &K.list_blocks;
     if (!strcmp(name, "t2j_spread")) return &K.t2j_spread;
     if (!strcmp(name, "t2j_wave_min")) return &K.t2j_wave_min;
+    if (!strcmp(name, "flat_wrap")) return &K.flat_wrap;
     return nullptr;
 }
 
@@ -144,7 +145,7 @@ int dg_ctx_create(int device, dg_ctx **out)
     static const struct { const char *env; const char *name; } envk[] = {
         {"DG_FLAT", "flat"}, {"DG_WAVE_MIN", "wave_min"}, {"DG_WAVE_OCC", "wave_occ"},
         {"DG_SMALL_MPW", "small_mpw"}, {"DG_LIST_BLOCKS", "list_blocks"}, {"DG_T2J_SPREAD", "t2j_spread"},
-        {"DG_T2J_WAVE_MIN", "t2j_wave_min"}};
+        {"DG_T2J_WAVE_MIN", "t2j_wave_min"}, {"DG_FLAT_WRAP", "flat_wrap"}};
     for (const auto &e : envk) {
         const char *v = getenv(e.env);
         if (v && *v) *knob_ref(c, e.name) = strtoll(v, nullptr, 10);
@@ -244,6 +245,54 @@ static bool flat_root(const dg_desc *d, uint32_t root, uint64_t flags)
         }
     }
     return true;
+}
+
+/* Wrapped mode of the flat kernel (FlatParams::wrap): the root R is a
+ * struct of at most 64 fields, one or more of them of a flat struct type W
+ * (flat_root's conditions); a message that is one such member converts on
+ * the flat kernel when nothing else of R needs writing at its '}' under these
+ * flags (j2t_write_unset_fields, native/thrift.c:258-310: no REQUIRED field
+ * left, none DEFAULT with F_WRITE_DEFAULT or OPTIONAL with F_WRITE_OPTIONAL,
+ * no F_TRACE_BACK field cache), the member's field has no value mapping in
+ * play and is not a skipped Base. Returns the fields allowed (bit = index in
+ * R), 0 = not applicable. */
+static uint64_t wrap_root(const dg_desc *d, uint32_t root, uint64_t flags, uint32_t *inner)
+{
+    const dg_desc_hdr &h = d->hdr;
+    if (d->hblob.size() < h.total_len || h.version < 2 || h.total_len > FL_DESC || root >= h.n_types) return 0;
+    const uint8_t *b = d->hblob.data();
+    const dg_type *T = (const dg_type *)(b + h.off_types);
+    if (T[root].ttype != DG_T_STRUCT) return 0;
+    const dg_struct &rs = ((const dg_struct *)(b + h.off_structs))[T[root].st];
+    if (rs.req_words != 1 || rs.n_fields > 64 || ((flags & DG_F_ENABLE_HM) && (rs.flags & DG_SF_HTTP_MAPPING))) return 0;
+    const dg_field *F = (const dg_field *)(b + h.off_fields);
+    const uint64_t req = ((const uint64_t *)(b + h.off_reqwords))[rs.req_begin];
+    uint32_t w = DG_NONE;
+    for (uint32_t k = 0; k < rs.n_fields && w == DG_NONE; k++) {
+        const uint32_t t = F[rs.field_begin + k].type;
+        if (T[t].ttype == DG_T_STRUCT && flat_root(d, t, flags)) w = t;
+    }
+    if (w == DG_NONE) return 0;
+    uint64_t ok = 0;
+    for (uint32_t k = 0; k < rs.n_fields; k++) {
+        const dg_field &f = F[rs.field_begin + k];
+        if (f.type != w || ((flags & DG_F_ENABLE_VM) && f.vm != DG_VM_NONE) ||
+            ((f.flags & DG_FF_REQUEST_BASE) && (flags & DG_F_NO_WRITE_BASE)))
+            continue;
+        bool fine = true;
+        for (uint32_t j = 0; j < rs.n_fields && fine; j++) {
+            if (j == k || !((req >> j) & 1)) continue;
+            const dg_field &g = F[rs.field_begin + j];
+            if (g.flags & DG_FF_REQUEST_BASE) continue;
+            if ((flags & DG_F_TRACE_BACK) || g.required == DG_REQ_REQUIRED ||
+                ((flags & DG_F_WRITE_DEFAULT) && g.required == DG_REQ_DEFAULT) ||
+                ((flags & DG_F_WRITE_OPTIONAL) && g.required == DG_REQ_OPTIONAL))
+                fine = false;
+        }
+        if (fine) ok |= 1ull << k;
+    }
+    *inner = w;
+    return ok;
 }
 
 int dg_desc_create(dg_ctx *c, const void *blob, size_t len, dg_desc **out)
@@ -351,6 +400,7 @@ static int enqueue(dg_ctx *c, Scratch *x, const dg_desc *d, uint32_t root, const
     const bool use_flat = K.flat >= 0 ? K.flat != 0
                                       : (flags & DG_F_FLAT_PATH) != 0 ||
                                             (!(flags & DG_F_NO_FLAT_PATH) && (max_len == 0 || max_len <= FL_MAXLEN));
+    const bool no_flat = (flags & DG_F_NO_FLAT_PATH) != 0 || K.flat == 0;
     flags &= ~(DG_F_NO_WAVE_PATH | DG_F_FLAT_PATH | DG_F_NO_FLAT_PATH);
     Params P;
     P.root = root;
@@ -432,13 +482,21 @@ static int enqueue(dg_ctx *c, Scratch *x, const dg_desc *d, uint32_t root, const
         S.hdr = d->hdr;
         S.bail_count = x->d_counts;
         S.bail_list = x->d_bail_list;
-        if (use_flat && flat_root(d, root, flags)) {
-            /* flat root struct: a lane group per message, a lane per field */
+        uint32_t inner = DG_NONE;
+        const uint64_t wrap_ok = (K.flat_wrap != 0 && !no_flat && !flat_root(d, root, flags))
+                                     ? wrap_root(d, root, flags, &inner)
+                                     : 0;
+        if ((use_flat && flat_root(d, root, flags)) || wrap_ok) {
+            /* flat root struct: a lane group per message, a lane per field;
+             * or a root whose messages wrap one flat struct (FlatParams::wrap) */
             FlatParams FP;
             FP.blob = d->d_blob;
             FP.hdr = d->hdr;
             FP.bail_count = x->d_counts;
             FP.bail_list = x->d_bail_list;
+            FP.wrap = wrap_ok ? 1u : 0u;
+            FP.wrap_inner = wrap_ok ? inner : 0u;
+            FP.wrap_ok = wrap_ok;
             launch_flat_kernel(dim3((uint32_t)((n + FL_MPB - 1) / FL_MPB)), s, P1, FP);
         } else {
             const uint64_t mpb = (uint64_t)SM_WAVES * (uint64_t)(mpw >= 64 ? 64 : mpw == 16 ? 16 : 32);

@@ -13,7 +13,7 @@
  *     the device and launches convert + pack on the batch's own stream; a
  *     completer thread downloads [ret | packed offsets], then exactly the
  *     packed bytes, and wakes the callers, who copy their results out.
- *     AGG_INFLIGHT batches rotate, so uploads, kernels and downloads of
+ *     the ring's batches (8) rotate, so uploads, kernels and downloads of
  *     consecutive batches overlap.
  *
  *  2. dg_j2t_pipeline_host: one large host batch (pinned buffers) streamed
@@ -69,20 +69,27 @@ struct SubRef {
     uint64_t bytes;     /* its JSON bytes */
 };
 
-/* Gather of an aggregator batch: block b copies part b's JSON from pinned
- * host memory (16-byte aligned loads over the link, through LDS) to
- * d_json + jbase, byte-exact at the words it shares with its neighbours,
- * and its message ends to loc[gbase ..]; one launch instead of two copies
- * per part. cap_n: the ends area of every part (u64 entries). */
+/* Gather of an aggregator batch: block (b, y) copies bytes [y G, y G + G)
+ * of part b's JSON from pinned host memory (16-byte aligned loads over the
+ * link, through LDS) to d_json + jbase, byte-exact at the words it shares
+ * with its neighbours; blocks (b, 0) also copy the part's message ends to
+ * loc[gbase ..]. One launch instead of two copies per part, and enough
+ * blocks to keep many reads over the link in flight. cap_n: the ends area
+ * of every part (u64 entries). */
+constexpr uint64_t AGG_GATHER_BYTES = 16384; /* G: JSON bytes per gather block */
 __global__ __launch_bounds__(256) void agg_gather_kernel(const SubRef *tab, uint64_t cap_n, uint8_t *d_json,
                                                          uint64_t *loc)
 {
     __shared__ __attribute__((aligned(16))) uint64_t st[4096 / 8 + 2];
     const SubRef r = tab[blockIdx.x];
-    for (uint64_t j = threadIdx.x; j < r.n; j += 256) loc[r.gbase + j] = ((const uint64_t *)(const void *)r.h)[j];
+    const uint64_t y0 = (uint64_t)blockIdx.y * AGG_GATHER_BYTES;
+    if (y0 >= r.bytes && (blockIdx.y || !r.n)) return;
+    if (blockIdx.y == 0)
+        for (uint64_t j = threadIdx.x; j < r.n; j += 256) loc[r.gbase + j] = ((const uint64_t *)(const void *)r.h)[j];
     const uint8_t *src = r.h + 8 * cap_n; /* 16-aligned (cap_n even, see dg_agg_create2) */
-    for (uint64_t c0 = 0; c0 < r.bytes; c0 += 4096) {
-        const uint64_t cn = r.bytes - c0 < 4096 ? r.bytes - c0 : 4096;
+    const uint64_t yend = y0 + AGG_GATHER_BYTES < r.bytes ? y0 + AGG_GATHER_BYTES : r.bytes;
+    for (uint64_t c0 = y0; c0 < yend; c0 += 4096) {
+        const uint64_t cn = yend - c0 < 4096 ? yend - c0 : 4096;
         __syncthreads();
         for (uint64_t k = threadIdx.x; k * 16 < cn; k += 256)
             ((uint4 *)(void *)st)[k] = ((const uint4 *)(const void *)(src + c0))[k];
@@ -237,7 +244,7 @@ struct DevBuf {
 
 /* ---------------- the aggregator ---------------- */
 
-constexpr int AGG_INFLIGHT = 4;
+constexpr int AGG_RING_MAX = 16; /* batches in the ring (dg_agg::ring, DG_AGG_RING, default 8) */
 constexpr int AGG_SLOTS = 256; /* caller threads per aggregator (more convert alone, dg_j2t_do) */
 
 /* one caller thread's part of one batch (its own cache lines) */
@@ -293,7 +300,8 @@ struct dg_agg {
     std::chrono::nanoseconds max_wait;
     uint64_t id;
     Batch *b = nullptr;
-    std::atomic<uint64_t> open{0};   /* the open generation; batch b[open % AGG_INFLIGHT] */
+    int ring = 8;                    /* batches in the ring: one filling, the rest converting or being taken */
+    std::atomic<uint64_t> open{0};   /* the open generation; batch b[open % ring] */
     std::atomic<int> nslots{0};
     std::atomic<uint8_t> ready[AGG_SLOTS];
     std::mutex mu;                   /* open changes, frees, flusher wakeups, completer queue */
@@ -345,7 +353,7 @@ int dg_agg::slot()
     } else {
         bool ok = true;
         (void)hipSetDevice(ctx->device);
-        for (int k = 0; k < AGG_INFLIGHT && ok; k++) {
+        for (int k = 0; k < ring && ok; k++) {
             uint64_t cap = 0;
             uint8_t *h = nullptr;
             ok = grow_pinned(h, cap, 8 * cap_n + cap_b + 64) == DG_OK;
@@ -394,8 +402,11 @@ int dg_agg::launch(Batch *x)
         if (x->sub[s].n.load(std::memory_order_relaxed)) max_len = std::max<uint64_t>(max_len, x->sub[s].maxlen);
     /* one gather launch reads every part straight from pinned host memory
      * (the table too), then the offsets */
-    hipLaunchKernelGGL(agg_gather_kernel, dim3(nsub), dim3(256), 0, x->s, x->h_tab, (uint64_t)cap_n, x->dv.d_json,
-                       x->d_loc);
+    uint64_t maxb = 0;
+    for (uint32_t k = 0; k < nsub; k++) maxb = std::max<uint64_t>(maxb, x->h_tab[k].bytes);
+    const uint32_t gy = (uint32_t)std::max<uint64_t>(1, (maxb + AGG_GATHER_BYTES - 1) / AGG_GATHER_BYTES);
+    hipLaunchKernelGGL(agg_gather_kernel, dim3(nsub, gy), dim3(256), 0, x->s, x->h_tab, (uint64_t)cap_n,
+                       x->dv.d_json, x->d_loc);
     HIPCHK(hipGetLastError());
     uint64_t *d_in = x->dv.d_off, *d_oo = d_in + N + 1;
     hipLaunchKernelGGL(agg_offsets_kernel, dim3((uint32_t)((N + 255) / 256)), dim3(256), 0, x->s, x->h_tab, nsub,
@@ -410,7 +421,7 @@ void dg_agg::run_flusher()
 {
     for (;;) {
         const uint64_t g = open.load(std::memory_order_acquire);
-        Batch *x = &b[g % AGG_INFLIGHT];
+        Batch *x = &b[g % ring];
         uint64_t t0 = now_ns();
         {
             /* until a caller asks for the seal (its sub-batch is full), the
@@ -438,7 +449,7 @@ void dg_agg::run_flusher()
             }
         }
         /* the next batch of the ring, once its callers have taken their results */
-        Batch *y = &b[(g + 1) % AGG_INFLIGHT];
+        Batch *y = &b[(g + 1) % ring];
         uint64_t t1 = now_ns();
         prof[0].fetch_add(t1 - t0, std::memory_order_relaxed);
         {
@@ -590,10 +601,11 @@ int dg_agg_create2(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, uint64_
     a->id = g_agg_ids.fetch_add(1);
     a->asym = sys_membarrier(MEMBARRIER_CMD_REGISTER_PRIVATE_EXPEDITED) == 0;
     for (auto &r : a->ready) r.store(0, std::memory_order_relaxed);
-    a->b = new Batch[AGG_INFLIGHT];
+    if (const char *e = getenv("DG_AGG_RING")) a->ring = std::max(2, std::min(AGG_RING_MAX, atoi(e)));
+    a->b = new Batch[a->ring];
     int rc = DG_OK;
     (void)hipSetDevice(ctx->device);
-    for (int k = 0; k < AGG_INFLIGHT && rc == DG_OK; k++) {
+    for (int k = 0; k < a->ring && rc == DG_OK; k++) {
         Batch &x = a->b[k];
         hipError_t e = hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&x.ev_hdr, hipEventDisableTiming);
@@ -635,7 +647,7 @@ int dg_agg_submit(dg_agg *a, const uint8_t *json, size_t len, int nonblock, dg_a
     if (s < 0) return DG_OK; /* converted alone by dg_agg_wait */
     for (;;) {
         const uint64_t g = a->open.load(std::memory_order_seq_cst);
-        Batch *x = &a->b[g % AGG_INFLIGHT];
+        Batch *x = &a->b[g % a->ring];
         Sub &u = x->sub[s];
         if (a->asym) {
             u.busy.store(1, std::memory_order_relaxed);
@@ -677,6 +689,13 @@ int dg_agg_submit(dg_agg *a, const uint8_t *json, size_t len, int nonblock, dg_a
         if (a->stop) return set_err(DG_E_INVALID, "aggregator closed");
         a->cv_open.wait(lk, [&] { return a->open.load(std::memory_order_acquire) != g || a->stop; });
     }
+}
+
+int dg_agg_ready(dg_agg *a, const dg_agg_ticket *t)
+{
+    if (!a || !t) return 0;
+    const Batch *x = (const Batch *)t->batch;
+    return !x || x->done_g.load(std::memory_order_acquire) >= t->gen;
 }
 
 int dg_agg_wait(dg_agg *a, dg_agg_ticket *t, uint8_t *out, size_t out_cap, size_t *out_len, uint64_t *ret)
@@ -773,7 +792,7 @@ void dg_agg_destroy(dg_agg *a)
         a->completer.join();
     }
     if (a->b) {
-        for (int k = 0; k < AGG_INFLIGHT; k++) {
+        for (int k = 0; k < a->ring; k++) {
             Batch &x = a->b[k];
             if (x.s) (void)hipStreamSynchronize(x.s);
             for (Sub &u : x.sub) (void)hipHostFree(u.h);
@@ -983,6 +1002,9 @@ int dg_agg_drive(dg_agg *a, const uint8_t *arena, const uint64_t *in_off, uint64
             };
             for (uint64_t i = lo; i < hi; i++) {
                 while (i - h >= (uint64_t)window) finish();
+                /* results already back are taken at once (an event loop's
+                 * completions): their batches free early */
+                while (h < i && dg_agg_ready(a, &ring[(int)((h - lo) % window)])) finish();
                 const int k = (int)((i - lo) % window);
                 t0[k] = dg_agg::now_ns();
                 for (;;) {

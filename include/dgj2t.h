@@ -77,6 +77,8 @@ int dg_ctx_counters(dg_ctx *ctx, uint64_t *out, int n, int reset);
  *   "small_mpw"   DG_SMALL_MPW    small-kernel messages per wave (64); 0 = lane kernel
  *   "list_blocks" DG_LIST_BLOCKS  grid of the exact-machine list pass (16)
  *   "t2j_spread"  DG_T2J_SPREAD   0 auto, 1, 2 or 4 lanes per t2j message
+ *   "t2j_wave_min" DG_T2J_WAVE_MIN t2j messages longer than this take the t2j wave kernel (512; 0 never)
+ *   "flat_wrap"   DG_FLAT_WRAP    -1 auto, 0 off: the flat kernel for {"key":{flat}} members of a non-flat root
  * Unknown names return DG_E_INVALID. Thread-safe (the context lock). */
 int dg_ctx_set_knob(dg_ctx *ctx, const char *name, int64_t value);
 int dg_ctx_get_knob(dg_ctx *ctx, const char *name, int64_t *value);
@@ -281,6 +283,9 @@ typedef struct dg_agg_ticket {
 } dg_agg_ticket;
 int dg_agg_submit(dg_agg *agg, const uint8_t *json, size_t len, int nonblock, dg_agg_ticket *t);
 int dg_agg_wait(dg_agg *agg, dg_agg_ticket *t, uint8_t *out, size_t out_cap, size_t *out_len, uint64_t *ret);
+/* 1 when dg_agg_wait on the ticket would not block (its batch is converted),
+ * else 0: an event loop takes its completions as they come. */
+int dg_agg_ready(dg_agg *agg, const dg_agg_ticket *t);
 /* batches flushed and messages converted so far */
 int dg_agg_stats(dg_agg *agg, uint64_t *batches, uint64_t *msgs);
 /* diagnostics: n <= 12 summed counters (ns unless noted) (flusher waiting for a seal,

@@ -154,3 +154,86 @@ def test_flat_lengths_up_to_256():
     for extra in (FLAT, 0, NO_FLAT):
         bad = _compare(fl, msgs, 0x1 | extra)
         assert not bad, (extra, bad[:4])
+
+
+def _wrap_desc():
+    """Mixed-like root: two members of one flat struct type (both wrap),
+    one of a non-flat type, a REQUIRED-free rest."""
+    inner = W.simple_desc()
+    nest = T.struct_type("N", [T.FieldDescriptor(1, "l", T.list_of(T.builtin("i32")), T.OPTIONAL)])
+    return T.struct_type("Wrap", [
+        T.FieldDescriptor(1, "Flat", inner, T.DEFAULT),
+        T.FieldDescriptor(2, "Nested", nest, T.DEFAULT),
+        T.FieldDescriptor(4, "Other", inner, T.OPTIONAL, alias="other"),
+        T.FieldDescriptor(5, "n", T.builtin("i32"), T.OPTIONAL),
+    ])
+
+
+def _wrap_msgs(rng, k):
+    out = []
+    for _ in range(k):
+        s = W.simple_obj(rng)
+        out.append(rng.choice([b'{"Flat":%s}', b'{"other":%s}', b' { "Flat" :\n%s } ', b'{"Other":%s}'])
+                   % s.encode())
+    return out
+
+
+def test_flat_wrapped_members_vs_oracle():
+    """{"key":{flat}} members of a non-flat root on the flat kernel's wrapped
+    mode (FlatParams::wrap): the outer header, the inner fields, two STOPs --
+    byte-identical to the reference; every well-formed one stays on the flat
+    kernel (no bail); the odd shapes decline to the list pass and still come
+    out exact."""
+    ctx = conv.default_context()
+    rng = random.Random(31)
+    td = _wrap_desc()
+    fl = T.flatten(td)
+    msgs = [m for m in _wrap_msgs(rng, 6000) if len(m) <= 256]
+    ctx.stats(reset=True)
+    bad = _compare(fl, msgs, 0x1 | FLAT)
+    bails, _ = ctx.stats(reset=True)
+    assert not bad, bad[:4]
+    assert bails == 0, bails
+    odd = [b'{"Flat":{}}', b'{"Flat":null}', b'{"Flat":{"ByteField":1},"Flat":{}}', b'{"Fl\\u0061t":{"ByteField":1}}',
+           b'{"Nested":{"l":[1,2]}}', b'{"Flat":{"ByteField":1}', b'{"Flat":{"ByteField":1}}}', b'{"zz":{"a":1}}',
+           b'{"Flat":{"ByteField":1},"n":3}', b'{"n":3,"Flat":{"ByteField":1}}', b'{"Flat":[1]}', b'{"Flat":{"a":{}}}',
+           b'{"Flat":{"ByteField":{}}}', b'{"Flat" {"ByteField":1}}', b'{"Flat":{"ByteField":1} }x',
+           b'{"Flat":{"StringField":"}"}}', b'{"Flat":{"StringField":"{"},"x":1}', b'{"Flat":{"I32Field":1,"I32Field":2}}',
+           b'{"Flat":{"ByteField":300}}', b'{}', b'{"Flat":{"ByteField":1},}', b'{"Other":{"ByteField":1}}']
+    for flags in (0x1, 0x0, 0x3, 0x7, 0x21, 0x81):
+        for extra in (FLAT, 0, NO_FLAT):
+            bad = _compare(fl, odd + msgs[:300], flags | extra)
+            assert not bad, (hex(flags), extra, bad[:4])
+
+
+def test_flat_wrapped_mixed_batch():
+    """A C5-style batch (flat / nested / large members of workloads.Mixed)
+    through the default routing: the flat kernel's wrapped mode, the wave
+    kernel for the long ones, the list pass -- identical to the reference."""
+    rng = random.Random(45)
+    td = W.mixed_desc()
+    fl = T.flatten(td)
+    msgs = W.gen_mixed_batch(rng, 3000, large_scale=0.05)
+    assert not _compare(fl, msgs, 0x1)
+    assert not _compare(fl, msgs, 0x7)
+
+
+def test_flat_task_cap_path():
+    """More string chunk tasks in one block than FL_MAXTASK (512): the
+    messages past the cap decline (their task slots marked empty) and the
+    list pass redoes them; the ones within it stay exact (round 3's fault:
+    stale task slots past the cap)."""
+    td = T.struct_type("Five", [T.FieldDescriptor(k + 1, c, T.builtin("string"), T.OPTIONAL)
+                                for k, c in enumerate("abcde")] +
+                       [T.FieldDescriptor(6, "z", T.builtin("binary"), T.OPTIONAL)])
+    fl = T.flatten(td)
+    rng = random.Random(3)
+    msgs = []
+    for k in range(64 * 20):
+        parts = ['"%s":"%s"' % (c, "".join(rng.choice("abcdefgh") for _ in range(33 + (k % 3)))) for c in "abcde"]
+        if k % 4 == 0:
+            parts.append('"z":"QUJDREVGR0hJSktMTU5PUFFSU1RVVldY"')
+        m = ("{" + ",".join(parts) + "}").encode()
+        assert len(m) <= 256
+        msgs.append(m)
+    assert not _compare(fl, msgs, 0x1 | FLAT)
