@@ -29,7 +29,7 @@ __attribute__((visibility("hidden"))) int set_err(int code, const char *fmt, ...
  * share lists or counters; past that cap a scratch is shared and the next
  * launch on another stream waits for its previous launch (hipStreamWaitEvent
  * on `done`), which keeps the ordering rule true in every case. */
-constexpr int DG_MAX_SCRATCH = 8;
+constexpr int DG_MAX_SCRATCH = 24; /* an aggregator ring (<= 16 streams) + the context's + in-flight side streams */
 constexpr uint32_t DG_NCOUNTS = 12;
 constexpr uint32_t DG_J2T_COUNTS_BYTES = 6 * 4;
 constexpr uint32_t DG_T2J_DEEP_COUNT = 8;
@@ -189,4 +189,4 @@ __attribute__((visibility("hidden"))) int dg_i_convert_pack(
     dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *d_json, const uint64_t *d_in_off, uint64_t n,
     uint64_t flags, uint8_t *d_out, const uint64_t *d_out_off, uint32_t *d_out_len, uint64_t *d_ret, uint8_t *d_packed,
     uint64_t *d_pack_off, hipStream_t s, uint64_t max_len, const uint64_t *base_in = nullptr, uint64_t dst_cap = 0,
-    hipEvent_t pack_after = nullptr, int base_mod16 = 0);
+    hipEvent_t pack_after = nullptr, int base_mod16 = 0, uint64_t *ret_dst = nullptr);

@@ -561,9 +561,9 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
                 if (staged) {
                     ok = 1;
                     lw = (uint32_t)(((a - base) >> 3) << 3) | (uint32_t)(a & 7);
-                } else if ((a & 7) + n64 <= FL_MAXLEN) {
-                    ok = 1;
-                    lw = (tid * FL_SLOTW) << 3 | (uint32_t)(a & 7);
+                } else {
+                    ok = 1; /* its own 256-byte slot, realigned to byte 0 */
+                    lw = (tid * FL_SLOTW) << 3;
                 }
             }
         }
@@ -581,13 +581,18 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
     __syncthreads();
     const uint32_t g = tid & 3, m1 = tid >> 2; /* phase 1: 4 lanes per message */
     if (!staged) {
-        /* a span too long for the stage (large messages in between): each
-         * message that fits its own 256-byte slot is copied there */
+        /* a span too long for the stage (large messages in between, as in a
+         * mixed batch): each message is copied to its own 256-byte slot,
+         * shifted to start at byte 0 (two aligned global words per word; the
+         * arena has 16 readable bytes past its end) */
         if (tid < FL_G * FL_MPB && L.ok[m1]) {
             const uint64_t a = P.in_off[b0 + m1];
-            const uint32_t nw = (uint32_t)(((a & 7) + L.n[m1] + 7) >> 3);
+            const uint32_t nw = (L.n[m1] + 7) >> 3, sh = (uint32_t)(a & 7) << 3;
             const glb_u64 *gsrc = (const glb_u64 *)(const void *)P.json + (a >> 3);
-            for (uint32_t w = g; w < nw; w += FL_G) L.in[(L.lw[m1] >> 3) + w] = gsrc[w];
+            for (uint32_t w = g; w < nw; w += FL_G) {
+                const uint64_t lo = gsrc[w], hi = gsrc[w + 1];
+                L.in[(L.lw[m1] >> 3) + w] = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+            }
         }
         __syncthreads();
     }

@@ -691,7 +691,8 @@ int dg_j2t_batch_device_inflight(dg_ctx *c, const dg_desc *d, uint32_t root, con
 static int pack_scan_nolock(dg_ctx *c, const uint8_t *d_out, const uint64_t *d_out_off, const uint32_t *d_out_len,
                             const uint64_t *d_ret, uint64_t n, const uint8_t *hdr, uint32_t hdr_len, const uint8_t *ftr,
                             uint32_t ftr_len, uint8_t *d_dst, uint64_t *d_dst_off, hipStream_t s,
-                            const uint64_t *base_in = nullptr, uint64_t dst_cap = 0, int base_mod16 = 0);
+                            const uint64_t *base_in = nullptr, uint64_t dst_cap = 0, int base_mod16 = 0,
+                            uint64_t *ret_dst = nullptr);
 
 /* Host batch: ONE pinned upload [in_off | out_off | JSON], the kernels, a
  * device packing pass (used slot prefixes back to back, failed messages
@@ -942,7 +943,7 @@ int dg_pack_device(dg_ctx *c, const uint8_t *d_out, const uint64_t *d_out_off, c
 static int pack_scan_nolock(dg_ctx *c, const uint8_t *d_out, const uint64_t *d_out_off, const uint32_t *d_out_len,
                             const uint64_t *d_ret, uint64_t n, const uint8_t *hdr, uint32_t hdr_len, const uint8_t *ftr,
                             uint32_t ftr_len, uint8_t *d_dst, uint64_t *d_dst_off, hipStream_t s,
-                            const uint64_t *base_in, uint64_t dst_cap, int base_mod16)
+                            const uint64_t *base_in, uint64_t dst_cap, int base_mod16, uint64_t *ret_dst)
 {
     if (n == 0) {
         if (base_in && !base_mod16) HIPCHK(hipMemcpyAsync(d_dst_off, base_in, 8, hipMemcpyDefault, s));
@@ -958,6 +959,7 @@ static int pack_scan_nolock(dg_ctx *c, const uint8_t *d_out, const uint64_t *d_o
     fr.dst_cap = dst_cap;
     fr.base_mod16 = base_mod16 ? 1u : 0u;
     fr.phase_add = (uint32_t)(base_mod16 >> 1) & 15; /* dg_i_convert_pack: 1 | phase << 1 */
+    fr.ret_dst = ret_dst;
     if (hdr) {
         /* header at 0, footer 8-aligned after it; both followed by >= 16 readable bytes */
         const uint32_t fo = (hdr_len + 7) & ~7u;
@@ -1007,7 +1009,8 @@ static int pack_scan(dg_ctx *c, const uint8_t *d_out, const uint64_t *d_out_off,
 int dg_i_convert_pack(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *d_json, const uint64_t *d_in_off,
                       uint64_t n, uint64_t flags, uint8_t *d_out, const uint64_t *d_out_off, uint32_t *d_out_len,
                       uint64_t *d_ret, uint8_t *d_packed, uint64_t *d_pack_off, hipStream_t s, uint64_t max_len,
-                      const uint64_t *base_in, uint64_t dst_cap, hipEvent_t pack_after, int base_mod16)
+                      const uint64_t *base_in, uint64_t dst_cap, hipEvent_t pack_after, int base_mod16,
+                      uint64_t *ret_dst)
 {
     std::lock_guard<std::mutex> g(c->mu);
     HIPCHK(hipSetDevice(c->device));
@@ -1015,7 +1018,7 @@ int dg_i_convert_pack(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
     if (rc) return rc;
     if (pack_after) HIPCHK(hipStreamWaitEvent(s, pack_after, 0));
     return pack_scan_nolock(c, d_out, d_out_off, d_out_len, d_ret, n, nullptr, 0, nullptr, 0, d_packed, d_pack_off, s,
-                            base_in, dst_cap, base_mod16);
+                            base_in, dst_cap, base_mod16, ret_dst);
 }
 
 extern "C" {

@@ -72,20 +72,34 @@ struct SubRef {
 /* Gather of an aggregator batch: block (b, y) copies bytes [y G, y G + G)
  * of part b's JSON from pinned host memory (16-byte aligned loads over the
  * link, through LDS) to d_json + jbase, byte-exact at the words it shares
- * with its neighbours; blocks (b, 0) also copy the part's message ends to
- * loc[gbase ..]. One launch instead of two copies per part, and enough
- * blocks to keep many reads over the link in flight. cap_n: the ends area
- * of every part (u64 entries). */
+ * with its neighbours; blocks (b, 0) also turn the part's message ends into
+ * the batch's in_off / out_off entries (and the last part's block writes
+ * entry N and the 64 zero bytes after the JSON). One launch for the whole
+ * upload, with enough blocks to keep many reads over the link in flight.
+ * cap_n: the ends area of every part (u64 entries). */
 constexpr uint64_t AGG_GATHER_BYTES = 16384; /* G: JSON bytes per gather block */
 __global__ __launch_bounds__(256) void agg_gather_kernel(const SubRef *tab, uint64_t cap_n, uint8_t *d_json,
-                                                         uint64_t *loc)
+                                                         uint64_t N, uint64_t B, uint64_t *in_off, uint64_t *out_off)
 {
     __shared__ __attribute__((aligned(16))) uint64_t st[4096 / 8 + 2];
     const SubRef r = tab[blockIdx.x];
     const uint64_t y0 = (uint64_t)blockIdx.y * AGG_GATHER_BYTES;
     if (y0 >= r.bytes && (blockIdx.y || !r.n)) return;
-    if (blockIdx.y == 0)
-        for (uint64_t j = threadIdx.x; j < r.n; j += 256) loc[r.gbase + j] = ((const uint64_t *)(const void *)r.h)[j];
+    if (blockIdx.y == 0) {
+        const uint64_t *ends = (const uint64_t *)(const void *)r.h;
+        for (uint64_t j = threadIdx.x; j < r.n; j += 256) {
+            const uint64_t start = r.jbase + (j ? ends[j - 1] : 0);
+            in_off[r.gbase + j] = start;
+            out_off[r.gbase + j] = slot_off(start, r.gbase + j);
+        }
+        if (r.gbase + r.n == N) {
+            if (threadIdx.x == 0) {
+                in_off[N] = B;
+                out_off[N] = slot_off(B, N);
+            }
+            if (threadIdx.x < 64) d_json[B + threadIdx.x] = 0;
+        }
+    }
     const uint8_t *src = r.h + 8 * cap_n; /* 16-aligned (cap_n even, see dg_agg_create2) */
     const uint64_t yend = y0 + AGG_GATHER_BYTES < r.bytes ? y0 + AGG_GATHER_BYTES : r.bytes;
     for (uint64_t c0 = y0; c0 < yend; c0 += 4096) {
@@ -113,31 +127,6 @@ __global__ __launch_bounds__(256) void agg_gather_kernel(const SubRef *tab, uint
                 }
             }
         }
-    }
-}
-
-/* in_off/out_off of an aggregator batch from its sub-batches' message ends
- * (loc[i] = end of global message i within its sub-batch's JSON) */
-__global__ __launch_bounds__(256) void agg_offsets_kernel(const SubRef *tab, uint32_t nsub, const uint64_t *loc,
-                                                          uint64_t N, uint64_t *in_off, uint64_t *out_off, uint8_t *pad)
-{
-    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (blockIdx.x == 0 && threadIdx.x < 64) pad[threadIdx.x] = 0; /* 64 zero bytes after the JSON */
-    if (i >= N) return;
-    uint32_t lo = 0, hi = nsub; /* the last sub-batch with gbase <= i */
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) / 2;
-        if (tab[mid].gbase <= i) lo = mid;
-        else hi = mid;
-    }
-    const SubRef s = tab[lo];
-    const uint64_t start = i == s.gbase ? s.jbase : s.jbase + loc[i - 1];
-    in_off[i] = start;
-    out_off[i] = slot_off(start, i);
-    if (i + 1 == N) {
-        const uint64_t end = s.jbase + loc[i];
-        in_off[N] = end;
-        out_off[N] = slot_off(end, N);
     }
 }
 
@@ -234,9 +223,8 @@ struct DevBuf {
                 hipEvent_t ev)
     {
         int rc = dg_i_convert_pack(c, d, root, json, in_off, n, flags, d_out, out_off, d_ol, d_ret, h_dst, h_dst_off,
-                                   s, max_len, base_in, dst_cap, pack_after);
+                                   s, max_len, base_in, dst_cap, pack_after, 0, h_ret);
         if (rc) return rc;
-        HIPCHK(hipMemcpyAsync(h_ret, d_ret, 8 * n, hipMemcpyDeviceToHost, s));
         HIPCHK(hipEventRecord(ev, s));
         return DG_OK;
     }
@@ -277,7 +265,6 @@ struct Batch {
     uint8_t *h_packed = nullptr; uint64_t h_packed_cap = 0; /* pinned packed Thrift */
     SubRef *h_tab = nullptr;                                /* pinned sub-batch table */
     SubRef *d_tab = nullptr;
-    uint64_t *d_loc = nullptr; uint64_t loc_cap = 0;        /* message ends, by global index */
     std::atomic<uint64_t> done_g{0};  /* last generation whose results are readable */
     std::mutex mu;
     std::condition_variable cv;
@@ -393,7 +380,6 @@ int dg_agg::launch(Batch *x)
     HIPCHK(hipSetDevice(ctx->device));
     int rc;
     if ((rc = x->dv.reserve(N, B))) return rc;
-    if ((rc = grow(x->d_loc, x->loc_cap, N + 1))) return rc;
     if ((rc = grow_pinned(x->h_hdr, x->h_hdr_cap, 16 * N + 8))) return rc;
     if ((rc = grow_pinned(x->h_packed, x->h_packed_cap, slot_off(B, N) + 64))) return rc; /* >= any packed size */
     /* the parts' longest message (the callers track it) picks the kernels */
@@ -405,12 +391,9 @@ int dg_agg::launch(Batch *x)
     uint64_t maxb = 0;
     for (uint32_t k = 0; k < nsub; k++) maxb = std::max<uint64_t>(maxb, x->h_tab[k].bytes);
     const uint32_t gy = (uint32_t)std::max<uint64_t>(1, (maxb + AGG_GATHER_BYTES - 1) / AGG_GATHER_BYTES);
-    hipLaunchKernelGGL(agg_gather_kernel, dim3(nsub, gy), dim3(256), 0, x->s, x->h_tab, (uint64_t)cap_n,
-                       x->dv.d_json, x->d_loc);
-    HIPCHK(hipGetLastError());
     uint64_t *d_in = x->dv.d_off, *d_oo = d_in + N + 1;
-    hipLaunchKernelGGL(agg_offsets_kernel, dim3((uint32_t)((N + 255) / 256)), dim3(256), 0, x->s, x->h_tab, nsub,
-                       x->d_loc, N, d_in, d_oo, x->dv.d_json + B);
+    hipLaunchKernelGGL(agg_gather_kernel, dim3(nsub, gy), dim3(256), 0, x->s, x->h_tab, (uint64_t)cap_n,
+                       x->dv.d_json, N, B, d_in, d_oo);
     HIPCHK(hipGetLastError());
     uint64_t *h_ret = (uint64_t *)(void *)x->h_hdr;
     return x->dv.convert(ctx, desc, root, flags, N, x->dv.d_json, d_in, d_oo, max_len, x->s, h_ret, x->h_packed,
@@ -797,7 +780,6 @@ void dg_agg_destroy(dg_agg *a)
             if (x.s) (void)hipStreamSynchronize(x.s);
             for (Sub &u : x.sub) (void)hipHostFree(u.h);
             x.dv.release();
-            (void)hipFree(x.d_loc);
             (void)hipFree(x.d_tab);
             (void)hipHostFree(x.h_tab);
             (void)hipHostFree(x.h_hdr);

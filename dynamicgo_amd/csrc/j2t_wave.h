@@ -1343,6 +1343,7 @@ struct MsgFrame {
      * aligned copy-out (dg_j2t_pipeline_host) */
     uint32_t base_mod16;
     uint32_t phase_add; /* base_mod16: added before the mod (the destination's own address phase) */
+    uint64_t *ret_dst;  /* optional: a copy of ret (e.g. pinned host memory: the aggregator's download) */
 };
 
 template <int V>
@@ -1396,6 +1397,7 @@ __global__ __launch_bounds__(256) void dg_pack_scan_kernel(const uint8_t *out, c
         const uint64_t tile = red[0] + red[1] + red[2] + red[3];
         const uint64_t pos = base + wpre + incl - len;
         if (i < hi) dst_off[i] = pos;
+        if (fr.ret_dst && i < hi) fr.ret_dst[i] = fr.ret[i];
         s_pos[tid] = pos;
         s_len[tid] = len;
         __syncthreads();
