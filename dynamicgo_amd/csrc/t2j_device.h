@@ -443,12 +443,20 @@ DGI void emit_default(Out &o, const DV &D, const dg_field &fd, uint8_t tt)
 
 template <class S, class FP, class DV>
 DGI uint64_t t2j_convert(const DV &D, const T2JSide &X, S src, uint32_t root, uint64_t opts, Out &o, FP fr,
-                         uint32_t fstride, uint32_t cap, gu64 *wide = nullptr, uint32_t widecap = 0)
+                         uint32_t fstride, uint32_t cap, gu64 *wide = nullptr, uint32_t widecap = 0,
+                         uint64_t *aux = nullptr)
 {
     T2JRd<S> r{src, 0};
     uint32_t sp = 0;
     uint32_t wlen = 0; /* words of `wide` in use: requires bitmaps of open structs of > 64 fields */
     auto F = [&](uint32_t k) -> auto & { return fr[k * fstride]; };
+    /* the root struct's Go-side options (conv/t2j/impl.go:74-187): the
+     * exception field being converted (DG_T2J_CONVERT_EXC), a response-base
+     * value being skipped (DG_T2J_SKIP_RESP_BASE, its span to aux) */
+    bool exc = false;
+    bool base_pend = false;
+    int64_t base_s0 = 0;
+    if (aux) *aux = ~0ull;
 
     /* the value of type td at the reader: scalars written, containers opened
      * (their header read and checked, the frame pushed) */
@@ -648,6 +656,46 @@ DGI uint64_t t2j_convert(const DV &D, const T2JSide &X, S src, uint32_t root, ui
         return t2j_err(DG_T2J_E_READ, r.p, RD_BAD_SIZE); /* default: errInvalidDataSize */
     };
 
+    /* handleUnsets -> HandleRequires (thrift/utils.go:149-176), ascending id */
+    auto unsets = [&](auto &f, const dg_struct &sd) -> uint64_t {
+        for (uint32_t w = 0; w < sd.req_words; w++) {
+            uint64_t bits = sd.req_words == 1 ? f.u : (uint64_t)wide[(uint32_t)f.u + w];
+            while (bits) {
+                const uint32_t k = w * 64 + (uint32_t)__builtin_ctzll(bits);
+                bits &= bits - 1;
+                const dg_field fd = ldrec(&D.F[sd.field_begin + k]);
+                if (fd.required == DG_REQ_REQUIRED && !(opts & DG_T2J_WRITE_REQUIRE))
+                    return t2j_err(DG_T2J_E_MISS_REQUIRED, r.p, fd.id);
+                if ((fd.required == DG_REQ_DEFAULT && !(opts & DG_T2J_WRITE_DEFAULT)) ||
+                    (fd.required == DG_REQ_OPTIONAL && !(opts & DG_T2J_WRITE_OPTIONAL) && fd.dflt_len == DG_NONE))
+                    continue;
+                const uint8_t ftt = ldrec(&D.T[fd.type]).ttype;
+                if (fd.dflt_len != DG_NONE && !(ftt == DG_T_BOOL || num_bytes(ftt) || ftt == DG_T_STRING))
+                    return t2j_err(DG_T2J_E_NEEDS_HOST, r.p, fd.id); /* a container constant's JSONValue() */
+                if (f.i) o.w8(',');
+                f.i = 1;
+                const dg_t2j_field xf = ldrec(&X.X[sd.field_begin + k]);
+                emit_side(o, X, xf.name_off, xf.name_len); /* "name": */
+                if (fd.dflt_len != DG_NONE) {
+                    /* DefaultValue().JSONValue() (thrift/idl.go:834-955): EncodeInt64 /
+                     * EncodeFloat64 / EncodeString / true|false of the IDL constant, here
+                     * from its Thrift bytes in the descriptor pool */
+                    emit_default(o, D, fd, ftt);
+                    continue;
+                }
+                switch (ftt) { /* writeDefaultOrEmpty conv/t2j/impl.go:440-468 */
+                case DG_T_BOOL: o.wle('f' | ('a' << 8) | ('l' << 16) | ('s' << 24) | (0x65ull << 32), 5); break;
+                case DG_T_BYTE: case DG_T_I16: case DG_T_I32: case DG_T_I64: case DG_T_DOUBLE: o.w8('0'); break;
+                case DG_T_STRING: o.wle('"' | ('"' << 8), 2); break;
+                case DG_T_LIST: case DG_T_SET: o.wle('[' | (']' << 8), 2); break;
+                case DG_T_MAP: case DG_T_STRUCT: o.wle('{' | ('}' << 8), 2); break;
+                default: return t2j_err(DG_T2J_E_UNSUPPORTED, r.p, ldrec(&D.T[fd.type]).ttype);
+                }
+            }
+        }
+        return 0;
+    };
+
     uint64_t e = value(root);
     if (e) return e;
     while (sp) {
@@ -656,46 +704,21 @@ DGI uint64_t t2j_convert(const DV &D, const T2JSide &X, S src, uint32_t root, ui
         case TF_STRUCT: {
             const dg_type st = ldrec(&D.T[f.td]);
             const dg_struct sd = ldrec(&D.S[st.st]);
+            if (sp == 1) {
+                if (base_pend) { /* the skipped response base ends here */
+                    *aux = (uint64_t)base_s0 | ((uint64_t)r.p << 32);
+                    base_pend = false;
+                }
+                if (exc) { /* the exception field is done: unsets, then the error (impl.go:173-187) */
+                    if ((e = unsets(f, sd))) return e;
+                    return t2j_err(DG_T2J_E_EXCEPTION, r.p, 0);
+                }
+            }
             if (!r.need(1)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
             const uint8_t t = r.u8();
             if (!ttype_valid(t)) return t2j_err(DG_T2J_E_READ, r.p, RD_BAD_TYPE);
             if (t == 0) {
-                /* handleUnsets -> HandleRequires (thrift/utils.go:149-176), ascending id */
-                for (uint32_t w = 0; w < sd.req_words; w++) {
-                uint64_t bits = sd.req_words == 1 ? f.u : (uint64_t)wide[(uint32_t)f.u + w];
-                while (bits) {
-                    const uint32_t k = w * 64 + (uint32_t)__builtin_ctzll(bits);
-                    bits &= bits - 1;
-                    const dg_field fd = ldrec(&D.F[sd.field_begin + k]);
-                    if (fd.required == DG_REQ_REQUIRED && !(opts & DG_T2J_WRITE_REQUIRE))
-                        return t2j_err(DG_T2J_E_MISS_REQUIRED, r.p, fd.id);
-                    if ((fd.required == DG_REQ_DEFAULT && !(opts & DG_T2J_WRITE_DEFAULT)) ||
-                        (fd.required == DG_REQ_OPTIONAL && !(opts & DG_T2J_WRITE_OPTIONAL) && fd.dflt_len == DG_NONE))
-                        continue;
-                    const uint8_t ftt = ldrec(&D.T[fd.type]).ttype;
-                    if (fd.dflt_len != DG_NONE && !(ftt == DG_T_BOOL || num_bytes(ftt) || ftt == DG_T_STRING))
-                        return t2j_err(DG_T2J_E_NEEDS_HOST, r.p, fd.id); /* a container constant's JSONValue() */
-                    if (f.i) o.w8(',');
-                    f.i = 1;
-                    const dg_t2j_field xf = ldrec(&X.X[sd.field_begin + k]);
-                    emit_side(o, X, xf.name_off, xf.name_len); /* "name": */
-                    if (fd.dflt_len != DG_NONE) {
-                        /* DefaultValue().JSONValue() (thrift/idl.go:834-955): EncodeInt64 /
-                         * EncodeFloat64 / EncodeString / true|false of the IDL constant, here
-                         * from its Thrift bytes in the descriptor pool */
-                        emit_default(o, D, fd, ftt);
-                        continue;
-                    }
-                    switch (ftt) { /* writeDefaultOrEmpty conv/t2j/impl.go:440-468 */
-                    case DG_T_BOOL: o.wle('f' | ('a' << 8) | ('l' << 16) | ('s' << 24) | (0x65ull << 32), 5); break;
-                    case DG_T_BYTE: case DG_T_I16: case DG_T_I32: case DG_T_I64: case DG_T_DOUBLE: o.w8('0'); break;
-                    case DG_T_STRING: o.wle('"' | ('"' << 8), 2); break;
-                    case DG_T_LIST: case DG_T_SET: o.wle('[' | (']' << 8), 2); break;
-                    case DG_T_MAP: case DG_T_STRUCT: o.wle('{' | ('}' << 8), 2); break;
-                    default: return t2j_err(DG_T2J_E_UNSUPPORTED, r.p, ldrec(&D.T[fd.type]).ttype);
-                    }
-                }
-                }
+                if ((e = unsets(f, sd))) return e;
                 o.w8('}');
                 if (sd.req_words != 1) wlen -= sd.req_words;
                 sp--;
@@ -713,11 +736,35 @@ DGI uint64_t t2j_convert(const DV &D, const T2JSide &X, S src, uint32_t root, ui
             if (sd.req_words == 1) f.u &= ~(1ull << k);
             else wide[(uint32_t)f.u + (k >> 6)] &= ~(1ull << (k & 63));
             f.n = k + 1;
+            const dg_field fd = ldrec(&D.F[fi]);
+            if (sp == 1 && (opts & DG_T2J_SKIP_RESP_BASE) && (fd.flags & DG_FF_RESPONSE_BASE) && aux) {
+                /* readResponseBase (impl.go:54-72): SkipType(STRUCT), no key */
+                base_s0 = r.p;
+                if ((e = skip(DG_T_STRUCT, T2J_SKIP_DEPTH, false))) return e;
+                base_pend = true;
+                continue;
+            }
             if (f.i) o.w8(',');
             f.i = 1;
             const dg_t2j_field xf = ldrec(&X.X[fi]);
             emit_side(o, X, xf.key_off, xf.key_len); /* "alias": */
-            const dg_field fd = ldrec(&D.F[fi]);
+            if (sp == 1 && (opts & DG_T2J_CONVERT_EXC) && id != 0) { /* only the exception field's data */
+                o.set_len(0);
+                exc = true;
+            }
+            if ((opts & DG_T2J_ENABLE_VM) && fd.vm == DG_VM_BODY_DYNAMIC) {
+                /* agwBodyDynamic.Read (thrift/annotation/value_mapping.go:84-99): the raw bytes */
+                const uint8_t ft = ldrec(&D.T[fd.type]).ttype;
+                if (ft != DG_T_STRING) return t2j_err(DG_T2J_E_CONVERT, r.p, 0x200u | ft);
+                if (!r.need(4)) return t2j_err(DG_T2J_E_READ, r.p, RD_EOF);
+                const int32_t sz = (int32_t)r.be(4);
+                if (sz < 0 || !r.need(sz)) return t2j_err(DG_T2J_E_READ, r.p, RD_BAD_SIZE);
+                int32_t q = 0;
+                for (; q + 8 <= sz; q += 8) o.wle(r.src.get8(r.p + q), 8);
+                if (q < sz) o.wle(r.src.get8(r.p + q), (uint32_t)(sz - q));
+                r.p += sz;
+                continue;
+            }
             if ((opts & DG_T2J_ENABLE_VM) && fd.vm != DG_VM_NONE) {
                 /* apiJSConv.Read (thrift/annotation/value_mapping.go:143-214) */
                 if (fd.vm != DG_VM_JSCONV) return t2j_err(DG_T2J_E_NEEDS_HOST, r.p, fd.vm);
@@ -876,6 +923,7 @@ struct T2JParams {
     const uint8_t *blob;      /* descriptor (device) */
     dg_desc_hdr hdr;
     const uint8_t *side;      /* t2j side table (device) */
+    uint64_t *aux;            /* DG_T2J_SKIP_RESP_BASE: per message the response base's span (or NULL) */
     uint32_t *deep_list;      /* messages nested beyond the LDS frames */
     uint32_t *deep_count;     /* their number (reset by the host after the deep pass) */
     uint8_t *ws;              /* deep pass: T2J_DEEP_DEPTH frames per lane */
@@ -902,7 +950,7 @@ DGI T2JSide t2j_side(const uint8_t *side)
 DGI void t2j_store(const T2JParams &P, uint64_t i, uint64_t r, Out &o)
 {
     uint32_t olen = 0;
-    if (r == 0) {
+    if (r == 0 || (uint8_t)r == DG_T2J_E_EXCEPTION) { /* the exception's JSON is kept */
         o.finish();
         if (o.len > o.cap) {
             const uint64_t need = o.len;

@@ -32,7 +32,7 @@ static uint32_t t2j_spread(const dg_ctx *c, uint64_t max_len)
  * event after. */
 static int t2j_launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *src, const uint64_t *in_off,
                       uint64_t n, uint64_t opts, uint8_t *out, const uint64_t *out_off, uint32_t *out_len,
-                      uint64_t *ret, hipStream_t s, uint64_t max_len)
+                      uint64_t *ret, hipStream_t s, uint64_t max_len, uint64_t *aux = nullptr)
 {
     if (n == 0) return DG_OK;
     if (!d->d_side) return set_err(DG_E_DESC, "descriptor has no t2j side table (dg_desc_attach_t2j)");
@@ -47,7 +47,8 @@ static int t2j_launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
         HIPCHK(hipEventCreateWithFlags(&c->ws_t2j_done, hipEventDisableTiming));
     }
     const uint64_t wmin = (uint64_t)c->knobs.t2j_wave_min;
-    const bool wave = wmin > 0 && d->hdr.total_len <= 16384 && d->hdr.n_fields <= 1024 && /* T2W_FX */
+    /* the root-level Go-side options run on the lane kernel only */
+    const bool wave = !(opts & (DG_T2J_CONVERT_EXC | DG_T2J_SKIP_RESP_BASE)) && wmin > 0 && d->hdr.total_len <= 16384 && d->hdr.n_fields <= 1024 && /* T2W_FX */
                       d->side_len <= 12288 /* T2W_SIDE */ && (max_len == 0 || max_len > wmin);
     if (wave) {
         if ((rc = grow_x(x, x->t2j_big, x->t2j_big_cap, n))) return rc;
@@ -75,6 +76,7 @@ static int t2j_launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
     P.deep_count = x->d_counts + DG_T2J_DEEP_COUNT;
     P.ws = c->ws_t2j;
     P.stats = c->d_stats;
+    P.aux = (opts & DG_T2J_SKIP_RESP_BASE) ? aux : nullptr;
     hipError_t e = hipSuccess;
     if (wave) {
         T2JParams P1 = P;
@@ -175,6 +177,18 @@ int dg_t2j_batch_device_ml(dg_ctx *c, const dg_desc *d, uint32_t root, const uin
     return t2j_launch(c, d, root, d_thrift, d_in_off, n, opts, d_out, d_out_off, d_out_len, d_ret, s, max_len);
 }
 
+int dg_t2j_batch_device_aux(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *d_thrift,
+                            const uint64_t *d_in_off, uint64_t n, uint64_t opts, uint8_t *d_out,
+                            const uint64_t *d_out_off, uint32_t *d_out_len, uint64_t *d_ret, uint64_t *d_aux,
+                            void *stream, uint64_t max_len)
+{
+    if (!c || !d || ((opts & DG_T2J_SKIP_RESP_BASE) && !d_aux)) return set_err(DG_E_INVALID, "bad args");
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    return t2j_launch(c, d, root, d_thrift, d_in_off, n, opts, d_out, d_out_off, d_out_len, d_ret, s, max_len, d_aux);
+}
+
 int dg_t2j_batch_device(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *d_thrift, const uint64_t *d_in_off,
                         uint64_t n, uint64_t opts, uint8_t *d_out, const uint64_t *d_out_off, uint32_t *d_out_len,
                         uint64_t *d_ret, void *stream)
@@ -183,11 +197,13 @@ int dg_t2j_batch_device(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_
                                   0);
 }
 
-int dg_t2j_batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *thrift, const uint64_t *in_off,
-                      uint64_t n, uint64_t opts, uint8_t *out, uint64_t out_cap, uint64_t *out_off, uint64_t *ret,
-                      uint64_t *out_need)
+static int t2j_batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *thrift, const uint64_t *in_off,
+                          uint64_t n, uint64_t opts, uint8_t *out, uint64_t out_cap, uint64_t *out_off, uint64_t *ret,
+                          uint64_t *out_need, uint64_t *aux)
 {
-    if (!c || !d || (!thrift && n) || !in_off || !out_off || (!ret && n)) return set_err(DG_E_INVALID, "bad args");
+    if (!c || !d || (!thrift && n) || !in_off || !out_off || (!ret && n) ||
+        ((opts & DG_T2J_SKIP_RESP_BASE) && n && !aux))
+        return set_err(DG_E_INVALID, "bad args");
     std::lock_guard<std::mutex> g(c->mu);
     HIPCHK(hipSetDevice(c->device));
     const uint64_t base = in_off[0];
@@ -218,6 +234,7 @@ int dg_t2j_batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
         if ((rc = grow(c->d_out_off, c->d_oo_cap, m + 1))) return rc;
         if ((rc = grow(c->d_out_len, c->d_ol_cap, m + 1))) return rc;
         if ((rc = grow(c->d_ret, c->d_ret_cap, m + 1))) return rc;
+        if (aux && (rc = grow(c->d_aux, c->d_aux_cap, m + 1))) return rc;
         if (pass == 0) {
             HIPCHK(hipMemcpyAsync(c->d_json, thrift + base, io[m], hipMemcpyHostToDevice, s));
         } else {
@@ -229,10 +246,11 @@ int dg_t2j_batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
         HIPCHK(hipMemcpyAsync(c->d_in_off, io.data(), (m + 1) * 8, hipMemcpyHostToDevice, s));
         HIPCHK(hipMemcpyAsync(c->d_out_off, so.data(), (m + 1) * 8, hipMemcpyHostToDevice, s));
         if ((rc = t2j_launch(c, d, root, c->d_json, c->d_in_off, m, opts, c->d_out, c->d_out_off, c->d_out_len,
-                             c->d_ret, s, max_len)))
+                             c->d_ret, s, max_len, aux ? c->d_aux : nullptr)))
             return rc;
-        std::vector<uint64_t> r(m);
+        std::vector<uint64_t> r(m), ax(aux ? m : 0);
         std::vector<uint32_t> l(m);
+        if (aux) HIPCHK(hipMemcpyAsync(ax.data(), c->d_aux, m * 8, hipMemcpyDeviceToHost, s));
         HIPCHK(hipMemcpyAsync(r.data(), c->d_ret, m * 8, hipMemcpyDeviceToHost, s));
         HIPCHK(hipMemcpyAsync(l.data(), c->d_out_len, m * 4, hipMemcpyDeviceToHost, s));
         const uint64_t off0 = stage.size();
@@ -244,6 +262,7 @@ int dg_t2j_batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
             const uint64_t i = todo[k];
             ret[i] = r[k];
             olen[i] = l[k];
+            if (aux) aux[i] = ax[k];
             slot_of[i] = off0 + so[k];
             if ((uint8_t)r[k] == DG_ST_OUT_OVERFLOW) {
                 if (pass == 1)
@@ -256,7 +275,7 @@ int dg_t2j_batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
     uint64_t total = 0;
     out_off[0] = 0;
     for (uint64_t i = 0; i < n; i++) {
-        if (ret[i] != 0) olen[i] = 0;
+        if (ret[i] != 0 && (uint8_t)ret[i] != DG_T2J_E_EXCEPTION) olen[i] = 0; /* the exception's JSON is kept */
         total += olen[i];
         out_off[i + 1] = total;
     }
@@ -265,6 +284,20 @@ int dg_t2j_batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
     for (uint64_t i = 0; i < n; i++)
         if (olen[i]) memcpy(out + out_off[i], stage.data() + slot_of[i], olen[i]);
     return DG_OK;
+}
+
+int dg_t2j_batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *thrift, const uint64_t *in_off,
+                      uint64_t n, uint64_t opts, uint8_t *out, uint64_t out_cap, uint64_t *out_off, uint64_t *ret,
+                      uint64_t *out_need)
+{
+    return t2j_batch_host(c, d, root, thrift, in_off, n, opts, out, out_cap, out_off, ret, out_need, nullptr);
+}
+
+int dg_t2j_batch_host_aux(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *thrift, const uint64_t *in_off,
+                          uint64_t n, uint64_t opts, uint8_t *out, uint64_t out_cap, uint64_t *out_off, uint64_t *ret,
+                          uint64_t *out_need, uint64_t *aux)
+{
+    return t2j_batch_host(c, d, root, thrift, in_off, n, opts, out, out_cap, out_off, ret, out_need, aux);
 }
 
 }  // extern "C"

@@ -34,7 +34,7 @@ __global__ __launch_bounds__(T2J_BLOCK) void t2j_kernel(T2JParams P)
         o.init(P.out + P.out_off[i], P.out_off[i + 1] - P.out_off[i]);
         const uint64_t r = t2j_convert(D, X, s, P.root, P.opts, o,
                                        (__attribute__((address_space(3))) T2JFrame *)(void *)&lf[slot], MPB,
-                                       T2J_LDS_DEPTH);
+                                       T2J_LDS_DEPTH, nullptr, 0, P.aux ? P.aux + i : nullptr);
         if ((uint8_t)r == DG_ST_DEEP) {
             P.deep_list[atomicAdd(P.deep_count, 1u)] = (uint32_t)i;
             continue;
@@ -123,7 +123,8 @@ __global__ __launch_bounds__(T2J_BLOCK) void t2j_deep_kernel(T2JParams P)
         s.init((glb_u64 *)(const void *)(P.src + (a & ~7ull)), (int64_t)(a & 7), (int64_t)(b - a));
         Out o;
         o.init(P.out + P.out_off[i], P.out_off[i + 1] - P.out_off[i]);
-        uint64_t r = t2j_convert(D, X, s, P.root, P.opts, o, fr, 1, T2J_DEEP_DEPTH, wide, T2J_WIDE_WORDS);
+        uint64_t r = t2j_convert(D, X, s, P.root, P.opts, o, fr, 1, T2J_DEEP_DEPTH, wide, T2J_WIDE_WORDS,
+                                 P.aux ? P.aux + i : nullptr);
         if ((uint8_t)r == DG_ST_DEEP) r = t2j_err(DG_T2J_E_DEPTH, 0, T2J_DEEP_DEPTH);
         t2j_store(P, i, r, o);
     }

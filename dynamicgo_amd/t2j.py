@@ -8,15 +8,21 @@ Reference surface (Go):
   the options it reads                 conv/api.go:52-121 (conv.Options)
 
 Every call runs the HIP kernels in libdgj2t.so; there is no CPU fallback.
-The Go-side options -- EnableHttpMapping (http.ResponseSetter callbacks),
-EnableThriftBase (base.BaseResponse from the context) and ConvertException --
-are not device features: they raise here, as the Go shim keeps them on the
-host (INTEGRATION.md).
+The Go-side options are split between the device and this host part:
+  * ConvertException (conv/t2j/impl.go:154-187): the device stops at the root's
+    exception field and keeps its JSON (DG_T2J_E_EXCEPTION); here it becomes
+    the error, errors.New(json), as Do returns it;
+  * EnableThriftBase with a context BaseResp (readResponseBase,
+    impl.go:54-72): the device skips the root's response-base field and
+    reports its span; here the BaseResp is FastRead from those bytes;
+  * EnableHttpMapping (writeHttpValue, impl.go:515-588): the mapped fields'
+    values go to the http.ResponseSetter, see do_batch.
 """
 from __future__ import annotations
 
 import ctypes as C
-from typing import List, Optional, Sequence, Tuple
+import struct as _st
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -34,9 +40,11 @@ T2J_WRITE_DEFAULT = 1 << 5
 T2J_WRITE_REQUIRE = 1 << 6
 T2J_WRITE_OPTIONAL = 1 << 7
 T2J_ENABLE_VM = 1 << 8
+T2J_CONVERT_EXC = 1 << 9
+T2J_SKIP_RESP_BASE = 1 << 10
 
 (E_READ, E_UNKNOWN_FIELD, E_DISMATCH_TYPE, E_UNSUPPORTED, E_NAN_INF, E_MISS_REQUIRED, E_NEEDS_HOST, E_DEPTH, E_WRITE,
- E_CONVERT) = range(1, 11)
+ E_CONVERT, E_EXCEPTION) = range(1, 12)
 
 # the meta.ErrCode behaviour the reference wraps each failure in
 # (conv/t2j/impl.go: wrapError call sites; meta/error.go)
@@ -48,11 +56,16 @@ _BEHAVIOR = {E_READ: "ErrRead", E_UNKNOWN_FIELD: "ErrUnknownField", E_DISMATCH_T
 _READ_REASON = {1: "EOF", 2: "invalid data type", 3: "invalid data length", 4: "depth limit exceeded"}
 
 
-def to_t2j_opts(o: Options) -> int:
-    """The conv.Options fields conv/t2j/impl.go reads, as DG_T2J_* bits."""
-    if o.EnableHttpMapping or o.EnableThriftBase or o.ConvertException:
-        raise ValueError("EnableHttpMapping / EnableThriftBase / ConvertException are Go-side t2j features")
+def to_t2j_opts(o: Options, base: bool = False) -> int:
+    """The conv.Options fields conv/t2j/impl.go reads, as DG_T2J_* bits;
+    base: a BaseResp is in the context (EnableThriftBase skips the field)."""
+    if o.EnableHttpMapping:
+        raise ValueError("EnableHttpMapping: use BinaryConv.do_batch_http (the ResponseSetter callbacks)")
     f = 0
+    if o.ConvertException:
+        f |= T2J_CONVERT_EXC
+    if o.EnableThriftBase and base:
+        f |= T2J_SKIP_RESP_BASE
     if o.ByteAsUint8:
         f |= T2J_BYTE_AS_UINT8
     if o.Int642String:
@@ -107,6 +120,120 @@ class T2JError(Exception):
         return f"code {c} value {v} at byte {self.pos}"
 
 
+class T2JException(Exception):
+    """ConvertException (conv/t2j/impl.go:183-185): the message held an
+    exception field; the error's text is that field's JSON, errors.New(json)."""
+
+    def __init__(self, js: bytes):
+        super().__init__(js.decode("utf-8", "replace"))
+        self.json = js
+
+
+class ThriftReadError(ValueError):
+    pass
+
+
+def _skip(b: bytes, p: int, t: int, depth: int = 64) -> int:
+    """skipType on Thrift binary (thrift/binary_skip.go), host side: the
+    position after the value of wire type t at p."""
+    fs = {2: 1, 3: 1, 6: 2, 8: 4, 4: 8, 10: 8}.get(t)
+    if fs:
+        if p + fs > len(b):
+            raise ThriftReadError("EOF")
+        return p + fs
+    if depth <= 0:
+        raise ThriftReadError("depth limit exceeded")
+    if t == 11:
+        if p + 4 > len(b):
+            raise ThriftReadError("EOF")
+        n = _st.unpack_from(">I", b, p)[0]
+        if p + 4 + n > len(b):
+            raise ThriftReadError("EOF")
+        return p + 4 + n
+    if t == 12:
+        while True:
+            if p >= len(b):
+                raise ThriftReadError("EOF")
+            ft = b[p]
+            p += 1
+            if ft == 0:
+                return p
+            p = _skip(b, p + 2, ft, depth - 1)
+    if t == 13:
+        if p + 6 > len(b):
+            raise ThriftReadError("EOF")
+        kt, vt, n = b[p], b[p + 1], _st.unpack_from(">i", b, p + 2)[0]
+        p += 6
+        for _ in range(max(n, 0)):
+            p = _skip(b, _skip(b, p, kt, depth - 1), vt, depth - 1)
+        return p
+    if t in (14, 15):
+        if p + 5 > len(b):
+            raise ThriftReadError("EOF")
+        et, n = b[p], _st.unpack_from(">i", b, p + 1)[0]
+        p += 5
+        for _ in range(max(n, 0)):
+            p = _skip(b, p, et, depth - 1)
+        return p
+    raise ThriftReadError("invalid data type %d" % t)
+
+
+class BaseResp:
+    """base.BaseResp (testdata/idl/base.thrift:19-23: 1: string StatusMessage
+    = "", 2: i32 StatusCode = 0, 3: optional map<string, string> Extra), the
+    context object EnableThriftBase fills (conv.CtxKeyThriftRespBase)."""
+
+    def __init__(self, StatusMessage: str = "", StatusCode: int = 0, Extra: Optional[Dict[str, str]] = None):
+        self.StatusMessage, self.StatusCode, self.Extra = StatusMessage, StatusCode, Extra
+
+    def __eq__(self, o):
+        return isinstance(o, BaseResp) and (self.StatusMessage, self.StatusCode, self.Extra) == \
+            (o.StatusMessage, o.StatusCode, o.Extra)
+
+    def __repr__(self):
+        return "BaseResp(%r, %r, %r)" % (self.StatusMessage, self.StatusCode, self.Extra)
+
+    def fast_read(self, b: bytes):
+        """The kitex FastRead: fields by id and wire type, others skipped."""
+        p = 0
+
+        def rstr(p):
+            if p + 4 > len(b):
+                raise ThriftReadError("EOF")
+            n = _st.unpack_from(">I", b, p)[0]
+            if p + 4 + n > len(b):
+                raise ThriftReadError("EOF")
+            return b[p + 4:p + 4 + n].decode("utf-8", "surrogateescape"), p + 4 + n
+        while True:
+            if p >= len(b):
+                raise ThriftReadError("EOF")
+            t = b[p]
+            if t == 0:
+                return p + 1
+            if p + 3 > len(b):
+                raise ThriftReadError("EOF")
+            fid = _st.unpack_from(">h", b, p + 1)[0]
+            p += 3
+            if fid == 1 and t == 11:
+                self.StatusMessage, p = rstr(p)
+            elif fid == 2 and t == 8:
+                if p + 4 > len(b):
+                    raise ThriftReadError("EOF")
+                self.StatusCode = _st.unpack_from(">i", b, p)[0]
+                p += 4
+            elif fid == 3 and t == 13 and p + 6 <= len(b) and b[p] == 11 and b[p + 1] == 11:
+                n = _st.unpack_from(">i", b, p + 2)[0]
+                p += 6
+                m = {}
+                for _ in range(max(n, 0)):
+                    k, p = rstr(p)
+                    v, p = rstr(p)
+                    m[k] = v
+                self.Extra = m
+            else:
+                p = _skip(b, p, t)
+
+
 class BinaryConv:
     """t2j.BinaryConv (conv/t2j/conv.go:30-95) on the MI355X."""
 
@@ -133,23 +260,59 @@ class BinaryConv:
         self._flat_cache[id(desc)] = (desc, f)
         return f
 
-    def do(self, desc, tbytes: bytes) -> Optional[bytes]:
+    def do(self, desc, tbytes: bytes, resp=None, base: Optional[BaseResp] = None) -> Optional[bytes]:
         """Do: JSON bytes (None when empty, as the reference returns nil) or
-        raises T2JError."""
-        outs, rets = self.do_batch(desc, [tbytes])
-        if rets[0] != 0:
-            raise T2JError(int(rets[0]))
+        raises T2JError / T2JException (ConvertException) / ThriftReadError
+        (the context BaseResp did not read). resp: the context's
+        http.ResponseSetter (EnableHttpMapping); base: its BaseResp, filled
+        in place (EnableThriftBase)."""
+        outs, errs = self.do_batch_errors(desc, [tbytes], [resp], [base])
+        if errs[0] is not None:
+            raise errs[0]
         return outs[0] if outs[0] else None
 
-    def do_into(self, desc, tbytes: bytes, buf: bytearray):
-        """DoInto: appends to buf."""
-        out = self.do(desc, tbytes)
+    def do_into(self, desc, tbytes: bytes, buf: bytearray, resp=None, base: Optional[BaseResp] = None):
+        """DoInto: appends to buf (also the exception's JSON before raising
+        T2JException, as the reference leaves it in the buffer)."""
+        try:
+            out = self.do(desc, tbytes, resp, base)
+        except T2JException as e:
+            buf.extend(e.json)
+            raise
         if out:
             buf.extend(out)
 
+    def do_batch_errors(self, desc, msgs: Sequence[bytes], resps=None, bases=None):
+        """Do over a batch with the context's objects per message: (outputs,
+        errors) with errors[i] None, T2JError, T2JException or
+        ThriftReadError."""
+        n = len(msgs)
+        bases = list(bases) if bases is not None else [None] * n
+        outs, rets, aux = self._batch(desc, msgs, with_base=any(b is not None for b in bases))
+        errs: List[Optional[Exception]] = [None] * n
+        for i in range(n):
+            r = int(rets[i])
+            if (r & 0xFF) == E_EXCEPTION:
+                errs[i], outs[i] = T2JException(outs[i]), b""
+                continue
+            if r != 0:
+                errs[i] = T2JError(r)
+                continue
+            if bases[i] is not None and aux is not None and int(aux[i]) != 2**64 - 1:
+                lo, hi = int(aux[i]) & 0xFFFFFFFF, int(aux[i]) >> 32
+                try:
+                    bases[i].fast_read(bytes(msgs[i][lo:hi]))  # readResponseBase's FastRead
+                except ThriftReadError as e:
+                    errs[i], outs[i] = e, b""
+        return outs, errs
+
     def do_batch(self, desc, msgs: Sequence[bytes]) -> Tuple[List[bytes], np.ndarray]:
         """Batch of independent Thrift messages -> (JSON outputs, statuses)."""
-        opts = to_t2j_opts(self.opts)
+        outs, rets, _ = self._batch(desc, msgs)
+        return outs, rets
+
+    def _batch(self, desc, msgs: Sequence[bytes], with_base: bool = False):
+        opts = to_t2j_opts(self.opts, with_base)
         flat = self._flat(desc)
         ctx = self._ctx()
         n = len(msgs)
@@ -164,16 +327,19 @@ class BinaryConv:
         need = C.c_uint64(0)
         L = _lib.lib()
         d = ctx.desc_t2j(flat)
-        rc = L.dg_t2j_batch_host(ctx.h, d, flat.root_type, arena.ctypes.data, in_off.ctypes.data, n, opts,
-                                 out.ctypes.data, cap, out_off.ctypes.data, rets.ctypes.data, C.byref(need))
-        if rc == -3 and need.value > cap:
-            cap = int(need.value) + 64
-            out = np.zeros(cap, dtype=np.uint8)
-            rc = L.dg_t2j_batch_host(ctx.h, d, flat.root_type, arena.ctypes.data, in_off.ctypes.data, n, opts,
-                                     out.ctypes.data, cap, out_off.ctypes.data, rets.ctypes.data, C.byref(need))
+        aux = np.zeros(max(n, 1), dtype=np.uint64) if opts & T2J_SKIP_RESP_BASE else None
+        for _ in range(2):
+            rc = L.dg_t2j_batch_host_aux(ctx.h, d, flat.root_type, arena.ctypes.data, in_off.ctypes.data, n, opts,
+                                         out.ctypes.data, cap, out_off.ctypes.data, rets.ctypes.data,
+                                         C.byref(need), aux.ctypes.data if aux is not None else None)
+            if rc == -3 and need.value > cap:
+                cap = int(need.value) + 64
+                out = np.zeros(cap, dtype=np.uint8)
+                continue
+            break
         _lib.check(rc)
         outs = [out[int(out_off[i]):int(out_off[i + 1])].tobytes() for i in range(n)]
-        return outs, rets[:n]
+        return outs, rets[:n], aux
 
     def do_device(self, desc, thrift, in_off, out, out_off, out_len, ret, stream=None):
         """Device-resident batch over torch tensors: thrift uint8[>= in_off[-1]

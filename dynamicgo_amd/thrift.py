@@ -355,7 +355,7 @@ def flatten(root: TypeDescriptor) -> FlatDescriptor:
         findex = {id(f): fbegin + i for i, f in enumerate(fields)}
         for f in fields:
             field_objs.append(f)
-            fl = (1 if f.is_request_base else 0) | (2 if f.http_mappings else 0)
+            fl = (1 if f.is_request_base else 0) | (2 if f.http_mappings else 0) | (16 if f.is_response_base else 0)
             if sd.names.get(f.alias) is f:
                 fl |= 4  # DG_FF_ALIAS_SELF
             if b'"' not in f.alias.encode() and b"\\" not in f.alias.encode():
@@ -712,13 +712,20 @@ class IDLFile:
                         annos = p.annotations()
                         p.sep()
                         args.append(_PField(fid, req, t, an, None, annos))
+                    throws = []
                     if p.accept("throws"):
                         p.expect("(")
                         while not p.accept(")"):
-                            p.next()
+                            fid = int(p.next()[1], 0)
+                            p.expect(":")
+                            if p.peek()[1] in ("required", "optional"):
+                                p.next()
+                            t = p.ptype()
+                            throws.append(_PField(fid, "default", t, p.ident(), None, p.annotations()))
+                            p.sep()
                     p.annotations()
                     p.sep()
-                    funcs[fname] = (rt, args)
+                    funcs[fname] = (rt, args, throws)
                 self.services[name] = funcs
                 p.annotations()
             else:
@@ -865,7 +872,7 @@ def _parse_service(path: str, src: str, includes: Dict[str, str], opts: Options,
     sname = service or list(root.services)[-1]
     comp = _Compiler(root, opts)
     funcs = {}
-    for fname, (rt, args) in root.services[sname].items():
+    for fname, (rt, args, throws) in root.services[sname].items():
         cache: dict = {}
         req_sd = StructDescriptor(fname + "_args")
         for a in args:
@@ -873,8 +880,13 @@ def _parse_service(path: str, src: str, includes: Dict[str, str], opts: Options,
         req_td = TypeDescriptor(STRUCT, fname + "_args", struct=req_sd)
         resp_td = None
         if rt.name != "void":
+            # parseResponse (thrift/idl.go:490-537): the result wrapper, the
+            # response as field 0 with no name, the first thrown exception
             resp_sd = StructDescriptor(fname + "_result")
-            resp_sd.add_field(FieldDescriptor(0, "success", comp.ptype(root, rt, {}, 0), OPTIONAL))
+            resp_sd.add_field(FieldDescriptor(0, "", comp.ptype(root, rt, {}, 0), OPTIONAL, alias=""))
+            if throws:
+                e = throws[0]
+                resp_sd.add_field(FieldDescriptor(e.id, e.name, comp.ptype(root, e.type, {}, 0), OPTIONAL))
             resp_td = TypeDescriptor(STRUCT, fname + "_result", struct=resp_sd)
         funcs[fname] = FunctionDescriptor(fname, req_td, resp_td)
     return ServiceDescriptor(sname, funcs)

@@ -354,6 +354,19 @@ int dg_t2j_batch_host(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, cons
                       const uint64_t *in_off, uint64_t n, uint64_t opts, uint8_t *out, uint64_t out_cap,
                       uint64_t *out_off, uint64_t *ret, uint64_t *out_need);
 
+/* dg_t2j_batch_device_ml / dg_t2j_batch_host with the device part of the Go-side options
+ * device part (dgj2t_defs.h DG_T2J_CONVERT_EXC, DG_T2J_SKIP_RESP_BASE): aux
+ * (n u64, device resp. host memory) receives each message's response-base
+ * span when DG_T2J_SKIP_RESP_BASE is set (may be NULL otherwise); a
+ * DG_T2J_E_EXCEPTION message keeps its JSON in out. */
+int dg_t2j_batch_device_aux(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, const uint8_t *d_thrift,
+                            const uint64_t *d_in_off, uint64_t n, uint64_t opts, uint8_t *d_out,
+                            const uint64_t *d_out_off, uint32_t *d_out_len, uint64_t *d_ret, uint64_t *d_aux,
+                            void *stream, uint64_t max_len);
+int dg_t2j_batch_host_aux(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, const uint8_t *thrift,
+                          const uint64_t *in_off, uint64_t n, uint64_t opts, uint8_t *out, uint64_t out_cap,
+                          uint64_t *out_off, uint64_t *ret, uint64_t *out_need, uint64_t *aux);
+
 /* Timing helper for benchmarks: launch the device batch `iters` times on the
  * context stream bracketed by HIP events; returns total milliseconds of GPU
  * time in *ms (events are recorded on the stream the kernels run on). */

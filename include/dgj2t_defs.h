@@ -118,7 +118,18 @@ typedef struct dg_cb_tables {
 #define DG_T2J_WRITE_DEFAULT (1ull << 5)     /* WriteDefaultField */
 #define DG_T2J_WRITE_REQUIRE (1ull << 6)     /* WriteRequireField */
 #define DG_T2J_WRITE_OPTIONAL (1ull << 7)    /* WriteOptionalField */
-#define DG_T2J_ENABLE_VM (1ull << 8)         /* EnableValueMapping (api.js_conv) */
+#define DG_T2J_ENABLE_VM (1ull << 8)         /* EnableValueMapping (api.js_conv, agw.body_dynamic) */
+/* the Go-side options, with the host's part done around the kernels
+ * (dynamicgo_amd.t2j): */
+#define DG_T2J_CONVERT_EXC (1ull << 9)       /* ConvertException: the ROOT struct's first field with a non-zero id
+                                                ends the conversion (conv/t2j/impl.go:154-159,173-187): status
+                                                DG_T2J_E_EXCEPTION, out = that field's value JSON (then any unset
+                                                fields written by handleUnsets) */
+#define DG_T2J_SKIP_RESP_BASE (1ull << 10)   /* EnableThriftBase with a context BaseResp (readResponseBase,
+                                                conv/t2j/impl.go:54-72,120-128): the ROOT's response-base fields
+                                                (DG_FF_RESPONSE_BASE) are skipped as STRUCTs, no key written; the
+                                                last one's value span [lo, hi) of the message goes to aux as
+                                                lo | hi << 32 (~0: none) for the host to FastRead */
 
 /* t2j per-message status codes (bits 0-7 of the status word; pos = Thrift
  * read offset, value as noted). The reference returns Go errors whose
@@ -134,6 +145,7 @@ typedef struct dg_cb_tables {
 #define DG_T2J_E_DEPTH 8          /* nesting beyond 4096 containers (the GPU's frame budget; Go recurses further) */
 #define DG_T2J_E_WRITE 9          /* ErrWrite: a truncated BYTE/I16/I32/I64/DOUBLE value (doRecurse wraps those reads
                                      as meta.ErrWrite, conv/t2j/impl.go:200-236); value = RD_EOF (1) */
+#define DG_T2J_E_EXCEPTION 11     /* DG_T2J_CONVERT_EXC: the exception field's JSON is the output (Go: errors.New(out)) */
 #define DG_T2J_E_CONVERT 10       /* ErrConvert: a map key failed (buildinTypeToKey, wrapped as meta.ErrConvert by
                                      conv/t2j/impl.go:355-358): value = the read reason (RD_*), or 0x100 | type for
                                      a key type it does not support */

@@ -69,6 +69,7 @@
                                  (lets the fast path confirm a predicted key by one compare) */
 #define DG_FF_KEY_PLAIN 8u    /* the alias has no '"' and no '\\' byte: a JSON key equal to it
                                  ends right after it (no escape can start inside it) */
+#define DG_FF_RESPONSE_BASE 16u /* FieldDescriptor.isResponseBase (t2j, EnableThriftBase) */
 
 /* dg_field.vm (reference native/thrift.h:64-67) */
 #define DG_VM_NONE 0

@@ -253,16 +253,28 @@ class RefT2J:
                            C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]
 
     def t2j(self, flat, side: bytes, thrift: bytes, opts: int, root: Optional[int] = None) -> Tuple[int, bytes]:
+        """(status, JSON): JSON b"" on error, except the exception's JSON
+        with ConvertException (status 11)."""
+        return self.t2j2(flat, side, thrift, opts, root)[:2]
+
+    def t2j2(self, flat, side: bytes, thrift: bytes, opts: int, root: Optional[int] = None):
+        """t2j plus the response-base span (DG_T2J_SKIP_RESP_BASE): (status,
+        JSON, lo | hi << 32 or 2**64 - 1)."""
+        f = self.lib.dgref_t2j2
+        f.restype = C.c_uint64
+        f.argtypes = [C.c_char_p, C.c_char_p, C.c_uint32, C.c_char_p, C.c_size_t, C.c_uint64,
+                      C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t), C.POINTER(C.c_uint64)]
         root = flat.root_type if root is None else root
         cap = 8 * len(thrift) + 4096
+        aux = C.c_uint64(0)
         for _ in range(2):
             out = C.create_string_buffer(cap)
             ol = C.c_size_t(0)
-            ret = int(self.f(flat.blob, side, root, thrift, len(thrift), opts, out, cap, C.byref(ol)))
-            if ret != 0:
-                return ret, b""
+            ret = int(f(flat.blob, side, root, thrift, len(thrift), opts, out, cap, C.byref(ol), C.byref(aux)))
+            if ret != 0 and (ret & 0xFF) != 11:
+                return ret, b"", int(aux.value)
             if ol.value <= cap:
-                return 0, out.raw[:ol.value]
+                return ret, out.raw[:ol.value], int(aux.value)
             cap = ol.value + 64
         raise RuntimeError("t2j oracle output did not fit")
 

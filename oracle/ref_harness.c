@@ -747,6 +747,7 @@ typedef struct {
     const dg_t2j_field *X;
     const char *XP; /* side-table pool */
     uint64_t opts;
+    uint64_t *aux; /* DG_T2J_SKIP_RESP_BASE: the base field's span (lo | hi << 32) */
 } T2J;
 
 #define T2J_ERR(code, pos, val) ((uint64_t)(code) | ((uint64_t)(pos) << 8) | ((uint64_t)(val) << 40))
@@ -991,6 +992,15 @@ static uint64_t t2j_append_int(const T2J *c, uint8_t t, TRd *r, JBuf *o)
 
 static uint64_t t2j_vm(const T2J *c, const dg_field *f, TRd *r, JBuf *o)
 {
+    if (f->vm == DG_VM_BODY_DYNAMIC) { /* agwBodyDynamic.Read (thrift/annotation/value_mapping.go:84-99) */
+        if (c->T[f->type].ttype != 11) return T2J_ERR(DG_T2J_E_CONVERT, r->p, 0x200u | c->T[f->type].ttype);
+        if (!rd_need(r, 4)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_EOF);
+        int32_t sz = (int32_t)rd_be(r, 4);
+        if (sz < 0 || !rd_need(r, (size_t)sz)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_BAD_SIZE);
+        jb_put(o, r->b + r->p, (size_t)sz); /* the raw bytes are the JSON */
+        r->p += (size_t)sz;
+        return 0;
+    }
     if (f->vm != DG_VM_JSCONV)
         return T2J_ERR(DG_T2J_E_NEEDS_HOST, r->p, f->vm);
     if (c->T[f->type].ttype == 15) { /* LIST: ReadListBegin, elements by the wire type */
@@ -1012,10 +1022,11 @@ static uint64_t t2j_vm(const T2J *c, const dg_field *f, TRd *r, JBuf *o)
     return t2j_append_int(c, c->T[f->type].ttype, r, o);
 }
 
-/* a STRUCT value (conv/t2j/impl.go:265-339; the top level :89-187 is the same
- * without HTTP mapping / exceptions / ThriftBase, which the GPU path leaves
- * to the Go host) */
-static uint64_t t2j_struct(const T2J *c, uint32_t td, TRd *r, JBuf *o)
+/* a STRUCT value (conv/t2j/impl.go:265-339); top: the root struct (do(),
+ * impl.go:74-187): response-base fields skipped (readResponseBase, the span
+ * to c->aux) and the exception field (ConvertException) ending it. HTTP
+ * mapping stays with the Go host. */
+static uint64_t t2j_struct_at(const T2J *c, uint32_t td, TRd *r, JBuf *o, int top)
 {
     const dg_struct *sd = &c->S[c->T[td].st];
     jb_c(o, '{');
@@ -1023,7 +1034,7 @@ static uint64_t t2j_struct(const T2J *c, uint32_t td, TRd *r, JBuf *o)
     uint32_t nw = sd->req_words < 64 ? sd->req_words : 64;
     for (uint32_t w = 0; w < nw; w++)
         req[w] = c->R[sd->req_begin + w];
-    int comma = 0;
+    int comma = 0, exc_done = 0;
     for (;;) {
         if (!rd_need(r, 1)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_EOF);
         uint8_t t = r->b[r->p++];
@@ -1041,15 +1052,28 @@ static uint64_t t2j_struct(const T2J *c, uint32_t td, TRd *r, JBuf *o)
         const dg_field *f = &c->F[fi];
         uint32_t k = (uint32_t)fi - sd->field_begin;
         req[k / 64] &= ~(1ull << (k % 64)); /* r.Set(id, Optional) */
+        if (top && (c->opts & DG_T2J_SKIP_RESP_BASE) && (f->flags & DG_FF_RESPONSE_BASE)) {
+            size_t s0 = r->p; /* readResponseBase: SkipType(STRUCT), the bytes to base.FastRead */
+            int se = t2j_skip(r, 12, 1023);
+            if (se) return T2J_ERR(DG_T2J_E_READ, r->p, se);
+            if (c->aux) *c->aux = (uint64_t)s0 | ((uint64_t)r->p << 32);
+            continue;
+        }
         if (comma) jb_c(o, ',');
         else comma = 1;
         const dg_t2j_field *x = &c->X[fi];
         jb_string(o, (const uint8_t *)c->XP + x->alias_off, x->alias_len);
         jb_c(o, ':');
+        const int exc = top && (c->opts & DG_T2J_CONVERT_EXC) && id != 0;
+        if (exc) o->len = 0; /* only the exception field's data */
         uint64_t e;
         if ((c->opts & DG_T2J_ENABLE_VM) && f->vm != DG_VM_NONE) e = t2j_vm(c, f, r, o);
         else e = t2j_value(c, f->type, r, o);
         if (e) return e;
+        if (exc) {
+            exc_done = 1;
+            break;
+        }
     }
     /* handleUnsets -> HandleRequires (thrift/utils.go:149-176), ascending id */
     for (uint32_t k = 0; k < sd->n_fields; k++) {
@@ -1069,9 +1093,12 @@ static uint64_t t2j_struct(const T2J *c, uint32_t td, TRd *r, JBuf *o)
         uint64_t e = t2j_default_or_empty(c, f, r->p, o);
         if (e) return e;
     }
+    if (exc_done) return T2J_ERR(DG_T2J_E_EXCEPTION, r->p, 0); /* err = errors.New(string(*out)) */
     jb_c(o, '}');
     return 0;
 }
+
+static uint64_t t2j_struct(const T2J *c, uint32_t td, TRd *r, JBuf *o) { return t2j_struct_at(c, td, r, o, 0); }
 
 /* doRecurse (conv/t2j/impl.go:189-393) */
 static uint64_t t2j_value(const T2J *c, uint32_t td, TRd *r, JBuf *o)
@@ -1225,6 +1252,7 @@ static void t2j_init(T2J *c, const uint8_t *blob, const uint8_t *side, uint64_t 
     c->X = (const dg_t2j_field *)(side + xh->off_fields);
     c->XP = (const char *)(side + xh->off_pool);
     c->opts = opts;
+    c->aux = NULL;
 }
 
 /* BinaryConv.Do (conv/t2j/conv.go:50-75 + impl.go:74-187): one message into
@@ -1234,6 +1262,8 @@ static uint64_t t2j_do(const T2J *c, uint32_t root, const uint8_t *thrift, size_
 {
     TRd r = {thrift, n, 0};
     o->len = 0;
+    if (c->aux) *c->aux = ~0ull;
+    if (c->T[root].ttype == 12) return t2j_struct_at(c, root, &r, o, 1);
     return t2j_value(c, root, &r, o);
 }
 
@@ -1244,8 +1274,26 @@ uint64_t dgref_t2j(const uint8_t *blob, const uint8_t *side, uint32_t root, cons
     t2j_init(&c, blob, side, opts);
     JBuf o = {(char *)malloc(256), 0, 256};
     uint64_t e = t2j_do(&c, root, thrift, n, &o);
-    *out_len = e ? 0 : o.len;
-    if (!e && o.len <= cap)
+    const int keep = !e || (e & 0xFF) == DG_T2J_E_EXCEPTION;
+    *out_len = keep ? o.len : 0;
+    if (keep && o.len <= cap)
+        memcpy(out, o.b, o.len);
+    free(o.b);
+    return e;
+}
+
+/* dgref_t2j with the response-base span (DG_T2J_SKIP_RESP_BASE) */
+uint64_t dgref_t2j2(const uint8_t *blob, const uint8_t *side, uint32_t root, const uint8_t *thrift, size_t n,
+                    uint64_t opts, uint8_t *out, size_t cap, size_t *out_len, uint64_t *aux)
+{
+    T2J c;
+    t2j_init(&c, blob, side, opts);
+    c.aux = aux;
+    JBuf o = {(char *)malloc(256), 0, 256};
+    uint64_t e = t2j_do(&c, root, thrift, n, &o);
+    const int keep = !e || (e & 0xFF) == DG_T2J_E_EXCEPTION;
+    *out_len = keep ? o.len : 0;
+    if (keep && o.len <= cap)
         memcpy(out, o.b, o.len);
     free(o.b);
     return e;

@@ -445,3 +445,69 @@ def test_wave_path_nested_and_escapes(chk, knob):
     for opts in (0, NOB64):
         bad = compare(chk, fl, msgs, opts)
         assert not bad, bad[:3]
+
+
+# ---- the Go-side options: ConvertException, EnableThriftBase, agw.body_dynamic ----
+CONV_EXC, SKIP_BASE = 1 << 9, 1 << 10
+
+
+def test_agw_body_dynamic_read(chk):
+    """TestAGWBodyDynamic (conv/t2j/conv_test.go:266-286) through Do, and a
+    fuzz of the body_dynamic read against the checker."""
+    from test_t2j_oracle import _example3_svc, error_resp_thrift
+    td = _example3_svc().functions()["ErrorMethod"].response().struct.fields[0].type
+    assert t2j.BinaryConv(conv.Options(EnableValueMapping=True)).do(td, error_resp_thrift()) == \
+        b'{"Int64":1,"Xjson":{"b":1}}'
+    assert t2j.BinaryConv(conv.Options()).do(td, error_resp_thrift()) == b'{"Int64":1,"Xjson":"{\\"b\\":1}"}'
+    fl = T.flatten(td)
+    rng = random.Random(4)
+    msgs = []
+    for k in range(500):
+        body = bytes(rng.choice(b'{}[]":,ab01 ') for _ in range(rng.randint(0, 40)))
+        m = b"\x0a\x00\x02" + struct.pack(">q", k) + b"\x0b\x00\x04" + struct.pack(">i", len(body)) + body + b"\x00"
+        if k % 7 == 0:
+            m = m[:rng.randint(0, len(m))]  # truncated
+        msgs.append(m)
+    for opts in (VM, 0, VM | WDEF):
+        assert not compare(chk, fl, msgs, opts)
+
+
+def test_convert_exception(chk):
+    """TestException (conv/t2j/conv_test.go:310-330): Do raises with the
+    exception's JSON as the text; the device keeps the JSON (status 11)."""
+    from test_t2j_oracle import _example3_svc, exception_result_thrift
+    td = _example3_svc().functions()["ExampleMethod"].response()
+    with pytest.raises(t2j.T2JException) as ei:
+        t2j.BinaryConv(conv.Options(ConvertException=True)).do(td, exception_result_thrift())
+    assert str(ei.value) == '{"code":400,"msg":"this is an exception"}'
+    fl = T.flatten(td)
+    succ_only = exception_result_thrift()
+    succ_only = succ_only[:succ_only.index(b"\x0c\x00\x01")] + b"\x00"
+    msgs = [exception_result_thrift(), succ_only, exception_result_thrift()[:-3]]
+    for opts in (CONV_EXC, CONV_EXC | WDEF | WREQ | WOPT, 0):
+        assert not compare(chk, fl, msgs, opts)
+
+
+def test_response_base(chk):
+    """TestThriftResponseBase (conv/t2j/conv_test.go:232-264): with a
+    context BaseResp the JSON has no BaseResp and the context object holds
+    what it held."""
+    import json
+    import os
+    from test_t2j_oracle import _example3_svc
+    td = _example3_svc(T.Options(enable_thrift_base=True)).functions()["ExampleMethod"].response().struct.fields[0].type
+    src = open(os.path.join(os.path.dirname(__file__), "golden", "example3resp.bin"), "rb").read()
+    cv = t2j.BinaryConv(conv.Options(EnableThriftBase=True))
+    plain = json.loads(cv.do(td, src))
+    base = t2j.BaseResp()
+    got = json.loads(cv.do(td, src, base=base))
+    want = plain.pop("BaseResp")
+    assert got == plain
+    assert (base.StatusMessage, base.StatusCode, base.Extra or {}) == \
+        (want["StatusMessage"], want["StatusCode"], want.get("Extra") or {})
+    fl = T.flatten(td)
+    side = T.flatten_t2j(fl)
+    outs, errs = cv.do_batch_errors(td, [src] * 3, bases=[t2j.BaseResp() for _ in range(3)])
+    assert all(e is None for e in errs)
+    r, js, aux = chk.t2j2(fl, side, src, SKIP_BASE)
+    assert outs[0] == js

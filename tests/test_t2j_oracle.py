@@ -96,3 +96,76 @@ def test_generated_messages(chk):
             ok += 1
     assert ok > 150
     assert {1, 3}.issubset(codes), codes  # ErrRead, ErrDismatchType
+
+
+# ---- the Go-side options: ConvertException, EnableThriftBase, agw.body_dynamic ----
+T2J_CONVERT_EXC, T2J_SKIP_RESP_BASE = 1 << 9, 1 << 10
+
+
+def _example3_svc(opts=None):
+    import os
+    from schemas import IDL_DIR
+    T.init_agw_annos()
+    return T.new_descriptor_from_path(os.path.join(IDL_DIR, "example3.thrift"), opts)
+
+
+def error_resp_thrift():
+    """example3.ExampleErrorResp{Int64: 1, Xjson: `{"b":1}`} (FastWrite, id order)."""
+    return b"\x0a\x00\x02" + struct.pack(">q", 1) + b"\x0b\x00\x04" + struct.pack(">i", 7) + b'{"b":1}' + b"\x00"
+
+
+def exception_result_thrift():
+    """ExampleServiceExampleMethodResult{Success: ExampleResp{Status: 202},
+    Err: Exception{Code: 400, Msg: "this is an exception"}}."""
+    succ = (b"\x0b\x00\x01" + struct.pack(">i", 0) + b"\x08\x00\x03" + struct.pack(">i", 202) +
+            b"\x0a\x00\x06" + struct.pack(">q", 0) + b"\x04\x7f\xff" + struct.pack(">d", 0.0) + b"\x00")
+    msg = b"this is an exception"
+    exc = b"\x08\x00\x01" + struct.pack(">i", 400) + b"\x0b\x00\xff" + struct.pack(">i", len(msg)) + msg + b"\x00"
+    return b"\x0c\x00\x00" + succ + b"\x0c\x00\x01" + exc + b"\x00"
+
+
+def test_agw_body_dynamic_read(chk):
+    """TestAGWBodyDynamic (conv/t2j/conv_test.go:266-286)."""
+    td = _example3_svc().functions()["ErrorMethod"].response().struct.fields[0].type
+    fl = T.flatten(td)
+    side = T.flatten_t2j(fl)
+    assert chk.t2j(fl, side, error_resp_thrift(), T2J_ENABLE_VM) == (0, b'{"Int64":1,"Xjson":{"b":1}}')
+    assert chk.t2j(fl, side, error_resp_thrift(), 0) == (0, b'{"Int64":1,"Xjson":"{\\"b\\":1}"}')
+
+
+def test_convert_exception(chk):
+    """TestException (conv/t2j/conv_test.go:310-330): the whole result, the
+    error text is the exception's JSON."""
+    td = _example3_svc().functions()["ExampleMethod"].response()
+    fl = T.flatten(td)
+    side = T.flatten_t2j(fl)
+    r, js = chk.t2j(fl, side, exception_result_thrift(), T2J_CONVERT_EXC)
+    assert r & 0xFF == 11 and js == b'{"code":400,"msg":"this is an exception"}'
+    r, js = chk.t2j(fl, side, exception_result_thrift(), 0)  # without the option: both fields as JSON
+    assert r == 0 and js.startswith(b'{"":{') and js.endswith(b'"err":{"code":400,"msg":"this is an exception"}}')
+
+
+def test_response_base_skipped(chk):
+    """TestThriftResponseBase (conv/t2j/conv_test.go:232-264): with a context
+    BaseResp the root's BaseResp field is skipped and its bytes reported."""
+    import json
+    import os
+    from schemas import IDL_DIR
+    td = _example3_svc(T.Options(enable_thrift_base=True)).functions()["ExampleMethod"].response().struct.fields[0].type
+    fl = T.flatten(td)
+    side = T.flatten_t2j(fl)
+    src = open(os.path.join(os.path.dirname(IDL_DIR), "example3resp.bin"), "rb").read()
+    r0, js0, _ = chk.t2j2(fl, side, src, 0)
+    r1, js1, aux = chk.t2j2(fl, side, src, T2J_SKIP_RESP_BASE)
+    assert r0 == 0 and r1 == 0
+    a, b = json.loads(js0), json.loads(js1)
+    assert "BaseResp" in a and "BaseResp" not in b
+    a.pop("BaseResp")
+    assert a == b
+    lo, hi = aux & 0xFFFFFFFF, aux >> 32
+    from dynamicgo_amd.t2j import BaseResp
+    br = BaseResp()
+    br.fast_read(src[lo:hi])
+    want = json.loads(js0)["BaseResp"]
+    assert (br.StatusMessage, br.StatusCode) == (want["StatusMessage"], want["StatusCode"])
+    assert (br.Extra or {}) == (want.get("Extra") or {})
