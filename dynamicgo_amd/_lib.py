@@ -19,7 +19,8 @@ EXPORTS = ["dg_last_error", "dg_build_info", "dg_ctx_create", "dg_ctx_destroy", 
            "dg_j2t_batch_device_inflight",
            "dg_slot_bound", "dg_j2t_batch_host", "dg_j2t_batch_host_hm", "dg_j2t_batch_host_cb", "dg_j2t_do", "dg_pack_device", "dg_pack_device_scan", "dg_pack_device_framed", "dg_agg_create", "dg_agg_create2", "dg_agg_do",
            "dg_agg_submit", "dg_agg_wait", "dg_agg_ready", "dg_agg_stats", "dg_agg_profile", "dg_agg_destroy", "dg_agg_drive", "dg_j2t_pipeline_host", "dg_bench_device", "dg_desc_attach_t2j", "dg_t2j_slot_bound", "dg_t2j_batch_device", "dg_t2j_batch_device_ml",
-           "dg_t2j_batch_host", "dg_t2j_batch_device_aux", "dg_t2j_batch_host_aux"]
+           "dg_t2j_batch_host", "dg_t2j_batch_device_aux", "dg_t2j_batch_host_aux",
+           "dg_t2j_batch_device_cb", "dg_t2j_batch_host_cb"]
 
 _lib = None
 
@@ -91,6 +92,8 @@ def lib() -> C.CDLL:
         "dg_t2j_batch_host": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, u64, vp, vp, P64]),
         "dg_t2j_batch_device_aux": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, vp, vp, vp, vp, vp, u64]),
         "dg_t2j_batch_host_aux": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, u64, vp, vp, P64, vp]),
+        "dg_t2j_batch_device_cb": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, vp, vp, vp, vp, vp, vp, vp, u64]),
+        "dg_t2j_batch_host_cb": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, u64, vp, vp, P64, vp, vp]),
         "dg_bench_device": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, vp, vp, vp, i32, C.POINTER(C.c_float)]),
     }
     for name, (res, args) in sig.items():

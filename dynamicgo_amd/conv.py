@@ -82,6 +82,8 @@ class Options:
     EncodeNullJSONForInfOrNan: bool = False
     ConvertException: bool = False
     WriteHttpValueFallback: bool = False
+    OmitHttpMappingErrors: bool = False
+    UseKitexHttpEncoding: bool = False
 
 
 def to_flags(o: Options) -> int:

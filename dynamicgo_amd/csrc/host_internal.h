@@ -99,6 +99,7 @@ struct dg_ctx {
     uint32_t *d_out_len = nullptr; uint64_t d_ol_cap = 0;
     uint64_t *d_ret = nullptr; uint64_t d_ret_cap = 0;
     uint64_t *d_aux = nullptr; uint64_t d_aux_cap = 0;       /* t2j: per-message response-base spans */
+    uint8_t *d_cb = nullptr; uint64_t d_cb_cap = 0;          /* t2j: callback answers (entries + bytes) */
     uint8_t *d_pack = nullptr; uint64_t d_pack_cap = 0;      /* packed Thrift (dg_pack_device_scan) */
     uint64_t *d_pack_off = nullptr; uint64_t d_po_cap = 0;
     uint8_t *h_up = nullptr; uint64_t h_up_cap = 0;          /* pinned: offsets + JSON, one H2D */

@@ -192,6 +192,7 @@ void dg_ctx_destroy(dg_ctx *c)
     (void)hipFree(c->d_out_len);
     (void)hipFree(c->d_ret);
     (void)hipFree(c->d_aux);
+    (void)hipFree(c->d_cb);
     (void)hipFree(c->d_pack);
     (void)hipFree(c->d_pack_off);
     (void)hipHostFree(c->h_up);

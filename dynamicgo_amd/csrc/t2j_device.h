@@ -441,11 +441,19 @@ DGI void emit_default(Out &o, const DV &D, const dg_field &fd, uint8_t tt)
     }
 }
 
-template <class S, class FP, class DV>
+/* GO: the root-level Go-side options are compiled in (DG_T2J_CONVERT_EXC,
+ * DG_T2J_SKIP_RESP_BASE, DG_T2J_HM); the plain instance keeps the lane
+ * kernel's registers at occupancy 4 (113 vs 139 VGPRs) */
+template <bool GO, class S, class FP, class DV>
 DGI uint64_t t2j_convert(const DV &D, const T2JSide &X, S src, uint32_t root, uint64_t opts, Out &o, FP fr,
                          uint32_t fstride, uint32_t cap, gu64 *wide = nullptr, uint32_t widecap = 0,
-                         uint64_t *aux = nullptr)
+                         uint64_t *aux = nullptr, const dg_cb_entry *ans = nullptr, const uint8_t *ans_bytes = nullptr)
 {
+    if (!GO) {
+        opts &= ~(uint64_t)(DG_T2J_CONVERT_EXC | DG_T2J_SKIP_RESP_BASE | DG_T2J_HM);
+        aux = nullptr;
+        ans = nullptr;
+    }
     T2JRd<S> r{src, 0};
     uint32_t sp = 0;
     uint32_t wlen = 0; /* words of `wide` in use: requires bitmaps of open structs of > 64 fields */
@@ -457,6 +465,36 @@ DGI uint64_t t2j_convert(const DV &D, const T2JSide &X, S src, uint32_t root, ui
     bool base_pend = false;
     int64_t base_s0 = 0;
     if (aux) *aux = ~0ull;
+    /* DG_T2J_HM: the host's answers to writeHttpValue, one byte per call in
+     * call order (dg_cb_entry): 0 = the response took the value, 1 = write it
+     * to the JSON as well, 2 = still open: convert the container value to
+     * JSON and stop with it (the calls its conversion makes follow it). A
+     * call past the answers stops the message at the value. */
+    uint32_t ans_seen = 0; /* calls so far */
+    auto take = [&](uint8_t &a) -> bool {
+        const uint32_t k = ans_seen++;
+        if (!ans || k >= ans->count) return false;
+        a = ans_bytes[ans->off + k];
+        return true;
+    };
+    uint32_t cb_fi = ~0u, cb_sp = 0, cb_idx = 0;
+    int64_t cb_s0 = 0;
+    /* a stop's record: its payload (a mapped container's JSON, else nothing)
+     * and a 16-byte trailer: kind (1 mapped value, 2 unset mapped field) |
+     * resp << 8 | the call's index << 16, the field's index, the value's span */
+    auto stop = [&](uint32_t kind, uint32_t idx, uint32_t fi, int64_t s0, int64_t s1) -> uint64_t {
+        if (idx > 0xFFFF) return t2j_err(DG_T2J_E_DEPTH, r.p, idx); /* more calls than a record counts */
+        o.wle((uint64_t)kind | ((uint64_t)idx << 16) | ((uint64_t)fi << 32), 8);
+        o.wle((uint64_t)(uint32_t)s0 | ((uint64_t)(uint32_t)s1 << 32), 8);
+        return t2j_err(DG_T2J_E_CALLBACK, r.p, kind & 0xFF);
+    };
+    /* bit k: frame k is a struct with a ResponseSetter: the root (do()), a
+     * root field's struct value (doRecurse(resp), conv/t2j/impl.go:167) and
+     * the value writeHttpValue converts to JSON (impl.go:565); their fields'
+     * values and container elements get nil (impl.go:327,360,383) */
+    uint64_t respm = 0;
+    bool push_resp = (opts & DG_T2J_HM) != 0; /* the next struct value pushed gets one: first the root */
+    auto resp_level = [&]() -> bool { return sp - 1 < 64 && ((respm >> (sp - 1)) & 1); };
 
     /* the value of type td at the reader: scalars written, containers opened
      * (their header read and checked, the frame pushed) */
@@ -530,6 +568,7 @@ DGI uint64_t t2j_convert(const DV &D, const T2JSide &X, S src, uint32_t root, ui
                 u = wlen;
                 wlen += sd.req_words;
             }
+            if (sp < 64) respm = push_resp ? respm | (1ull << sp) : respm & ~(1ull << sp);
             auto &f = F(sp++);
             f.kind = TF_STRUCT;
             f.td = td;
@@ -657,7 +696,7 @@ DGI uint64_t t2j_convert(const DV &D, const T2JSide &X, S src, uint32_t root, ui
     };
 
     /* handleUnsets -> HandleRequires (thrift/utils.go:149-176), ascending id */
-    auto unsets = [&](auto &f, const dg_struct &sd) -> uint64_t {
+    auto unsets = [&](auto &f, const dg_struct &sd, bool resp) -> uint64_t {
         for (uint32_t w = 0; w < sd.req_words; w++) {
             uint64_t bits = sd.req_words == 1 ? f.u : (uint64_t)wide[(uint32_t)f.u + w];
             while (bits) {
@@ -670,6 +709,16 @@ DGI uint64_t t2j_convert(const DV &D, const T2JSide &X, S src, uint32_t root, ui
                     (fd.required == DG_REQ_OPTIONAL && !(opts & DG_T2J_WRITE_OPTIONAL) && fd.dflt_len == DG_NONE))
                     continue;
                 const uint8_t ftt = ldrec(&D.T[fd.type]).ttype;
+                if ((opts & DG_T2J_HM) && (fd.flags & DG_FF_HTTP_MAPPING)) {
+                    /* handleUnsets (impl.go:401-429): writeHttpValue of the default first, at
+                     * every level (resp may be nil there) */
+                    uint8_t a;
+                    if (!take(a)) {
+                        o.set_len(0);
+                        return stop(2 | (resp ? 0x100u : 0u), ans_seen - 1, sd.field_begin + k, 0, 0);
+                    }
+                    if (a == 0) continue;
+                }
                 if (fd.dflt_len != DG_NONE && !(ftt == DG_T_BOOL || num_bytes(ftt) || ftt == DG_T_STRING))
                     return t2j_err(DG_T2J_E_NEEDS_HOST, r.p, fd.id); /* a container constant's JSONValue() */
                 if (f.i) o.w8(',');
@@ -697,8 +746,10 @@ DGI uint64_t t2j_convert(const DV &D, const T2JSide &X, S src, uint32_t root, ui
     };
 
     uint64_t e = value(root);
+    push_resp = false;
     if (e) return e;
     while (sp) {
+        if (cb_fi != ~0u && sp == cb_sp) return stop(1 | 0x100u, cb_idx, cb_fi, cb_s0, r.p); /* the mapped value read */
         auto &f = F(sp - 1);
         switch (f.kind) {
         case TF_STRUCT: {
@@ -710,7 +761,7 @@ DGI uint64_t t2j_convert(const DV &D, const T2JSide &X, S src, uint32_t root, ui
                     base_pend = false;
                 }
                 if (exc) { /* the exception field is done: unsets, then the error (impl.go:173-187) */
-                    if ((e = unsets(f, sd))) return e;
+                    if ((e = unsets(f, sd, resp_level()))) return e;
                     return t2j_err(DG_T2J_E_EXCEPTION, r.p, 0);
                 }
             }
@@ -718,7 +769,7 @@ DGI uint64_t t2j_convert(const DV &D, const T2JSide &X, S src, uint32_t root, ui
             const uint8_t t = r.u8();
             if (!ttype_valid(t)) return t2j_err(DG_T2J_E_READ, r.p, RD_BAD_TYPE);
             if (t == 0) {
-                if ((e = unsets(f, sd))) return e;
+                if ((e = unsets(f, sd, resp_level()))) return e;
                 o.w8('}');
                 if (sd.req_words != 1) wlen -= sd.req_words;
                 sp--;
@@ -743,6 +794,34 @@ DGI uint64_t t2j_convert(const DV &D, const T2JSide &X, S src, uint32_t root, ui
                 if ((e = skip(DG_T_STRUCT, T2J_SKIP_DEPTH, false))) return e;
                 base_pend = true;
                 continue;
+            }
+            if ((fd.flags & DG_FF_HTTP_MAPPING) && (opts & DG_T2J_HM) && resp_level()) {
+                /* writeHttpValue (impl.go:132-142, 296-306): the host's answer, or a stop
+                 * with the value's span (and a container's JSON, impl.go:561-574) */
+                uint8_t a;
+                const uint8_t dt = ldrec(&D.T[fd.type]).ttype;
+                if (!take(a)) { /* a new call: the host reads the value at the stop's position */
+                    o.set_len(0);
+                    return stop(1 | 0x100u, ans_seen - 1, (uint32_t)fi, r.p, r.p);
+                }
+                if (a == 2 && (dt == DG_T_STRUCT || dt == DG_T_MAP || dt == DG_T_LIST || dt == DG_T_SET)) {
+                    /* the call needs the value's JSON (doRecurse(resp), impl.go:561-574):
+                     * converted here, the calls it makes answered after this one's */
+                    cb_s0 = r.p;
+                    cb_fi = (uint32_t)fi;
+                    cb_sp = sp;
+                    cb_idx = ans_seen - 1;
+                    o.set_len(0);
+                    push_resp = true;
+                    e = value(fd.type);
+                    push_resp = false;
+                    if (e) return e;
+                    continue; /* stops when the frames are back at cb_sp */
+                }
+                if (a == 0) { /* the response took it: the value is consumed */
+                    if ((e = skip(dt, T2J_SKIP_DEPTH, false))) return e;
+                    continue;
+                }
             }
             if (f.i) o.w8(',');
             f.i = 1;
@@ -822,7 +901,10 @@ DGI uint64_t t2j_convert(const DV &D, const T2JSide &X, S src, uint32_t root, ui
                 if (ft == DG_T_LIST) o.w8(']');
                 continue;
             }
-            if ((e = value(fd.type))) return e;
+            push_resp = sp == 1 && (respm & 1); /* do() passes resp to its fields' values */
+            e = value(fd.type);
+            push_resp = false;
+            if (e) return e;
             continue;
         }
         case TF_LIST: {
@@ -924,6 +1006,8 @@ struct T2JParams {
     dg_desc_hdr hdr;
     const uint8_t *side;      /* t2j side table (device) */
     uint64_t *aux;            /* DG_T2J_SKIP_RESP_BASE: per message the response base's span (or NULL) */
+    const dg_cb_entry *ans_tab; /* DG_T2J_HM: per message the host's writeHttpValue answers (or NULL) */
+    const uint8_t *ans_bytes;
     uint32_t *deep_list;      /* messages nested beyond the LDS frames */
     uint32_t *deep_count;     /* their number (reset by the host after the deep pass) */
     uint8_t *ws;              /* deep pass: T2J_DEEP_DEPTH frames per lane */
@@ -950,7 +1034,7 @@ DGI T2JSide t2j_side(const uint8_t *side)
 DGI void t2j_store(const T2JParams &P, uint64_t i, uint64_t r, Out &o)
 {
     uint32_t olen = 0;
-    if (r == 0 || (uint8_t)r == DG_T2J_E_EXCEPTION) { /* the exception's JSON is kept */
+    if (r == 0 || (uint8_t)r == DG_T2J_E_EXCEPTION || (uint8_t)r == DG_T2J_E_CALLBACK) { /* kept: the exception's JSON, the stop's record */
         o.finish();
         if (o.len > o.cap) {
             const uint64_t need = o.len;

@@ -32,7 +32,8 @@ static uint32_t t2j_spread(const dg_ctx *c, uint64_t max_len)
  * event after. */
 static int t2j_launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *src, const uint64_t *in_off,
                       uint64_t n, uint64_t opts, uint8_t *out, const uint64_t *out_off, uint32_t *out_len,
-                      uint64_t *ret, hipStream_t s, uint64_t max_len, uint64_t *aux = nullptr)
+                      uint64_t *ret, hipStream_t s, uint64_t max_len, uint64_t *aux = nullptr,
+                      const dg_cb_entry *ans = nullptr, const uint8_t *ans_bytes = nullptr)
 {
     if (n == 0) return DG_OK;
     if (!d->d_side) return set_err(DG_E_DESC, "descriptor has no t2j side table (dg_desc_attach_t2j)");
@@ -48,7 +49,7 @@ static int t2j_launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
     }
     const uint64_t wmin = (uint64_t)c->knobs.t2j_wave_min;
     /* the root-level Go-side options run on the lane kernel only */
-    const bool wave = !(opts & (DG_T2J_CONVERT_EXC | DG_T2J_SKIP_RESP_BASE)) && wmin > 0 && d->hdr.total_len <= 16384 && d->hdr.n_fields <= 1024 && /* T2W_FX */
+    const bool wave = !(opts & (DG_T2J_CONVERT_EXC | DG_T2J_SKIP_RESP_BASE | DG_T2J_HM)) && wmin > 0 && d->hdr.total_len <= 16384 && d->hdr.n_fields <= 1024 && /* T2W_FX */
                       d->side_len <= 12288 /* T2W_SIDE */ && (max_len == 0 || max_len > wmin);
     if (wave) {
         if ((rc = grow_x(x, x->t2j_big, x->t2j_big_cap, n))) return rc;
@@ -77,6 +78,8 @@ static int t2j_launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
     P.ws = c->ws_t2j;
     P.stats = c->d_stats;
     P.aux = (opts & DG_T2J_SKIP_RESP_BASE) ? aux : nullptr;
+    P.ans_tab = (opts & DG_T2J_HM) ? ans : nullptr;
+    P.ans_bytes = ans_bytes;
     hipError_t e = hipSuccess;
     if (wave) {
         T2JParams P1 = P;
@@ -189,6 +192,20 @@ int dg_t2j_batch_device_aux(dg_ctx *c, const dg_desc *d, uint32_t root, const ui
     return t2j_launch(c, d, root, d_thrift, d_in_off, n, opts, d_out, d_out_off, d_out_len, d_ret, s, max_len, d_aux);
 }
 
+int dg_t2j_batch_device_cb(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *d_thrift,
+                           const uint64_t *d_in_off, uint64_t n, uint64_t opts, uint8_t *d_out,
+                           const uint64_t *d_out_off, uint32_t *d_out_len, uint64_t *d_ret, uint64_t *d_aux,
+                           const dg_cb_entry *d_ans, const uint8_t *d_ans_bytes, void *stream, uint64_t max_len)
+{
+    if (!c || !d || ((opts & DG_T2J_SKIP_RESP_BASE) && !d_aux) || (d_ans && !d_ans_bytes))
+        return set_err(DG_E_INVALID, "bad args");
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    return t2j_launch(c, d, root, d_thrift, d_in_off, n, opts, d_out, d_out_off, d_out_len, d_ret, s, max_len, d_aux,
+                      d_ans, d_ans_bytes);
+}
+
 int dg_t2j_batch_device(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *d_thrift, const uint64_t *d_in_off,
                         uint64_t n, uint64_t opts, uint8_t *d_out, const uint64_t *d_out_off, uint32_t *d_out_len,
                         uint64_t *d_ret, void *stream)
@@ -199,11 +216,15 @@ int dg_t2j_batch_device(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_
 
 static int t2j_batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *thrift, const uint64_t *in_off,
                           uint64_t n, uint64_t opts, uint8_t *out, uint64_t out_cap, uint64_t *out_off, uint64_t *ret,
-                          uint64_t *out_need, uint64_t *aux)
+                          uint64_t *out_need, uint64_t *aux, const dg_cb_tables *cb)
 {
     if (!c || !d || (!thrift && n) || !in_off || !out_off || (!ret && n) ||
-        ((opts & DG_T2J_SKIP_RESP_BASE) && n && !aux))
+        ((opts & DG_T2J_SKIP_RESP_BASE) && n && !aux) || (cb && cb->ans_tab && cb->len && !cb->bytes))
         return set_err(DG_E_INVALID, "bad args");
+    const dg_cb_entry *ans = cb && (opts & DG_T2J_HM) ? cb->ans_tab : nullptr;
+    for (uint64_t i = 0; ans && i < n; i++) /* one byte per answer, inside the bytes (read unchecked) */
+        if (ans[i].off + ans[i].count > cb->len)
+            return set_err(DG_E_INVALID, "callback answers of message %llu outside the bytes", (unsigned long long)i);
     std::lock_guard<std::mutex> g(c->mu);
     HIPCHK(hipSetDevice(c->device));
     const uint64_t base = in_off[0];
@@ -235,6 +256,14 @@ static int t2j_batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint
         if ((rc = grow(c->d_out_len, c->d_ol_cap, m + 1))) return rc;
         if ((rc = grow(c->d_ret, c->d_ret_cap, m + 1))) return rc;
         if (aux && (rc = grow(c->d_aux, c->d_aux_cap, m + 1))) return rc;
+        if (ans) { /* [m entries | the answer bytes] */
+            if ((rc = grow(c->d_cb, c->d_cb_cap, 8 * m + cb->len + 8))) return rc;
+            std::vector<dg_cb_entry> e(m);
+            for (uint64_t k = 0; k < m; k++) e[k] = ans[todo[k]];
+            HIPCHK(hipMemcpyAsync(c->d_cb, e.data(), 8 * m, hipMemcpyHostToDevice, s));
+            if (cb->len) HIPCHK(hipMemcpyAsync(c->d_cb + 8 * m, cb->bytes, cb->len, hipMemcpyHostToDevice, s));
+            HIPCHK(hipStreamSynchronize(s)); /* e is a local */
+        }
         if (pass == 0) {
             HIPCHK(hipMemcpyAsync(c->d_json, thrift + base, io[m], hipMemcpyHostToDevice, s));
         } else {
@@ -246,7 +275,8 @@ static int t2j_batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint
         HIPCHK(hipMemcpyAsync(c->d_in_off, io.data(), (m + 1) * 8, hipMemcpyHostToDevice, s));
         HIPCHK(hipMemcpyAsync(c->d_out_off, so.data(), (m + 1) * 8, hipMemcpyHostToDevice, s));
         if ((rc = t2j_launch(c, d, root, c->d_json, c->d_in_off, m, opts, c->d_out, c->d_out_off, c->d_out_len,
-                             c->d_ret, s, max_len, aux ? c->d_aux : nullptr)))
+                             c->d_ret, s, max_len, aux ? c->d_aux : nullptr,
+                             ans ? (const dg_cb_entry *)(const void *)c->d_cb : nullptr, ans ? c->d_cb + 8 * m : nullptr)))
             return rc;
         std::vector<uint64_t> r(m), ax(aux ? m : 0);
         std::vector<uint32_t> l(m);
@@ -275,7 +305,8 @@ static int t2j_batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint
     uint64_t total = 0;
     out_off[0] = 0;
     for (uint64_t i = 0; i < n; i++) {
-        if (ret[i] != 0 && (uint8_t)ret[i] != DG_T2J_E_EXCEPTION) olen[i] = 0; /* the exception's JSON is kept */
+        if (ret[i] != 0 && (uint8_t)ret[i] != DG_T2J_E_EXCEPTION && (uint8_t)ret[i] != DG_T2J_E_CALLBACK)
+            olen[i] = 0; /* kept: the exception's JSON, a stop's record */
         total += olen[i];
         out_off[i + 1] = total;
     }
@@ -290,14 +321,21 @@ int dg_t2j_batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
                       uint64_t n, uint64_t opts, uint8_t *out, uint64_t out_cap, uint64_t *out_off, uint64_t *ret,
                       uint64_t *out_need)
 {
-    return t2j_batch_host(c, d, root, thrift, in_off, n, opts, out, out_cap, out_off, ret, out_need, nullptr);
+    return t2j_batch_host(c, d, root, thrift, in_off, n, opts, out, out_cap, out_off, ret, out_need, nullptr, nullptr);
 }
 
 int dg_t2j_batch_host_aux(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *thrift, const uint64_t *in_off,
                           uint64_t n, uint64_t opts, uint8_t *out, uint64_t out_cap, uint64_t *out_off, uint64_t *ret,
                           uint64_t *out_need, uint64_t *aux)
 {
-    return t2j_batch_host(c, d, root, thrift, in_off, n, opts, out, out_cap, out_off, ret, out_need, aux);
+    return t2j_batch_host(c, d, root, thrift, in_off, n, opts, out, out_cap, out_off, ret, out_need, aux, nullptr);
+}
+
+int dg_t2j_batch_host_cb(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *thrift, const uint64_t *in_off,
+                         uint64_t n, uint64_t opts, uint8_t *out, uint64_t out_cap, uint64_t *out_off, uint64_t *ret,
+                         uint64_t *out_need, uint64_t *aux, const dg_cb_tables *cb)
+{
+    return t2j_batch_host(c, d, root, thrift, in_off, n, opts, out, out_cap, out_off, ret, out_need, aux, cb);
 }
 
 }  // extern "C"

@@ -10,7 +10,7 @@ namespace dg {
  * (measured, LICM off): t2j-c2 (~100 B) 0.0705 / 0.0739 / 0.0977 ms at spread
  * 1 / 2 / 4; t2j-c3 (~1.2 KB) 5.59 / 3.95 / 3.76 ms. The host picks it from
  * the batch's longest message (t2j_spread). */
-template <uint32_t SP>
+template <uint32_t SP, bool GO>
 __global__ __launch_bounds__(T2J_BLOCK) void t2j_kernel(T2JParams P)
 {
     constexpr uint32_t MPB = T2J_BLOCK / SP; /* messages per block */
@@ -32,9 +32,10 @@ __global__ __launch_bounds__(T2J_BLOCK) void t2j_kernel(T2JParams P)
         s.init((glb_u64 *)(const void *)(P.src + (a & ~7ull)), (int64_t)(a & 7), (int64_t)(b - a));
         Out o;
         o.init(P.out + P.out_off[i], P.out_off[i + 1] - P.out_off[i]);
-        const uint64_t r = t2j_convert(D, X, s, P.root, P.opts, o,
+        const uint64_t r = t2j_convert<GO>(D, X, s, P.root, P.opts, o,
                                        (__attribute__((address_space(3))) T2JFrame *)(void *)&lf[slot], MPB,
-                                       T2J_LDS_DEPTH, nullptr, 0, P.aux ? P.aux + i : nullptr);
+                                       T2J_LDS_DEPTH, nullptr, 0, P.aux ? P.aux + i : nullptr,
+                                       P.ans_tab ? P.ans_tab + i : nullptr, P.ans_bytes);
         if ((uint8_t)r == DG_ST_DEEP) {
             P.deep_list[atomicAdd(P.deep_count, 1u)] = (uint32_t)i;
             continue;
@@ -106,6 +107,7 @@ __global__ __launch_bounds__(64 * T2W_WAVES) __attribute__((amdgpu_waves_per_eu(
  * struct of more than 64 fields), rerun from the start with T2J_DEEP_DEPTH
  * frames and T2J_WIDE_WORDS requires words per lane in device memory; a grid-stride loop over the queue (the grid is
  * small: deep messages are rare) */
+template <bool GO>
 __global__ __launch_bounds__(T2J_BLOCK) void t2j_deep_kernel(T2JParams P)
 {
     const uint32_t cnt = *(volatile uint32_t *)P.deep_count;
@@ -123,24 +125,34 @@ __global__ __launch_bounds__(T2J_BLOCK) void t2j_deep_kernel(T2JParams P)
         s.init((glb_u64 *)(const void *)(P.src + (a & ~7ull)), (int64_t)(a & 7), (int64_t)(b - a));
         Out o;
         o.init(P.out + P.out_off[i], P.out_off[i + 1] - P.out_off[i]);
-        uint64_t r = t2j_convert(D, X, s, P.root, P.opts, o, fr, 1, T2J_DEEP_DEPTH, wide, T2J_WIDE_WORDS,
-                                 P.aux ? P.aux + i : nullptr);
+        uint64_t r = t2j_convert<GO>(D, X, s, P.root, P.opts, o, fr, 1, T2J_DEEP_DEPTH, wide, T2J_WIDE_WORDS,
+                                 P.aux ? P.aux + i : nullptr, P.ans_tab ? P.ans_tab + i : nullptr, P.ans_bytes);
         if ((uint8_t)r == DG_ST_DEEP) r = t2j_err(DG_T2J_E_DEPTH, 0, T2J_DEEP_DEPTH);
         t2j_store(P, i, r, o);
     }
 }
 
+/* the Go-side options (the lane kernel only: t2j_launch keeps them off
+ * the wave kernel) take the GO instances, spread 1 */
+static inline bool t2j_go(const T2JParams &P)
+{
+    return (P.opts & (DG_T2J_CONVERT_EXC | DG_T2J_SKIP_RESP_BASE | DG_T2J_HM)) != 0;
+}
+
 void launch_t2j_pass(uint64_t n, hipStream_t s, const T2JParams &P, uint32_t spread)
 {
+    if (t2j_go(P)) spread = 1;
     const uint32_t mpb = T2J_BLOCK / spread, blocks = (uint32_t)((n + mpb - 1) / mpb);
-    if (spread == 1) hipLaunchKernelGGL(t2j_kernel<1>, dim3(blocks), dim3(T2J_BLOCK), 0, s, P);
-    else if (spread == 4) hipLaunchKernelGGL(t2j_kernel<4>, dim3(blocks), dim3(T2J_BLOCK), 0, s, P);
-    else hipLaunchKernelGGL(t2j_kernel<2>, dim3(blocks), dim3(T2J_BLOCK), 0, s, P);
+    if (t2j_go(P)) hipLaunchKernelGGL((t2j_kernel<1, true>), dim3(blocks), dim3(T2J_BLOCK), 0, s, P);
+    else if (spread == 1) hipLaunchKernelGGL((t2j_kernel<1, false>), dim3(blocks), dim3(T2J_BLOCK), 0, s, P);
+    else if (spread == 4) hipLaunchKernelGGL((t2j_kernel<4, false>), dim3(blocks), dim3(T2J_BLOCK), 0, s, P);
+    else hipLaunchKernelGGL((t2j_kernel<2, false>), dim3(blocks), dim3(T2J_BLOCK), 0, s, P);
 }
 
 void launch_t2j_list(uint32_t blocks, hipStream_t s, const T2JParams &P)
 {
-    hipLaunchKernelGGL(t2j_kernel<1>, dim3(blocks), dim3(T2J_BLOCK), 0, s, P);
+    if (t2j_go(P)) hipLaunchKernelGGL((t2j_kernel<1, true>), dim3(blocks), dim3(T2J_BLOCK), 0, s, P);
+    else hipLaunchKernelGGL((t2j_kernel<1, false>), dim3(blocks), dim3(T2J_BLOCK), 0, s, P);
 }
 
 void launch_t2j_wave(uint32_t blocks, hipStream_t s, const T2JParams &P, const T2WParams &W)
@@ -154,6 +166,7 @@ uint64_t t2j_wave_ws_bytes(uint32_t blocks) { return (uint64_t)blocks * T2W_WAVE
 
 void launch_t2j_deep(hipStream_t s, const T2JParams &P)
 {
-    hipLaunchKernelGGL(t2j_deep_kernel, dim3(T2J_DEEP_BLOCKS), dim3(T2J_BLOCK), 0, s, P);
+    if (t2j_go(P)) hipLaunchKernelGGL(t2j_deep_kernel<true>, dim3(T2J_DEEP_BLOCKS), dim3(T2J_BLOCK), 0, s, P);
+    else hipLaunchKernelGGL(t2j_deep_kernel<false>, dim3(T2J_DEEP_BLOCKS), dim3(T2J_BLOCK), 0, s, P);
 }
 }  // namespace dg

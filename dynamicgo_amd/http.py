@@ -51,8 +51,16 @@ class ConvError(Exception):
 
 
 # ---------------------------------------------------------------- requests
+_TOKEN = frozenset(b"!#$%&'*+-.^_`|~0123456789abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ")
+
+
 def _canon_header(k: str) -> str:
-    """textproto.CanonicalMIMEHeaderKey."""
+    """textproto.CanonicalMIMEHeaderKey: unchanged when a byte is not a token
+    byte (validHeaderFieldByte), else upper case at the start and after each
+    '-', lower case elsewhere."""
+    b = k.encode("utf-8", "surrogateescape")
+    if any(c not in _TOKEN for c in b):
+        return k
     return "-".join(p[:1].upper() + p[1:].lower() for p in k.split("-"))
 
 
@@ -194,6 +202,105 @@ class HTTPRequest:
 
     def get_body(self) -> bytes:
         return self.body
+
+
+# ---------------------------------------------------------------- responses
+def _sanitize_cookie_value(v: bytes) -> bytes:
+    """net/http sanitizeCookieValue: bytes outside 0x20-0x7e, '"', ';' and
+    '\\' dropped; quoted when it holds ' ' or ','."""
+    v = bytes(c for c in v if 0x20 <= c < 0x7F and c not in b'";\\')
+    if v and (b" " in v or b"," in v):
+        return b'"' + v + b'"'
+    return v
+
+
+def cookie_string(name: str, value: bytes) -> str:
+    """(&http.Cookie{Name, Value}).String() (net/http/cookie.go): "" for an
+    invalid name (empty or a non-token rune), else name=sanitized value."""
+    nb = name.encode("utf-8", "surrogateescape")
+    if not nb or any(c not in _TOKEN for c in nb):
+        return ""
+    return name + "=" + _sanitize_cookie_value(value).decode("latin-1")
+
+
+class HTTPResponse:
+    """http.HTTPResponse (http/http.go:304-346), the ResponseSetter t2j's
+    HTTP mapping writes: status code, headers (Set-Cookie lines for cookies),
+    raw body. Values are Go strings: bytes, kept as str by surrogateescape."""
+
+    def __init__(self):
+        self.status_code = 0
+        self.headers: Dict[str, List[str]] = {}
+        self.body: Optional[bytes] = None
+
+    def set_status_code(self, code: int):
+        self.status_code = code
+
+    def set_header(self, key: str, val: str):
+        self.headers[_canon_header(key)] = [val]  # Header.Set
+
+    def set_cookie(self, key: str, val: str):
+        self.headers.setdefault("Set-Cookie", []).append(
+            cookie_string(key, val.encode("utf-8", "surrogateescape")))
+
+    def set_raw_body(self, body: bytes):
+        self.body = bytes(body)
+
+    def get_header(self, key: str) -> str:
+        """Header.Get"""
+        v = self.headers.get(_canon_header(key))
+        return v[0] if v else ""
+
+    def cookies(self) -> List[Tuple[str, str]]:
+        """Response.Cookies() for the lines set_cookie writes: (name, value)
+        with the quotes of a quoted value removed (readSetCookies)."""
+        out = []
+        for line in self.headers.get("Set-Cookie", ()):
+            k, eq, v = line.partition("=")
+            if not eq or not k:
+                continue
+            if len(v) > 1 and v[0] == '"' and v[-1] == '"':
+                v = v[1:-1]
+            out.append((k, v))
+        return out
+
+
+def _parse_atoi(s: str) -> int:
+    """strconv.Atoi (base 10, int64 range)."""
+    if not re.fullmatch(r"[+-]?[0-9]+", s):
+        raise ValueError('strconv.Atoi: parsing %r: invalid syntax' % s)
+    v = int(s)
+    if not -(1 << 63) <= v < (1 << 63):
+        raise ValueError('strconv.Atoi: parsing %r: value out of range' % s)
+    return v
+
+
+def mapping_response(kind: str, value: str, resp, field: T.FieldDescriptor, val: bytes) -> Optional[Exception]:
+    """HttpMapping.Response (thrift/annotation/http_mapping.go:119-351): None
+    when the value was set, else the error the Go method returns. resp None
+    is a nil ResponseSetter (handleUnsets below the root): the Go methods that
+    touch it panic there, raised here as an error whatever the options."""
+    sval = bytes(val).decode("utf-8", "surrogateescape")
+    if kind in ("api.header", "api.cookie", "api.raw_body", "api.http_code") and resp is None:
+        raise ConvError("ErrConvert", "nil ResponseSetter (%s): the reference panics here" % kind)
+    if kind == "api.header":
+        resp.set_header(value, sval)
+    elif kind == "api.cookie":
+        resp.set_cookie(value, sval)
+    elif kind == "api.raw_body":
+        resp.set_raw_body(bytes(val))
+    elif kind == "api.http_code":
+        try:
+            resp.set_status_code(_parse_atoi(sval))
+        except ValueError as e:
+            return e
+    elif kind == "api.raw_uri":
+        return None
+    else:  # query, path, body, form, no_body_struct: errNotImplemented (register.go:74-76)
+        name = {"api.query": "apiQuery", "api.path": "apiPath", "api.body": "apiBody", "api.form": "apiPostForm",
+                "api.no_body_struct": "apiNoBodyStruct"}.get(kind, kind)
+        return ConvError("ErrUnsupportedType", "%s not support http response!" % name)
+    return None
 
 
 # ---------------------------------------------------------------- annotations

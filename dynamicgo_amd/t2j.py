@@ -15,18 +15,26 @@ The Go-side options are split between the device and this host part:
   * EnableThriftBase with a context BaseResp (readResponseBase,
     impl.go:54-72): the device skips the root's response-base field and
     reports its span; here the BaseResp is FastRead from those bytes;
-  * EnableHttpMapping (writeHttpValue, impl.go:515-588): the mapped fields'
-    values go to the http.ResponseSetter, see do_batch.
+  * EnableHttpMapping (writeHttpValue, impl.go:515-588; handleUnsets
+    :401-429): the device stops a message at each writeHttpValue call
+    (DG_T2J_E_CALLBACK, the field and the value's position); here the call
+    runs -- the value read by the mapping's encoding (Thrift bytes, text,
+    the kitex string, or its JSON, which the device converts when asked) and
+    HttpMapping.Response on the http.ResponseSetter -- and the message is
+    converted again with the answer (taken / write to the JSON as well).
 """
 from __future__ import annotations
 
 import ctypes as C
+import math
 import struct as _st
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
 from . import _lib
+from . import http as H
+from . import thrift as T
 from .conv import Context, Options, default_context
 from .thrift import FlatDescriptor, flatten
 
@@ -42,9 +50,10 @@ T2J_WRITE_OPTIONAL = 1 << 7
 T2J_ENABLE_VM = 1 << 8
 T2J_CONVERT_EXC = 1 << 9
 T2J_SKIP_RESP_BASE = 1 << 10
+T2J_HM = 1 << 11
 
 (E_READ, E_UNKNOWN_FIELD, E_DISMATCH_TYPE, E_UNSUPPORTED, E_NAN_INF, E_MISS_REQUIRED, E_NEEDS_HOST, E_DEPTH, E_WRITE,
- E_CONVERT, E_EXCEPTION) = range(1, 12)
+ E_CONVERT, E_EXCEPTION, E_CALLBACK) = range(1, 13)
 
 # the meta.ErrCode behaviour the reference wraps each failure in
 # (conv/t2j/impl.go: wrapError call sites; meta/error.go)
@@ -58,10 +67,11 @@ _READ_REASON = {1: "EOF", 2: "invalid data type", 3: "invalid data length", 4: "
 
 def to_t2j_opts(o: Options, base: bool = False) -> int:
     """The conv.Options fields conv/t2j/impl.go reads, as DG_T2J_* bits;
-    base: a BaseResp is in the context (EnableThriftBase skips the field)."""
-    if o.EnableHttpMapping:
-        raise ValueError("EnableHttpMapping: use BinaryConv.do_batch_http (the ResponseSetter callbacks)")
+    base: a BaseResp is in the context (EnableThriftBase skips the field).
+    EnableHttpMapping needs a ResponseSetter (Do, conv/t2j/conv.go:53-65)."""
     f = 0
+    if o.EnableHttpMapping:
+        f |= T2J_HM
     if o.ConvertException:
         f |= T2J_CONVERT_EXC
     if o.EnableThriftBase and base:
@@ -234,6 +244,299 @@ class BaseResp:
                 p = _skip(b, p, t)
 
 
+# ------------------------------------------------------------ writeHttpValue
+def f64toa(v: float) -> str:
+    """json.EncodeFloat64 (internal/json/encoding.go:78, native f64toa
+    native/fastfloat.c:349-404): integers below 2^53 in full, else the
+    shortest round-trip digits as a decimal, or d.ddde[+-]x when the decimal
+    exponent is < -6 or > 20; nothing for NaN and Inf."""
+    if math.isnan(v) or math.isinf(v):
+        return ""
+    sign = "-" if math.copysign(1.0, v) < 0 else ""
+    a = abs(v)
+    if a == 0:
+        return sign + "0"
+    if a.is_integer() and a < 2.0 ** 53:
+        return sign + str(int(a))
+    mant, _, e = repr(a).partition("e")
+    ip, _, fp = mant.partition(".")
+    raw = (ip + fp).lstrip("0")
+    digs = raw.rstrip("0")
+    exp = (int(e) if e else 0) - len(fp) + (len(raw) - len(digs))
+    nd = len(digs)
+    dot = nd + exp
+    if dot - 1 < -6 or dot - 1 > 20:
+        x = dot - 1
+        out = digs[0] + ("." + digs[1:] if nd > 1 else "") + "e" + ("-" if x < 0 else "+") + str(abs(x))
+    elif dot <= 0:
+        out = "0." + "0" * (-dot) + digs
+    elif nd > dot:
+        out = digs[:dot] + "." + digs[dot:]
+    else:
+        out = digs + "0" * (dot - nd)
+    return sign + out
+
+
+def _go_g(v: float) -> str:
+    """strconv.FormatFloat(v, 'g', -1, 64), what fmt's %v prints."""
+    if math.isnan(v):
+        return "NaN"
+    if math.isinf(v):
+        return "+Inf" if v > 0 else "-Inf"
+    if v == 0:
+        return "-0" if math.copysign(1.0, v) < 0 else "0"
+    mant, _, e = repr(abs(v)).partition("e")
+    ip, _, fp = mant.partition(".")
+    raw = (ip + fp).lstrip("0")
+    digs = raw.rstrip("0") or "0"
+    exp = (int(e) if e else 0) - len(fp) + (len(raw) - len(digs))
+    x = len(digs) + exp - 1  # decimal exponent of the first digit
+    sign = "-" if v < 0 else ""
+    # shortest 'g': %e when x < -4 or x >= eprec, eprec = 6 (strconv/ftoa.go)
+    if x < -4 or x >= 6:
+        m = digs[0] + ("." + digs[1:] if len(digs) > 1 else "")
+        return sign + m + "e" + ("-" if x < 0 else "+") + ("%02d" % abs(x))
+    dot = x + 1
+    if dot <= 0:
+        return sign + "0." + "0" * (-dot) + digs
+    if len(digs) > dot:
+        return sign + digs[:dot] + "." + digs[dot:]
+    return sign + digs + "0" * (dot - len(digs))
+
+
+def _go_f(v: float) -> str:
+    """strconv.FormatFloat(v, 'f', -1, 64)."""
+    if math.isnan(v):
+        return "NaN"
+    if math.isinf(v):
+        return "+Inf" if v > 0 else "-Inf"
+    if v == 0:
+        return "-0" if math.copysign(1.0, v) < 0 else "0"
+    mant, _, e = repr(abs(v)).partition("e")
+    ip, _, fp = mant.partition(".")
+    raw = (ip + fp).lstrip("0")
+    digs = raw.rstrip("0")
+    exp = (int(e) if e else 0) - len(fp) + (len(raw) - len(digs))
+    dot = len(digs) + exp
+    sign = "-" if v < 0 else ""
+    if dot <= 0:
+        return sign + "0." + "0" * (-dot) + digs
+    if len(digs) > dot:
+        return sign + digs[:dot] + "." + digs[dot:]
+    return sign + digs + "0" * (dot - len(digs))
+
+
+class _Rd:
+    """BinaryProtocol's reads over one buffer (thrift/binary.go:688-817)."""
+
+    def __init__(self, b: bytes, p: int):
+        self.b, self.p = b, p
+
+    def next(self, k: int) -> bytes:
+        if self.p + k > len(self.b):
+            raise ThriftReadError("EOF")
+        v = self.b[self.p:self.p + k]
+        self.p += k
+        return v
+
+    def u8(self) -> int:
+        return self.next(1)[0]
+
+    def be(self, k: int, signed: bool = True) -> int:
+        return int.from_bytes(self.next(k), "big", signed=signed)
+
+    def string(self) -> bytes:
+        n = self.be(4)
+        if n < 0 or n > len(self.b) - self.p:
+            raise ThriftReadError("invalid data length")
+        return self.next(n)
+
+
+def _encode_text(t: T.TypeDescriptor, rd: _Rd, o: Options) -> bytes:
+    """ReadStringWithDesc = EncodeText(asJson false), the scalar cases
+    (thrift/binary.go:834-905): the text of a non-complex value. A BYTE reads
+    as Go's byte, so both ByteAsUint8 branches print it unsigned."""
+    tt = t.type
+    if tt == T.BOOL:
+        return b"true" if rd.u8() == 1 else b"false"
+    if tt == T.BYTE:
+        return str(rd.u8()).encode()
+    if tt in (T.I16, T.I32, T.I64):
+        return str(rd.be({T.I16: 2, T.I32: 4, T.I64: 8}[tt])).encode()
+    if tt == T.DOUBLE:
+        return f64toa(_st.unpack(">d", rd.next(8))[0]).encode()
+    if tt == T.STRING:
+        v = rd.string()
+        if not o.NoBase64Binary and t.is_binary():
+            import base64
+            return base64.b64encode(v)
+        return bytes(v)
+    raise H.ConvError("ErrUnsupportedType", "text encoding of type %d (no registered mapping reads it)" % tt)
+
+
+def _read_any(t: T.TypeDescriptor, rd: _Rd, o: Options):
+    """ReadAnyWithDesc (thrift/binary.go:1008-1166) into tagged Python values
+    for the kitex string: ("i", int), ("f", float), ("b", bool), ("s",
+    bytes), ("y", bytes) for binary, ("l", [...]), ("m", [(k, v)...])."""
+    tt = t.type
+    if tt == T.BOOL:
+        return ("b", rd.u8() == 1)
+    if tt == T.BYTE:
+        v = rd.u8()
+        return ("i", v if o.ByteAsUint8 else (v - 256 if v > 127 else v))
+    if tt in (T.I16, T.I32, T.I64):
+        return ("i", rd.be({T.I16: 2, T.I32: 4, T.I64: 8}[tt]))
+    if tt == T.DOUBLE:
+        return ("f", _st.unpack(">d", rd.next(8))[0])
+    if tt == T.STRING:
+        return ("y" if t.is_binary() else "s", bytes(rd.string()))
+    if tt in (T.LIST, T.SET):
+        et, n = rd.u8(), rd.be(4)
+        if et != t.elem.type:
+            raise H.ConvError("ErrConvert", "dismatched primitive types")
+        return ("l", [_read_any(t.elem, rd, o) for _ in range(max(n, 0))])
+    if tt == T.MAP:
+        kt, vt, n = rd.u8(), rd.u8(), rd.be(4)
+        if vt != t.elem.type or kt != t.key.type:
+            raise H.ConvError("ErrConvert", "dismatched primitive types")
+        if kt not in (T.STRING, T.BYTE, T.I16, T.I32, T.I64, T.BOOL, T.DOUBLE):
+            raise H.ConvError("ErrUnsupportedType", "kitex string of a map keyed by pointers (unordered in Go)")
+        m = {}
+        for _ in range(max(n, 0)):
+            if kt == T.STRING:
+                k = ("s", bytes(rd.string()))
+            elif kt in (T.BYTE, T.I16, T.I32, T.I64):  # ReadInt: signed
+                k = ("i", rd.be({T.BYTE: 1, T.I16: 2, T.I32: 4, T.I64: 8}[kt]))
+            else:
+                k = _read_any(t.key, rd, o)
+            m[k] = _read_any(t.elem, rd, o)  # a repeated key: the last value
+        return ("m", list(m.items()))
+    if tt == T.STRUCT:
+        m = {}
+        while True:
+            ft = rd.u8()
+            if ft == 0:
+                return ("m", list(m.items()))
+            fid = rd.be(2)
+            f = t.struct.field_by_id(fid)
+            if f is None:
+                if o.DisallowUnknownField:
+                    raise H.ConvError("ErrUnknownField", "unknown field %d" % fid)
+                rd.p = _skip(rd.b, rd.p, ft)
+                continue
+            m[("s", f.alias.encode())] = _read_any(f.type, rd, o)
+    raise H.ConvError("ErrUnsupportedType", "unsupported type %d" % tt)
+
+
+def _go_v(x) -> bytes:
+    """fmt's %v of what ReadAnyWithDesc returns (maps printed key-sorted)."""
+    k, v = x
+    if k == "i":
+        return str(v).encode()
+    if k == "f":
+        return _go_g(v).encode()
+    if k == "b":
+        return b"true" if v else b"false"
+    if k == "s":
+        return v
+    if k == "y":
+        return b"[" + b" ".join(str(c).encode() for c in v) + b"]"
+    if k == "l":
+        return b"[" + b" ".join(_go_v(e) for e in v) + b"]"
+    items = sorted(v, key=lambda kv: (kv[0][1] if kv[0][0] != "b" else int(kv[0][1])))
+    return b"map[" + b" ".join(_go_v(a) + b":" + _go_v(b) for a, b in items) + b"]"
+
+
+def _kitex_to_string(x) -> bytes:
+    """primitive.KitexToString (internal/primitive/impl.go:191-215)."""
+    k, v = x
+    if k == "f":
+        return _go_f(v).encode()
+    if k == "l":
+        return b",".join(_kitex_to_string(e) for e in v)
+    return _go_v(x)
+
+
+def _is_complex(t: T.TypeDescriptor) -> bool:
+    return t.type in (T.STRUCT, T.MAP, T.LIST, T.SET)
+
+
+def _needs_json(field: T.FieldDescriptor, o: Options) -> bool:
+    """Whether writeHttpValue reads the value as JSON (doRecurse, impl.go:
+    561-574) for one of the field's mappings."""
+    return _is_complex(field.type) and not o.UseKitexHttpEncoding and \
+        any(H.mapping_encoding(k) == H.ENCODING_JSON for k, _ in field.http_mappings)
+
+
+def _empty_json(t: T.TypeDescriptor, b: bytes, o: Options) -> bytes:
+    """doRecurse of a handleUnsets default (WriteDefaultOrEmpty bytes) of a
+    container type: empty containers only; other constants are not
+    restated here (parity unpinned)."""
+    if t.type in (T.LIST, T.SET) and b[1:5] == b"\0\0\0\0":
+        return b"[]"
+    if t.type == T.MAP and b[2:6] == b"\0\0\0\0":
+        return b"{}"
+    if t.type == T.STRUCT and b == b"\0":
+        for f in sorted(t.struct.fields, key=lambda f: f.id):
+            if t.struct.requires.get(f.id, False) or f.default_value is not None or \
+                    o.WriteDefaultField or o.WriteOptionalField:
+                raise H.ConvError("ErrUnsupportedType", "JSON of an unset mapped struct with fields to write "
+                                  "(not restated; parity unpinned)")
+        return b"{}"
+    raise H.ConvError("ErrUnsupportedType", "JSON of a container constant for an unset mapped field "
+                      "(not restated; parity unpinned)")
+
+
+def write_http_value(o: Options, resp, field: T.FieldDescriptor, buf: bytes, p: int,
+                     json_val: Optional[bytes]) -> Tuple[bool, int]:
+    """writeHttpValue (conv/t2j/impl.go:515-588) with the value at buf[p:]:
+    (ok, the position after what it read). json_val: the value's JSON when
+    _needs_json (the device's conversion, or _empty_json's). Raises the error
+    the reference returns (read failures, a Response error unless
+    OmitHttpMappingErrors)."""
+    thrift_val = text_val = None
+    rd = _Rd(buf, p)
+    ok = False
+    for kind, value in field.http_mappings:
+        enc = H.mapping_encoding(kind)
+        if enc == H.ENCODING_THRIFT_BINARY:
+            if thrift_val is None:
+                s0 = rd.p
+                try:
+                    rd.p = _skip(rd.b, rd.p, field.type.type, 1023)
+                except ThriftReadError as e:
+                    raise H.ConvError("ErrRead", "", e)
+                thrift_val = bytes(rd.b[s0:rd.p])
+            val = thrift_val
+        elif enc == H.ENCODING_TEXT or not _is_complex(field.type):
+            if text_val is None:
+                try:
+                    text_val = _encode_text(field.type, rd, o)
+                except ThriftReadError as e:
+                    raise H.ConvError("ErrRead", "reading thrift value of '%s' failed, thrift pos:%d" %
+                                      (field.name, rd.p), e)
+            val = text_val
+        elif o.UseKitexHttpEncoding:
+            if text_val is None:
+                try:
+                    text_val = _kitex_to_string(_read_any(field.type, rd, o))
+                except ThriftReadError as e:
+                    raise H.ConvError("ErrRead", "reading thrift value of '%s' failed, thrift pos:%d" %
+                                      (field.name, rd.p), e)
+            val = text_val
+        else:  # EncodingJSON
+            if json_val is None:
+                raise H.ConvError("ErrUnsupportedType", "JSON value of '%s' read twice (not restated)" % field.name)
+            val = json_val
+        err = H.mapping_response(kind, value, resp, field, val)
+        if err is None:
+            ok = True
+            break
+        if not o.OmitHttpMappingErrors:
+            raise err
+    return ok, rd.p
+
+
 class BinaryConv:
     """t2j.BinaryConv (conv/t2j/conv.go:30-95) on the MI355X."""
 
@@ -284,13 +587,47 @@ class BinaryConv:
 
     def do_batch_errors(self, desc, msgs: Sequence[bytes], resps=None, bases=None):
         """Do over a batch with the context's objects per message: (outputs,
-        errors) with errors[i] None, T2JError, T2JException or
-        ThriftReadError."""
+        errors) with errors[i] None, T2JError, T2JException, ThriftReadError
+        or http.ConvError (the HTTP mapping's Go-side errors). resps: each
+        message's http.ResponseSetter (EnableHttpMapping needs one, Do
+        conv/t2j/conv.go:53-65); bases: its BaseResp (EnableThriftBase)."""
         n = len(msgs)
+        resps = list(resps) if resps is not None else [None] * n
         bases = list(bases) if bases is not None else [None] * n
-        outs, rets, aux = self._batch(desc, msgs, with_base=any(b is not None for b in bases))
+        hm = bool(self.opts.EnableHttpMapping)
         errs: List[Optional[Exception]] = [None] * n
+        outs: List[bytes] = [b""] * n
+        rets = np.zeros(max(n, 1), dtype=np.uint64)
+        aux: List[Optional[int]] = [None] * n
+        pending = []
         for i in range(n):
+            if hm and resps[i] is None:
+                errs[i] = H.ConvError("ErrInvalidParam", "no http response in context")
+            else:
+                pending.append(i)
+        answers = {i: bytearray() for i in pending} if hm else None
+        with_base = any(b is not None for b in bases)
+        flat = self._flat(desc) if hm else None
+        while pending:
+            o, r, a = self._batch(desc, [msgs[i] for i in pending], with_base,
+                                  [answers[i] for i in pending] if hm else None)
+            nxt = []
+            for k, i in enumerate(pending):
+                rr = int(r[k])
+                if hm and (rr & 0xFF) == E_CALLBACK:
+                    try:
+                        self._serve(flat, msgs[i], resps[i], answers[i], o[k])
+                        nxt.append(i)
+                    except (H.ConvError, ValueError, ThriftReadError) as e:
+                        errs[i] = e
+                    continue
+                outs[i], rets[i] = o[k], rr
+                aux[i] = int(a[k]) if a is not None else None
+            pending = nxt
+        for i in range(n):
+            if errs[i] is not None:
+                outs[i] = b""
+                continue
             r = int(rets[i])
             if (r & 0xFF) == E_EXCEPTION:
                 errs[i], outs[i] = T2JException(outs[i]), b""
@@ -298,20 +635,57 @@ class BinaryConv:
             if r != 0:
                 errs[i] = T2JError(r)
                 continue
-            if bases[i] is not None and aux is not None and int(aux[i]) != 2**64 - 1:
-                lo, hi = int(aux[i]) & 0xFFFFFFFF, int(aux[i]) >> 32
+            if bases[i] is not None and aux[i] is not None and aux[i] != 2**64 - 1:
+                lo, hi = aux[i] & 0xFFFFFFFF, aux[i] >> 32
                 try:
                     bases[i].fast_read(bytes(msgs[i][lo:hi]))  # readResponseBase's FastRead
                 except ThriftReadError as e:
                     errs[i], outs[i] = e, b""
         return outs, errs
 
+    def _serve(self, flat: FlatDescriptor, msg: bytes, resp, answers: bytearray, rec: bytes):
+        """One writeHttpValue call the device stopped at (DG_T2J_E_CALLBACK,
+        include/dgj2t_defs.h): run it and record the answer for the rerun."""
+        w0, w1 = _st.unpack_from("<QQ", rec, len(rec) - 16)
+        payload = bytes(rec[:-16])
+        kind, has_resp, idx, fi = w0 & 0xFF, (w0 >> 8) & 1, (w0 >> 16) & 0xFFFF, w0 >> 32
+        s0 = w1 & 0xFFFFFFFF
+        field = flat.fields[fi]
+        o = self.opts
+        if kind == 1:  # a mapped field's value (impl.go:132-142, 296-306)
+            done = idx < len(answers) and answers[idx] == 2
+            if not done:
+                if idx != len(answers):
+                    raise H.ConvError("ErrConvert", "callback %d out of order (%d answers)" % (idx, len(answers)))
+                if _needs_json(field, o):
+                    answers.append(2)  # the device converts the value first
+                    return
+            try:
+                ok, _ = write_http_value(o, resp, field, msg, s0, payload if done else None)
+            except H.ConvError as e:
+                raise H.ConvError(e.behavior, "mapping field %s failed: %s" % (field.name, e))
+            except ValueError as e:  # a Response's plain error: unwrapError -> ErrConvert
+                raise H.ConvError("ErrConvert", "mapping field %s failed" % field.name, e)
+            del answers[idx:]
+            answers.append(1 if (o.WriteHttpValueFallback and not ok) else 0)
+            return
+        # kind 2: handleUnsets (impl.go:401-429), the default or empty value
+        if idx != len(answers):
+            raise H.ConvError("ErrConvert", "callback %d out of order (%d answers)" % (idx, len(answers)))
+        dflt = H.write_default_or_empty(field)
+        jv = _empty_json(field.type, dflt, o) if _needs_json(field, o) else None
+        ok, _ = write_http_value(o, resp if has_resp else None, field, dflt, 0, jv)
+        answers.append(0 if ok else 1)
+
     def do_batch(self, desc, msgs: Sequence[bytes]) -> Tuple[List[bytes], np.ndarray]:
-        """Batch of independent Thrift messages -> (JSON outputs, statuses)."""
+        """Batch of independent Thrift messages -> (JSON outputs, statuses).
+        EnableHttpMapping needs the ResponseSetters: do_batch_errors."""
+        if self.opts.EnableHttpMapping:
+            raise ValueError("EnableHttpMapping: use do_batch_errors with the ResponseSetters")
         outs, rets, _ = self._batch(desc, msgs)
         return outs, rets
 
-    def _batch(self, desc, msgs: Sequence[bytes], with_base: bool = False):
+    def _batch(self, desc, msgs: Sequence[bytes], with_base: bool = False, answers=None):
         opts = to_t2j_opts(self.opts, with_base)
         flat = self._flat(desc)
         ctx = self._ctx()
@@ -328,10 +702,20 @@ class BinaryConv:
         L = _lib.lib()
         d = ctx.desc_t2j(flat)
         aux = np.zeros(max(n, 1), dtype=np.uint64) if opts & T2J_SKIP_RESP_BASE else None
+        cb = None
+        if answers is not None:
+            tab = (_lib.VMEntry * max(n, 1))()
+            blob = bytearray()
+            for k, a in enumerate(answers):
+                tab[k].off, tab[k].count = len(blob), len(a)
+                blob += a
+            ab = np.frombuffer(bytes(blob) + b"\0" * 8, dtype=np.uint8)
+            cb = _lib.CBTables(None, 0, C.cast(tab, C.c_void_p), ab.ctypes.data, len(blob))
         for _ in range(2):
-            rc = L.dg_t2j_batch_host_aux(ctx.h, d, flat.root_type, arena.ctypes.data, in_off.ctypes.data, n, opts,
-                                         out.ctypes.data, cap, out_off.ctypes.data, rets.ctypes.data,
-                                         C.byref(need), aux.ctypes.data if aux is not None else None)
+            rc = L.dg_t2j_batch_host_cb(ctx.h, d, flat.root_type, arena.ctypes.data, in_off.ctypes.data, n, opts,
+                                        out.ctypes.data, cap, out_off.ctypes.data, rets.ctypes.data,
+                                        C.byref(need), aux.ctypes.data if aux is not None else None,
+                                        C.byref(cb) if cb is not None else None)
             if rc == -3 and need.value > cap:
                 cap = int(need.value) + 64
                 out = np.zeros(cap, dtype=np.uint8)
@@ -347,6 +731,8 @@ class BinaryConv:
         ret int64[n]. Asynchronous on `stream` (default: torch's current
         stream). Statuses DG_ST_OUT_OVERFLOW (0xF0) leave out_len = the bytes
         the message needs."""
+        if self.opts.EnableHttpMapping:
+            raise ValueError("EnableHttpMapping: use do_batch_errors with the ResponseSetters")
         opts = to_t2j_opts(self.opts)
         flat = self._flat(desc)
         ctx = self._ctx()

@@ -366,6 +366,21 @@ int dg_t2j_batch_device_aux(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type
 int dg_t2j_batch_host_aux(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, const uint8_t *thrift,
                           const uint64_t *in_off, uint64_t n, uint64_t opts, uint8_t *out, uint64_t out_cap,
                           uint64_t *out_off, uint64_t *ret, uint64_t *out_need, uint64_t *aux);
+/* ... and EnableHttpMapping's response side (DG_T2J_HM; conv/t2j/impl.go:
+ * 132-142, 296-306, writeHttpValue 515-588; HandleRequires' mapped unsets):
+ * a mapped field of the root struct or of a struct that is a root field's
+ * value stops the message with DG_T2J_E_CALLBACK and a 16-byte record in out
+ * (dgj2t_defs.h). The host runs writeHttpValue (dynamicgo_amd/t2j.py) and
+ * converts the message again with its answers: ans_tab (n entries, device
+ * resp. host memory) indexes one byte per answer in the answer bytes, consumed
+ * in the order the stops come. cb: only ans_tab, bytes and len are read. */
+int dg_t2j_batch_device_cb(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, const uint8_t *d_thrift,
+                           const uint64_t *d_in_off, uint64_t n, uint64_t opts, uint8_t *d_out,
+                           const uint64_t *d_out_off, uint32_t *d_out_len, uint64_t *d_ret, uint64_t *d_aux,
+                           const dg_cb_entry *d_ans, const uint8_t *d_ans_bytes, void *stream, uint64_t max_len);
+int dg_t2j_batch_host_cb(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, const uint8_t *thrift,
+                         const uint64_t *in_off, uint64_t n, uint64_t opts, uint8_t *out, uint64_t out_cap,
+                         uint64_t *out_off, uint64_t *ret, uint64_t *out_need, uint64_t *aux, const dg_cb_tables *cb);
 
 /* Timing helper for benchmarks: launch the device batch `iters` times on the
  * context stream bracketed by HIP events; returns total milliseconds of GPU

@@ -125,6 +125,9 @@ typedef struct dg_cb_tables {
                                                 ends the conversion (conv/t2j/impl.go:154-159,173-187): status
                                                 DG_T2J_E_EXCEPTION, out = that field's value JSON (then any unset
                                                 fields written by handleUnsets) */
+#define DG_T2J_HM (1ull << 11)               /* EnableHttpMapping (writeHttpValue, conv/t2j/impl.go:515-588): mapped
+                                                fields of the root struct and of its fields' struct values stop for
+                                                the host (DG_T2J_E_CALLBACK) */
 #define DG_T2J_SKIP_RESP_BASE (1ull << 10)   /* EnableThriftBase with a context BaseResp (readResponseBase,
                                                 conv/t2j/impl.go:54-72,120-128): the ROOT's response-base fields
                                                 (DG_FF_RESPONSE_BASE) are skipped as STRUCTs, no key written; the
@@ -146,6 +149,15 @@ typedef struct dg_cb_tables {
 #define DG_T2J_E_WRITE 9          /* ErrWrite: a truncated BYTE/I16/I32/I64/DOUBLE value (doRecurse wraps those reads
                                      as meta.ErrWrite, conv/t2j/impl.go:200-236); value = RD_EOF (1) */
 #define DG_T2J_E_EXCEPTION 11     /* DG_T2J_CONVERT_EXC: the exception field's JSON is the output (Go: errors.New(out)) */
+#define DG_T2J_E_CALLBACK 12      /* DG_T2J_HM: a writeHttpValue call for the host. out: the payload (the JSON
+                                     of a mapped container value, else empty), then a 16-byte trailer of two
+                                     little-endian u64: kind (1 a mapped field's value, 2 an unset mapped
+                                     field HandleRequires writes) | has-ResponseSetter << 8 | the call's
+                                     index << 16 | the field's descriptor index << 32, and the value's start
+                                     | its end << 32 (kind 1). The host answers each call (dg_cb_tables
+                                     ans_tab, one byte per call in call order: 0 = the response took it, 1 =
+                                     write it to the JSON as well, 2 = open: the calls converting its value
+                                     follow) and converts the message again. */
 #define DG_T2J_E_CONVERT 10       /* ErrConvert: a map key failed (buildinTypeToKey, wrapped as meta.ErrConvert by
                                      conv/t2j/impl.go:355-358): value = the read reason (RD_*), or 0x100 | type for
                                      a key type it does not support */

@@ -278,6 +278,29 @@ class RefT2J:
             cap = ol.value + 64
         raise RuntimeError("t2j oracle output did not fit")
 
+    def t2j3(self, flat, side: bytes, thrift: bytes, opts: int, answers: bytes = b"", root: Optional[int] = None):
+        """t2j2 with the host's writeHttpValue answers (DG_T2J_HM, one byte
+        per call): (status, JSON or a stop's record, base span)."""
+        f = self.lib.dgref_t2j3
+        f.restype = C.c_uint64
+        f.argtypes = [C.c_char_p, C.c_char_p, C.c_uint32, C.c_char_p, C.c_size_t, C.c_uint64,
+                      C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t), C.POINTER(C.c_uint64), C.c_char_p,
+                      C.c_uint32]
+        root = flat.root_type if root is None else root
+        cap = 8 * len(thrift) + 4096
+        aux = C.c_uint64(0)
+        for _ in range(2):
+            out = C.create_string_buffer(cap)
+            ol = C.c_size_t(0)
+            ret = int(f(flat.blob, side, root, thrift, len(thrift), opts, out, cap, C.byref(ol), C.byref(aux),
+                        bytes(answers), len(answers)))
+            if ret != 0 and (ret & 0xFF) not in (11, 12):
+                return ret, b"", int(aux.value)
+            if ol.value <= cap:
+                return ret, out.raw[:ol.value], int(aux.value)
+            cap = ol.value + 64
+        raise RuntimeError("t2j oracle output did not fit")
+
 
     def t2j_timed(self, flat, side: bytes, arena: np.ndarray, in_off: np.ndarray, opts: int, cpus: Sequence[int],
                   reps: int, root: Optional[int] = None) -> float:

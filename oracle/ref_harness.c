@@ -748,6 +748,11 @@ typedef struct {
     const char *XP; /* side-table pool */
     uint64_t opts;
     uint64_t *aux; /* DG_T2J_SKIP_RESP_BASE: the base field's span (lo | hi << 32) */
+    /* DG_T2J_HM: the host's answers to writeHttpValue calls, in call order
+     * (0 taken, 1 write to the JSON too, 2 open), and the calls so far */
+    const uint8_t *ans;
+    uint32_t n_ans;
+    uint32_t *seen;
 } T2J;
 
 #define T2J_ERR(code, pos, val) ((uint64_t)(code) | ((uint64_t)(pos) << 8) | ((uint64_t)(val) << 40))
@@ -918,7 +923,19 @@ static int32_t t2j_field_by_id(const T2J *c, const dg_struct *sd, uint16_t id)
     return -1;
 }
 
-static uint64_t t2j_value(const T2J *c, uint32_t td, TRd *r, JBuf *o);
+static uint64_t t2j_value_r(const T2J *c, uint32_t td, TRd *r, JBuf *o, int resp);
+static uint64_t t2j_value(const T2J *c, uint32_t td, TRd *r, JBuf *o) { return t2j_value_r(c, td, r, o, 0); }
+
+/* a writeHttpValue call the host must make (DG_T2J_E_CALLBACK): the record
+ * after the payload already in o, as include/dgj2t_defs.h lays it out */
+static uint64_t t2j_stop(TRd *r, JBuf *o, uint32_t kind, uint32_t idx, uint32_t fi, size_t s0, size_t s1)
+{
+    if (idx > 0xFFFF) return T2J_ERR(DG_T2J_E_DEPTH, r->p, idx);
+    uint64_t w[2] = {(uint64_t)kind | ((uint64_t)idx << 16) | ((uint64_t)fi << 32),
+                     (uint64_t)(uint32_t)s0 | ((uint64_t)(uint32_t)s1 << 32)};
+    jb_put(o, w, 16);
+    return T2J_ERR(DG_T2J_E_CALLBACK, r->p, kind & 0xFF);
+}
 
 /* writeDefaultOrEmpty (conv/t2j/impl.go:440-468) */
 static uint64_t t2j_default_or_empty(const T2J *c, const dg_field *f, size_t pos, JBuf *o)
@@ -1024,9 +1041,11 @@ static uint64_t t2j_vm(const T2J *c, const dg_field *f, TRd *r, JBuf *o)
 
 /* a STRUCT value (conv/t2j/impl.go:265-339); top: the root struct (do(),
  * impl.go:74-187): response-base fields skipped (readResponseBase, the span
- * to c->aux) and the exception field (ConvertException) ending it. HTTP
- * mapping stays with the Go host. */
-static uint64_t t2j_struct_at(const T2J *c, uint32_t td, TRd *r, JBuf *o, int top)
+ * to c->aux) and the exception field (ConvertException) ending it. resp: a
+ * ResponseSetter is passed here (the root, a root field's struct value, a
+ * value writeHttpValue converts): its mapped fields go to writeHttpValue
+ * (impl.go:132-142, 296-306), the Go host's part, asked for by a stop. */
+static uint64_t t2j_struct_at(const T2J *c, uint32_t td, TRd *r, JBuf *o, int top, int resp)
 {
     const dg_struct *sd = &c->S[c->T[td].st];
     jb_c(o, '{');
@@ -1059,6 +1078,28 @@ static uint64_t t2j_struct_at(const T2J *c, uint32_t td, TRd *r, JBuf *o, int to
             if (c->aux) *c->aux = (uint64_t)s0 | ((uint64_t)r->p << 32);
             continue;
         }
+        if ((c->opts & DG_T2J_HM) && resp && (f->flags & DG_FF_HTTP_MAPPING)) {
+            const uint32_t idx = (*c->seen)++;
+            const int a = idx < c->n_ans ? c->ans[idx] : 2;
+            const uint8_t dt = c->T[f->type].ttype;
+            if (idx >= c->n_ans) { /* a new call: the host reads the value at r->p */
+                o->len = 0;
+                return t2j_stop(r, o, 1 | 0x100u, idx, (uint32_t)fi, r->p, r->p);
+            }
+            if (a == 2 && (dt == 12 || dt == 13 || dt == 14 || dt == 15)) {
+                /* the call needs the container's JSON (doRecurse(resp), impl.go:561-574) */
+                size_t s0 = r->p;
+                o->len = 0;
+                uint64_t e = t2j_value_r(c, f->type, r, o, 1);
+                if (e) return e;
+                return t2j_stop(r, o, 1 | 0x100u, idx, (uint32_t)fi, s0, r->p);
+            }
+            if (a == 0) { /* the response took it (!WriteHttpValueFallback || ok) */
+                int se = t2j_skip(r, dt, 1023);
+                if (se) return T2J_ERR(DG_T2J_E_READ, r->p, se);
+                continue;
+            }
+        }
         if (comma) jb_c(o, ',');
         else comma = 1;
         const dg_t2j_field *x = &c->X[fi];
@@ -1068,7 +1109,7 @@ static uint64_t t2j_struct_at(const T2J *c, uint32_t td, TRd *r, JBuf *o, int to
         if (exc) o->len = 0; /* only the exception field's data */
         uint64_t e;
         if ((c->opts & DG_T2J_ENABLE_VM) && f->vm != DG_VM_NONE) e = t2j_vm(c, f, r, o);
-        else e = t2j_value(c, f->type, r, o);
+        else e = t2j_value_r(c, f->type, r, o, top && resp); /* do() passes resp on (impl.go:167) */
         if (e) return e;
         if (exc) {
             exc_done = 1;
@@ -1084,7 +1125,15 @@ static uint64_t t2j_struct_at(const T2J *c, uint32_t td, TRd *r, JBuf *o, int to
         if ((f->required == DG_REQ_DEFAULT && !(c->opts & DG_T2J_WRITE_DEFAULT)) ||
             (f->required == DG_REQ_OPTIONAL && !(c->opts & DG_T2J_WRITE_OPTIONAL) && f->dflt_len == DG_NONE))
             continue;
-        if (f->flags & DG_FF_HTTP_MAPPING) { /* resp == nil below the top level; the top level is Go-side */ }
+        if ((c->opts & DG_T2J_HM) && (f->flags & DG_FF_HTTP_MAPPING)) {
+            /* handleUnsets (impl.go:401-429): writeHttpValue of the default first */
+            const uint32_t idx = (*c->seen)++;
+            if (idx >= c->n_ans) {
+                o->len = 0;
+                return t2j_stop(r, o, 2 | (resp ? 0x100u : 0u), idx, sd->field_begin + k, 0, 0);
+            }
+            if (c->ans[idx] == 0) continue;
+        }
         if (comma) jb_c(o, ','); /* EncodeArrayComma */
         else comma = 1;
         const dg_t2j_field *x = &c->X[sd->field_begin + k];
@@ -1098,10 +1147,8 @@ static uint64_t t2j_struct_at(const T2J *c, uint32_t td, TRd *r, JBuf *o, int to
     return 0;
 }
 
-static uint64_t t2j_struct(const T2J *c, uint32_t td, TRd *r, JBuf *o) { return t2j_struct_at(c, td, r, o, 0); }
-
-/* doRecurse (conv/t2j/impl.go:189-393) */
-static uint64_t t2j_value(const T2J *c, uint32_t td, TRd *r, JBuf *o)
+/* doRecurse (conv/t2j/impl.go:189-393); resp reaches a STRUCT only */
+static uint64_t t2j_value_r(const T2J *c, uint32_t td, TRd *r, JBuf *o, int resp)
 {
     const dg_type *t = &c->T[td];
     switch (t->ttype) {
@@ -1171,7 +1218,7 @@ static uint64_t t2j_value(const T2J *c, uint32_t td, TRd *r, JBuf *o)
         return 0;
     }
     case 12:
-        return t2j_struct(c, td, r, o);
+        return t2j_struct_at(c, td, r, o, 0, resp);
     case 13: {
         if (!rd_need(r, 1)) return T2J_ERR(DG_T2J_E_READ, r->p, RD_EOF);
         uint8_t kt = r->b[r->p++];
@@ -1251,8 +1298,11 @@ static void t2j_init(T2J *c, const uint8_t *blob, const uint8_t *side, uint64_t 
     const dg_t2j_hdr *xh = (const dg_t2j_hdr *)side;
     c->X = (const dg_t2j_field *)(side + xh->off_fields);
     c->XP = (const char *)(side + xh->off_pool);
-    c->opts = opts;
+    c->opts = opts & ~(uint64_t)DG_T2J_HM; /* dgref_t2j3 only: it has the answers */
     c->aux = NULL;
+    c->ans = NULL;
+    c->n_ans = 0;
+    c->seen = NULL;
 }
 
 /* BinaryConv.Do (conv/t2j/conv.go:50-75 + impl.go:74-187): one message into
@@ -1263,7 +1313,8 @@ static uint64_t t2j_do(const T2J *c, uint32_t root, const uint8_t *thrift, size_
     TRd r = {thrift, n, 0};
     o->len = 0;
     if (c->aux) *c->aux = ~0ull;
-    if (c->T[root].ttype == 12) return t2j_struct_at(c, root, &r, o, 1);
+    if (c->seen) *c->seen = 0;
+    if (c->T[root].ttype == 12) return t2j_struct_at(c, root, &r, o, 1, (c->opts & DG_T2J_HM) != 0);
     return t2j_value(c, root, &r, o);
 }
 
@@ -1292,6 +1343,30 @@ uint64_t dgref_t2j2(const uint8_t *blob, const uint8_t *side, uint32_t root, con
     JBuf o = {(char *)malloc(256), 0, 256};
     uint64_t e = t2j_do(&c, root, thrift, n, &o);
     const int keep = !e || (e & 0xFF) == DG_T2J_E_EXCEPTION;
+    *out_len = keep ? o.len : 0;
+    if (keep && o.len <= cap)
+        memcpy(out, o.b, o.len);
+    free(o.b);
+    return e;
+}
+
+/* dgref_t2j2 with the host's writeHttpValue answers (DG_T2J_HM); a
+ * DG_T2J_E_CALLBACK keeps its record in out */
+uint64_t dgref_t2j3(const uint8_t *blob, const uint8_t *side, uint32_t root, const uint8_t *thrift, size_t n,
+                    uint64_t opts, uint8_t *out, size_t cap, size_t *out_len, uint64_t *aux, const uint8_t *ans,
+                    uint32_t n_ans)
+{
+    T2J c;
+    t2j_init(&c, blob, side, opts);
+    uint32_t seen = 0;
+    c.opts = opts;
+    c.aux = aux;
+    c.ans = ans;
+    c.n_ans = n_ans;
+    c.seen = &seen;
+    JBuf o = {(char *)malloc(256), 0, 256};
+    uint64_t e = t2j_do(&c, root, thrift, n, &o);
+    const int keep = !e || (e & 0xFF) == DG_T2J_E_EXCEPTION || (e & 0xFF) == DG_T2J_E_CALLBACK;
     *out_len = keep ? o.len : 0;
     if (keep && o.len <= cap)
         memcpy(out, o.b, o.len);

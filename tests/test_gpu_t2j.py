@@ -511,3 +511,124 @@ def test_response_base(chk):
     assert all(e is None for e in errs)
     r, js, aux = chk.t2j2(fl, side, src, SKIP_BASE)
     assert outs[0] == js
+
+
+# ---- EnableHttpMapping: the device's writeHttpValue stops against the harness ----
+HM = 1 << 11
+
+
+def gpu_t2j_ans(flat, msgs, opts, answers):
+    """dg_t2j_batch_host_cb with each message's answers -> (outs, rets)."""
+    ctx = conv.default_context()
+    n = len(msgs)
+    a, off = W.arena(msgs)
+    cap = int(off[-1]) * 8 + 64 * n + 65536
+    out = np.zeros(cap, dtype=np.uint8)
+    oo = np.zeros(n + 1, dtype=np.uint64)
+    rets = np.zeros(max(n, 1), dtype=np.uint64)
+    need = C.c_uint64(0)
+    tab = (_lib.VMEntry * max(n, 1))()
+    blob = bytearray()
+    for k, an in enumerate(answers):
+        tab[k].off, tab[k].count = len(blob), len(an)
+        blob += an
+    ab = np.frombuffer(bytes(blob) + b"\0" * 8, dtype=np.uint8)
+    cb = _lib.CBTables(None, 0, C.cast(tab, C.c_void_p), ab.ctypes.data, len(blob))
+    _lib.check(_lib.lib().dg_t2j_batch_host_cb(ctx.h, ctx.desc_t2j(flat), flat.root_type, a.ctypes.data,
+                                               off.ctypes.data, n, opts, out.ctypes.data, cap, oo.ctypes.data,
+                                               rets.ctypes.data, C.byref(need), None, C.byref(cb)))
+    return [out[int(oo[i]):int(oo[i + 1])].tobytes() for i in range(n)], rets[:n]
+
+
+def hm_desc():
+    """Mapped fields at the root, in a root field's struct (resp passed on),
+    in list / map elements (nil resp), inside a mapped container (its JSON
+    conversion passes resp), with required / optional / default ones."""
+    hdr = lambda k: [("api.header", k)]
+    s2 = T.struct_type("S2", [T.FieldDescriptor(1, "v", T.builtin("i32"), T.OPTIONAL, http_mappings=hdr("s2v")),
+                              T.FieldDescriptor(2, "w", T.builtin("string"), T.REQUIRED, http_mappings=hdr("s2w"))])
+    s = T.struct_type("S", [T.FieldDescriptor(1, "a", T.builtin("string"), http_mappings=hdr("a")),
+                            T.FieldDescriptor(2, "b", T.builtin("byte"), T.OPTIONAL, http_mappings=[("api.cookie", "b")]),
+                            T.FieldDescriptor(3, "x", s2, http_mappings=hdr("x")),
+                            T.FieldDescriptor(4, "r", T.builtin("string"), T.REQUIRED,
+                                              http_mappings=[("api.raw_body", "")]),
+                            T.FieldDescriptor(5, "n", T.builtin("i64"))])
+    return T.struct_type("R", [
+        T.FieldDescriptor(1, "h", T.builtin("string"), http_mappings=hdr("h")),
+        T.FieldDescriptor(2, "c", T.builtin("i32"), http_mappings=[("api.http_code", "")]),
+        T.FieldDescriptor(3, "s", s, http_mappings=[("api.cookie", "s")]),
+        T.FieldDescriptor(4, "t", s),
+        T.FieldDescriptor(5, "l", T.list_of(s), T.OPTIONAL),
+        T.FieldDescriptor(6, "m", T.map_of(T.builtin("string"), s), T.OPTIONAL),
+        T.FieldDescriptor(7, "d", T.builtin("double"), T.REQUIRED, http_mappings=hdr("d")),
+        T.FieldDescriptor(8, "q", T.builtin("i64"), T.OPTIONAL, http_mappings=[("api.query", "q")]),
+        T.FieldDescriptor(9, "k", T.list_of(T.builtin("i32")), http_mappings=hdr("k"))])
+
+
+def test_hm_stops_vs_harness(chk):
+    """Random messages (and mutated ones) under DG_T2J_HM, answered at
+    random (taken / write as well / open for the JSON) call after call: at
+    every step the device's status word and record (or final JSON) equal the
+    harness's for the same answers."""
+    td = hm_desc()
+    fl = T.flatten(td)
+    side = T.flatten_t2j(fl)
+    rng = random.Random(11)
+    msgs = [t2jgen.gen_thrift(rng, td) for _ in range(500)]
+    msgs += [t2jgen.mutate(rng, t2jgen.gen_thrift(rng, td)) for _ in range(200)]
+    seen = {"k1": 0, "k2": 0, "open": 0, "done": 0, "final": 0}
+    for opts in (HM, HM | WDEF | WREQ | WOPT, HM | NOB64 | B8 | DISALLOW):
+        answers = [bytearray() for _ in msgs]
+        live = list(range(len(msgs)))
+        for _step in range(60):
+            if not live:
+                break
+            outs, rets = gpu_t2j_ans(fl, [msgs[i] for i in live], opts, [answers[i] for i in live])
+            nxt = []
+            for k, i in enumerate(live):
+                er, eo, _ = chk.t2j3(fl, side, msgs[i], opts, bytes(answers[i]))
+                assert (int(rets[k]), outs[k]) == (er, eo), (i, hex(int(rets[k])), hex(er), outs[k][-40:],
+                                                            eo[-40:], bytes(answers[i]), msgs[i][:60].hex())
+                if (er & 0xFF) != 12:
+                    seen["final"] += 1
+                    continue
+                w0 = struct.unpack_from("<Q", eo, len(eo) - 16)[0]
+                kind, idx, fi = w0 & 0xFF, (w0 >> 16) & 0xFFFF, w0 >> 32
+                an = answers[i]
+                if idx < len(an) and an[idx] == 2:
+                    seen["done"] += 1
+                    del an[idx:]
+                    an.append(rng.randrange(2))
+                else:
+                    assert idx == len(an)
+                    seen["k%d" % kind] += 1
+                    container = fl.fields[fi].type.type in (T.STRUCT, T.MAP, T.LIST, T.SET)
+                    if kind == 1 and container and rng.random() < 0.6:
+                        seen["open"] += 1
+                        an.append(2)
+                    else:
+                        an.append(rng.randrange(2))
+                nxt.append(i)
+            live = nxt
+        assert not live
+    assert min(seen.values()) > 20, seen
+
+
+@pytest.mark.parametrize("name", ["test_http_mapping_fallback", "test_write_empty", "test_nobody_required_fields",
+                                  "test_json_string", "test_kitex_api_header", "test_default_value",
+                                  "test_optional_default_value", "test_conv_thrift2http", "test_errors"])
+def test_reference_http_mapping_cases(chk, monkeypatch, name):
+    """The reference's t2j HTTP-mapping tests (tests/test_t2j_http.py, there
+    over the harness) with the GPU doing the conversion."""
+    import inspect
+    import test_t2j_http as th
+    monkeypatch.setattr(th, "harness_conv", lambda _chk, o: t2j.BinaryConv(o))
+    fn = getattr(th, name)
+    if "nob64" in inspect.signature(fn).parameters:
+        for v in (False, True):
+            fn(chk, v)
+    elif "use_default" in inspect.signature(fn).parameters:
+        for v in (True, False):
+            fn(chk, v)
+    else:
+        fn(chk)
