@@ -227,27 +227,32 @@ def cpu_baseline(flat, arena, off, flags, budget_s: float = 6.0):
 
     def timed(a, o, cpus):
         t1 = ref.j2t_timed(flat, a, o, flags, cpus, 1)
-        reps = int(max(3, min(200, budget_s / 2 / max(t1, 1e-6))))
-        return ref.j2t_timed(flat, a, o, flags, cpus, reps), reps
+        reps = int(max(5, min(200, budget_s / 2 / max(t1, 1e-6))))
+        ts = []
+        ref.j2t_timed(flat, a, o, flags, cpus, reps, times=ts)
+        return float(np.median(ts)), ts
 
-    t_all, reps_all = timed(arena, off, phys[:cores_all])
-    t_share, reps_share = (t_all, reps_all) if cores == cores_all else timed(arena, off, phys[:cores])
+    t_all, ts_all = timed(arena, off, phys[:cores_all])
+    t_share, ts_share = (t_all, ts_all) if cores == cores_all else timed(arena, off, phys[:cores])
     # one core: a prefix of at most ~64 MB / 65536 messages
     k = int(min(n, 65536, max(1, np.searchsorted(off, off[0] + 64 * 1024 * 1024))))
     a1, o1 = arena[:int(off[k]) + 64], off[:k + 1]
-    t_one, reps_one = timed(a1, o1, phys[:1])
+    t_one, ts_one = timed(a1, o1, phys[:1])
     one_bytes = int(o1[-1] - o1[0])
+    spread = lambda nb, ts: {"min": round(nb / max(ts) / 1e9, 4), "max": round(nb / min(ts) / 1e9, 4)}
     return {"value": round(nbytes / t_all / 1e9, 4), "unit": "GB/s", "cores": cores_all, "kind": "reference",
+            "stat": "median of the passes", "range": spread(nbytes, ts_all),
             "cpu_model": cpu_model(), "msgs_per_s": round(n / t_all),
             "share": {"cores": cores, "value": round(nbytes / t_share / 1e9, 4), "msgs_per_s": round(n / t_share),
-                      "note": f"the {CPU_SHARE} CPUs per GPU the box grants"},
+                      "range": spread(nbytes, ts_share), "note": f"the {CPU_SHARE} CPUs per GPU the box grants"},
             "one_core_gbs": round(one_bytes / t_one / 1e9, 4), "one_core_ns_per_msg": round(t_one / k * 1e9, 1),
+            "one_core_range": spread(one_bytes, ts_one),
             "per_core_gbs": round(nbytes / t_all / 1e9 / cores_all, 4),
-            "sample": f"all-core: the rank's whole batch ({n} msgs, {nbytes} B), best of {reps_all} passes, "
-                      f"{cores_all} threads pinned to distinct physical cores of '{cpu_model()}' "
-                      f"(affinity: {logical} logical CPUs = {len(phys)} physical cores); share: {cores} cores, "
-                      f"best of {reps_share}; one-core: first {k} msgs ({one_bytes} B), best of {reps_one}; "
-                      f"reference native.c built by oracle/Makefile (clang -O3 -mavx2)"}
+            "sample": f"all-core: the rank's whole batch ({n} msgs, {nbytes} B), median (min/max in range) of "
+                      f"{len(ts_all)} passes, {cores_all} threads pinned to distinct physical cores of "
+                      f"'{cpu_model()}' (affinity: {logical} logical CPUs = {len(phys)} physical cores); share: "
+                      f"{cores} cores, {len(ts_share)} passes; one-core: first {k} msgs ({one_bytes} B), "
+                      f"{len(ts_one)} passes; reference native.c built by oracle/Makefile (clang -O3 -mavx2)"}
 
 
 # ---------------------------------------------------------------- end to end
@@ -322,6 +327,22 @@ def e2e_host_path(L, ctx, dh, root, flags, arena, off, dev, flat, reps: int = 5)
                       "best of %d per chunking" % reps}
 
 
+def same_outputs(d_oo, d_ol, a, b) -> bool:
+    """Whether two output buffers with the same slots (d_oo, int64 n+1) hold
+    the same bytes in every message's slot prefix of d_ol bytes (the slot
+    tails are never written)."""
+    import torch
+    n = d_ol.numel()
+    total = int(d_oo[-1].item())
+    if n == 0 or total == 0:
+        return True
+    seg = torch.repeat_interleave(torch.arange(n, device=d_oo.device), d_oo[1:] - d_oo[:-1])
+    pos = torch.arange(total, device=d_oo.device) - d_oo[:-1][seg]
+    valid = pos < d_ol.to(torch.int64)[seg]
+    del seg, pos
+    return bool(torch.equal(a[:total][valid], b[:total][valid]))
+
+
 # ---------------------------------------------------------------- t2j
 def cpu_baseline_t2j(flat, side, arena, off, opts, budget_s: float = 8.0):
     """The t2j checker (oracle/ref_harness.c dgref_t2j: conv/t2j's control
@@ -337,15 +358,20 @@ def cpu_baseline_t2j(flat, side, arena, off, opts, budget_s: float = 8.0):
     n = len(off) - 1
     nbytes = int(off[-1] - off[0])
     t1 = ref.t2j_timed(flat, side, arena, off, opts, phys[:cores], 1)
-    reps = int(max(3, min(200, budget_s / 2 / max(t1, 1e-6))))
-    t_all = ref.t2j_timed(flat, side, arena, off, opts, phys[:cores], reps)
-    t_one = ref.t2j_timed(flat, side, arena, off, opts, phys[:1], 3)
+    reps = int(max(5, min(200, budget_s / 2 / max(t1, 1e-6))))
+    ts, ts1 = [], []
+    ref.t2j_timed(flat, side, arena, off, opts, phys[:cores], reps, times=ts)
+    ref.t2j_timed(flat, side, arena, off, opts, phys[:1], 3, times=ts1)
+    t_all, t_one = float(np.median(ts)), float(np.median(ts1))
     return {"value": round(nbytes / t_all / 1e9, 4), "unit": "GB/s", "cores": cores, "kind": "port",
+            "stat": "median of the passes",
+            "range": {"min": round(nbytes / max(ts) / 1e9, 4), "max": round(nbytes / min(ts) / 1e9, 4)},
             "msgs_per_s": round(n / t_all), "one_core_gbs": round(nbytes / t_one / 1e9, 4),
-            "sample": f"the rank's whole Thrift batch ({n} msgs, {nbytes} B), best of {reps} passes, {cores} threads "
-                      f"pinned to distinct physical cores of '{cpu_model()}' ({logical} logical CPUs allowed); "
-                      f"one-core: same batch, best of 3; oracle/ref_harness.c dgref_t2j_timed (conv/t2j restated "
-                      f"in C over the reference's native quote/i64toa/f64toa/b64encode, clang -O3)"}
+            "sample": f"the rank's whole Thrift batch ({n} msgs, {nbytes} B), median (min/max in range) of {reps} "
+                      f"passes, {cores} threads pinned to distinct physical cores of '{cpu_model()}' ({logical} "
+                      f"logical CPUs allowed); one-core: same batch, median of 3; oracle/ref_harness.c "
+                      f"dgref_t2j_timed (conv/t2j restated in C over the reference's native "
+                      f"quote/i64toa/f64toa/b64encode, clang -O3)"}
 
 
 def bench_t2j(args, rank, world, dev, dist, backend, td, arena, off, meta):
@@ -456,7 +482,7 @@ def bench_t2j(args, rank, world, dev, dist, backend, td, arena, off, meta):
         step_inflight(args.warmup * depth)
         torch.cuda.synchronize()
         for _, o, jl, jr in sets[1:]:
-            if not (torch.equal(jr, d_jr) and torch.equal(jl, d_jl)):
+            if not (torch.equal(jr, d_jr) and torch.equal(jl, d_jl) and same_outputs(d_jo, d_jl, o, d_out)):
                 raise SystemExit("t2j in-flight output set differs from the serial one")
     if dist:
         torch.distributed.barrier()
@@ -585,7 +611,7 @@ def bench_agg(args, rank, world, dev, dist, backend, td, arena, off, meta):
         prof["ns_per_call_in_wait"] = round(pr[9] / ncalls, 1)
         prof["submits_without_open_batch"] = int(pr[10])
         L.dg_agg_destroy(h)
-        lt = lat[:m].astype(np.float64) / 1e3
+        lt = lat[:m][lat[:m] > 0].astype(np.float64) / 1e3  # every 8th call is timed (dg_agg_drive)
         runs.append({"threads": threads, "in_flight_per_thread": window, "per_thread_batch_share": per_thread,
                      "calls_per_step": m, "steps": steps,
                      "msgs_per_s": round(m * steps / wall), "gbs_json_in": round(int(off[m]) * steps / wall / 1e9, 3),
@@ -782,7 +808,7 @@ def main(argv=None):
         step_inflight(args.warmup * depth)
         torch.cuda.synchronize()
         for o in osets[1:]:
-            if not (torch.equal(o[2], d_ret) and torch.equal(o[1], d_ol)):
+            if not (torch.equal(o[2], d_ret) and torch.equal(o[1], d_ol) and same_outputs(d_oo, d_ol, o[0], d_out)):
                 raise SystemExit("in-flight output set differs from the serial one")
 
     # timed region: barrier + synchronize on both sides, max over ranks

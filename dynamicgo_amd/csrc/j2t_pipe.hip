@@ -33,6 +33,7 @@
 #include <deque>
 #include <mutex>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include <linux/membarrier.h>
@@ -275,6 +276,11 @@ struct Batch {
 
 std::atomic<uint64_t> g_agg_ids{1};
 
+/* live aggregators by id: a thread that exits hands its parts back to the
+ * ones still alive (ThreadParts' destructor) */
+std::mutex g_reg_mu;
+std::unordered_map<uint64_t, dg_agg *> g_reg;
+
 }  // namespace
 
 struct dg_agg {
@@ -311,6 +317,12 @@ struct dg_agg {
         return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now().time_since_epoch()).count();
     }
     int slot();
+    std::vector<int> free_slots;     /* parts of exited threads (under mu) */
+    void release_slot(int s)
+    {
+        std::lock_guard<std::mutex> g(mu);
+        free_slots.push_back(s);
+    }
     void wake_flusher()
     {
         { std::lock_guard<std::mutex> g(mu); }
@@ -321,20 +333,40 @@ struct dg_agg {
     int launch(Batch *x);
 };
 
-/* this thread's slot (sub-batch index), registered on first use: its
- * pinned regions in every batch of the ring; -1 when all are taken */
+namespace {
+/* the parts this thread holds, by aggregator id; handed back at thread exit */
+struct ThreadParts {
+    std::vector<std::pair<uint64_t, int>> v;
+    ~ThreadParts()
+    {
+        std::lock_guard<std::mutex> g(g_reg_mu);
+        for (const auto &e : v) {
+            auto it = g_reg.find(e.first);
+            if (it != g_reg.end() && e.second >= 0) it->second->release_slot(e.second);
+        }
+    }
+};
+thread_local ThreadParts t_parts;
+}  // namespace
+
+/* this thread's slot (sub-batch index), registered on first use: an exited
+ * thread's part, else new pinned regions in every batch of the ring; -1 when
+ * all are taken */
 int dg_agg::slot()
 {
-    struct TL {
-        uint64_t id;
-        int slot;
-    };
-    thread_local TL tl[8] = {};
-    thread_local int tl_next = 0;
-    for (const TL &e : tl)
-        if (e.id == id) return e.slot;
-    int s = nslots.fetch_add(1, std::memory_order_seq_cst);
-    if (s >= AGG_SLOTS) {
+    for (const auto &e : t_parts.v)
+        if (e.first == id) return e.second;
+    int s = -1;
+    {
+        std::lock_guard<std::mutex> g(mu);
+        if (!free_slots.empty()) {
+            s = free_slots.back();
+            free_slots.pop_back();
+        }
+    }
+    if (s >= 0) {
+        /* its regions exist; its previous owner has no message left in it */
+    } else if ((s = nslots.fetch_add(1, std::memory_order_seq_cst)) >= AGG_SLOTS) {
         nslots.fetch_sub(1);
         s = -1;
     } else {
@@ -349,8 +381,7 @@ int dg_agg::slot()
         ready[s].store(ok ? 1 : 2, std::memory_order_release);
         if (!ok) s = -1;
     }
-    tl[tl_next] = TL{id, s};
-    tl_next = (tl_next + 1) % 8;
+    t_parts.v.emplace_back(id, s);
     return s;
 }
 
@@ -605,6 +636,10 @@ int dg_agg_create2(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, uint64_
     a->open.store(1);
     a->b[1].free_ = false;
     a->b[1].g = 1;
+    {
+        std::lock_guard<std::mutex> g(g_reg_mu);
+        g_reg[a->id] = a;
+    }
     a->flusher = std::thread([a] { a->run_flusher(); });
     a->completer = std::thread([a] { a->run_completer(); });
     *out = a;
@@ -627,7 +662,10 @@ int dg_agg_submit(dg_agg *a, const uint8_t *json, size_t len, int nonblock, dg_a
     t->len = len;
     t->batch = nullptr;
     const int s = len > a->cap_b ? -1 : a->slot();
-    if (s < 0) return DG_OK; /* converted alone by dg_agg_wait */
+    if (s < 0) { /* converted alone by dg_agg_wait */
+        a->prof[11].fetch_add(1, std::memory_order_relaxed);
+        return DG_OK;
+    }
     for (;;) {
         const uint64_t g = a->open.load(std::memory_order_seq_cst);
         Batch *x = &a->b[g % a->ring];
@@ -764,6 +802,10 @@ int dg_agg_profile(dg_agg *a, uint64_t *out, int n)
 void dg_agg_destroy(dg_agg *a)
 {
     if (!a) return;
+    {
+        std::lock_guard<std::mutex> g(g_reg_mu);
+        g_reg.erase(a->id);
+    }
     if (a->flusher.joinable()) {
         {
             std::lock_guard<std::mutex> lk(a->mu);
@@ -950,6 +992,8 @@ int dg_j2t_pipeline_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8
     return fits ? DG_OK : set_err(DG_E_NOMEM, "output needs %llu bytes", (unsigned long long)need);
 }
 
+static const uint64_t DRIVE_SAMPLE = 8; /* power of two */
+
 int dg_agg_drive(dg_agg *a, const uint8_t *arena, const uint64_t *in_off, uint64_t n, int threads, int window,
                  uint8_t *out, const uint64_t *out_off, uint64_t *out_len, uint64_t *ret, uint32_t *lat_ns,
                  double *seconds)
@@ -970,15 +1014,24 @@ int dg_agg_drive(dg_agg *a, const uint8_t *arena, const uint64_t *in_off, uint64
             while (!go.load(std::memory_order_acquire)) std::this_thread::yield();
             uint64_t h = lo;
             uint64_t ts_sub = 0, ts_wait = 0, n_again = 0;
+            /* the clock is read for every DRIVE_SAMPLE-th call only (about
+             * 20 ns a read: five reads per call would be a fifth of a call's
+             * host cost); the profile counters are scaled back up */
+            auto sampled = [&](uint64_t j) { return (j & (DRIVE_SAMPLE - 1)) == 0; };
             auto finish = [&]() {
                 const uint64_t j = h++;
                 const int k = (int)((j - lo) % window);
                 size_t ol = 0;
-                const uint64_t w0 = dg_agg::now_ns();
+                const bool smp = sampled(j);
+                const uint64_t w0 = smp ? dg_agg::now_ns() : 0;
                 int rc = dg_agg_wait(a, &ring[k], out + out_off[j], out_off[j + 1] - out_off[j], &ol, &ret[j]);
-                const uint64_t w1 = dg_agg::now_ns();
-                ts_wait += w1 - w0;
-                if (lat_ns) lat_ns[j] = (uint32_t)std::min<int64_t>(w1 - t0[k], 0xffffffffll);
+                if (smp) {
+                    const uint64_t w1 = dg_agg::now_ns();
+                    ts_wait += (w1 - w0) * DRIVE_SAMPLE;
+                    if (lat_ns) lat_ns[j] = (uint32_t)std::min<int64_t>(w1 - t0[k], 0xffffffffll);
+                } else if (lat_ns) {
+                    lat_ns[j] = 0;
+                }
                 out_len[j] = ol;
                 if (rc) failed.fetch_add(1);
             };
@@ -988,11 +1041,12 @@ int dg_agg_drive(dg_agg *a, const uint8_t *arena, const uint64_t *in_off, uint64
                  * completions): their batches free early */
                 while (h < i && dg_agg_ready(a, &ring[(int)((h - lo) % window)])) finish();
                 const int k = (int)((i - lo) % window);
-                t0[k] = dg_agg::now_ns();
+                const bool smp = sampled(i);
+                if (smp) t0[k] = dg_agg::now_ns();
                 for (;;) {
-                    const uint64_t s0 = dg_agg::now_ns();
+                    const uint64_t s0 = smp ? dg_agg::now_ns() : 0;
                     int rc = dg_agg_submit(a, arena + in_off[i], in_off[i + 1] - in_off[i], 1, &ring[k]);
-                    ts_sub += dg_agg::now_ns() - s0;
+                    if (smp) ts_sub += (dg_agg::now_ns() - s0) * DRIVE_SAMPLE;
                     if (rc == DG_OK) break;
                     n_again++;
                     if (rc != DG_E_AGAIN) {

@@ -292,7 +292,10 @@ int dg_agg_stats(dg_agg *agg, uint64_t *batches, uint64_t *msgs);
  * for a free batch, issuing a batch; completer waiting for the header, for
  * the packed bytes; seal to issued; issued to done; callers blocked in
  * dg_agg_wait; dg_agg_drive: time in submit, in wait, and the count of
- * submits that met no open batch) */
+ * submits that met no open batch; the count of calls converted alone by
+ * dg_j2t_do: longer than a part, or no part left for their thread).
+ * A part (one of 256) belongs to a calling thread from its first call until
+ * the thread exits; an exited thread's part goes to the next new thread. */
 int dg_agg_profile(dg_agg *agg, uint64_t *out, int n);
 /* converts what is still queued, then stops the flusher (every ticket must
  * have been waited for) */
@@ -302,7 +305,9 @@ void dg_agg_destroy(dg_agg *agg);
  * contiguous share of the n messages through the aggregator with up to
  * `window` requests in flight, message i's result into
  * out[out_off[i] .. out_off[i+1]) with out_len[i], ret[i], and, if lat_ns,
- * its submit-to-result latency. *seconds = wall time of the whole run. */
+ * its submit-to-result latency for every 8th message (0 for the others: the
+ * clock is read for a sample of the calls only). *seconds = wall time of
+ * the whole run. */
 int dg_agg_drive(dg_agg *agg, const uint8_t *arena, const uint64_t *in_off, uint64_t n, int threads, int window,
                  uint8_t *out, const uint64_t *out_off, uint64_t *out_len, uint64_t *ret, uint32_t *lat_ns,
                  double *seconds);

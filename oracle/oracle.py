@@ -211,8 +211,9 @@ class _Base:
 
 
     def j2t_timed(self, flat, arena: np.ndarray, in_off: np.ndarray, flags: int, cpus: Sequence[int],
-                  reps: int, root: Optional[int] = None) -> float:
-        """bench.py cpu_baseline: best-of-`reps` seconds for the whole arena,
+                  reps: int, root: Optional[int] = None, times: Optional[list] = None) -> float:
+        """bench.py cpu_baseline: best-of-`reps` seconds for the whole arena
+        (every pass's seconds appended to `times` when given),
         len(cpus) threads each pinned to one of `cpus` (byte-balanced shards,
         outputs preallocated here and first touched by an untimed pass).
         Reference harness only (oracle/_ref: dgref_j2t_timed)."""
@@ -232,13 +233,15 @@ class _Base:
         out_len = np.zeros(n, dtype=np.uint32)
         rets = np.zeros(n, dtype=np.uint64)
         cpu_arr = (C.c_int * len(cpus))(*cpus)
-        best = C.c_double(-1.0)
+        best = (C.c_double * (reps + 1))()
         root = flat.root_type if root is None else root
         rc = f(self._desc(flat.blob), root, arena.ctypes.data, in_off.ctypes.data, n, flags, out.ctypes.data,
-               out_off.ctypes.data, out_len.ctypes.data, rets.ctypes.data, len(cpus), cpu_arr, reps, C.byref(best))
+               out_off.ctypes.data, out_len.ctypes.data, rets.ctypes.data, len(cpus), cpu_arr, reps, best)
         if rc != 0:
             raise RuntimeError("dgref_j2t_timed failed")
-        return float(best.value)
+        if times is not None:
+            times.extend(float(best[1 + r]) for r in range(reps))
+        return float(best[0])
 
 
 class RefT2J:
@@ -303,8 +306,9 @@ class RefT2J:
 
 
     def t2j_timed(self, flat, side: bytes, arena: np.ndarray, in_off: np.ndarray, opts: int, cpus: Sequence[int],
-                  reps: int, root: Optional[int] = None) -> float:
-        """bench.py t2j cpu_baseline: best-of-`reps` seconds for the whole
+                  reps: int, root: Optional[int] = None, times: Optional[list] = None) -> float:
+        """bench.py t2j cpu_baseline: best-of-`reps` seconds (each pass's to
+        `times` when given) for the whole
         arena, len(cpus) threads pinned one per cpu (dgref_t2j_timed)."""
         f = self.lib.dgref_t2j_timed
         f.restype = C.c_int
@@ -320,13 +324,15 @@ class RefT2J:
         out_len = np.zeros(n, dtype=np.uint32)
         rets = np.zeros(n, dtype=np.uint64)
         cpu_arr = (C.c_int * len(cpus))(*cpus)
-        best = C.c_double(-1.0)
+        best = (C.c_double * (reps + 1))()
         root = flat.root_type if root is None else root
         rc = f(flat.blob, side, root, arena.ctypes.data, in_off.ctypes.data, n, opts, out.ctypes.data,
-               out_off.ctypes.data, out_len.ctypes.data, rets.ctypes.data, len(cpus), cpu_arr, reps, C.byref(best))
+               out_off.ctypes.data, out_len.ctypes.data, rets.ctypes.data, len(cpus), cpu_arr, reps, best)
         if rc != 0:
             raise RuntimeError("dgref_t2j_timed failed")
-        return float(best.value)
+        if times is not None:
+            times.extend(float(best[1 + r]) for r in range(reps))
+        return float(best[0])
 
 
 def RefT2JOracle() -> Optional[RefT2J]:

@@ -632,7 +632,7 @@ int dgref_j2t_batch(void *desc, uint32_t root, const uint8_t *json, const uint64
  * contiguous byte-balanced shard, run one untimed warm-up pass (first touch
  * of the caller's preallocated outputs) and then `reps` passes; between
  * passes all threads meet at a barrier, so a pass's time is the slowest
- * shard's. Returns the best pass in seconds through *best_s. */
+ * shard's. best_s[0]: the best pass in seconds, best_s[1 + r]: pass r. */
 typedef struct {
     Job job;
     int cpu, tid, reps;
@@ -673,8 +673,9 @@ static void *run_timed(void *arg)
         pthread_barrier_wait(t->bar);
         if (t->tid == 0 && r >= 0) {
             double dt = now_s() - t0;
-            if (*t->best < 0 || dt < *t->best)
-                *t->best = dt;
+            if (t->best[0] < 0 || dt < t->best[0])
+                t->best[0] = dt;
+            t->best[1 + r] = dt;
         }
     }
     ctx_free(c);
@@ -691,7 +692,7 @@ int dgref_j2t_timed(void *desc, uint32_t root, const uint8_t *json, const uint64
     pthread_t *th = (pthread_t *)calloc(nthreads, sizeof(pthread_t));
     pthread_barrier_t bar;
     pthread_barrier_init(&bar, NULL, (unsigned)nthreads);
-    double best = -1;
+    best_s[0] = -1;
     uint64_t total = in_off[n] - in_off[0];
     uint64_t lo = 0;
     for (int t = 0; t < nthreads; t++) {
@@ -704,7 +705,7 @@ int dgref_j2t_timed(void *desc, uint32_t root, const uint8_t *json, const uint64
         tj[t].tid = t;
         tj[t].reps = reps;
         tj[t].bar = &bar;
-        tj[t].best = &best;
+        tj[t].best = best_s;
         lo = hi;
     }
     for (int t = 0; t < nthreads; t++)
@@ -714,7 +715,6 @@ int dgref_j2t_timed(void *desc, uint32_t root, const uint8_t *json, const uint64
     pthread_barrier_destroy(&bar);
     free(tj);
     free(th);
-    *best_s = best;
     return 0;
 }
 
@@ -1420,8 +1420,9 @@ static void *run_t2j_timed(void *arg)
         pthread_barrier_wait(t->bar);
         if (t->tid == 0 && rep >= 0) {
             double dt = now_s() - t0;
-            if (*t->best < 0 || dt < *t->best)
-                *t->best = dt;
+            if (t->best[0] < 0 || dt < t->best[0])
+                t->best[0] = dt;
+            t->best[1 + rep] = dt;
         }
     }
     free(o.b);
@@ -1438,7 +1439,7 @@ int dgref_t2j_timed(const uint8_t *blob, const uint8_t *side, uint32_t root, con
     pthread_t *th = (pthread_t *)calloc(nthreads, sizeof(pthread_t));
     pthread_barrier_t bar;
     pthread_barrier_init(&bar, NULL, (unsigned)nthreads);
-    double best = -1;
+    best_s[0] = -1;
     uint64_t total = in_off[n] - in_off[0];
     uint64_t lo = 0;
     for (int t = 0; t < nthreads; t++) {
@@ -1460,7 +1461,7 @@ int dgref_t2j_timed(const uint8_t *blob, const uint8_t *side, uint32_t root, con
         tj[t].tid = t;
         tj[t].reps = reps;
         tj[t].bar = &bar;
-        tj[t].best = &best;
+        tj[t].best = best_s;
         lo = hi;
     }
     for (int t = 0; t < nthreads; t++)
@@ -1470,6 +1471,5 @@ int dgref_t2j_timed(const uint8_t *blob, const uint8_t *side, uint32_t root, con
     pthread_barrier_destroy(&bar);
     free(tj);
     free(th);
-    *best_s = best;
     return 0;
 }

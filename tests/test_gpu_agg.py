@@ -185,3 +185,29 @@ def test_pipeline_host_pinned_direct(chunks, shift):
         assert int(oo[-1]) == need.value
         got = [(int(rr[i]), ob[oo[i]:oo[i + 1]].tobytes()) for i in range(n)]
         assert got == [(r, o if r == 0 else b"") for r, o in want]
+
+
+def test_aggregator_parts_return_at_thread_exit():
+    """400 short-lived threads (more than the 256 parts), each one
+    blocking Do: an exited thread's part goes to the next thread, so no call
+    falls back to the unbatched path, and every result is the oracle's."""
+    td = W.nesting_i64_desc()
+    fl = T.flatten(td)
+    msgs = W.gen_nested_batch(random.Random(8), 400)
+    chk = oracle.RefOracle() or oracle.PortOracle()
+    agg = conv.Aggregator(td, conv.Options(), max_batch=64, max_wait_us=50)
+    got = [None] * len(msgs)
+
+    def one(i):
+        got[i] = agg.do(msgs[i]) or b""
+
+    for k in range(0, len(msgs), 8):  # 8 at a time, each thread gone before the next wave
+        ths = [threading.Thread(target=one, args=(i,)) for i in range(k, min(k + 8, len(msgs)))]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join(timeout=60)
+    prof = agg.profile()
+    agg.close()
+    assert prof[11] == 0, prof
+    assert got == [chk.j2t(fl, m, 1)[1] for m in msgs]
