@@ -50,6 +50,7 @@ static int t2j_launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
     const uint64_t wmin = (uint64_t)c->knobs.t2j_wave_min;
     /* the root-level Go-side options run on the lane kernel only */
     const bool wave = !(opts & (DG_T2J_CONVERT_EXC | DG_T2J_SKIP_RESP_BASE | DG_T2J_HM)) && wmin > 0 && d->hdr.total_len <= 16384 && d->hdr.n_fields <= 1024 && /* T2W_FX */
+                      d->hdr.n_types < 4096 && /* a token's type index */
                       d->side_len <= 12288 /* T2W_SIDE */ && (max_len == 0 || max_len > wmin);
     if (wave) {
         if ((rc = grow_x(x, x->t2j_big, x->t2j_big_cap, n))) return rc;

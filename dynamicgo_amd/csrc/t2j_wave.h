@@ -169,13 +169,19 @@ DGI uint32_t fx_td(uint64_t v) { return (uint32_t)(v >> 32); }
 constexpr uint32_t T2W_FX = 1024; /* fields the LDS table holds (descriptors with more take the lane kernel) */
 
 /* Token sink of the batched walk: this lane's region of the wave's token
- * buffer (global memory, T2W_TOKCAP tokens of 16 bytes). */
-struct T2WTok {
-    uint32_t pos;  /* Thrift position of the value */
-    uint32_t aux;  /* TKF_KEYF: field index; TKF_KEYM: Thrift position of the key */
-    uint32_t td;   /* value type index */
-    uint32_t kind; /* TK_* | TKF_* | map key ttype << 8 */
-};
+ * buffer (global memory, T2W_TOKCAP tokens). A token is 8 bytes (16 before:
+ * the tokens' round trip through L2/HBM was most of t2j-c3's traffic):
+ *   pos (bits 0-20)   Thrift position of the value (messages < 2 MiB)
+ *   aux (21-41)       TKF_KEYF: field index; TKF_KEYM: Thrift position of the key
+ *   td  (42-53)       value type index (the wave path takes < 4096 types)
+ *   kind (54-59)      TK_* | TKF_*
+ *   kt  (60-63)       map key ttype */
+typedef uint64_t T2WTok;
+constexpr uint32_t T2W_POSBITS = 21;
+DGI uint64_t t2w_tok(uint32_t kind, uint32_t pos, uint32_t aux, uint32_t td, uint32_t kt)
+{
+    return (uint64_t)pos | ((uint64_t)aux << 21) | ((uint64_t)td << 42) | ((uint64_t)kind << 54) | ((uint64_t)kt << 60);
+}
 constexpr uint32_t T2W_TOKCAP = 192; /* tokens per message (more: the lane kernel) */
 constexpr uint32_t T2W_RING = 8;     /* tokens a walker keeps in LDS before writing them out together */
 constexpr uint32_t T2W_BD = 3;       /* frames kept in LDS per lane (the innermost is in registers) */
@@ -187,8 +193,7 @@ constexpr uint32_t T2W_BD = 3;       /* frames kept in LDS per lane (the innermo
  * and go to global memory T2W_RING at a time: a global store ahead of the
  * walk's next (dependent) load would make that load wait for the store's
  * acknowledgement too (one vmcnt counts both). */
-typedef uint32_t tok_v4 __attribute__((ext_vector_type(4))); /* a token as one 16-byte LDS word */
-typedef __attribute__((address_space(3))) tok_v4 lds_tok;
+typedef __attribute__((address_space(3))) uint64_t lds_tok;
 static_assert(T2W_RING * T2W_MPT * sizeof(T2WTok) <= T2W_MSG && T2W_TOKCAP % T2W_RING == 0, "ring in the stage");
 /* bytes [p, p + 16) of the message as two little-endian words: three
  * aligned words read at once (the third only when it lies within the 16
@@ -212,19 +217,15 @@ DGI int32_t t2w_walk(const DV &D, const __attribute__((address_space(3))) uint64
     const int64_t wmax = (src.off0 + n + 8) >> 3; /* the last word inside the 16 readable bytes past the end */
     int64_t p = 0;
     uint32_t sp = 0, nt = 0;
+    if (n >= ((int64_t)1 << T2W_POSBITS)) return -1; /* positions must fit a token */
     T2WFrame cur{};
     auto emit = [&](uint32_t kind, uint32_t pos, uint32_t aux, uint32_t td, uint32_t kt) -> bool {
         if (nt >= T2W_TOKCAP) return false;
-        tok_v4 t;
-        t.x = pos;
-        t.y = aux;
-        t.z = td;
-        t.w = kind | (kt << 8);
-        ring[(nt % T2W_RING) * T2W_MPT] = t;
+        ring[(nt % T2W_RING) * T2W_MPT] = t2w_tok(kind, pos, aux, td, kt);
         nt++;
         if (nt % T2W_RING == 0) {
 #pragma unroll
-            for (uint32_t j = 0; j < T2W_RING; j++) ((tok_v4 *)(void *)tok)[nt - T2W_RING + j] = ring[j * T2W_MPT];
+            for (uint32_t j = 0; j < T2W_RING; j++) tok[nt - T2W_RING + j] = ring[j * T2W_MPT];
         }
         return true;
     };
@@ -405,7 +406,7 @@ DGI int32_t t2w_walk(const DV &D, const __attribute__((address_space(3))) uint64
         if (act == 1) pop();
         else if (act == 2) push(f);
     }
-    for (uint32_t j = nt & ~(T2W_RING - 1); j < nt; j++) ((tok_v4 *)(void *)tok)[j] = ring[(j % T2W_RING) * T2W_MPT];
+    for (uint32_t j = nt & ~(T2W_RING - 1); j < nt; j++) tok[j] = ring[(j % T2W_RING) * T2W_MPT];
     return (int32_t)nt;
 }
 
@@ -488,12 +489,12 @@ DGI bool t2w_page(const T2JParams &P, const DV &D, const T2WSide &X, T2WLds &L, 
 {
     const uint64_t opts = P.opts;
     const bool b64 = !(opts & DG_T2J_NO_BASE64);
-        T2WTok tk{};
-        if (act) tk = tok[lane];
-        const uint32_t kd = tk.kind & 0xFF;
+        const T2WTok tk = act ? tok[lane] : 0ull;
+        const uint32_t kd = (uint32_t)(tk >> 54) & 63u;
         const uint32_t kind = kd & 7;
-        const uint32_t pos = tk.pos, aux = tk.aux, td = tk.td;
-        const uint32_t kt = tk.kind >> 8;
+        const uint32_t pos = (uint32_t)tk & 0x1FFFFFu, aux = (uint32_t)(tk >> 21) & 0x1FFFFFu;
+        const uint32_t td = (uint32_t)(tk >> 42) & 0xFFFu;
+        const uint32_t kt = (uint32_t)(tk >> 60);
         const bool keyf = act && (kd & TKF_KEYF), keym = act && (kd & TKF_KEYM), comma = act && (kd & TKF_COMMA);
         const bool isval = act && kind == TK_VAL;
         const dg_type vt = ldrec(&D.T[isval ? td : 0u]);
