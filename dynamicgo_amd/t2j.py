@@ -748,3 +748,102 @@ class BinaryConv:
 def new_binary_conv(opts: Optional[Options] = None) -> BinaryConv:
     """t2j.NewBinaryConv (conv/t2j/conv.go:35)."""
     return BinaryConv(opts)
+
+
+# ---------------------------------------------------------------- HTTPConv
+REPLY, EXCEPTION = 2, 3  # thrift.TMessageType (thrift/binary.go:52-57)
+
+
+def unwrap_binary_message(buf: bytes):
+    """thrift.UnwrapBinaryMessage (thrift/binary.go:193-220): (name, type,
+    seqID, the result field's id, its value bytes). Raises ThriftReadError
+    ("invalid version" for a malformed header, as ReadMessageBegin
+    reports every failure)."""
+    rd = _Rd(bytes(buf), 0)
+    try:
+        size = rd.be(4)  # int32
+        if size > 0 or (size & 0xFFFF0000) != 0x80010000:  # VERSION_MASK / VERSION_1
+            raise ThriftReadError("invalid version")
+        typ = size & 0xFF
+        name = bytes(rd.string()).decode("utf-8", "surrogateescape")
+        seq = rd.be(4)
+    except ThriftReadError:
+        raise ThriftReadError("invalid version")
+    t = rd.u8()
+    if t not in (0, 1, 2, 3, 4, 6, 8, 10, 11, 12, 13, 14, 15, 16, 17):
+        raise ThriftReadError("invalid data type")
+    fid = rd.be(2) if t != 0 else 0
+    if t == 0:
+        return name, typ, seq, fid, b""
+    if rd.p > len(rd.b) - 1:
+        raise ThriftReadError("EOF")
+    return name, typ, seq, fid, bytes(rd.b[rd.p:len(rd.b) - 1])
+
+
+class HTTPConv:
+    """t2j.HTTPConv (conv/t2j/http_conv.go:29-122): a Thrift REPLY (or
+    exception) message -> the http.ResponseSetter: mapped fields to headers,
+    cookies and the status code, the JSON body to SetRawBody. The body is
+    converted on the GPU with EnableHttpMapping (BinaryConv above)."""
+
+    def __init__(self, proto: int, fn_desc, conv: Optional[BinaryConv] = None):
+        if proto != H.ENCODING_THRIFT_BINARY:
+            raise ValueError("protocol %r is not supported" % proto)
+        res = fn_desc.response()
+        if res is None or res.struct.field_by_id(0) is None:
+            raise ValueError("response field is not found in function")
+        self.st = res.struct
+        self.conv = conv or BinaryConv()
+
+    def _desc(self, tbytes: bytes):
+        _, typ, _, fid, body = unwrap_binary_message(tbytes)
+        if typ != REPLY:
+            f = self.st.field_by_id(fid)
+            if f is None:
+                raise H.ConvError("ErrUnknownField", "exception field is not foud in function")
+            return f.type, body
+        if fid != 0:
+            raise H.ConvError("ErrInvalidParam", "unexpected response field id %d" % fid)
+        return self.st.field_by_id(0).type, body
+
+    def do_batch(self, resps: Sequence, msgs: Sequence[bytes], opts: Optional[Options] = None):
+        """Do over a batch: errors[i] None or the error; each response gets
+        its body. Messages are grouped by result type, one GPU batch each."""
+        import dataclasses
+        o = dataclasses.replace(opts or Options(), EnableHttpMapping=True)
+        self.conv.set_options(o)
+        n = len(msgs)
+        errs: List[Optional[Exception]] = [None] * n
+        groups: Dict[int, Tuple[object, List[int], List[bytes]]] = {}
+        for i, m in enumerate(msgs):
+            try:
+                td, body = self._desc(m)
+            except ThriftReadError as e:
+                errs[i] = H.ConvError("ErrRead", "", e)
+                continue
+            except H.ConvError as e:
+                errs[i] = e
+                continue
+            g = groups.setdefault(id(td), (td, [], []))
+            g[1].append(i)
+            g[2].append(body)
+        for td, idx, bodies in groups.values():
+            outs, es = self.conv.do_batch_errors(td, bodies, [resps[i] for i in idx])
+            for k, i in enumerate(idx):
+                if es[k] is not None:
+                    errs[i] = es[k]
+                else:
+                    resps[i].set_raw_body(outs[k] or b"")
+        return errs
+
+    def do(self, resp, tbytes: bytes, opts: Optional[Options] = None):
+        """HTTPConv.Do (conv/t2j/http_conv.go:53-85)."""
+        e = self.do_batch([resp], [tbytes], opts)[0]
+        if e is not None:
+            raise e
+
+    def do_into(self, resp, tbytes: bytes, buf: bytearray, opts: Optional[Options] = None):
+        """HTTPConv.DoInto (conv/t2j/http_conv.go:88-122): the body appended
+        to buf as well."""
+        self.do(resp, tbytes, opts)
+        buf.extend(resp.body or b"")

@@ -616,7 +616,8 @@ def test_hm_stops_vs_harness(chk):
 
 @pytest.mark.parametrize("name", ["test_http_mapping_fallback", "test_write_empty", "test_nobody_required_fields",
                                   "test_json_string", "test_kitex_api_header", "test_default_value",
-                                  "test_optional_default_value", "test_conv_thrift2http", "test_errors"])
+                                  "test_optional_default_value", "test_conv_thrift2http", "test_errors",
+                                  "test_http_conv"])
 def test_reference_http_mapping_cases(chk, monkeypatch, name):
     """The reference's t2j HTTP-mapping tests (tests/test_t2j_http.py, there
     over the harness) with the GPU doing the conversion."""

@@ -276,3 +276,49 @@ def test_go_formats():
     assert H.cookie_string("k", b"a b") == 'k="a b"'
     assert H._canon_header("content-type") == "Content-Type"
     assert H._canon_header("bad key") == "bad key"
+
+
+def wrap_binary_body(body: bytes, name: str, typ: int, fid: int, seq: int) -> bytes:
+    """thrift.WrapBinaryBody (thrift/binary.go): message header, the result
+    field's header, the body, STOP."""
+    nb = name.encode()
+    return (struct.pack(">I", 0x80010000 | typ) + struct.pack(">i", len(nb)) + nb + struct.pack(">i", seq) +
+            bytes([12]) + struct.pack(">h", fid) + body + b"\x00")
+
+
+def test_http_conv(chk):
+    """t2j.HTTPConv (conv/t2j/http_conv.go, ExampleHTTPConv_DoInto in
+    conv/t2j/example_test.go:55-86): the REPLY of example3resp.bin; the body
+    equals BinaryConv's with EnableHttpMapping, the headers and cookies are
+    set, the raw body is the JSON. An EXCEPTION reply converts its field's
+    type; a bad header or an unknown exception id errors."""
+    import os
+    g = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    fn = _example3_svc().functions()["ExampleMethod"]
+    data = open(os.path.join(g, "example3resp.bin"), "rb").read()
+    msg = wrap_binary_body(data, "ExampleMethod", t2j.REPLY, 0, 1)
+    assert t2j.unwrap_binary_message(msg) == ("ExampleMethod", t2j.REPLY, 1, 0, data)
+    opts = conv.Options(OmitHttpMappingErrors=True)
+    hc = t2j.HTTPConv(H.ENCODING_THRIFT_BINARY, fn, conv=harness_conv(chk, opts))
+    resp = H.HTTPResponse()
+    buf = bytearray()
+    hc.do_into(resp, msg, buf, opts)
+    want_resp = H.HTTPResponse()
+    want = harness_conv(chk, conv.Options(EnableHttpMapping=True, OmitHttpMappingErrors=True)).do(
+        resp_desc("ExampleMethod"), data, want_resp)
+    assert bytes(buf) == want and resp.body == want
+    assert resp.headers["Heeader"] == want_resp.headers["Heeader"] and resp.cookies() == want_resp.cookies()
+    # an exception reply: field 1 of the result (the declared exception)
+    exc = fld(8, 1, struct.pack(">i", 400)) + fld(11, 255, tstr("boom")) + b"\x00"
+    r2 = H.HTTPResponse()
+    hc.do(r2, wrap_binary_body(exc, "ExampleMethod", t2j.EXCEPTION, 1, 2), opts)
+    assert json.loads(r2.body) == {"code": 400, "msg": "boom"}
+    with pytest.raises(H.ConvError) as ei:
+        hc.do(H.HTTPResponse(), wrap_binary_body(exc, "ExampleMethod", t2j.EXCEPTION, 9, 2), opts)
+    assert ei.value.behavior == "ErrUnknownField"
+    with pytest.raises(H.ConvError) as ei:
+        hc.do(H.HTTPResponse(), wrap_binary_body(data, "ExampleMethod", t2j.REPLY, 3, 1), opts)
+    assert ei.value.behavior == "ErrInvalidParam"
+    with pytest.raises(H.ConvError) as ei:
+        hc.do(H.HTTPResponse(), b"\x00\x00\x00\x05hello", opts)
+    assert ei.value.behavior == "ErrRead"
