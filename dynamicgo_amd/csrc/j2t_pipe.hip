@@ -235,6 +235,7 @@ struct DevBuf {
 
 constexpr int AGG_RING_MAX = 16; /* batches in the ring (dg_agg::ring, DG_AGG_RING, default 8) */
 constexpr int AGG_SLOTS = 256; /* caller threads per aggregator (more convert alone, dg_j2t_do) */
+constexpr int AGG_EAGER_INFLIGHT = 2;
 
 /* one caller thread's part of one batch (its own cache lines) */
 struct alignas(128) Sub {
@@ -303,6 +304,11 @@ struct dg_agg {
     bool stop = false;
     bool asym = false; /* membarrier registered: callers use a compiler fence only */
     std::atomic<uint64_t> batches{0}, msgs{0};
+    /* non-empty batches issued and not yet complete: a batch whose callers
+     * all wait on it is sealed at once only while fewer than
+     * AGG_EAGER_INFLIGHT are (else when the next one completes), so blocking
+     * callers still coalesce while the GPU is busy */
+    std::atomic<int> busy_batches{0};
     /* where the time goes (ns, summed; dg_agg_profile): 0 flusher waiting for
      * a seal, 1 waiting for a free batch, 2 in launch (uploads + kernel
      * issue), 3 completer waiting for the header, 4 for the packed bytes,
@@ -499,6 +505,7 @@ void dg_agg::run_flusher()
         prof[2].fetch_add(x->t_launched - t2, std::memory_order_relaxed);
         prof[5].fetch_add(x->t_launched - t1, std::memory_order_relaxed);
         batches.fetch_add(x->n ? 1 : 0, std::memory_order_relaxed);
+        if (x->n) busy_batches.fetch_add(1, std::memory_order_seq_cst); /* before the completer can see x */
         msgs.fetch_add(x->n, std::memory_order_relaxed);
         {
             std::lock_guard<std::mutex> lk(mu);
@@ -541,6 +548,15 @@ void dg_agg::run_completer()
             x->done_g.store(x->g, std::memory_order_release);
         }
         x->cv.notify_all();
+        if (!empty) {
+            /* room in the pipeline: seal the open batch if all its callers wait on it */
+            busy_batches.fetch_sub(1, std::memory_order_seq_cst);
+            Batch *o = &b[open.load(std::memory_order_seq_cst) % ring];
+            const uint32_t parts = o->parts.load(std::memory_order_seq_cst);
+            if (parts && o->blocked.load(std::memory_order_seq_cst) >= parts &&
+                !o->seal_req.exchange(1, std::memory_order_acq_rel))
+                wake_flusher();
+        }
         if (empty) {
             std::lock_guard<std::mutex> lk(mu);
             x->free_ = true;
@@ -729,7 +745,8 @@ int dg_agg_wait(dg_agg *a, dg_agg_ticket *t, uint8_t *out, size_t out_cap, size_
         /* waiting on the open batch: once every thread with a message in it
          * waits on it, nothing more will come from them, so seal it now */
         if (a->open.load(std::memory_order_acquire) == t->gen &&
-            x->blocked.fetch_add(1, std::memory_order_acq_rel) + 1 >= x->parts.load(std::memory_order_acquire) &&
+            x->blocked.fetch_add(1, std::memory_order_seq_cst) + 1 >= x->parts.load(std::memory_order_seq_cst) &&
+            a->busy_batches.load(std::memory_order_seq_cst) < AGG_EAGER_INFLIGHT &&
             !x->seal_req.exchange(1, std::memory_order_acq_rel))
             a->wake_flusher();
         if (x->done_g.load(std::memory_order_acquire) < t->gen) {
