@@ -235,7 +235,7 @@ struct DevBuf {
 
 constexpr int AGG_RING_MAX = 16; /* batches in the ring (dg_agg::ring, DG_AGG_RING, default 8) */
 constexpr int AGG_SLOTS = 256; /* caller threads per aggregator (more convert alone, dg_j2t_do) */
-constexpr int AGG_EAGER_INFLIGHT = 2;
+constexpr int AGG_EAGER_INFLIGHT = 1;
 
 /* one caller thread's part of one batch (its own cache lines) */
 struct alignas(128) Sub {
