@@ -553,9 +553,10 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
             const uint64_t n64 = b - a;
             oa = P.out_off[i];
             cap = (uint32_t)min(P.out_off[i + 1] - oa, (uint64_t)0xFFFFFFFFu);
-            if (P.big_list && (n64 > P.big_max || n64 > FL_MAXLEN)) { /* the wave kernel */
+            const bool tobig = P.big_list && (n64 > P.big_max || n64 > FL_MAXLEN);
+            list_big_w(P, tobig, i, n64); /* the wave kernel */
+            if (tobig) {
                 big = 1;
-                list_big(P, i, n64);
             } else if (n64 > 0 && n64 <= FL_MAXLEN) {
                 n = (uint32_t)n64;
                 if (staged) {

@@ -104,11 +104,8 @@ __global__ __launch_bounds__(64 * SM_WAVES) __attribute__((amdgpu_waves_per_eu(D
             for (uint32_t k = 0; k < wc; k++) stage[wbase + k] = g[k];
         }
     }
-    if (!mine) return;
-    if (big) {
-        list_big(P, i, b - a);
-        return;
-    }
+    list_big_w(P, big, i, b - a);
+    if (!mine || big) return;
     const auto dv = desc_view<3>((const __attribute__((address_space(3))) uint8_t *)(void *)ldesc, S.hdr);
     const uint64_t oa = P.out_off[i], ob = P.out_off[i + 1];
     Out out;

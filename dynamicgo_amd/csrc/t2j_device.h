@@ -384,8 +384,100 @@ DGI int32_t t2j_field(const DV &D, const dg_struct &sd, uint32_t hint, uint16_t 
     return -1;
 }
 
+/* JSON output of one lane: Out's 8-byte word assembly, with completed words
+ * stored in aligned 16-byte pairs (one dwordx4 store per lane per 16 bytes,
+ * the width the L2 write counters and write-back handle whole; 8-byte stores
+ * of 64 lanes into 64 slots showed as 29.9 MB written on t2j-c2 for 13.6 MB
+ * of JSON). The first word of a pair waits in `wlo`. */
+struct JOut {
+    typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+    gu8 *b;
+    uint64_t cap;
+    uint64_t len;
+    uint64_t wbuf;  /* the word holding position len */
+    uint64_t wlo;   /* the completed first word of the pair holding len */
+    uint32_t sk;    /* the slot's first word within its 16-byte pair (0 or 1) */
+    bool wide;      /* slot base 8-aligned: word and pair stores allowed */
+
+    DGI void init(uint8_t *base, uint64_t c)
+    {
+        b = (gu8 *)(void *)base;
+        cap = c;
+        len = 0;
+        wbuf = wlo = 0;
+        wide = ((uintptr_t)base & 7) == 0;
+        sk = wide ? (uint32_t)(((uintptr_t)base >> 3) & 1) : 0u;
+    }
+    DGI void store_word(uint64_t wi, uint64_t v)
+    {
+        const uint64_t a = wi << 3;
+        if (wide && a + 8 <= cap) *(gu64 *)(b + a) = v;
+        else if (a < cap) Out::store_bytes(b, a, cap, v);
+    }
+    DGI uint64_t load_word(uint64_t wi) const
+    {
+        const uint64_t a = wi << 3;
+        if (wide && a + 8 <= cap) return *(const gu64 *)(b + a);
+        return a < cap ? Out::load_bytes(b, a, cap) : 0;
+    }
+    static __device__ __noinline__ void pair_edge(gu8 *b, uint64_t cap, bool wide, uint64_t wi, uint64_t w0, uint64_t w1)
+    {
+        for (uint32_t j = 0; j < 2; j++) {
+            if (wi + j < 1) continue;
+            const uint64_t a = (wi + j - 1) << 3, v = j ? w1 : w0;
+            if (wide && a + 8 <= cap) *(gu64 *)(b + a) = v;
+            else if (a < cap) Out::store_bytes(b, a, cap, v);
+        }
+    }
+    DGI void wle(uint64_t v, uint32_t n)
+    {
+        const uint32_t used = (uint32_t)(len & 7);
+        const uint32_t sh = used << 3;
+        if (n < 8) v &= (1ull << (n << 3)) - 1;
+        const uint64_t lo = (wbuf & ((1ull << sh) - 1)) | (v << sh);
+        const uint64_t hi = used ? (v >> (64 - sh)) : 0;
+        const uint64_t wi = len >> 3;
+        len += n;
+        if (used + n >= 8) {
+            if (((sk + (uint32_t)wi) & 1) == 0) {
+                wlo = lo;
+            } else if (wide && wi >= 1 && (wi + 1) * 8 <= cap) {
+                u64x2 p;
+                p.x = wlo;
+                p.y = lo;
+                *(__attribute__((address_space(1))) u64x2 *)(void *)(b + (wi - 1) * 8) = p; /* 16-byte aligned */
+            } else {
+                pair_edge(b, cap, wide, wi, wlo, lo);
+            }
+            wbuf = hi;
+        } else {
+            wbuf = lo;
+        }
+    }
+    DGI void w8(uint8_t v) { wle(v, 1); }
+    /* truncate to x <= len */
+    DGI void set_len(uint64_t x)
+    {
+        const uint64_t xw = x >> 3, lw = len >> 3;
+        if (((sk + xw) >> 1) != ((sk + lw) >> 1)) { /* x's pair is stored already: take it back */
+            if (((sk + (uint32_t)xw) & 1) && xw >= 1) wlo = load_word(xw - 1);
+            wbuf = (x & 7) ? load_word(xw) : 0;
+        } else if (xw != lw) {
+            wbuf = (x & 7) ? wlo : 0;
+        }
+        len = x;
+    }
+    /* the waiting first word of the open pair, and the partial word */
+    DGI void finish()
+    {
+        const uint64_t lw = len >> 3;
+        if (((sk + (uint32_t)lw) & 1) && lw >= 1) store_word(lw - 1, wlo);
+        if (len & 7) store_word(lw, wbuf);
+    }
+};
+
 /* side-table bytes [off, off+len) (8-aligned, 16 readable past the end) */
-DGI void emit_side(Out &o, const T2JSide &X, uint32_t off, uint32_t len)
+DGI void emit_side(JOut &o, const T2JSide &X, uint32_t off, uint32_t len)
 {
     const __attribute__((address_space(1))) uint64_t *w = (const __attribute__((address_space(1))) uint64_t *)(X.P + off);
     uint32_t i = 0;
@@ -411,7 +503,7 @@ DGI uint32_t num_bytes(uint8_t tt)
  * (thrift/idl.go:834-955: EncodeInt64 / EncodeFloat64 / EncodeString /
  * true|false), from its Thrift bytes in the descriptor pool */
 template <class DV>
-DGI void emit_default(Out &o, const DV &D, const dg_field &fd, uint8_t tt)
+DGI void emit_default(JOut &o, const DV &D, const dg_field &fd, uint8_t tt)
 {
     auto byte = [&](uint32_t k) -> uint64_t { return (uint8_t)D.P[fd.dflt_off + k]; };
     if (tt == DG_T_BOOL) {
@@ -445,7 +537,7 @@ DGI void emit_default(Out &o, const DV &D, const dg_field &fd, uint8_t tt)
  * DG_T2J_SKIP_RESP_BASE, DG_T2J_HM); the plain instance keeps the lane
  * kernel's registers at occupancy 4 (113 vs 139 VGPRs) */
 template <bool GO, class S, class FP, class DV>
-DGI uint64_t t2j_convert(const DV &D, const T2JSide &X, S src, uint32_t root, uint64_t opts, Out &o, FP fr,
+DGI uint64_t t2j_convert(const DV &D, const T2JSide &X, S src, uint32_t root, uint64_t opts, JOut &o, FP fr,
                          uint32_t fstride, uint32_t cap, gu64 *wide = nullptr, uint32_t widecap = 0,
                          uint64_t *aux = nullptr, const dg_cb_entry *ans = nullptr, const uint8_t *ans_bytes = nullptr)
 {
@@ -1031,7 +1123,7 @@ DGI T2JSide t2j_side(const uint8_t *side)
 }
 
 /* finish one message: overflow check, status and length */
-DGI void t2j_store(const T2JParams &P, uint64_t i, uint64_t r, Out &o)
+DGI void t2j_store(const T2JParams &P, uint64_t i, uint64_t r, JOut &o)
 {
     uint32_t olen = 0;
     if (r == 0 || (uint8_t)r == DG_T2J_E_EXCEPTION || (uint8_t)r == DG_T2J_E_CALLBACK) { /* kept: the exception's JSON, the stop's record */

@@ -24,13 +24,12 @@ __global__ __launch_bounds__(T2J_BLOCK) void t2j_kernel(T2JParams P)
     for (uint64_t k = (uint64_t)blockIdx.x * MPB + slot; k < cnt; k += (uint64_t)gridDim.x * MPB) {
         const uint64_t i = P.list ? (uint64_t)P.list[k] : k;
         const uint64_t a = P.in_off[i], b = P.in_off[i + 1];
-        if (P.big_list && b - a > P.big_min) { /* the wave kernel takes it */
-            P.big_list[atomicAdd(P.big_count, 1u)] = (uint32_t)i;
-            continue;
-        }
+        const bool big = P.big_list && b - a > P.big_min;
+        wave_push(P.big_list, P.big_count, big, (uint32_t)i); /* the wave kernel takes it */
+        if (big) continue;
         SrcT<glb_u64> s;
         s.init((glb_u64 *)(const void *)(P.src + (a & ~7ull)), (int64_t)(a & 7), (int64_t)(b - a));
-        Out o;
+        JOut o;
         o.init(P.out + P.out_off[i], P.out_off[i + 1] - P.out_off[i]);
         const uint64_t r = t2j_convert<GO>(D, X, s, P.root, P.opts, o,
                                        (__attribute__((address_space(3))) T2JFrame *)(void *)&lf[slot], MPB,
@@ -123,7 +122,7 @@ __global__ __launch_bounds__(T2J_BLOCK) void t2j_deep_kernel(T2JParams P)
         const uint64_t a = P.in_off[i], b = P.in_off[i + 1];
         SrcT<glb_u64> s;
         s.init((glb_u64 *)(const void *)(P.src + (a & ~7ull)), (int64_t)(a & 7), (int64_t)(b - a));
-        Out o;
+        JOut o;
         o.init(P.out + P.out_off[i], P.out_off[i + 1] - P.out_off[i]);
         uint64_t r = t2j_convert<GO>(D, X, s, P.root, P.opts, o, fr, 1, T2J_DEEP_DEPTH, wide, T2J_WIDE_WORDS,
                                  P.aux ? P.aux + i : nullptr, P.ans_tab ? P.ans_tab + i : nullptr, P.ans_bytes);
