@@ -61,7 +61,11 @@ static int scratch_new(dg_ctx *c, hipStream_t owner, Scratch **out)
     x->owner = owner;
     hipError_t e = hipEventCreateWithFlags(&x->done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipMalloc(&x->d_counts, DG_NCOUNTS * 4);
-    if (e == hipSuccess) e = hipMemset(x->d_counts, 0, DG_NCOUNTS * 4);
+    /* ordered before the owner stream's launches: a plain hipMemset runs on
+     * the null stream, which a non-blocking stream (the aggregator's) does
+     * not wait for -- its first batch then read uninitialised list counters
+     * and left messages unconverted (ret 0, no bytes) */
+    if (e == hipSuccess) e = hipMemsetAsync(x->d_counts, 0, DG_NCOUNTS * 4, owner);
     if (e == hipSuccess) e = hipMalloc(&x->ws_deep, DEEP_WS_STRIDE * DEEP_THREADS);
     if (e == hipSuccess) e = hipMalloc(&x->ws_wave, (size_t)c->n_cu * std::max(WV_BLOCKS_PER_CU, WV5_BLOCKS_PER_CU) * WV_WAVES * DCAP);
     if (e == hipSuccess) e = hipMalloc(&x->d_sums, (size_t)c->n_cu * 8);
@@ -140,6 +144,7 @@ int dg_ctx_create(int device, dg_ctx **out)
     HIPCHK(hipMemset(c->d_zero, 0, 16));
     HIPCHK(hipMalloc(&c->d_stats, 16 * 8));
     HIPCHK(hipMemset(c->d_stats, 0, 16 * 8));
+    HIPCHK(hipDeviceSynchronize()); /* the memsets done before any stream (blocking or not) uses the buffers */
     HIPCHK(hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device));
     /* routing knobs: the environment is read here, once per context */
     static const struct { const char *env; const char *name; } envk[] = {
@@ -345,7 +350,10 @@ int dg_ctx_stats(dg_ctx *c, uint64_t *bails, uint64_t *deeps, int reset)
     HIPCHK(hipMemcpy(h, c->d_stats, sizeof h, hipMemcpyDeviceToHost));
     if (bails) *bails = h[0];
     if (deeps) *deeps = h[1];
-    if (reset) HIPCHK(hipMemset(c->d_stats, 0, sizeof h));
+    if (reset) {
+        HIPCHK(hipMemset(c->d_stats, 0, sizeof h));
+        HIPCHK(hipDeviceSynchronize());
+    }
     return DG_OK;
 }
 
@@ -356,7 +364,10 @@ int dg_ctx_counters(dg_ctx *c, uint64_t *out, int n, int reset)
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpy(out, c->d_stats, (size_t)n * 8, hipMemcpyDeviceToHost));
-    if (reset) HIPCHK(hipMemset(c->d_stats, 0, 16 * 8));
+    if (reset) {
+        HIPCHK(hipMemset(c->d_stats, 0, 16 * 8));
+        HIPCHK(hipDeviceSynchronize());
+    }
     return DG_OK;
 }
 

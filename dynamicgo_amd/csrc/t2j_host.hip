@@ -158,6 +158,7 @@ int dg_desc_attach_t2j(dg_desc *d, const void *side, size_t len)
     HIPCHK(hipMalloc(&p, len + 16)); /* the kernel reads whole words past a key's end */
     HIPCHK(hipMemcpy(p, side, len, hipMemcpyHostToDevice));
     HIPCHK(hipMemset(p + len, 0, 16));
+    HIPCHK(hipDeviceSynchronize()); /* before launches on non-blocking streams read it */
     if (d->d_side) {
         HIPCHK(hipDeviceSynchronize()); /* launches in flight may read the old table */
         (void)hipFree(d->d_side);

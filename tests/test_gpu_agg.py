@@ -211,3 +211,22 @@ def test_aggregator_parts_return_at_thread_exit():
     agg.close()
     assert prof[11] == 0, prof
     assert got == [chk.j2t(fl, m, 1)[1] for m in msgs]
+
+
+def test_aggregator_fresh_contexts_first_batches():
+    """The first batches on a fresh context's streams: the per-stream list
+    counters must be zero before the aggregator's non-blocking streams use
+    them (a null-stream hipMemset was not ordered before those launches, and
+    the first batches left some messages unconverted: ret 0, no bytes)."""
+    td = W.nesting_i64_desc()
+    fl = T.flatten(td)
+    chk = oracle.RefOracle() or oracle.PortOracle()
+    msgs = W.gen_nested_batch(random.Random(9), 600)
+    want = [chk.j2t(fl, m, 1)[1] for m in msgs]
+    for rep in range(3):
+        ctx = conv.Context(0)
+        agg = conv.Aggregator(td, conv.Options(), max_batch=64, max_wait_us=200, ctx=ctx)
+        outs, rets, _, _ = agg.drive(msgs, threads=16, window=16)
+        agg.close()
+        assert [int(r) for r in rets] == [0] * len(msgs)
+        assert outs == want, rep
