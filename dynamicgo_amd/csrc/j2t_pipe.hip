@@ -131,14 +131,15 @@ __global__ __launch_bounds__(256) void agg_gather_kernel(const SubRef *tab, uint
     }
 }
 
-/* out_off of a chunk [a, a + m) of a host batch, from its raw offsets, and
- * the 64 zero bytes after its JSON */
+/* out_off of a chunk [a, a + m) of a host batch, from its raw offsets (in
+ * device or pinned host memory), and the 64 zero bytes after its staged JSON
+ * (pad; NULL when the kernels read the caller's pinned JSON in place) */
 __global__ __launch_bounds__(256) void pipe_slots_kernel(const uint64_t *in_off, uint64_t m, uint64_t *out_off,
                                                          uint8_t *pad)
 {
     const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (j <= m) out_off[j] = slot_off(in_off[j] - in_off[0], j);
-    if (blockIdx.x == 0 && threadIdx.x < 8) ((uint64_t *)(void *)pad)[threadIdx.x] = 0;
+    if (pad && blockIdx.x == 0 && threadIdx.x < 8) ((uint64_t *)(void *)pad)[threadIdx.x] = 0;
 }
 
 /* A chunk's results into pinned host memory, after the previous chunk's:
@@ -912,6 +913,16 @@ int dg_j2t_pipeline_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8
         p_ret = p_off + n + 1;
     }
     const uint32_t phase = (uint32_t)((uintptr_t)p_out & 15);
+    /* zero copy: when the JSON arena (with the 16 readable bytes past its end
+     * the kernels may touch) and the offsets are pinned, the kernels read
+     * them over the link themselves -- no hipMemcpyAsync per chunk, and the
+     * next chunk's reads overlap the previous chunk's copy-out */
+    void *dv_json = nullptr, *dv_end = nullptr, *dv_in = nullptr, *dv_in_end = nullptr;
+    const uint64_t jend = in_off[n] + 15;
+    const bool zc = host_pinned(json, &dv_json) && host_pinned(json + jend, &dv_end) &&
+                    (uint8_t *)dv_end - (uint8_t *)dv_json == (ptrdiff_t)jend && host_pinned(in_off, &dv_in) &&
+                    host_pinned(in_off + n, &dv_in_end) && (uint64_t *)dv_in_end - (uint64_t *)dv_in == (ptrdiff_t)n &&
+                    !getenv("DG_NO_ZERO_COPY");
     for (uint32_t k = 0; k < chunks; k++) {
         PipeBuf &p = *(PipeBuf *)c->pipe[k % nb];
         const uint64_t a = cb[k], m = cb[k + 1] - a, base = in_off[a], jb = base & ~15ull;
@@ -926,15 +937,26 @@ int dg_j2t_pipeline_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8
         uint64_t *d_in = p.dv.d_off, *d_oo = d_in + m + 1;
         uint64_t *d_po = (uint64_t *)(void *)p.d_packed;
         uint8_t *d_pk = p.d_packed + ((8 * (m + 1) + 15) & ~15ull);
-        HIPCHK(hipMemcpyAsync(d_in, in_off + a, 8 * (m + 1), hipMemcpyHostToDevice, p.s));
-        if (span) HIPCHK(hipMemcpyAsync(p.dv.d_json, json + jb, span, hipMemcpyHostToDevice, p.s));
-        hipLaunchKernelGGL(pipe_slots_kernel, dim3((uint32_t)((m + 256) / 256)), dim3(256), 0, p.s, d_in, m, d_oo,
-                           p.dv.d_json + span);
+        const uint8_t *j_base; /* the JSON the kernels read, in_off-relative */
+        const uint64_t *j_in;
+        if (zc) {
+            j_base = (const uint8_t *)dv_json;
+            j_in = (const uint64_t *)dv_in + a;
+            hipLaunchKernelGGL(pipe_slots_kernel, dim3((uint32_t)((m + 256) / 256)), dim3(256), 0, p.s, j_in, m, d_oo,
+                               (uint8_t *)nullptr);
+        } else {
+            HIPCHK(hipMemcpyAsync(d_in, in_off + a, 8 * (m + 1), hipMemcpyHostToDevice, p.s));
+            if (span) HIPCHK(hipMemcpyAsync(p.dv.d_json, json + jb, span, hipMemcpyHostToDevice, p.s));
+            hipLaunchKernelGGL(pipe_slots_kernel, dim3((uint32_t)((m + 256) / 256)), dim3(256), 0, p.s, d_in, m, d_oo,
+                               p.dv.d_json + span);
+            j_base = p.dv.d_json - jb;
+            j_in = d_in;
+        }
         HIPCHK(hipGetLastError());
         /* the packing needs the previous chunk's end (written by its copy-out) */
         PipeBuf *prev = k ? (PipeBuf *)c->pipe[(k - 1) % nb] : nullptr;
         const uint64_t *base_ptr = k ? p_off + a : nullptr;
-        if ((rc = dg_i_convert_pack(c, d, root, p.dv.d_json - jb, d_in, m, flags, p.dv.d_out, d_oo, p.dv.d_ol,
+        if ((rc = dg_i_convert_pack(c, d, root, j_base, j_in, m, flags, p.dv.d_out, d_oo, p.dv.d_ol,
                                     p.dv.d_ret, d_pk, d_po, p.s, max_len, base_ptr ? base_ptr : c->d_zero, 0,
                                     prev ? prev->ev_hdr : nullptr, 1 | (int)(phase << 1))))
             return rc;

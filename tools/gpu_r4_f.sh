@@ -8,8 +8,9 @@ trap "kill $HB 2>/dev/null" EXIT
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/gputest.log 2>&1 || { tail -40 $O/gputest.log; exit 1; }
 tail -1 $O/gputest.log
 for c in c2 c3 c5 t2j-c2 t2j-c3; do
-  timeout -k 10 300 python -u bench.py --config $c --steps 10 --warmup 3 --no-cpu-baseline --no-e2e > $O/$c.json 2> $O/$c.err || { tail -20 $O/$c.err; exit 1; }
-  python -c "import json;d=json.loads(open('$O/$c.json').read().strip().splitlines()[-1]);print('$c',d['value'],d['ms_per_step'],d['roofline']['kernel_ms'])"
+  E=--no-e2e; [ $c = c2 ] && E=
+  timeout -k 10 300 python -u bench.py --config $c --steps 10 --warmup 3 --no-cpu-baseline $E > $O/$c.json 2> $O/$c.err || { tail -20 $O/$c.err; exit 1; }
+  python -c "import json;d=json.loads(open('$O/$c.json').read().strip().splitlines()[-1]);print('$c',d['value'],d['ms_per_step'],d['roofline']['kernel_ms'],d.get('e2e_host'))"
 done
 timeout -k 10 400 python -u bench.py --config agg --steps 5 --warmup 2 > $O/agg.json 2> $O/agg.err || { tail -20 $O/agg.err; exit 1; }
 python -c "import json;d=json.loads(open('$O/agg.json').read().strip().splitlines()[-1]);print('agg',d['value'],d['cpu_baseline'] and (d['cpu_baseline']['value'], d['cpu_baseline']['share']),[ (r['threads'],r['msgs_per_s'],r['avg_batch'],r['lat_us_p50']) for r in d['config']['runs']])"
