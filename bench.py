@@ -390,7 +390,7 @@ def bench_t2j(args, rank, world, dev, dist, backend, td, arena, off, meta):
     n = len(off) - 1
     lens = np.diff(off).astype(np.int64)
     slots = np.zeros(n + 1, dtype=np.int64)
-    np.cumsum((lens * 4 + 64 + 7) & ~7, out=slots[1:])
+    np.cumsum((lens * 4 + 64 + 127) & ~127, out=slots[1:])  # dg_slot_bound
     d_json = torch.from_numpy(arena).to(dev)
     d_in = torch.from_numpy(off.astype(np.int64)).to(dev)
     d_j2t = torch.empty(int(slots[-1]) + 64, dtype=torch.uint8, device=dev)
@@ -414,7 +414,7 @@ def bench_t2j(args, rank, world, dev, dist, backend, td, arena, off, meta):
     h_thrift = d_thrift[:thrift_bytes + 64].cpu().numpy()
     tl = np.diff(toff).astype(np.int64)
     jslots = np.zeros(n + 1, dtype=np.int64)
-    np.cumsum((tl * 3 + 64 + 7) & ~7, out=jslots[1:])  # dg_t2j_slot_bound
+    np.cumsum((tl * 3 + 64 + 127) & ~127, out=jslots[1:])  # dg_t2j_slot_bound: 128-byte slots
     t_max = int(tl.max()) if n else 0  # the longest Thrift message: picks the kernel's lanes per message
     del d_j2t, d_json
     d_out = torch.empty(int(jslots[-1]) + 64, dtype=torch.uint8, device=dev)
@@ -600,8 +600,8 @@ def bench_agg(args, rank, world, dev, dist, backend, td, arena, off, meta):
         b = C.c_uint64(0)
         tot = C.c_uint64(0)
         _lib.check(L.dg_agg_stats(h, C.byref(b), C.byref(tot)))
-        pr = (C.c_uint64 * 12)()
-        _lib.check(L.dg_agg_profile(h, pr, 11))
+        pr = (C.c_uint64 * 16)()
+        _lib.check(L.dg_agg_profile(h, pr, 16))
         nb_ = max(1, b.value)
         prof = {k: round(pr[i] / nb_ / 1e3, 1) for i, k in enumerate(
             ("flusher_wait_seal", "flusher_wait_free", "flusher_issue", "completer_wait_hdr", "completer_wait_data",
@@ -610,6 +610,9 @@ def bench_agg(args, rank, world, dev, dist, backend, td, arena, off, meta):
         prof["ns_per_call_in_submit"] = round(pr[8] / ncalls, 1)
         prof["ns_per_call_in_wait"] = round(pr[9] / ncalls, 1)
         prof["submits_without_open_batch"] = int(pr[10])
+        prof["calls_converted_alone"] = int(pr[11])
+        for i, k in enumerate(("issue_wait_writers", "issue_buffers", "issue_gather", "issue_convert")):
+            prof[k] = round(pr[12 + i] / nb_ / 1e3, 1)
         L.dg_agg_destroy(h)
         lt = lat[:m][lat[:m] > 0].astype(np.float64) / 1e3  # every 8th call is timed (dg_agg_drive)
         runs.append({"threads": threads, "in_flight_per_thread": window, "per_thread_batch_share": per_thread,
@@ -746,7 +749,7 @@ def main(argv=None):
     lens = np.diff(off).astype(np.int64)
     max_len = int(lens.max()) if n else 0  # known to the host that built the arena (dg_j2t_batch_device_ml)
     slots = np.zeros(n + 1, dtype=np.int64)
-    np.cumsum((lens * 4 + 64 + 7) & ~7, out=slots[1:])  # dg_slot_bound: 8-aligned slots
+    np.cumsum((lens * 4 + 64 + 127) & ~127, out=slots[1:])  # dg_slot_bound: 128-byte slots (whole L2 lines)
     d_json = torch.from_numpy(arena).to(dev)
     d_in = torch.from_numpy(off.astype(np.int64)).to(dev)
     d_out = torch.empty(int(slots[-1]) + 64, dtype=torch.uint8, device=dev)

@@ -749,10 +749,10 @@ class Aggregator:
         return int(b.value), int(m.value)
 
     def profile(self) -> List[int]:
-        """dg_agg_profile's 12 counters (include/dgj2t.h); [11]: calls
+        """dg_agg_profile's 16 counters (include/dgj2t.h); [11]: calls
         converted alone (no part for their thread, or longer than a part)."""
-        out = (C.c_uint64 * 12)()
-        _lib.check(_lib.lib().dg_agg_profile(self.h, out, 12))
+        out = (C.c_uint64 * 16)()
+        _lib.check(_lib.lib().dg_agg_profile(self.h, out, 16))
         return [int(v) for v in out]
 
     def close(self):

@@ -371,7 +371,10 @@ int dg_ctx_counters(dg_ctx *c, uint64_t *out, int n, int reset)
     return DG_OK;
 }
 
-uint64_t dg_slot_bound(uint64_t len) { return (4 * len + 64 + 7) & ~7ull; }
+/* slots start at 128-byte boundaries: the L2 writes a partly written line
+ * back whole, so an output that straddles a line boundary it did not need
+ * to costs a line (C2: one line per message instead of two) */
+uint64_t dg_slot_bound(uint64_t len) { return (4 * len + 64 + 127) & ~127ull; }
 
 static int ensure_fast_ws(Scratch *x, uint64_t lanes)
 {

@@ -316,7 +316,7 @@ struct dg_agg {
      * 5 seal-to-launched, 6 launched-to-done, 7 callers blocked in wait;
      * dg_agg_drive: 8 in submit, 9 in wait, 10 submits that met no open
      * batch */
-    std::atomic<uint64_t> prof[12] = {};
+    std::atomic<uint64_t> prof[16] = {}; /* 12-15: launch()'s parts: busy flags, buffers, gather issue, convert issue */
     std::thread flusher, completer;
 
     static uint64_t now_ns()
@@ -399,6 +399,7 @@ int dg_agg::launch(Batch *x)
     const int ns = nslots.load(std::memory_order_seq_cst);
     uint32_t nsub = 0;
     uint64_t N = 0, B = 0;
+    const uint64_t l0 = now_ns();
     for (int s = 0; s < ns; s++) {
         Sub &u = x->sub[s];
         while (u.busy.load(std::memory_order_seq_cst)) std::this_thread::yield();
@@ -414,6 +415,8 @@ int dg_agg::launch(Batch *x)
     x->bytes = B;
     x->rc = DG_OK;
     x->active.store(nsub, std::memory_order_release);
+    const uint64_t l1 = now_ns();
+    prof[12].fetch_add(l1 - l0, std::memory_order_relaxed);
     if (!N) return DG_OK;
     HIPCHK(hipSetDevice(ctx->device));
     int rc;
@@ -430,12 +433,19 @@ int dg_agg::launch(Batch *x)
     for (uint32_t k = 0; k < nsub; k++) maxb = std::max<uint64_t>(maxb, x->h_tab[k].bytes);
     const uint32_t gy = (uint32_t)std::max<uint64_t>(1, (maxb + AGG_GATHER_BYTES - 1) / AGG_GATHER_BYTES);
     uint64_t *d_in = x->dv.d_off, *d_oo = d_in + N + 1;
+    const uint64_t l2 = now_ns();
     hipLaunchKernelGGL(agg_gather_kernel, dim3(nsub, gy), dim3(256), 0, x->s, x->h_tab, (uint64_t)cap_n,
                        x->dv.d_json, N, B, d_in, d_oo);
     HIPCHK(hipGetLastError());
+    const uint64_t l3 = now_ns();
     uint64_t *h_ret = (uint64_t *)(void *)x->h_hdr;
-    return x->dv.convert(ctx, desc, root, flags, N, x->dv.d_json, d_in, d_oo, max_len, x->s, h_ret, x->h_packed,
-                         h_ret + N, nullptr, 0, nullptr, x->ev_hdr);
+    rc = x->dv.convert(ctx, desc, root, flags, N, x->dv.d_json, d_in, d_oo, max_len, x->s, h_ret, x->h_packed,
+                       h_ret + N, nullptr, 0, nullptr, x->ev_hdr);
+    const uint64_t l4 = now_ns();
+    prof[13].fetch_add(l2 - l1, std::memory_order_relaxed);
+    prof[14].fetch_add(l3 - l2, std::memory_order_relaxed);
+    prof[15].fetch_add(l4 - l3, std::memory_order_relaxed);
+    return rc;
 }
 
 void dg_agg::run_flusher()
@@ -812,7 +822,7 @@ int dg_agg_stats(dg_agg *a, uint64_t *batches, uint64_t *msgs)
 
 int dg_agg_profile(dg_agg *a, uint64_t *out, int n)
 {
-    if (!a || !out || n < 0 || n > 12) return set_err(DG_E_INVALID, "bad args");
+    if (!a || !out || n < 0 || n > 16) return set_err(DG_E_INVALID, "bad args");
     for (int i = 0; i < n; i++) out[i] = a->prof[i].load();
     return DG_OK;
 }

@@ -168,7 +168,9 @@ int dg_desc_attach_t2j(dg_desc *d, const void *side, size_t len)
     return DG_OK;
 }
 
-uint64_t dg_t2j_slot_bound(uint64_t len) { return (3 * len + 64 + 7) & ~7ull; }
+/* 128-byte slots, like dg_slot_bound: t2j-c2's writes were 380 B per
+ * message (every line its 208 B of JSON touched) at 8-byte alignment */
+uint64_t dg_t2j_slot_bound(uint64_t len) { return (3 * len + 64 + 127) & ~127ull; }
 
 int dg_t2j_batch_device_ml(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *d_thrift,
                            const uint64_t *d_in_off, uint64_t n, uint64_t opts, uint8_t *d_out,

@@ -182,7 +182,9 @@ int dg_j2t_batch_device_inflight(dg_ctx *ctx, const dg_desc *desc, uint32_t root
                                  const uint64_t *d_in_off, uint64_t n, uint64_t flags, const uint64_t *d_out_off,
                                  const dg_out_set *sets, int depth, void *stream, uint64_t max_len, int iters);
 
-/* Output-slot size the device path uses by default for a message of len bytes. */
+/* Output-slot size the device path uses by default for a message of len
+ * bytes: 4 len + 64 rounded up to 128 (slots on L2-line boundaries: a line
+ * written in part is written back whole). */
 uint64_t dg_slot_bound(uint64_t len);
 
 /*
@@ -288,12 +290,14 @@ int dg_agg_wait(dg_agg *agg, dg_agg_ticket *t, uint8_t *out, size_t out_cap, siz
 int dg_agg_ready(dg_agg *agg, const dg_agg_ticket *t);
 /* batches flushed and messages converted so far */
 int dg_agg_stats(dg_agg *agg, uint64_t *batches, uint64_t *msgs);
-/* diagnostics: n <= 12 summed counters (ns unless noted) (flusher waiting for a seal,
+/* diagnostics: n <= 16 summed counters (ns unless noted) (flusher waiting for a seal,
  * for a free batch, issuing a batch; completer waiting for the header, for
  * the packed bytes; seal to issued; issued to done; callers blocked in
  * dg_agg_wait; dg_agg_drive: time in submit, in wait, and the count of
  * submits that met no open batch; the count of calls converted alone by
- * dg_j2t_do: longer than a part, or no part left for their thread).
+ * dg_j2t_do: longer than a part, or no part left for their thread; the
+ * flusher's issue split in four: waiting for the parts' writers, buffers,
+ * the gather launch, the conversion's launches).
  * A part (one of 256) belongs to a calling thread from its first call until
  * the thread exits; an exited thread's part goes to the next new thread. */
 int dg_agg_profile(dg_agg *agg, uint64_t *out, int n);
@@ -337,9 +341,9 @@ int dg_j2t_pipeline_host(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, c
  * 4096 frames per message; deeper still is DG_T2J_E_DEPTH.
  */
 int dg_desc_attach_t2j(dg_desc *desc, const void *side, size_t len);
-/* the slot size the host entry point gives a message of len Thrift bytes
- * (a guess: JSON has no fixed bound over Thrift; larger outputs overflow and
- * are rerun with their exact size) */
+/* the slot size the host entry point gives a message of len Thrift bytes:
+ * 3 len + 64 rounded up to 128 (a guess: JSON has no fixed bound over Thrift;
+ * larger outputs overflow and are rerun with their exact size) */
 uint64_t dg_t2j_slot_bound(uint64_t len);
 /* device buffers, stream-ordered, async; arena readable 16 bytes past the
  * last message; d_out_off 8-aligned slots */
