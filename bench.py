@@ -588,6 +588,10 @@ def bench_agg(args, rank, world, dev, dist, backend, td, arena, off, meta):
         m = n if window > 1 else min(n, 16384)  # one call in flight per thread: latency-bound, a shorter pass
         for _ in range(max(1, args.warmup // 2)):
             step(m)
+        # the profile counts from here: buffer growth in the warm-up is not the steady state
+        b0, tot0, pr0 = C.c_uint64(0), C.c_uint64(0), (C.c_uint64 * 16)()
+        _lib.check(L.dg_agg_stats(h, C.byref(b0), C.byref(tot0)))
+        _lib.check(L.dg_agg_profile(h, pr0, 16))
         steps = args.steps if ri == 0 else max(2, args.steps // 4)
         if dist:
             torch.distributed.barrier()
@@ -602,11 +606,12 @@ def bench_agg(args, rank, world, dev, dist, backend, td, arena, off, meta):
         _lib.check(L.dg_agg_stats(h, C.byref(b), C.byref(tot)))
         pr = (C.c_uint64 * 16)()
         _lib.check(L.dg_agg_profile(h, pr, 16))
-        nb_ = max(1, b.value)
+        pr = [pr[i] - pr0[i] for i in range(16)]
+        nb_ = max(1, b.value - b0.value)
         prof = {k: round(pr[i] / nb_ / 1e3, 1) for i, k in enumerate(
             ("flusher_wait_seal", "flusher_wait_free", "flusher_issue", "completer_wait_hdr", "completer_wait_data",
              "seal_to_issued", "issued_to_done", "callers_blocked"))}
-        ncalls = max(1, tot.value)
+        ncalls = max(1, tot.value - tot0.value)
         prof["ns_per_call_in_submit"] = round(pr[8] / ncalls, 1)
         prof["ns_per_call_in_wait"] = round(pr[9] / ncalls, 1)
         prof["submits_without_open_batch"] = int(pr[10])
@@ -621,7 +626,7 @@ def bench_agg(args, rank, world, dev, dist, backend, td, arena, off, meta):
                      "ms_per_step": round(wall / steps * 1e3, 3),
                      "lat_us_p50": round(float(np.percentile(lt, 50)), 1),
                      "lat_us_p99": round(float(np.percentile(lt, 99)), 1),
-                     "avg_batch": round(tot.value / max(1, b.value), 1), "wall_s": round(wall, 3),
+                     "avg_batch": round((tot.value - tot0.value) / nb_, 1), "wall_s": round(wall, 3),
                      "us_per_batch": prof})
         if ri == 0:
             value_wall, value_steps = wall, steps

@@ -122,6 +122,7 @@ struct dg_ctx {
     uint8_t *h_pipe_out = nullptr; uint64_t h_pipe_out_cap = 0; /* pinned staging when the caller's */
     uint8_t *h_pipe_aux = nullptr; uint64_t h_pipe_aux_cap = 0; /* buffers are pageable */
     uint64_t *d_zero = nullptr;                                 /* 8 zero bytes (device) */
+    uint64_t *d_pipe_cur = nullptr; uint64_t pipe_cur_cap = 0;  /* pipeline: chunk k's start in out (device) */
     /* dg_j2t_batch_device_inflight: the context's extra streams and their
      * fork/join events (created on first use) */
     std::vector<hipStream_t> side;

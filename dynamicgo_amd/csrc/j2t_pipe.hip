@@ -23,6 +23,7 @@
  */
 #include <hip/hip_runtime.h>
 
+#include <stdio.h>
 #include <stdint.h>
 #include <string.h>
 
@@ -152,14 +153,18 @@ __global__ __launch_bounds__(256) void pipe_slots_kernel(const uint64_t *in_off,
 __global__ __launch_bounds__(256) void pipe_copy_out_kernel(const uint8_t *src, const uint64_t *src_off, uint64_t n,
                                                             const uint64_t *ret_src, uint8_t *dst, uint64_t *dst_off,
                                                             uint64_t *ret_dst, const uint64_t *base_ptr,
-                                                            uint64_t dst_cap)
+                                                            uint64_t dst_cap, uint64_t *cur_out)
 {
-    const uint64_t base = base_ptr ? *(volatile const uint64_t *)base_ptr : 0;
+    __shared__ uint64_t s_base;
+    if (threadIdx.x == 0) s_base = base_ptr ? *(volatile const uint64_t *)base_ptr : 0;
+    __syncthreads();
+    const uint64_t base = s_base;
     const uint64_t ph = ((uintptr_t)dst + base) & 15, wb = base - ph; /* src[x] -> dst[wb + x] */
     const uint64_t tid = (uint64_t)blockIdx.x * 256 + threadIdx.x, nth = (uint64_t)gridDim.x * 256;
     for (uint64_t i = tid; i <= n; i += nth) {
         dst_off[i] = wb + src_off[i];
         if (i < n) ret_dst[i] = ret_src[i];
+        else *cur_out = wb + src_off[i]; /* the next chunk's base, in device memory */
     }
     const uint64_t end = src_off[n];
     /* local bytes below dst_cap: dst_cap - wb without the wrap of wb = base - ph
@@ -191,10 +196,18 @@ struct DevBuf {
         return off_cap >= 2 * (n + 1) && json_cap >= b + 64 + 16 && out_cap >= slot_off(b, n) + 64 &&
                ol_cap >= n + 1 && ret_cap >= n + 1;
     }
-    /* callers make sure no launch still uses the buffers when they grow */
-    int reserve(uint64_t n, uint64_t b)
+    /* callers make sure no launch still uses the buffers when they grow.
+     * Growth is sized for twice the batch that needed it (every buffer at
+     * once): hipFree waits for the whole device, so a ring of batches whose
+     * sizes wander must stop growing after its first few batches */
+    int reserve(uint64_t n, uint64_t b, bool exact = false)
     {
+        if (fits(n, b)) return DG_OK;
         int rc;
+        if (!exact) {
+            n = 2 * n + 64;
+            b = 2 * b + 4096;
+        }
         if ((rc = grow(d_off, off_cap, 2 * (n + 1)))) return rc;
         if ((rc = grow(d_json, json_cap, b + 64 + 16))) return rc;
         if ((rc = grow(d_out, out_cap, slot_off(b, n) + 64))) return rc;
@@ -237,6 +250,7 @@ struct DevBuf {
 constexpr int AGG_RING_MAX = 16; /* batches in the ring (dg_agg::ring, DG_AGG_RING, default 8) */
 constexpr int AGG_SLOTS = 256; /* caller threads per aggregator (more convert alone, dg_j2t_do) */
 constexpr int AGG_EAGER_INFLIGHT = 1;
+constexpr uint64_t AGG_EXACT_MAX = 64ull << 20; /* launch(): per-batch buffers sized for the parts' caps up to this */
 
 /* one caller thread's part of one batch (its own cache lines) */
 struct alignas(128) Sub {
@@ -420,9 +434,19 @@ int dg_agg::launch(Batch *x)
     if (!N) return DG_OK;
     HIPCHK(hipSetDevice(ctx->device));
     int rc;
-    if ((rc = x->dv.reserve(N, B))) return rc;
-    if ((rc = grow_pinned(x->h_hdr, x->h_hdr_cap, 16 * N + 8))) return rc;
-    if ((rc = grow_pinned(x->h_packed, x->h_packed_cap, slot_off(B, N) + 64))) return rc; /* >= any packed size */
+    /* Buffers for the largest batch the registered parts can make (their
+     * caps summed), so a batch never grows them again until a new thread
+     * registers: hipFree / hipHostFree wait for the whole device, every batch
+     * in flight. Above AGG_EXACT_MAX bytes of packed output, growth is for
+     * twice the batch that needed it instead. */
+    const uint64_t Nx = (uint64_t)ns * cap_n, Bx = (uint64_t)ns * cap_b;
+    const bool exact = slot_off(Bx, Nx) <= AGG_EXACT_MAX;
+    const uint64_t Ng = exact ? Nx : 2 * N + 64, Bg = exact ? Bx : 2 * B + 4096;
+    if ((rc = x->dv.reserve(exact ? Nx : N, exact ? Bx : B, exact))) return rc;
+    if (x->h_hdr_cap < 16 * N + 8 && (rc = grow_pinned(x->h_hdr, x->h_hdr_cap, 16 * Ng + 8))) return rc;
+    if (x->h_packed_cap < slot_off(B, N) + 64 && /* >= any packed size */
+        (rc = grow_pinned(x->h_packed, x->h_packed_cap, slot_off(Bg, Ng) + 64)))
+        return rc;
     /* the parts' longest message (the callers track it) picks the kernels */
     uint64_t max_len = 1;
     for (int s = 0; s < ns; s++)
@@ -619,6 +643,9 @@ void dg_i_pipe_free(dg_ctx *c)
         delete (PipeBuf *)q;
     }
     c->pipe.clear();
+    (void)hipFree(c->d_pipe_cur);
+    c->d_pipe_cur = nullptr;
+    c->pipe_cur_cap = 0;
     (void)hipHostFree(c->h_pipe_out);
     (void)hipHostFree(c->h_pipe_aux);
     c->h_pipe_out = c->h_pipe_aux = nullptr;
@@ -923,6 +950,14 @@ int dg_j2t_pipeline_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8
         p_ret = p_off + n + 1;
     }
     const uint32_t phase = (uint32_t)((uintptr_t)p_out & 15);
+    /* chunk k's start in out, written by chunk k-1's copy-out: the next
+     * chunk's kernels read it from device memory (one read per block), not
+     * over the link */
+    if (c->pipe_cur_cap < chunks + 1) {
+        HIPCHK(hipDeviceSynchronize()); /* no chain of an earlier call still reads it */
+        int rc;
+        if ((rc = grow(c->d_pipe_cur, c->pipe_cur_cap, (uint64_t)chunks + 1))) return rc;
+    }
     /* zero copy: when the JSON arena (with the 16 readable bytes past its end
      * the kernels may touch) and the offsets are pinned, the kernels read
      * them over the link themselves -- no hipMemcpyAsync per chunk, and the
@@ -933,6 +968,9 @@ int dg_j2t_pipeline_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8
                     (uint8_t *)dv_end - (uint8_t *)dv_json == (ptrdiff_t)jend && host_pinned(in_off, &dv_in) &&
                     host_pinned(in_off + n, &dv_in_end) && (uint64_t *)dv_in_end - (uint64_t *)dv_in == (ptrdiff_t)n &&
                     !getenv("DG_NO_ZERO_COPY");
+    if (getenv("DG_PIPE_DEBUG"))
+        fprintf(stderr, "dg_j2t_pipeline_host: n=%llu chunks=%u direct=%d zero_copy=%d\n", (unsigned long long)n,
+                chunks, (int)direct, (int)zc);
     for (uint32_t k = 0; k < chunks; k++) {
         PipeBuf &p = *(PipeBuf *)c->pipe[k % nb];
         const uint64_t a = cb[k], m = cb[k + 1] - a, base = in_off[a], jb = base & ~15ull;
@@ -965,7 +1003,7 @@ int dg_j2t_pipeline_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8
         HIPCHK(hipGetLastError());
         /* the packing needs the previous chunk's end (written by its copy-out) */
         PipeBuf *prev = k ? (PipeBuf *)c->pipe[(k - 1) % nb] : nullptr;
-        const uint64_t *base_ptr = k ? p_off + a : nullptr;
+        const uint64_t *base_ptr = k ? c->d_pipe_cur + k : nullptr;
         if ((rc = dg_i_convert_pack(c, d, root, j_base, j_in, m, flags, p.dv.d_out, d_oo, p.dv.d_ol,
                                     p.dv.d_ret, d_pk, d_po, p.s, max_len, base_ptr ? base_ptr : c->d_zero, 0,
                                     prev ? prev->ev_hdr : nullptr, 1 | (int)(phase << 1))))
@@ -973,7 +1011,7 @@ int dg_j2t_pipeline_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8
         const uint32_t cg = (uint32_t)std::min<uint64_t>(std::max<uint64_t>((span / 16 + 255) / 256, (m + 256) / 256),
                                                          (uint64_t)c->n_cu * 4);
         hipLaunchKernelGGL(pipe_copy_out_kernel, dim3(cg), dim3(256), 0, p.s, d_pk, d_po, m, p.dv.d_ret, p_out,
-                           p_off + a, p_ret + a, base_ptr, out_cap);
+                           p_off + a, p_ret + a, base_ptr, out_cap, c->d_pipe_cur + k + 1);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(p.ev_hdr, p.s));
     }

@@ -1380,8 +1380,11 @@ __global__ __launch_bounds__(256) void dg_pack_scan_kernel(const uint8_t *out, c
     uint64_t base = 0;
     for (uint32_t k = tid; k < b; k += 256) base += __hip_atomic_load(&sums[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     base = block_sum_u64(base, red);
-    if (fr.base_in) {
-        const uint64_t b0 = *(volatile const uint64_t *)fr.base_in;
+    if (fr.base_in) { /* one read per block (it may be pinned host memory) */
+        if (tid == 0) s_pos[0] = *(volatile const uint64_t *)fr.base_in;
+        __syncthreads();
+        const uint64_t b0 = s_pos[0];
+        __syncthreads();
         base += fr.base_mod16 ? ((b0 + fr.phase_add) & 15) : b0;
     }
     const uint64_t cap = fr.dst_cap ? fr.dst_cap : ~0ull;
