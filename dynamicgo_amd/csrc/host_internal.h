@@ -30,7 +30,7 @@ __attribute__((visibility("hidden"))) int set_err(int code, const char *fmt, ...
  * launch on another stream waits for its previous launch (hipStreamWaitEvent
  * on `done`), which keeps the ordering rule true in every case. */
 constexpr int DG_MAX_SCRATCH = 24; /* an aggregator ring (<= 16 streams) + the context's + in-flight side streams */
-constexpr uint32_t DG_NCOUNTS = 12;
+constexpr uint32_t DG_NCOUNTS = 16;
 constexpr uint32_t DG_J2T_COUNTS_BYTES = 6 * 4;
 constexpr uint32_t DG_T2J_DEEP_COUNT = 8;
 struct Scratch {
@@ -46,7 +46,8 @@ struct Scratch {
      *      [4] deep count, [5] blocks done (deep pass) -- [0..5] are reset by
      *      the launch's last kernel (list mode), or by a stream memset of
      *      DG_J2T_COUNTS_BYTES when an enqueue fails half way;
-     * pack: [6] arrivals, [7] departures of dg_pack_device_scan (self-reset);
+     * pack: [6] arrivals, [7] departures of dg_pack_device_scan, [12] its
+     *      slot-overflow count (MsgFrame::ovf_out) -- self-reset;
      * t2j: [8] deep-pass queue length, [9] long messages, [10] the wave
      *      kernel's queue, [11] its bails (reset by a stream memset after the
      *      t2j launch). */
@@ -77,7 +78,7 @@ struct Knobs {
     int64_t small_mpw = 64;
     int64_t list_blocks = 16;
     int64_t t2j_spread = 0;
-    int64_t t2j_wave_min = 512; /* t2j messages longer than this take the wave kernel (0: never) */
+    int64_t t2j_wave_min = 256; /* t2j messages longer than this take the wave kernel (0: never); r4k t2j-c3: 128 / 192 / 256 / 384 / 512 / 1024 -> 66.1 / 66.5 / 66.3 / 59.4 / 53.7 / 23.3 GB/s */
     int64_t flat_wrap = -1;     /* the flat kernel's wrapped mode for roots that wrap a flat struct (0: off) */
 };
 
@@ -121,6 +122,7 @@ struct dg_ctx {
     std::vector<void *> pipe;
     uint8_t *h_pipe_out = nullptr; uint64_t h_pipe_out_cap = 0; /* pinned staging when the caller's */
     uint8_t *h_pipe_aux = nullptr; uint64_t h_pipe_aux_cap = 0; /* buffers are pageable */
+    uint8_t *h_pipe_ovf = nullptr; uint64_t h_pipe_ovf_cap = 0; /* pipeline: slot overflows per chunk (pinned) */
     uint64_t *d_zero = nullptr;                                 /* 8 zero bytes (device) */
     uint64_t *d_pipe_cur = nullptr; uint64_t pipe_cur_cap = 0;  /* pipeline: chunk k's start in out (device) */
     /* dg_j2t_batch_device_inflight: the context's extra streams and their
@@ -187,9 +189,12 @@ __attribute__((visibility("hidden"))) int scratch_for(dg_ctx *c, hipStream_t s, 
  * positions start at *base_in, bytes past dst_cap are not written (0: no
  * limit); d_packed / d_pack_off may be pinned host memory; the packing
  * waits for pack_after (another stream's event) when it is set. base_mod16
- * = 1 | phase << 1: positions start at (*base_in + phase) & 15 instead. */
+ * = 1 | phase << 1: positions start at (*base_in + phase) & 15 instead.
+ * cur_out (device, optional): the end position (the next chunk's base).
+ * ovf_out (optional, e.g. pinned): the count of DG_ST_OUT_OVERFLOW messages. */
 __attribute__((visibility("hidden"))) int dg_i_convert_pack(
     dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *d_json, const uint64_t *d_in_off, uint64_t n,
     uint64_t flags, uint8_t *d_out, const uint64_t *d_out_off, uint32_t *d_out_len, uint64_t *d_ret, uint8_t *d_packed,
     uint64_t *d_pack_off, hipStream_t s, uint64_t max_len, const uint64_t *base_in = nullptr, uint64_t dst_cap = 0,
-    hipEvent_t pack_after = nullptr, int base_mod16 = 0, uint64_t *ret_dst = nullptr);
+    hipEvent_t pack_after = nullptr, int base_mod16 = 0, uint64_t *ret_dst = nullptr, uint64_t *cur_out = nullptr,
+    uint64_t *ovf_out = nullptr);

@@ -708,7 +708,7 @@ static int pack_scan_nolock(dg_ctx *c, const uint8_t *d_out, const uint64_t *d_o
                             const uint64_t *d_ret, uint64_t n, const uint8_t *hdr, uint32_t hdr_len, const uint8_t *ftr,
                             uint32_t ftr_len, uint8_t *d_dst, uint64_t *d_dst_off, hipStream_t s,
                             const uint64_t *base_in = nullptr, uint64_t dst_cap = 0, int base_mod16 = 0,
-                            uint64_t *ret_dst = nullptr);
+                            uint64_t *ret_dst = nullptr, uint64_t *cur_out = nullptr, uint64_t *ovf_out = nullptr);
 
 /* Host batch: ONE pinned upload [in_off | out_off | JSON], the kernels, a
  * device packing pass (used slot prefixes back to back, failed messages
@@ -959,11 +959,14 @@ int dg_pack_device(dg_ctx *c, const uint8_t *d_out, const uint64_t *d_out_off, c
 static int pack_scan_nolock(dg_ctx *c, const uint8_t *d_out, const uint64_t *d_out_off, const uint32_t *d_out_len,
                             const uint64_t *d_ret, uint64_t n, const uint8_t *hdr, uint32_t hdr_len, const uint8_t *ftr,
                             uint32_t ftr_len, uint8_t *d_dst, uint64_t *d_dst_off, hipStream_t s,
-                            const uint64_t *base_in, uint64_t dst_cap, int base_mod16, uint64_t *ret_dst)
+                            const uint64_t *base_in, uint64_t dst_cap, int base_mod16, uint64_t *ret_dst,
+                            uint64_t *cur_out, uint64_t *ovf_out)
 {
     if (n == 0) {
+        if (ovf_out) HIPCHK(hipMemsetAsync(ovf_out, 0, 8, s));
         if (base_in && !base_mod16) HIPCHK(hipMemcpyAsync(d_dst_off, base_in, 8, hipMemcpyDefault, s));
         else HIPCHK(hipMemsetAsync(d_dst_off, 0, 8, s));
+        if (cur_out) HIPCHK(hipMemcpyAsync(cur_out, d_dst_off, 8, hipMemcpyDefault, s));
         return DG_OK;
     }
     Scratch *x;
@@ -976,6 +979,8 @@ static int pack_scan_nolock(dg_ctx *c, const uint8_t *d_out, const uint64_t *d_o
     fr.base_mod16 = base_mod16 ? 1u : 0u;
     fr.phase_add = (uint32_t)(base_mod16 >> 1) & 15; /* dg_i_convert_pack: 1 | phase << 1 */
     fr.ret_dst = ret_dst;
+    fr.cur_out = cur_out;
+    fr.ovf_out = d_ret ? ovf_out : nullptr;
     if (hdr) {
         /* header at 0, footer 8-aligned after it; both followed by >= 16 readable bytes */
         const uint32_t fo = (hdr_len + 7) & ~7u;
@@ -1026,7 +1031,7 @@ int dg_i_convert_pack(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
                       uint64_t n, uint64_t flags, uint8_t *d_out, const uint64_t *d_out_off, uint32_t *d_out_len,
                       uint64_t *d_ret, uint8_t *d_packed, uint64_t *d_pack_off, hipStream_t s, uint64_t max_len,
                       const uint64_t *base_in, uint64_t dst_cap, hipEvent_t pack_after, int base_mod16,
-                      uint64_t *ret_dst)
+                      uint64_t *ret_dst, uint64_t *cur_out, uint64_t *ovf_out)
 {
     std::lock_guard<std::mutex> g(c->mu);
     HIPCHK(hipSetDevice(c->device));
@@ -1034,7 +1039,7 @@ int dg_i_convert_pack(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
     if (rc) return rc;
     if (pack_after) HIPCHK(hipStreamWaitEvent(s, pack_after, 0));
     return pack_scan_nolock(c, d_out, d_out_off, d_out_len, d_ret, n, nullptr, 0, nullptr, 0, d_packed, d_pack_off, s,
-                            base_in, dst_cap, base_mod16, ret_dst);
+                            base_in, dst_cap, base_mod16, ret_dst, cur_out, ovf_out);
 }
 
 extern "C" {

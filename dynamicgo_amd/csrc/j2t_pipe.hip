@@ -13,7 +13,7 @@
  *     the device and launches convert + pack on the batch's own stream; a
  *     completer thread downloads [ret | packed offsets], then exactly the
  *     packed bytes, and wakes the callers, who copy their results out.
- *     the ring's batches (8) rotate, so uploads, kernels and downloads of
+ *     the ring's batches (16) rotate, so uploads, kernels and downloads of
  *     consecutive batches overlap.
  *
  *  2. dg_j2t_pipeline_host: one large host batch (pinned buffers) streamed
@@ -247,7 +247,7 @@ struct DevBuf {
 
 /* ---------------- the aggregator ---------------- */
 
-constexpr int AGG_RING_MAX = 16; /* batches in the ring (dg_agg::ring, DG_AGG_RING, default 8) */
+constexpr int AGG_RING_MAX = 32; /* batches in the ring (dg_agg::ring, DG_AGG_RING, default 16) */
 constexpr int AGG_SLOTS = 256; /* caller threads per aggregator (more convert alone, dg_j2t_do) */
 constexpr int AGG_EAGER_INFLIGHT = 1;
 constexpr uint64_t AGG_EXACT_MAX = 64ull << 20; /* launch(): per-batch buffers sized for the parts' caps up to this */
@@ -309,7 +309,7 @@ struct dg_agg {
     std::chrono::nanoseconds max_wait;
     uint64_t id;
     Batch *b = nullptr;
-    int ring = 8;                    /* batches in the ring: one filling, the rest converting or being taken */
+    int ring = 16;                   /* batches in the ring: one filling, the rest converting or being taken (r4j: 16 threads 53.3M calls/s vs 48.5M at 8) */
     std::atomic<uint64_t> open{0};   /* the open generation; batch b[open % ring] */
     std::atomic<int> nslots{0};
     std::atomic<uint8_t> ready[AGG_SLOTS];
@@ -646,6 +646,9 @@ void dg_i_pipe_free(dg_ctx *c)
     (void)hipFree(c->d_pipe_cur);
     c->d_pipe_cur = nullptr;
     c->pipe_cur_cap = 0;
+    (void)hipHostFree(c->h_pipe_ovf);
+    c->h_pipe_ovf = nullptr;
+    c->h_pipe_ovf_cap = 0;
     (void)hipHostFree(c->h_pipe_out);
     (void)hipHostFree(c->h_pipe_aux);
     c->h_pipe_out = c->h_pipe_aux = nullptr;
@@ -958,6 +961,13 @@ int dg_j2t_pipeline_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8
         int rc;
         if ((rc = grow(c->d_pipe_cur, c->pipe_cur_cap, (uint64_t)chunks + 1))) return rc;
     }
+    /* each chunk's packing counts its overflowed slots here, so the host
+     * scans the status words (pinned: slow CPU reads) only when one did */
+    {
+        int rc;
+        if ((rc = grow_pinned(c->h_pipe_ovf, c->h_pipe_ovf_cap, 8ull * chunks))) return rc;
+    }
+    uint64_t *h_ovf = (uint64_t *)(void *)c->h_pipe_ovf;
     /* zero copy: when the JSON arena (with the 16 readable bytes past its end
      * the kernels may touch) and the offsets are pinned, the kernels read
      * them over the link themselves -- no hipMemcpyAsync per chunk, and the
@@ -968,9 +978,12 @@ int dg_j2t_pipeline_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8
                     (uint8_t *)dv_end - (uint8_t *)dv_json == (ptrdiff_t)jend && host_pinned(in_off, &dv_in) &&
                     host_pinned(in_off + n, &dv_in_end) && (uint64_t *)dv_in_end - (uint64_t *)dv_in == (ptrdiff_t)n &&
                     !getenv("DG_NO_ZERO_COPY");
+    /* staged (DG_PIPE_STAGED=1, the r4i layout): pack into device memory,
+     * then a copy-out kernel; else the packing writes the host buffers */
+    static const bool staged = getenv("DG_PIPE_STAGED") != nullptr;
     if (getenv("DG_PIPE_DEBUG"))
-        fprintf(stderr, "dg_j2t_pipeline_host: n=%llu chunks=%u direct=%d zero_copy=%d\n", (unsigned long long)n,
-                chunks, (int)direct, (int)zc);
+        fprintf(stderr, "dg_j2t_pipeline_host: n=%llu chunks=%u direct=%d zero_copy=%d staged=%d\n",
+                (unsigned long long)n, chunks, (int)direct, (int)zc, (int)staged);
     for (uint32_t k = 0; k < chunks; k++) {
         PipeBuf &p = *(PipeBuf *)c->pipe[k % nb];
         const uint64_t a = cb[k], m = cb[k + 1] - a, base = in_off[a], jb = base & ~15ull;
@@ -979,9 +992,9 @@ int dg_j2t_pipeline_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8
         const uint64_t span = in_off[a + m] - jb;
         const uint64_t pk = 8 * (m + 1) + 16 + slot_off(span, m) + 64; /* pack_off + phase + packed */
         int rc;
-        if (!p.dv.fits(m, span) || p.packed_cap < pk) HIPCHK(hipStreamSynchronize(p.s)); /* free to grow */
+        if (!p.dv.fits(m, span) || (staged && p.packed_cap < pk)) HIPCHK(hipStreamSynchronize(p.s)); /* free to grow */
         if ((rc = p.dv.reserve(m, span))) return rc;
-        if ((rc = grow(p.d_packed, p.packed_cap, pk))) return rc;
+        if (staged && (rc = grow(p.d_packed, p.packed_cap, pk))) return rc;
         uint64_t *d_in = p.dv.d_off, *d_oo = d_in + m + 1;
         uint64_t *d_po = (uint64_t *)(void *)p.d_packed;
         uint8_t *d_pk = p.d_packed + ((8 * (m + 1) + 15) & ~15ull);
@@ -1001,12 +1014,24 @@ int dg_j2t_pipeline_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8
             j_in = d_in;
         }
         HIPCHK(hipGetLastError());
-        /* the packing needs the previous chunk's end (written by its copy-out) */
+        /* the packing needs the previous chunk's end (written by its pack or copy-out) */
         PipeBuf *prev = k ? (PipeBuf *)c->pipe[(k - 1) % nb] : nullptr;
         const uint64_t *base_ptr = k ? c->d_pipe_cur + k : nullptr;
+        if (!staged) {
+            /* the packing's coalesced stores are the download: straight into
+             * out / out_off / ret (pinned), from the previous chunk's end */
+            if ((rc = dg_i_convert_pack(c, d, root, j_base, j_in, m, flags, p.dv.d_out, d_oo, p.dv.d_ol, p.dv.d_ret,
+                                        p_out, p_off + a, p.s, max_len, base_ptr ? base_ptr : c->d_zero, out_cap,
+                                        prev ? prev->ev_hdr : nullptr, 0, p_ret + a, c->d_pipe_cur + k + 1,
+                                        h_ovf + k)))
+                return rc;
+            HIPCHK(hipEventRecord(p.ev_hdr, p.s));
+            continue;
+        }
         if ((rc = dg_i_convert_pack(c, d, root, j_base, j_in, m, flags, p.dv.d_out, d_oo, p.dv.d_ol,
                                     p.dv.d_ret, d_pk, d_po, p.s, max_len, base_ptr ? base_ptr : c->d_zero, 0,
-                                    prev ? prev->ev_hdr : nullptr, 1 | (int)(phase << 1))))
+                                    prev ? prev->ev_hdr : nullptr, 1 | (int)(phase << 1), nullptr, nullptr,
+                                    h_ovf + k)))
             return rc;
         const uint32_t cg = (uint32_t)std::min<uint64_t>(std::max<uint64_t>((span / 16 + 255) / 256, (m + 256) / 256),
                                                          (uint64_t)c->n_cu * 4);
@@ -1027,8 +1052,10 @@ int dg_j2t_pipeline_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8
     }
     uint64_t need = cursor;
     std::vector<uint64_t> redo;
-    for (uint64_t i = 0; i < n; i++)
-        if ((uint8_t)ret[i] == DG_ST_OUT_OVERFLOW) redo.push_back(i);
+    for (uint32_t k = 0; k < chunks; k++)
+        if (h_ovf[k])
+            for (uint64_t i = cb[k]; i < cb[k + 1]; i++)
+                if ((uint8_t)ret[i] == DG_ST_OUT_OVERFLOW) redo.push_back(i);
     if (!redo.empty()) {
         /* slot overflows (rare): each alone at its exact size, spliced in
          * place; later messages move up */
@@ -1141,8 +1168,13 @@ int dg_agg_drive(dg_agg *a, const uint8_t *arena, const uint64_t *in_off, uint64
                         ring[k].batch = nullptr;
                         break;
                     }
-                    /* no open batch: the oldest one frees when its callers
-                     * (this thread among them) take their results */
+                    /* this thread's part of the open batch is full: the flip
+                     * comes once the next batch of the ring is free, i.e.
+                     * once its callers (this thread among them) have taken
+                     * their results. Block on the oldest call rather than
+                     * spin: spinning callers take the cores the flusher and
+                     * completer need (r4k: 16 threads 46.1M calls/s spinning,
+                     * 53.3M blocking in r4j; 64 threads 18.4M vs 42.2M) */
                     if (h < i) finish();
                     else std::this_thread::yield();
                 }

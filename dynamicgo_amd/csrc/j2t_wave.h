@@ -1344,6 +1344,8 @@ struct MsgFrame {
     uint32_t base_mod16;
     uint32_t phase_add; /* base_mod16: added before the mod (the destination's own address phase) */
     uint64_t *ret_dst;  /* optional: a copy of ret (e.g. pinned host memory: the aggregator's download) */
+    uint64_t *cur_out;  /* optional (device): the end position, dst_off[n] -- the next chunk's base_in */
+    uint64_t *ovf_out;  /* optional (ret set): the count of DG_ST_OUT_OVERFLOW messages (plain store) */
 };
 
 template <int V>
@@ -1354,6 +1356,7 @@ __global__ __launch_bounds__(256) void dg_pack_scan_kernel(const uint8_t *out, c
     __shared__ uint64_t red[4];
     __shared__ uint64_t s_pos[256];
     __shared__ uint32_t s_len[256];
+    __shared__ uint64_t s_end;
     const uint32_t G = gridDim.x, b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint64_t per = (n + G - 1) / G;
     const uint64_t lo = (uint64_t)b * per < n ? (uint64_t)b * per : n;
@@ -1367,11 +1370,19 @@ __global__ __launch_bounds__(256) void dg_pack_scan_kernel(const uint8_t *out, c
         const uint8_t c = (uint8_t)fr.ret[i];
         return !fr.hdr && (c == DG_ST_HM_END || c == 24u || c == DG_ST_HM_END_AT) ? out_len[i] : 0u;
     };
+    /* bytes, and (ovf_out) overflowed slots in bits 44+ of the same sum */
+    constexpr uint32_t OVF_SH = 44;
     uint64_t s = 0;
-    for (uint64_t i = lo + tid; i < hi; i += 256) s += msg_len(i);
+    for (uint64_t i = lo + tid; i < hi; i += 256) {
+        s += msg_len(i);
+        if (fr.ovf_out && (uint8_t)fr.ret[i] == DG_ST_OUT_OVERFLOW) s += 1ull << OVF_SH;
+    }
     s = block_sum_u64(s, red);
+    const uint32_t n_ovf = (uint32_t)(s >> OVF_SH);
+    s &= (1ull << OVF_SH) - 1;
     if (tid == 0) {
         __hip_atomic_store(&sums[b], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (n_ovf) __hip_atomic_fetch_add(&sync[6], n_ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_fetch_add(&sync[0], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         while (__hip_atomic_load(&sync[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < G)
             __builtin_amdgcn_s_sleep(4);
@@ -1405,6 +1416,58 @@ __global__ __launch_bounds__(256) void dg_pack_scan_kernel(const uint8_t *out, c
         s_len[tid] = len;
         __syncthreads();
         const uint32_t nt = hi - t0 < 256 ? (uint32_t)(hi - t0) : 256u;
+        if (!fr.hdr) {
+            /* Unframed: the tile's output is one contiguous byte range, so
+             * the block writes it word by word in address order -- every
+             * thread a destination word, a wave 512 contiguous bytes per
+             * store (coalesced; over the link when dst is pinned host
+             * memory) -- each word gathered from the message(s) it holds
+             * (binary search of the tile's positions in LDS). The words at
+             * both ends, shared with the neighbouring tiles, are written
+             * byte-exact. Messages that would end past cap form a suffix
+             * (positions rise): the range stops at the last that fits. */
+            if (tid == 0) s_end = s_pos[0];
+            __syncthreads();
+            if (tid < nt && s_pos[tid] + s_len[tid] <= cap &&
+                (tid + 1 == nt || s_pos[tid + 1] + s_len[tid + 1] > cap))
+                s_end = s_pos[tid] + s_len[tid];
+            __syncthreads();
+            const uint64_t P0 = s_pos[0], P1 = s_end;
+            const uintptr_t D = (uintptr_t)dst, A0 = D + P0, A1 = D + P1;
+            const uintptr_t wa = A0 & ~(uintptr_t)7, wb = (A1 + 7) & ~(uintptr_t)7;
+            const uint64_t nw = P1 > P0 ? (uint64_t)((wb - wa) >> 3) : 0;
+            for (uint64_t j = tid; j < nw; j += 256) {
+                const uintptr_t W = wa + 8 * j, lo = W < A0 ? A0 : W, hi2 = W + 8 > A1 ? A1 : W + 8;
+                const uint64_t p = (uint64_t)(lo - D);
+                uint32_t l = 0, h = nt; /* the last message starting at or before p */
+                while (h - l > 1) {
+                    const uint32_t m = (l + h) >> 1;
+                    if (s_pos[m] <= p) l = m;
+                    else h = m;
+                }
+                uint32_t k = l;
+                if (lo == W && hi2 == W + 8 && p + 8 <= s_pos[k] + s_len[k]) {
+                    /* inside one message: an unaligned 8-byte read of its
+                     * slot (8-aligned), as two words when it straddles; the
+                     * second holds a byte of the message, so it is in bounds */
+                    const uint64_t o = p - s_pos[k];
+                    const uint64_t *sw = (const uint64_t *)(const void *)(out + out_off[t0 + k] + (o & ~7ull));
+                    const uint32_t sh = (uint32_t)(o & 7) * 8;
+                    uint64_t v = sw[0];
+                    if (sh) v = (v >> sh) | (sw[1] << (64 - sh));
+                    *(gu64 *)(void *)W = v;
+                } else {
+                    for (uintptr_t q = lo; q < hi2; q++) {
+                        const uint64_t pq = (uint64_t)(q - D);
+                        while (pq >= s_pos[k] + s_len[k]) k++; /* pq < P1: stays in the tile */
+                        *(gu8 *)(void *)q = out[out_off[t0 + k] + (pq - s_pos[k])];
+                    }
+                }
+            }
+            base += tile;
+            __syncthreads();
+            continue;
+        }
         for (uint32_t k = w; k < nt; k += 4) {
             uint32_t nb = s_len[k];
             if (!nb || s_pos[k] + nb > cap) continue;
@@ -1429,11 +1492,16 @@ __global__ __launch_bounds__(256) void dg_pack_scan_kernel(const uint8_t *out, c
         __syncthreads();
     }
     if (tid == 0) {
-        if (b == G - 1) dst_off[n] = base; /* the last range ends at the grand total */
+        if (b == G - 1) { /* the last range ends at the grand total */
+            dst_off[n] = base;
+            if (fr.cur_out) *fr.cur_out = base;
+            if (fr.ovf_out) *fr.ovf_out = __hip_atomic_load(&sync[6], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         const uint32_t prev = __hip_atomic_fetch_add(&sync[1], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
         if (prev == G - 1) { /* every block is past its wait: reset for the next launch */
             __hip_atomic_store(&sync[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&sync[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&sync[6], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }
