@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <algorithm>
 #include <mutex>
@@ -143,7 +144,10 @@ static inline int grow_pinned(uint8_t *&p, uint64_t &cap, uint64_t want)
     p = nullptr;
     uint64_t nc = std::max<uint64_t>(want, cap * 2);
     nc = std::max<uint64_t>(nc, 1 << 16);
-    HIPCHK(hipHostMalloc((void **)&p, nc, hipHostMallocDefault));
+    /* DG_HOST_NUMA=1: on the allocating thread's NUMA node (its policy)
+     * instead of the driver's default placement */
+    static const unsigned fl = getenv("DG_HOST_NUMA") ? hipHostMallocNumaUser : hipHostMallocDefault;
+    HIPCHK(hipHostMalloc((void **)&p, nc, fl));
     cap = nc;
     return DG_OK;
 }

@@ -987,8 +987,15 @@ int dg_j2t_pipeline_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8
     for (uint32_t k = 0; k < chunks; k++) {
         PipeBuf &p = *(PipeBuf *)c->pipe[k % nb];
         const uint64_t a = cb[k], m = cb[k + 1] - a, base = in_off[a], jb = base & ~15ull;
-        uint64_t max_len = 1;
-        for (uint64_t j = a; j < a + m; j++) max_len = std::max<uint64_t>(max_len, in_off[j + 1] - in_off[j]);
+        /* the longest message picks the kernels; unknown (0) when the
+         * offsets are pinned: CPU reads of pinned memory run at ~10 GB/s (a
+         * 64K batch's offsets cost 50 us), and the kernels route long
+         * messages themselves */
+        uint64_t max_len = 0;
+        if (!zc) {
+            max_len = 1;
+            for (uint64_t j = a; j < a + m; j++) max_len = std::max<uint64_t>(max_len, in_off[j + 1] - in_off[j]);
+        }
         const uint64_t span = in_off[a + m] - jb;
         const uint64_t pk = 8 * (m + 1) + 16 + slot_off(span, m) + 64; /* pack_off + phase + packed */
         int rc;

@@ -445,6 +445,7 @@ struct JOut {
                 u64x2 p;
                 p.x = wlo;
                 p.y = lo;
+                /* (non-temporal stores here: 44.6 MB written on t2j-c2 instead of 24.7, r4m) */
                 *(__attribute__((address_space(1))) u64x2 *)(void *)(b + (wi - 1) * 8) = p; /* 16-byte aligned */
             } else {
                 pair_edge(b, cap, wide, wi, wlo, lo);

@@ -75,7 +75,13 @@ struct T2WLds {
     uint32_t cvs[64];   /* value string / body source */
     uint32_t cvn[64];   /* scan: value string length; write: body output offset */
 };
-constexpr uint32_t T2W_MPT = 16; /* messages a wave takes at once (one walker lane each) */
+#ifndef DG_T2W_MPT
+#define DG_T2W_MPT 16
+#endif
+/* messages a wave takes at once (one walker lane each). r4m, t2j-c3: 16 /
+ * 32 / 64 -> 1.21 / 1.49 / 2.33 ms (at 64 the frames and token rings cut
+ * the kernel to 2 waves/SIMD) */
+constexpr uint32_t T2W_MPT = DG_T2W_MPT;
 
 /* the t2j side table (keys) copied to LDS by the wave kernel */
 struct T2WSide {
@@ -183,7 +189,7 @@ DGI uint64_t t2w_tok(uint32_t kind, uint32_t pos, uint32_t aux, uint32_t td, uin
     return (uint64_t)pos | ((uint64_t)aux << 21) | ((uint64_t)td << 42) | ((uint64_t)kind << 54) | ((uint64_t)kt << 60);
 }
 constexpr uint32_t T2W_TOKCAP = 192; /* tokens per message (more: the lane kernel) */
-constexpr uint32_t T2W_RING = 8;     /* tokens a walker keeps in LDS before writing them out together */
+constexpr uint32_t T2W_RING = T2W_MPT >= 64 ? 4 : 8; /* tokens a walker keeps in LDS before writing them out together */
 constexpr uint32_t T2W_BD = 3;       /* frames kept in LDS per lane (the innermost is in registers) */
 
 /* One lane walks its whole message (doRecurse's order, conv/t2j/impl.go:
