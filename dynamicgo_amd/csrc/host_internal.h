@@ -68,6 +68,10 @@ struct Scratch {
     uint64_t t2j_big_cap = 0;
     uint32_t *t2j_bail = nullptr;  /* t2j: the wave kernel's bails ([11] counts them) */
     uint64_t t2j_bail_cap = 0;
+    /* a second stream of this scratch's launches (created on first use): the
+     * t2j wave kernel runs on it beside the lane pass (Knobs::t2j_overlap) */
+    hipStream_t side = nullptr;
+    hipEvent_t side_go = nullptr, side_done = nullptr;
 };
 constexpr uint32_t FRAME_CAP = 4096;
 
@@ -79,6 +83,7 @@ struct Knobs {
     int64_t small_mpw = 64;
     int64_t list_blocks = 16;
     int64_t t2j_spread = 0;
+    int64_t t2j_overlap = 1;    /* t2j: the wave kernel on a second stream beside the lane pass (0: one stream) */
     int64_t t2j_wave_min = 256; /* t2j messages longer than this take the wave kernel (0: never); r4k t2j-c3: 128 / 192 / 256 / 384 / 512 / 1024 -> 66.1 / 66.5 / 66.3 / 59.4 / 53.7 / 23.3 GB/s */
     int64_t flat_wrap = -1;     /* the flat kernel's wrapped mode for roots that wrap a flat struct (0: off) */
 };

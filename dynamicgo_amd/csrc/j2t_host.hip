@@ -51,6 +51,10 @@ static void scratch_free(Scratch *x)
     (void)hipFree(x->t2j_list);
     (void)hipFree(x->t2j_big);
     (void)hipFree(x->t2j_bail);
+    if (x->side) (void)hipStreamSynchronize(x->side);
+    if (x->side_go) (void)hipEventDestroy(x->side_go);
+    if (x->side_done) (void)hipEventDestroy(x->side_done);
+    if (x->side) (void)hipStreamDestroy(x->side);
     if (x->done) (void)hipEventDestroy(x->done);
     delete x;
 }
@@ -116,6 +120,7 @@ static int64_t *knob_ref(dg_ctx *c, const char *name)
     if (!strcmp(name, "list_blocks")) return &K.list_blocks;
     if (!strcmp(name, "t2j_spread")) return &K.t2j_spread;
     if (!strcmp(name, "t2j_wave_min")) return &K.t2j_wave_min;
+    if (!strcmp(name, "t2j_overlap")) return &K.t2j_overlap;
     if (!strcmp(name, "flat_wrap")) return &K.flat_wrap;
     return nullptr;
 }
@@ -150,7 +155,7 @@ int dg_ctx_create(int device, dg_ctx **out)
     static const struct { const char *env; const char *name; } envk[] = {
         {"DG_FLAT", "flat"}, {"DG_WAVE_MIN", "wave_min"}, {"DG_WAVE_OCC", "wave_occ"},
         {"DG_SMALL_MPW", "small_mpw"}, {"DG_LIST_BLOCKS", "list_blocks"}, {"DG_T2J_SPREAD", "t2j_spread"},
-        {"DG_T2J_WAVE_MIN", "t2j_wave_min"}, {"DG_FLAT_WRAP", "flat_wrap"}};
+        {"DG_T2J_WAVE_MIN", "t2j_wave_min"}, {"DG_T2J_OVERLAP", "t2j_overlap"}, {"DG_FLAT_WRAP", "flat_wrap"}};
     for (const auto &e : envk) {
         const char *v = getenv(e.env);
         if (v && *v) *knob_ref(c, e.name) = strtoll(v, nullptr, 10);

@@ -1111,6 +1111,7 @@ struct T2JParams {
     uint32_t *big_list;
     uint32_t *big_count;
     uint64_t big_min;
+    uint32_t skip_big;        /* messages longer than big_min are skipped, not listed (t2j_route_kernel listed them) */
     const uint32_t *list;
     const uint32_t *list_count;
     unsigned long long *stats; /* DG_T2W_PROF builds: phase cycles of the wave kernel (dg_ctx_counters 2..) */
@@ -1159,6 +1160,7 @@ struct T2WParams {
 uint64_t t2j_wave_ws_bytes(uint32_t blocks);
 constexpr uint32_t T2W_BPC = 4; /* wave-kernel blocks per CU in the grid */
 void launch_t2j_list(uint32_t blocks, hipStream_t s, const T2JParams &P); /* list mode, 1 lane per message */
+void launch_t2j_route(uint64_t n, hipStream_t s, const T2JParams &P);      /* big_list by length only */
 void launch_t2j_wave(uint32_t blocks, hipStream_t s, const T2JParams &P, const T2WParams &W);
 void launch_t2j_deep(hipStream_t s, const T2JParams &P);
 

@@ -56,9 +56,21 @@ static int t2j_launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
         if ((rc = grow_x(x, x->t2j_big, x->t2j_big_cap, n))) return rc;
         if ((rc = grow_x(x, x->t2j_bail, x->t2j_bail_cap, n))) return rc;
         if (!c->ws_t2w) HIPCHK(hipMalloc(&c->ws_t2w, t2j_wave_ws_bytes((uint32_t)c->n_cu * T2W_BPC)));
+    }
+    /* overlapped form: the wave kernel (and its bails' list pass) on the
+     * scratch's second stream, beside the lane pass over the short ones, so
+     * the lane pass fills the CUs the persistent wave grid leaves idle */
+    const bool ovl = wave && c->knobs.t2j_overlap != 0;
+    if (ovl && !x->side) {
+        HIPCHK(hipStreamCreateWithFlags(&x->side, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&x->side_go, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&x->side_done, hipEventDisableTiming));
+    }
+    hipStream_t ws = ovl ? x->side : s; /* the wave kernel's stream */
+    if (wave) {
         /* one token workspace per context, like the deep workspace: a wave
          * pass on another stream waits for the previous one */
-        if (c->ws_t2w_last && c->ws_t2w_last != s) HIPCHK(hipStreamWaitEvent(s, c->ws_t2w_done, 0));
+        if (c->ws_t2w_last && c->ws_t2w_last != ws) HIPCHK(hipStreamWaitEvent(ws, c->ws_t2w_done, 0));
     }
     T2JParams P;
     memset(&P, 0, sizeof P);
@@ -87,26 +99,43 @@ static int t2j_launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
         P1.big_list = x->t2j_big;
         P1.big_count = x->d_counts + DG_T2J_DEEP_COUNT + 1;
         P1.big_min = wmin;
-        launch_t2j_pass(n, s, P1, 1); /* the short ones: full waves */
+        if (ovl) {
+            launch_t2j_route(n, s, P1); /* the long ones, by length */
+            if ((e = hipGetLastError()) == hipSuccess) e = hipEventRecord(x->side_go, s);
+            if (e == hipSuccess) e = hipStreamWaitEvent(ws, x->side_go, 0);
+            P1.skip_big = 1;
+            P1.big_list = nullptr;
+            P1.big_count = nullptr;
+        }
+        if (e == hipSuccess) launch_t2j_pass(n, s, P1, 1); /* the short ones: full waves */
         T2WParams W;
         W.list = x->t2j_big;
-        W.count = P1.big_count;
+        W.count = x->d_counts + DG_T2J_DEEP_COUNT + 1;
         W.queue = x->d_counts + DG_T2J_DEEP_COUNT + 2;
         W.bail_list = x->t2j_bail;
         W.bail_count = x->d_counts + DG_T2J_DEEP_COUNT + 3;
         const uint32_t wblocks = (uint32_t)c->n_cu * T2W_BPC; /* the token regions are sized for it */
         W.tok = c->ws_t2w;
         W.side_len = (uint32_t)d->side_len;
-        if ((e = hipGetLastError()) == hipSuccess) {
-            launch_t2j_wave(wblocks, s, P, W);
+        if (e == hipSuccess && (e = hipGetLastError()) == hipSuccess) {
+            launch_t2j_wave(wblocks, ws, P, W);
             e = hipGetLastError();
         }
         if (e == hipSuccess) {
             T2JParams P3 = P;
             P3.list = x->t2j_bail;
             P3.list_count = W.bail_count;
-            launch_t2j_list(64, s, P3);
+            launch_t2j_list(64, ws, P3);
             e = hipGetLastError();
+        }
+        if (e == hipSuccess) {
+            if (!c->ws_t2w_done) e = hipEventCreateWithFlags(&c->ws_t2w_done, hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventRecord(c->ws_t2w_done, ws);
+            if (e == hipSuccess) c->ws_t2w_last = ws;
+        }
+        if (ovl && e == hipSuccess) { /* the deep pass takes both passes' queue */
+            e = hipEventRecord(x->side_done, ws);
+            if (e == hipSuccess) e = hipStreamWaitEvent(s, x->side_done, 0);
         }
     } else {
         launch_t2j_pass(n, s, P, t2j_spread(c, max_len));
@@ -122,11 +151,6 @@ static int t2j_launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
     }
     if (e == hipSuccess) e = hipEventRecord(c->ws_t2j_done, s);
     if (e == hipSuccess) c->ws_t2j_last = s;
-    if (wave && e == hipSuccess) {
-        if (!c->ws_t2w_done) e = hipEventCreateWithFlags(&c->ws_t2w_done, hipEventDisableTiming);
-        if (e == hipSuccess) e = hipEventRecord(c->ws_t2w_done, s);
-        if (e == hipSuccess) c->ws_t2w_last = s;
-    }
     (void)hipMemsetAsync(x->d_counts + DG_T2J_DEEP_COUNT, 0, 16, s);
     HIPCHK(hipEventRecord(x->done, s));
     x->used = true;

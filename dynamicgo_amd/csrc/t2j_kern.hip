@@ -24,8 +24,8 @@ __global__ __launch_bounds__(T2J_BLOCK) void t2j_kernel(T2JParams P)
     for (uint64_t k = (uint64_t)blockIdx.x * MPB + slot; k < cnt; k += (uint64_t)gridDim.x * MPB) {
         const uint64_t i = P.list ? (uint64_t)P.list[k] : k;
         const uint64_t a = P.in_off[i], b = P.in_off[i + 1];
-        const bool big = P.big_list && b - a > P.big_min;
-        wave_push(P.big_list, P.big_count, big, (uint32_t)i); /* the wave kernel takes it */
+        const bool big = (P.big_list || P.skip_big) && b - a > P.big_min;
+        if (!P.skip_big) wave_push(P.big_list, P.big_count, big, (uint32_t)i); /* the wave kernel takes it */
         if (big) continue;
         SrcT<glb_u64> s;
         s.init((glb_u64 *)(const void *)(P.src + (a & ~7ull)), (int64_t)(a & 7), (int64_t)(b - a));
@@ -41,6 +41,15 @@ __global__ __launch_bounds__(T2J_BLOCK) void t2j_kernel(T2JParams P)
         }
         t2j_store(P, i, r, o);
     }
+}
+
+/* the long messages listed by length alone (the wave kernel's list, ahead
+ * of the lane pass, which then skips them: t2j_launch's overlapped form) */
+__global__ __launch_bounds__(256) void t2j_route_kernel(T2JParams P)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const bool big = i < P.n && P.in_off[i + 1] - P.in_off[i] > P.big_min;
+    wave_push(P.big_list, P.big_count, big, (uint32_t)i);
 }
 
 /* the long messages (t2j_wave.h): a persistent grid; each wave takes
@@ -146,6 +155,11 @@ void launch_t2j_pass(uint64_t n, hipStream_t s, const T2JParams &P, uint32_t spr
     else if (spread == 1) hipLaunchKernelGGL((t2j_kernel<1, false>), dim3(blocks), dim3(T2J_BLOCK), 0, s, P);
     else if (spread == 4) hipLaunchKernelGGL((t2j_kernel<4, false>), dim3(blocks), dim3(T2J_BLOCK), 0, s, P);
     else hipLaunchKernelGGL((t2j_kernel<2, false>), dim3(blocks), dim3(T2J_BLOCK), 0, s, P);
+}
+
+void launch_t2j_route(uint64_t n, hipStream_t s, const T2JParams &P)
+{
+    hipLaunchKernelGGL(t2j_route_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, P);
 }
 
 void launch_t2j_list(uint32_t blocks, hipStream_t s, const T2JParams &P)
