@@ -83,7 +83,7 @@ struct Knobs {
     int64_t small_mpw = 64;
     int64_t list_blocks = 16;
     int64_t t2j_spread = 0;
-    int64_t t2j_overlap = 1;    /* t2j: the wave kernel on a second stream beside the lane pass (0: one stream) */
+    int64_t t2j_overlap = 0;    /* t2j: 1 = the wave kernel on a second stream beside the lane pass; r4n t2j-c3: 65.1 GB/s with, 66.6 without (the lane pass is ~15 us of 1.21 ms, the route kernel adds 14) */
     int64_t t2j_wave_min = 256; /* t2j messages longer than this take the wave kernel (0: never); r4k t2j-c3: 128 / 192 / 256 / 384 / 512 / 1024 -> 66.1 / 66.5 / 66.3 / 59.4 / 53.7 / 23.3 GB/s */
     int64_t flat_wrap = -1;     /* the flat kernel's wrapped mode for roots that wrap a flat struct (0: off) */
 };
