@@ -447,6 +447,25 @@ def test_wave_path_nested_and_escapes(chk, knob):
         assert not bad, bad[:3]
 
 
+@pytest.mark.parametrize("wmin", [64, 256])
+def test_wave_path_overlapped(chk, knob, wmin):
+    """t2j_overlap 1: the route kernel lists the long messages, the wave
+    kernel (and its bails' list pass) runs on the scratch's second stream
+    beside the lane pass, which skips them. Mixed short / long / mutated
+    messages, so all three passes and the deep pass have work."""
+    knob("t2j_overlap", 1)
+    knob("t2j_wave_min", wmin)
+    ntd = W.nesting_i64_desc()
+    nfl = T.flatten(ntd)
+    rng = random.Random(45 + wmin)
+    js = W.gen_nested_batch(rng, 500)
+    thr, rets = conv.BinaryConv(conv.Options()).do_batch(ntd, js)
+    assert not any(int(r) for r in rets)
+    thr = list(thr) + [t2jgen.mutate(rng, bytes(m)) for m in thr[:150]]
+    bad = compare(chk, nfl, thr, 0)
+    assert not bad, bad[:3]
+
+
 # ---- the Go-side options: ConvertException, EnableThriftBase, agw.body_dynamic ----
 CONV_EXC, SKIP_BASE = 1 << 9, 1 << 10
 
