@@ -189,6 +189,11 @@ static inline int grow_x(Scratch *x, T *&p, uint64_t &cap, uint64_t want)
     return grow(p, cap, want);
 }
 
+/* before streams s[0..n) are destroyed: the device is synchronized, the
+ * scratches they own are freed, and no other scratch keeps one of them as
+ * the stream of its last launch (takes the ctx mutex) */
+__attribute__((visibility("hidden"))) void dg_i_scratch_release(dg_ctx *c, const hipStream_t *s, int n);
+
 /* the scratch for a launch on stream s (ctx mutex held) */
 __attribute__((visibility("hidden"))) int scratch_for(dg_ctx *c, hipStream_t s, Scratch **out);
 

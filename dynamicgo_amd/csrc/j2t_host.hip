@@ -82,6 +82,38 @@ static int scratch_new(dg_ctx *c, hipStream_t owner, Scratch **out)
     return DG_OK;
 }
 
+void dg_i_scratch_release(dg_ctx *c, const hipStream_t *s, int n)
+{
+    if (!c || n <= 0) return;
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    (void)hipDeviceSynchronize(); /* nothing is pending on any scratch after this */
+    std::vector<Scratch *> keep;
+    for (Scratch *x : c->scratch) {
+        bool owned = false, last = false;
+        for (int k = 0; k < n; k++) {
+            owned |= x->owner == s[k];
+            last |= x->last == s[k];
+        }
+        if (owned) {
+            x->used = false; /* done (synchronized): scratch_free waits on nothing */
+            scratch_free(x);
+            continue;
+        }
+        if (last) {
+            x->used = false;
+            x->last = nullptr;
+        }
+        keep.push_back(x);
+    }
+    c->scratch.swap(keep);
+    c->rr = 0;
+    for (int k = 0; k < n; k++) { /* the t2j workspaces' last streams */
+        if (c->ws_t2j_last == s[k]) c->ws_t2j_last = nullptr;
+        if (c->ws_t2w_last == s[k]) c->ws_t2w_last = nullptr;
+    }
+}
+
 /* The scratch for a launch on stream s (ctx mutex held); orders s after the
  * scratch's previous launch when that ran on another stream. */
 int scratch_for(dg_ctx *c, hipStream_t s, Scratch **out)

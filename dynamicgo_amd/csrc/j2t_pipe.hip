@@ -875,6 +875,15 @@ void dg_agg_destroy(dg_agg *a)
         a->completer.join();
     }
     if (a->b) {
+        /* the context's scratches owned by (or last used on) the batch
+         * streams go before the streams do: an event last recorded on a
+         * destroyed stream is not safe to wait on later (HIP then reported
+         * "operation not permitted on an event last recorded in a capturing
+         * stream" from a later launch that grew a reused scratch) */
+        std::vector<hipStream_t> ss;
+        for (int k = 0; k < a->ring; k++)
+            if (a->b[k].s) ss.push_back(a->b[k].s);
+        dg_i_scratch_release(a->ctx, ss.data(), (int)ss.size());
         for (int k = 0; k < a->ring; k++) {
             Batch &x = a->b[k];
             if (x.s) (void)hipStreamSynchronize(x.s);

@@ -463,7 +463,29 @@ struct JOut {
             } else {
                 const uint32_t q = (gk + (uint32_t)wi) & 7;
                 g[q * gs] = lo;
+#if DG_T2W_GINL
+                if (q == 7) {
+                    if (wi >= 7 && (wi + 1) * 8 <= cap) { /* a whole aligned group: inline, no call */
+                        typedef __attribute__((address_space(1))) u64x2 gu64x2;
+                        gu64x2 *d = (gu64x2 *)(void *)(b + (wi - 7) * 8);
+#pragma unroll
+                        for (uint32_t j = 0; j < 3; j++) {
+                            u64x2 p;
+                            p.x = g[(2 * j) * gs];
+                            p.y = g[(2 * j + 1) * gs];
+                            d[j] = p;
+                        }
+                        u64x2 p;
+                        p.x = g[6 * gs];
+                        p.y = lo;
+                        d[3] = p;
+                    } else {
+                        flush(b, cap, g, gs, gk, wi >= 7 ? wi - 7 : 0, wi);
+                    }
+                }
+#else
                 if (q == 7) flush(b, cap, g, gs, gk, wi >= 7 ? wi - 7 : 0, wi);
+#endif
             }
             wbuf = hi;
         } else {
