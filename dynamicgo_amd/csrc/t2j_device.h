@@ -29,12 +29,7 @@
 
 namespace dg {
 
-#ifndef DG_T2W_JDEPTH
-#define DG_T2W_JDEPTH 10
-#endif
-/* frames per lane in LDS: 10 x 24 B + JOut's 64-byte group = 304 B per lane,
- * 76 KiB per 256-lane block, two blocks per CU (12 frames without the group) */
-constexpr uint32_t T2J_LDS_DEPTH = DG_T2W_JDEPTH;
+constexpr uint32_t T2J_LDS_DEPTH = 12;   /* frames per lane in LDS */
 constexpr uint32_t T2J_DEEP_DEPTH = 4096; /* frames per lane in the deep rerun */
 constexpr uint32_t T2J_WIDE_WORDS = 1024; /* deep rerun: requires words per lane for structs of > 64 fields */
 constexpr uint32_t T2J_BLOCK = 256;
@@ -389,35 +384,29 @@ DGI int32_t t2j_field(const DV &D, const dg_struct &sd, uint32_t hint, uint16_t 
     return -1;
 }
 
-/* JSON output of one lane: Out's 8-byte word assembly. Completed words
- * collect in the lane's 64-byte group in LDS (the group of the slot's
- * address space they fall in) and a completed group goes out as four
- * 16-byte stores at once. 64 lanes writing 64 slots word by word leave L2
- * lines half written long enough to be written back twice: 8-byte stores
- * showed 29.9 MB written on t2j-c2 for 13.6 MB of JSON and status words,
- * 16-byte pair stores 24.5 MB, non-temporal pair stores 44.6 MB. */
-typedef __attribute__((address_space(3))) uint64_t lds_w64;
+/* JSON output of one lane: Out's 8-byte word assembly, with completed words
+ * stored in aligned 16-byte pairs (one dwordx4 store per lane per 16 bytes,
+ * the width the L2 write counters and write-back handle whole; 8-byte stores
+ * of 64 lanes into 64 slots showed as 29.9 MB written on t2j-c2 for 13.6 MB
+ * of JSON). The first word of a pair waits in `wlo`. */
 struct JOut {
     typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
     gu8 *b;
     uint64_t cap;
     uint64_t len;
     uint64_t wbuf;  /* the word holding position len */
-    lds_w64 *g;     /* this lane's group: word q at g[q * gs] */
-    uint32_t gs;    /* lanes sharing the group array (word-major: no bank conflicts) */
-    uint32_t gk;    /* the slot's first word within its 64-byte group */
-    bool wide;      /* slot base 8-aligned: word and group stores allowed */
+    uint64_t wlo;   /* the completed first word of the pair holding len */
+    uint32_t sk;    /* the slot's first word within its 16-byte pair (0 or 1) */
+    bool wide;      /* slot base 8-aligned: word and pair stores allowed */
 
-    DGI void init(uint8_t *base, uint64_t c, lds_w64 *grp, uint32_t stride)
+    DGI void init(uint8_t *base, uint64_t c)
     {
         b = (gu8 *)(void *)base;
         cap = c;
         len = 0;
-        wbuf = 0;
-        g = grp;
-        gs = stride;
+        wbuf = wlo = 0;
         wide = ((uintptr_t)base & 7) == 0;
-        gk = wide ? (uint32_t)(((uintptr_t)base >> 3) & 7) : 0u;
+        sk = wide ? (uint32_t)(((uintptr_t)base >> 3) & 1) : 0u;
     }
     DGI void store_word(uint64_t wi, uint64_t v)
     {
@@ -425,26 +414,18 @@ struct JOut {
         if (wide && a + 8 <= cap) *(gu64 *)(b + a) = v;
         else if (a < cap) Out::store_bytes(b, a, cap, v);
     }
-    /* words [w0, w1] of the slot from the group (w1 - w0 < 8): a whole
-     * aligned group as four 16-byte stores, else word by word */
-    static __device__ __noinline__ void flush(gu8 *b, uint64_t cap, const lds_w64 *g, uint32_t gs, uint32_t gk,
-                                              uint64_t w0, uint64_t w1)
+    DGI uint64_t load_word(uint64_t wi) const
     {
-        if (w1 - w0 == 7 && ((gk + w0) & 7) == 0 && (w1 + 1) * 8 <= cap) {
-            typedef __attribute__((address_space(1))) u64x2 gu64x2;
-            gu64x2 *d = (gu64x2 *)(void *)(b + w0 * 8);
-#pragma unroll
-            for (uint32_t j = 0; j < 4; j++) {
-                u64x2 p;
-                p.x = g[(2 * j) * gs];
-                p.y = g[(2 * j + 1) * gs];
-                d[j] = p;
-            }
-            return;
-        }
-        for (uint64_t w = w0; w <= w1; w++) {
-            const uint64_t a = w << 3, v = g[((gk + w) & 7) * gs];
-            if (a + 8 <= cap) *(gu64 *)(b + a) = v;
+        const uint64_t a = wi << 3;
+        if (wide && a + 8 <= cap) return *(const gu64 *)(b + a);
+        return a < cap ? Out::load_bytes(b, a, cap) : 0;
+    }
+    static __device__ __noinline__ void pair_edge(gu8 *b, uint64_t cap, bool wide, uint64_t wi, uint64_t w0, uint64_t w1)
+    {
+        for (uint32_t j = 0; j < 2; j++) {
+            if (wi + j < 1) continue;
+            const uint64_t a = (wi + j - 1) << 3, v = j ? w1 : w0;
+            if (wide && a + 8 <= cap) *(gu64 *)(b + a) = v;
             else if (a < cap) Out::store_bytes(b, a, cap, v);
         }
     }
@@ -458,34 +439,18 @@ struct JOut {
         const uint64_t wi = len >> 3;
         len += n;
         if (used + n >= 8) {
-            if (!wide) {
-                store_word(wi, lo);
+            if (((sk + (uint32_t)wi) & 1) == 0) {
+                wlo = lo;
+            } else if (wide && wi >= 1 && (wi + 1) * 8 <= cap) {
+                u64x2 p;
+                p.x = wlo;
+                p.y = lo;
+                /* (non-temporal stores here: 44.6 MB written on t2j-c2 instead of 24.7, r4m;
+                 * whole 64-byte groups staged in LDS, branch wip-jout-groups: 16.6 MB
+                 * written, but the kernel 52.4 -> 59.7 us, r4o/r4p) */
+                *(__attribute__((address_space(1))) u64x2 *)(void *)(b + (wi - 1) * 8) = p; /* 16-byte aligned */
             } else {
-                const uint32_t q = (gk + (uint32_t)wi) & 7;
-                g[q * gs] = lo;
-#if DG_T2W_GINL
-                if (q == 7) {
-                    if (wi >= 7 && (wi + 1) * 8 <= cap) { /* a whole aligned group: inline, no call */
-                        typedef __attribute__((address_space(1))) u64x2 gu64x2;
-                        gu64x2 *d = (gu64x2 *)(void *)(b + (wi - 7) * 8);
-#pragma unroll
-                        for (uint32_t j = 0; j < 3; j++) {
-                            u64x2 p;
-                            p.x = g[(2 * j) * gs];
-                            p.y = g[(2 * j + 1) * gs];
-                            d[j] = p;
-                        }
-                        u64x2 p;
-                        p.x = g[6 * gs];
-                        p.y = lo;
-                        d[3] = p;
-                    } else {
-                        flush(b, cap, g, gs, gk, wi >= 7 ? wi - 7 : 0, wi);
-                    }
-                }
-#else
-                if (q == 7) flush(b, cap, g, gs, gk, wi >= 7 ? wi - 7 : 0, wi);
-#endif
+                pair_edge(b, cap, wide, wi, wlo, lo);
             }
             wbuf = hi;
         } else {
@@ -493,20 +458,23 @@ struct JOut {
         }
     }
     DGI void w8(uint8_t v) { wle(v, 1); }
-    /* back to an empty output (the only truncation t2j_convert makes) */
-    DGI void reset()
+    /* truncate to x <= len */
+    DGI void set_len(uint64_t x)
     {
-        len = 0;
-        wbuf = 0;
+        const uint64_t xw = x >> 3, lw = len >> 3;
+        if (((sk + xw) >> 1) != ((sk + lw) >> 1)) { /* x's pair is stored already: take it back */
+            if (((sk + (uint32_t)xw) & 1) && xw >= 1) wlo = load_word(xw - 1);
+            wbuf = (x & 7) ? load_word(xw) : 0;
+        } else if (xw != lw) {
+            wbuf = (x & 7) ? wlo : 0;
+        }
+        len = x;
     }
-    /* the open group's completed words, and the partial word */
+    /* the waiting first word of the open pair, and the partial word */
     DGI void finish()
     {
         const uint64_t lw = len >> 3;
-        if (wide) {
-            const uint32_t q = (gk + (uint32_t)lw) & 7; /* lw's place in its group */
-            if (q && lw) flush(b, cap, g, gs, gk, lw >= q ? lw - q : 0, lw - 1);
-        }
+        if (((sk + (uint32_t)lw) & 1) && lw >= 1) store_word(lw - 1, wlo);
         if (len & 7) store_word(lw, wbuf);
     }
 };
@@ -841,7 +809,7 @@ DGI uint64_t t2j_convert(const DV &D, const T2JSide &X, S src, uint32_t root, ui
                      * every level (resp may be nil there) */
                     uint8_t a;
                     if (!take(a)) {
-                        o.reset();
+                        o.set_len(0);
                         return stop(2 | (resp ? 0x100u : 0u), ans_seen - 1, sd.field_begin + k, 0, 0);
                     }
                     if (a == 0) continue;
@@ -928,7 +896,7 @@ DGI uint64_t t2j_convert(const DV &D, const T2JSide &X, S src, uint32_t root, ui
                 uint8_t a;
                 const uint8_t dt = ldrec(&D.T[fd.type]).ttype;
                 if (!take(a)) { /* a new call: the host reads the value at the stop's position */
-                    o.reset();
+                    o.set_len(0);
                     return stop(1 | 0x100u, ans_seen - 1, (uint32_t)fi, r.p, r.p);
                 }
                 if (a == 2 && (dt == DG_T_STRUCT || dt == DG_T_MAP || dt == DG_T_LIST || dt == DG_T_SET)) {
@@ -938,7 +906,7 @@ DGI uint64_t t2j_convert(const DV &D, const T2JSide &X, S src, uint32_t root, ui
                     cb_fi = (uint32_t)fi;
                     cb_sp = sp;
                     cb_idx = ans_seen - 1;
-                    o.reset();
+                    o.set_len(0);
                     push_resp = true;
                     e = value(fd.type);
                     push_resp = false;
@@ -955,7 +923,7 @@ DGI uint64_t t2j_convert(const DV &D, const T2JSide &X, S src, uint32_t root, ui
             const dg_t2j_field xf = ldrec(&X.X[fi]);
             emit_side(o, X, xf.key_off, xf.key_len); /* "alias": */
             if (sp == 1 && (opts & DG_T2J_CONVERT_EXC) && id != 0) { /* only the exception field's data */
-                o.reset();
+                o.set_len(0);
                 exc = true;
             }
             if ((opts & DG_T2J_ENABLE_VM) && fd.vm == DG_VM_BODY_DYNAMIC) {

@@ -15,7 +15,6 @@ __global__ __launch_bounds__(T2J_BLOCK) void t2j_kernel(T2JParams P)
 {
     constexpr uint32_t MPB = T2J_BLOCK / SP; /* messages per block */
     __shared__ __attribute__((aligned(16))) T2JFrame lf[T2J_LDS_DEPTH * MPB];
-    __shared__ uint64_t s_og[8 * MPB]; /* JOut's 64-byte groups, word-major */
     if (threadIdx.x % SP) return;
     const uint32_t slot = threadIdx.x / SP;
     const auto D = desc_view<1>((const __attribute__((address_space(1))) uint8_t *)(const void *)P.blob, P.hdr);
@@ -31,7 +30,7 @@ __global__ __launch_bounds__(T2J_BLOCK) void t2j_kernel(T2JParams P)
         SrcT<glb_u64> s;
         s.init((glb_u64 *)(const void *)(P.src + (a & ~7ull)), (int64_t)(a & 7), (int64_t)(b - a));
         JOut o;
-        o.init(P.out + P.out_off[i], P.out_off[i + 1] - P.out_off[i], (lds_w64 *)(void *)&s_og[slot], MPB);
+        o.init(P.out + P.out_off[i], P.out_off[i + 1] - P.out_off[i]);
         const uint64_t r = t2j_convert<GO>(D, X, s, P.root, P.opts, o,
                                        (__attribute__((address_space(3))) T2JFrame *)(void *)&lf[slot], MPB,
                                        T2J_LDS_DEPTH, nullptr, 0, P.aux ? P.aux + i : nullptr,
@@ -119,7 +118,6 @@ __global__ __launch_bounds__(64 * T2W_WAVES) __attribute__((amdgpu_waves_per_eu(
 template <bool GO>
 __global__ __launch_bounds__(T2J_BLOCK) void t2j_deep_kernel(T2JParams P)
 {
-    __shared__ uint64_t s_og[8 * T2J_BLOCK]; /* JOut's 64-byte groups */
     const uint32_t cnt = *(volatile uint32_t *)P.deep_count;
     const uint32_t lane = blockIdx.x * T2J_BLOCK + threadIdx.x;
     const auto D = desc_view<1>((const __attribute__((address_space(1))) uint8_t *)(const void *)P.blob, P.hdr);
@@ -134,7 +132,7 @@ __global__ __launch_bounds__(T2J_BLOCK) void t2j_deep_kernel(T2JParams P)
         SrcT<glb_u64> s;
         s.init((glb_u64 *)(const void *)(P.src + (a & ~7ull)), (int64_t)(a & 7), (int64_t)(b - a));
         JOut o;
-        o.init(P.out + P.out_off[i], P.out_off[i + 1] - P.out_off[i], (lds_w64 *)(void *)&s_og[threadIdx.x], T2J_BLOCK);
+        o.init(P.out + P.out_off[i], P.out_off[i + 1] - P.out_off[i]);
         uint64_t r = t2j_convert<GO>(D, X, s, P.root, P.opts, o, fr, 1, T2J_DEEP_DEPTH, wide, T2J_WIDE_WORDS,
                                  P.aux ? P.aux + i : nullptr, P.ans_tab ? P.ans_tab + i : nullptr, P.ans_bytes);
         if ((uint8_t)r == DG_ST_DEEP) r = t2j_err(DG_T2J_E_DEPTH, 0, T2J_DEEP_DEPTH);
