@@ -1,4 +1,4 @@
-# round 4 profiles: GPU suite, smoke, every bench line, kernel stats, t2j traffic (PMC, separate passes)
+# round profiles (r4z): GPU suite, smoke, every bench line, kernel stats, t2j traffic (PMC, separate passes)
 set -o pipefail
 O=gpurun_out/r4z
 mkdir -p $O
