@@ -572,7 +572,7 @@ def bench_agg(args, rank, world, dev, dist, backend, td, arena, off, meta):
     max_wait_us = 200
     runs = []
     for ri, (threads, window) in enumerate(AGG_RUNS):
-        per_thread = max(64, window // 4)
+        per_thread = max(64, window // int(os.environ.get("DG_BENCH_AGG_SHARE_DIV", "4")))
         if ri == 0:
             max_batch = per_thread
         h = C.c_void_p()
