@@ -550,7 +550,7 @@ def bench_agg(args, rank, world, dev, dist, backend, td, arena, off, meta):
     submit + wait) from `threads` OS threads, as the reference's
     b.RunParallel benchmark does from goroutines (conv/j2t/conv_timing_test.go:
     76-99); the aggregator coalesces them into device batches (upload,
-    convert, pack, download overlapped over 4 batches in flight). A step is
+    convert, pack, download overlapped over the ring's 16 batches). A step is
     one pass over all calls; wall-clock timed, host memory in and out."""
     import torch
     import ctypes as C
