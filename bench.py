@@ -721,7 +721,9 @@ def main(argv=None):
     dev = torch.device("cuda", local % ndev)
     torch.cuda.set_device(dev)
     backend = os.environ.get("DG_DIST_BACKEND", "nccl" if ndev >= world else "gloo")
-    dist = world > 1
+    # DG_FORCE_DIST=1: the distributed branch at world size 1 as well (the
+    # RCCL leg on a one-GPU box: tests/test_gpu_dist.py)
+    dist = world > 1 or os.environ.get("DG_FORCE_DIST") == "1"
     if dist:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         kw = {"device_id": dev} if backend == "nccl" else {}

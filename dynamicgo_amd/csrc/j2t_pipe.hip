@@ -986,7 +986,8 @@ int dg_j2t_pipeline_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8
     const bool zc = host_pinned(json, &dv_json) && host_pinned(json + jend, &dv_end) &&
                     (uint8_t *)dv_end - (uint8_t *)dv_json == (ptrdiff_t)jend && host_pinned(in_off, &dv_in) &&
                     host_pinned(in_off + n, &dv_in_end) && (uint64_t *)dv_in_end - (uint64_t *)dv_in == (ptrdiff_t)n &&
-                    !getenv("DG_NO_ZERO_COPY");
+                    ((uintptr_t)dv_json & 15) == 0 && /* the flat kernel loads 16-byte words from the arena's base */
+                    ((uintptr_t)dv_in & 7) == 0 && !getenv("DG_NO_ZERO_COPY");
     /* staged (DG_PIPE_STAGED=1, the r4i layout): pack into device memory,
      * then a copy-out kernel; else the packing writes the host buffers */
     static const bool staged = getenv("DG_PIPE_STAGED") != nullptr;

@@ -606,24 +606,30 @@ class BinaryConv:
             else:
                 pending.append(i)
         answers = {i: bytearray() for i in pending} if hm else None
-        with_base = any(b is not None for b in bases)
         flat = self._flat(desc) if hm else None
         while pending:
-            o, r, a = self._batch(desc, [msgs[i] for i in pending], with_base,
-                                  [answers[i] for i in pending] if hm else None)
             nxt = []
-            for k, i in enumerate(pending):
-                rr = int(r[k])
-                if hm and (rr & 0xFF) == E_CALLBACK:
-                    try:
-                        self._serve(flat, msgs[i], resps[i], answers[i], o[k])
-                        nxt.append(i)
-                    except (H.ConvError, ValueError, ThriftReadError) as e:
-                        errs[i] = e
+            # readResponseBase skips the field only when the context holds a
+            # BaseResp (conv/t2j/impl.go:54-58, 120-127): messages with and
+            # without one run as separate launches with their own options
+            for with_base in (True, False):
+                grp = [i for i in pending if (bases[i] is not None) == with_base]
+                if not grp:
                     continue
-                outs[i], rets[i] = o[k], rr
-                aux[i] = int(a[k]) if a is not None else None
-            pending = nxt
+                o, r, a = self._batch(desc, [msgs[i] for i in grp], with_base,
+                                      [answers[i] for i in grp] if hm else None)
+                for k, i in enumerate(grp):
+                    rr = int(r[k])
+                    if hm and (rr & 0xFF) == E_CALLBACK:
+                        try:
+                            self._serve(flat, msgs[i], resps[i], answers[i], o[k])
+                            nxt.append(i)
+                        except (H.ConvError, ValueError, ThriftReadError) as e:
+                            errs[i] = e
+                        continue
+                    outs[i], rets[i] = o[k], rr
+                    aux[i] = int(a[k]) if a is not None else None
+            pending = sorted(nxt)
         for i in range(n):
             if errs[i] is not None:
                 outs[i] = b""

@@ -144,13 +144,15 @@ def test_pipeline_host_overflow_splice_and_nomem():
     assert [(int(r), o) for r, o in zip(rets, outs)] == [(r, o) for r, o in want]
 
 
-@pytest.mark.parametrize("chunks,shift", [(1, 0), (5, 0), (1, 3), (4, 11)])
-def test_pipeline_host_pinned_direct(chunks, shift):
+@pytest.mark.parametrize("chunks,shift,jshift", [(1, 0, 0), (5, 0, 0), (1, 3, 0), (4, 11, 0), (1, 0, 5), (3, 2, 8)])
+def test_pipeline_host_pinned_direct(chunks, shift, jshift):
     """With pinned host buffers the chained packing writes the caller's
     out / out_off straight from the GPU; a too-small out_cap writes nothing
     past it and reports the exact need. shift: `out` starts that many bytes
     into a pinned allocation (not 16-aligned: the first chunk's copy-out
-    must not drop its bytes)."""
+    must not drop its bytes). jshift: the JSON arena starts that many bytes
+    into a pinned allocation (not 16-aligned, so the kernels must
+    not read it in place with 16-byte loads; the staged copy is used)."""
     import ctypes as C
     import numpy as np
     import torch
@@ -162,7 +164,9 @@ def test_pipeline_host_pinned_direct(chunks, shift):
     want = [chk.j2t(fl, m, 1) for m in msgs]
     n = len(msgs)
     a, off = W.arena(msgs)
-    h_json = torch.from_numpy(a).pin_memory()
+    h_jbuf = torch.zeros(len(a) + jshift, dtype=torch.uint8).pin_memory()
+    h_jbuf[jshift:] = torch.from_numpy(a)
+    h_json = h_jbuf[jshift:]
     h_in = torch.from_numpy(off.astype(np.int64)).pin_memory()
     cv = conv.BinaryConv(conv.Options())
     ctx = cv._ctx()

@@ -530,6 +530,16 @@ def test_response_base(chk):
     assert all(e is None for e in errs)
     r, js, aux = chk.t2j2(fl, side, src, SKIP_BASE)
     assert outs[0] == js
+    # a mixed batch: only the messages whose context holds a BaseResp skip
+    # the field (readResponseBase returns false without one, impl.go:54-58)
+    bases = [t2j.BaseResp(), None, t2j.BaseResp(), None]
+    outs, errs = cv.do_batch_errors(td, [src] * 4, bases=bases)
+    assert all(e is None for e in errs)
+    for k in range(4):
+        alone = cv.do(td, src, base=t2j.BaseResp() if bases[k] is not None else None)
+        assert outs[k] == alone, k
+    assert json.loads(outs[1]) == dict(plain, BaseResp=want)
+    assert json.loads(outs[0]) == plain
 
 
 # ---- EnableHttpMapping: the device's writeHttpValue stops against the harness ----

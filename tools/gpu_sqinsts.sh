@@ -1,11 +1,14 @@
-# instructions per message of the wave kernels (SQ_INSTS_*; one PMC pass each config)
+# instructions per message and wave-cycle breakdown (SQ counters; one PMC pass each)
+# usage: O=gpurun_out/r5a CONFIGS="c2 c2s" bash tools/gpu_sqinsts.sh
 set -o pipefail
-O=gpurun_out/r4u
-PMC=${PMC:-"SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES"}
-TAG=${TAG:-sq_}
+O=${O:-gpurun_out/r5a}
+CONFIGS=${CONFIGS:-"c3 t2j-c3"}
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-for c in c3 t2j-c3; do
-  timeout -s KILL 90 rocprofv3 --pmc $PMC --kernel-trace --output-format csv -d $O/$TAG$c -o run -- python3 -u bench.py --config $c --steps 2 --warmup 1 --no-cpu-baseline --no-e2e --inflight 1 > $O/$TAG$c.log 2>&1 || { tail -20 $O/$TAG$c.log; exit 1; }
+for c in $CONFIGS; do
+  for pass in insts cycles; do
+    if [ $pass = insts ]; then PMC="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES"; else PMC="SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY"; fi
+    timeout -s KILL 90 rocprofv3 --pmc $PMC --kernel-trace --output-format csv -d $O/sq_${pass}_$c -o run -- python3 -u bench.py --config $c --steps 2 --warmup 1 --no-cpu-baseline --no-e2e --inflight 1 > $O/sq_${pass}_$c.log 2>&1 || { tail -20 $O/sq_${pass}_$c.log; exit 1; }
+  done
 done
 find $O -name "*counter_collection.csv"
