@@ -18,7 +18,8 @@ EXPORTS = ["dg_last_error", "dg_build_info", "dg_ctx_create", "dg_ctx_destroy", 
            "dg_j2t_batch_device_ml", "dg_j2t_batch_device_hm", "dg_j2t_batch_device_cb", "dg_j2t_batch_device_iters",
            "dg_j2t_batch_device_inflight",
            "dg_slot_bound", "dg_j2t_batch_host", "dg_j2t_batch_host_hm", "dg_j2t_batch_host_cb", "dg_j2t_do", "dg_pack_device", "dg_pack_device_scan", "dg_pack_device_framed", "dg_agg_create", "dg_agg_create2", "dg_agg_do",
-           "dg_agg_submit", "dg_agg_wait", "dg_agg_ready", "dg_agg_stats", "dg_agg_profile", "dg_agg_destroy", "dg_agg_drive", "dg_j2t_pipeline_host", "dg_bench_device", "dg_desc_attach_t2j", "dg_t2j_slot_bound", "dg_t2j_batch_device", "dg_t2j_batch_device_ml",
+           "dg_agg_submit", "dg_agg_wait", "dg_agg_ready", "dg_agg_stats", "dg_agg_profile", "dg_agg_destroy", "dg_agg_drive", "dg_agg_wait_gen", "dg_agg_ticket_gen", "dg_agg_set_knob",
+           "dg_agg_gateway_drive", "dg_j2t_pipeline_host", "dg_bench_device", "dg_desc_attach_t2j", "dg_t2j_slot_bound", "dg_t2j_batch_device", "dg_t2j_batch_device_ml",
            "dg_t2j_batch_host", "dg_t2j_batch_device_aux", "dg_t2j_batch_host_aux",
            "dg_t2j_batch_device_cb", "dg_t2j_batch_host_cb"]
 
@@ -81,6 +82,10 @@ def lib() -> C.CDLL:
         "dg_agg_wait": (i32, [vp, vp, vp, sz, C.POINTER(sz), P64]),
         "dg_agg_ready": (i32, [vp, vp]),
         "dg_agg_drive": (i32, [vp, vp, vp, u64, i32, i32, vp, vp, vp, vp, vp, C.POINTER(C.c_double)]),
+        "dg_agg_wait_gen": (i32, [vp, u64, u32, P64]),
+        "dg_agg_ticket_gen": (u64, [vp]),
+        "dg_agg_set_knob": (i32, [vp, C.c_char_p, C.c_int64]),
+        "dg_agg_gateway_drive": (i32, [vp, vp, vp, u64, i32, i32, vp, vp, vp, vp, vp, C.POINTER(C.c_double), vp]),
         "dg_j2t_pipeline_host": (i32, [vp, vp, u32, vp, vp, u64, u64, u32, vp, u64, vp, vp, P64]),
         "dg_agg_stats": (i32, [vp, P64, P64]),
         "dg_agg_profile": (i32, [vp, P64, i32]),

@@ -742,6 +742,36 @@ class Aggregator:
         outs = [out[int(out_off[i]):int(out_off[i]) + int(out_len[i])].tobytes() for i in range(n)]
         return outs, rets[:n], lat[:n], secs.value
 
+    def set_knob(self, name: str, value: int):
+        """dg_agg_set_knob: "depth" (seal as soon as fewer than depth batches
+        convert; for callers that park instead of blocking), "max_wait_us"."""
+        _lib.check(_lib.lib().dg_agg_set_knob(self.h, name.encode(), int(value)))
+
+    def gateway(self, msgs: Sequence[bytes], callers: int = 1024, workers: int = 16):
+        """The gateway shape (dg_agg_gateway_drive): `callers` logical callers
+        with one call in flight each -- goroutines in Do -- multiplexed over
+        `workers` OS threads, woken per converted generation by one poller
+        (dg_agg_wait_gen). Returns (outputs, statuses, latency ns of every 8th
+        message, wall seconds, stats [parks, retries, wake-ups, callers])."""
+        n = len(msgs)
+        lens = np.fromiter((len(m) for m in msgs), dtype=np.uint64, count=n)
+        in_off = np.zeros(n + 1, dtype=np.uint64)
+        np.cumsum(lens, out=in_off[1:])
+        arena = np.frombuffer(b"".join(msgs) + b"\0" * 16, dtype=np.uint8)
+        out_off = np.zeros(n + 1, dtype=np.uint64)
+        np.cumsum(lens * 4 + 4096, out=out_off[1:])
+        out = np.zeros(int(out_off[-1]) + 64, dtype=np.uint8)
+        out_len = np.zeros(max(n, 1), dtype=np.uint64)
+        rets = np.zeros(max(n, 1), dtype=np.uint64)
+        lat = np.zeros(max(n, 1), dtype=np.uint32)
+        st = np.zeros(4, dtype=np.uint64)
+        secs = C.c_double(0)
+        _lib.check(_lib.lib().dg_agg_gateway_drive(self.h, arena.ctypes.data, in_off.ctypes.data, n, workers, callers,
+                                                   out.ctypes.data, out_off.ctypes.data, out_len.ctypes.data,
+                                                   rets.ctypes.data, lat.ctypes.data, C.byref(secs), st.ctypes.data))
+        outs = [out[int(out_off[i]):int(out_off[i]) + int(out_len[i])].tobytes() for i in range(n)]
+        return outs, rets[:n], lat[:n], secs.value, [int(v) for v in st]
+
     def stats(self) -> Tuple[int, int]:
         """(batches flushed, messages converted)."""
         b, m = C.c_uint64(0), C.c_uint64(0)

@@ -30,7 +30,8 @@ __attribute__((visibility("hidden"))) int set_err(int code, const char *fmt, ...
  * share lists or counters; past that cap a scratch is shared and the next
  * launch on another stream waits for its previous launch (hipStreamWaitEvent
  * on `done`), which keeps the ordering rule true in every case. */
-constexpr int DG_MAX_SCRATCH = 24; /* an aggregator ring (<= 16 streams) + the context's + in-flight side streams */
+constexpr int DG_MAX_SCRATCH = 40; /* an aggregator ring (<= AGG_RING_MAX = 24 streams) + the context's stream
+                                    * + the in-flight side streams (<= 7) + the host pipeline's 3 */
 constexpr uint32_t DG_NCOUNTS = 16;
 constexpr uint32_t DG_J2T_COUNTS_BYTES = 6 * 4;
 constexpr uint32_t DG_T2J_DEEP_COUNT = 8;

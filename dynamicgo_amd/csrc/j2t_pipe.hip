@@ -247,14 +247,21 @@ struct DevBuf {
 
 /* ---------------- the aggregator ---------------- */
 
-constexpr int AGG_RING_MAX = 32; /* batches in the ring (dg_agg::ring, DG_AGG_RING, default 16) */
-constexpr int AGG_SLOTS = 256; /* caller threads per aggregator (more convert alone, dg_j2t_do) */
+constexpr int AGG_RING_MAX = 24; /* batches in the ring (dg_agg::ring, DG_AGG_RING, default 16): each batch stream
+                                  * gets its own device scratch (DG_MAX_SCRATCH covers the ring + the context's own) */
+constexpr int AGG_SLOTS = 256;  /* parts per batch */
+constexpr int AGG_SHARED = 32;  /* the last AGG_SHARED parts are shared: a thread that finds the exclusive parts
+                                 * taken writes one of these under its lock (no call converts alone for want of
+                                 * a part, whatever the number of threads) */
+constexpr int AGG_EXCL = AGG_SLOTS - AGG_SHARED;
+constexpr int AGG_GEN_RING = 64; /* dg_agg_gateway_drive: parked callers by generation (> AGG_RING_MAX + 2) */
 constexpr int AGG_EAGER_INFLIGHT = 1;
 constexpr uint64_t AGG_EXACT_MAX = 64ull << 20; /* launch(): per-batch buffers sized for the parts' caps up to this */
 
 /* one caller thread's part of one batch (its own cache lines) */
 struct alignas(128) Sub {
-    std::atomic<uint32_t> busy{0}; /* 1 while the owner writes a message (the seal handshake) */
+    std::atomic<uint32_t> busy{0}; /* 1 while the owner writes a message (the seal handshake; for a shared part
+                                    * also the lock among its writers) */
     std::atomic<uint32_t> n{0};    /* messages committed */
     uint64_t bytes = 0;            /* JSON bytes committed (owner-written) */
     uint64_t maxlen = 0;           /* its longest message (owner-written) */
@@ -311,7 +318,19 @@ struct dg_agg {
     Batch *b = nullptr;
     int ring = 16;                   /* batches in the ring: one filling, the rest converting or being taken (r4j: 16 threads 53.3M calls/s vs 48.5M at 8) */
     std::atomic<uint64_t> open{0};   /* the open generation; batch b[open % ring] */
-    std::atomic<int> nslots{0};
+    std::atomic<int> nslots{0};      /* exclusive parts handed out (<= AGG_EXCL) */
+    std::atomic<int> nshared{0};     /* shared parts whose regions exist */
+    std::atomic<uint32_t> shared_rr{0};
+    /* depth > 0 (dg_agg_set_knob "depth"): the flusher also seals the open
+     * batch as soon as it holds a message and fewer than `depth` batches
+     * are converting -- the policy for callers that do not block in
+     * dg_agg_wait (goroutines parked on a channel, an event loop) */
+    std::atomic<int> depth{0};
+    /* every generation <= done_upto is converted and readable (the completer
+     * finishes batches in generation order); dg_agg_wait_gen blocks on it */
+    std::atomic<uint64_t> done_upto{0};
+    std::mutex gen_mu;
+    std::condition_variable cv_gen;
     std::atomic<uint8_t> ready[AGG_SLOTS];
     std::mutex mu;                   /* open changes, frees, flusher wakeups, completer queue */
     std::condition_variable cv_flush, cv_open, cv_done;
@@ -337,7 +356,13 @@ struct dg_agg {
     {
         return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now().time_since_epoch()).count();
     }
-    int slot();
+    int slot(bool &shared);
+    /* parts to scan at a seal: the exclusive ones handed out, then the shared ones */
+    int nparts() const
+    {
+        const int sh = nshared.load(std::memory_order_seq_cst);
+        return sh ? AGG_EXCL + sh : std::min(nslots.load(std::memory_order_seq_cst), AGG_EXCL);
+    }
     std::vector<int> free_slots;     /* parts of exited threads (under mu) */
     void release_slot(int s)
     {
@@ -357,13 +382,17 @@ struct dg_agg {
 namespace {
 /* the parts this thread holds, by aggregator id; handed back at thread exit */
 struct ThreadParts {
-    std::vector<std::pair<uint64_t, int>> v;
+    std::vector<std::pair<uint64_t, int>> v; /* (aggregator id, part); part | 0x10000 = shared */
     ~ThreadParts()
     {
+        /* an exclusive part goes to the next new thread. Tickets this thread
+         * submitted stay valid: dg_agg_wait may take them from any thread
+         * (a goroutine resumes on another OS thread), and the next owner
+         * appends behind them in the open batch */
         std::lock_guard<std::mutex> g(g_reg_mu);
         for (const auto &e : v) {
             auto it = g_reg.find(e.first);
-            if (it != g_reg.end() && e.second >= 0) it->second->release_slot(e.second);
+            if (it != g_reg.end() && e.second >= 0 && e.second < AGG_EXCL) it->second->release_slot(e.second);
         }
     }
 };
@@ -373,11 +402,15 @@ thread_local ThreadParts t_parts;
 /* this thread's slot (sub-batch index), registered on first use: an exited
  * thread's part, else new pinned regions in every batch of the ring; -1 when
  * all are taken */
-int dg_agg::slot()
+int dg_agg::slot(bool &shared)
 {
     for (const auto &e : t_parts.v)
-        if (e.first == id) return e.second;
+        if (e.first == id) {
+            shared = e.second >= AGG_EXCL;
+            return e.second;
+        }
     int s = -1;
+    shared = false;
     {
         std::lock_guard<std::mutex> g(mu);
         if (!free_slots.empty()) {
@@ -386,10 +419,32 @@ int dg_agg::slot()
         }
     }
     if (s >= 0) {
-        /* its regions exist; its previous owner has no message left in it */
-    } else if ((s = nslots.fetch_add(1, std::memory_order_seq_cst)) >= AGG_SLOTS) {
+        /* its regions exist */
+    } else if ((s = nslots.fetch_add(1, std::memory_order_seq_cst)) >= AGG_EXCL) {
         nslots.fetch_sub(1);
-        s = -1;
+        /* the exclusive parts are taken: a shared one, round robin; its
+         * regions are made once, by whoever gets it first */
+        shared = true;
+        const int k = (int)(shared_rr.fetch_add(1, std::memory_order_relaxed) % AGG_SHARED);
+        s = AGG_EXCL + k;
+        std::lock_guard<std::mutex> g(mu);
+        while (nshared.load(std::memory_order_relaxed) <= k) {
+            const int j = AGG_EXCL + nshared.load(std::memory_order_relaxed);
+            bool ok = true;
+            (void)hipSetDevice(ctx->device);
+            for (int r = 0; r < ring && ok; r++) {
+                uint64_t cap = 0;
+                uint8_t *h = nullptr;
+                ok = grow_pinned(h, cap, 8 * cap_n + cap_b + 64) == DG_OK;
+                b[r].sub[j].h = h;
+            }
+            if (!ok) {
+                s = -1;
+                break;
+            }
+            ready[j].store(1, std::memory_order_release);
+            nshared.fetch_add(1, std::memory_order_seq_cst);
+        }
     } else {
         bool ok = true;
         (void)hipSetDevice(ctx->device);
@@ -410,7 +465,7 @@ int dg_agg::launch(Batch *x)
 {
     /* the sub-batches: every registered slot, once its owner is not in the
      * middle of a message (it saw the old generation open before the flip) */
-    const int ns = nslots.load(std::memory_order_seq_cst);
+    const int ns = nparts();
     uint32_t nsub = 0;
     uint64_t N = 0, B = 0;
     const uint64_t l0 = now_ns();
@@ -485,6 +540,8 @@ void dg_agg::run_flusher()
             for (;;) {
                 if (x->seal_req.load(std::memory_order_acquire)) break;
                 const uint64_t t0 = x->t_first.load(std::memory_order_acquire);
+                const int dp = depth.load(std::memory_order_relaxed);
+                if (dp > 0 && t0 && !stop && busy_batches.load(std::memory_order_seq_cst) < dp) break;
                 if (stop) {
                     if (!t0) {
                         inflight.push_back(nullptr); /* the completer's exit marker */
@@ -512,7 +569,7 @@ void dg_agg::run_flusher()
             cv_flush.wait(lk, [&] { return y->free_; });
             y->free_ = false;
         }
-        const int ns = nslots.load(std::memory_order_acquire);
+        const int ns = nparts();
         for (int s = 0; s < ns; s++) {
             y->sub[s].n.store(0, std::memory_order_relaxed);
             y->sub[s].bytes = 0;
@@ -583,9 +640,15 @@ void dg_agg::run_completer()
             x->done_g.store(x->g, std::memory_order_release);
         }
         x->cv.notify_all();
+        {
+            std::lock_guard<std::mutex> lk(gen_mu);
+            done_upto.store(x->g, std::memory_order_release);
+        }
+        cv_gen.notify_all();
         if (!empty) {
             /* room in the pipeline: seal the open batch if all its callers wait on it */
             busy_batches.fetch_sub(1, std::memory_order_seq_cst);
+            if (depth.load(std::memory_order_relaxed) > 0) wake_flusher(); /* room under the depth */
             Batch *o = &b[open.load(std::memory_order_seq_cst) % ring];
             const uint32_t parts = o->parts.load(std::memory_order_seq_cst);
             if (parts && o->blocked.load(std::memory_order_seq_cst) >= parts &&
@@ -718,7 +781,8 @@ int dg_agg_submit(dg_agg *a, const uint8_t *json, size_t len, int nonblock, dg_a
     t->json = len ? json : &empty;
     t->len = len;
     t->batch = nullptr;
-    const int s = len > a->cap_b ? -1 : a->slot();
+    bool shared = false;
+    const int s = len > a->cap_b ? -1 : a->slot(shared);
     if (s < 0) { /* converted alone by dg_agg_wait */
         a->prof[11].fetch_add(1, std::memory_order_relaxed);
         return DG_OK;
@@ -727,7 +791,10 @@ int dg_agg_submit(dg_agg *a, const uint8_t *json, size_t len, int nonblock, dg_a
         const uint64_t g = a->open.load(std::memory_order_seq_cst);
         Batch *x = &a->b[g % a->ring];
         Sub &u = x->sub[s];
-        if (a->asym) {
+        if (shared) { /* the part's lock among its writers, and the seal handshake (a locked RMW is a full fence) */
+            for (uint32_t z = 0; !u.busy.compare_exchange_weak(z, 1, std::memory_order_seq_cst); z = 0)
+                std::this_thread::yield();
+        } else if (a->asym) {
             u.busy.store(1, std::memory_order_relaxed);
             std::atomic_signal_fence(std::memory_order_seq_cst); /* the flusher's membarrier is the fence */
         } else {
@@ -1208,6 +1275,203 @@ int dg_agg_drive(dg_agg *a, const uint8_t *arena, const uint64_t *in_off, uint64
     for (auto &x : th) x.join();
     *seconds = std::chrono::duration<double>(Clock::now() - ts).count();
     return failed.load() ? set_err(DG_E_HIP, "%d aggregator calls failed", failed.load()) : DG_OK;
+}
+
+
+int dg_agg_set_knob(dg_agg *a, const char *name, int64_t value)
+{
+    if (!a || !name) return set_err(DG_E_INVALID, "bad args");
+    if (!strcmp(name, "depth")) {
+        a->depth.store((int)std::max<int64_t>(0, std::min<int64_t>(value, a->ring - 2)), std::memory_order_relaxed);
+    } else if (!strcmp(name, "max_wait_us")) {
+        if (value < 0) return set_err(DG_E_INVALID, "max_wait_us < 0");
+        std::lock_guard<std::mutex> g(a->mu);
+        a->max_wait = std::chrono::microseconds(value);
+    } else {
+        return set_err(DG_E_INVALID, "unknown aggregator knob '%s'", name);
+    }
+    a->wake_flusher();
+    return DG_OK;
+}
+
+int dg_agg_wait_gen(dg_agg *a, uint64_t after, uint32_t timeout_us, uint64_t *done)
+{
+    if (!a || !done) return set_err(DG_E_INVALID, "bad args");
+    if (a->done_upto.load(std::memory_order_acquire) <= after && timeout_us) {
+        std::unique_lock<std::mutex> lk(a->gen_mu);
+        a->cv_gen.wait_for(lk, std::chrono::microseconds(timeout_us),
+                           [&] { return a->done_upto.load(std::memory_order_acquire) > after; });
+    }
+    *done = a->done_upto.load(std::memory_order_acquire);
+    return DG_OK;
+}
+
+uint64_t dg_agg_ticket_gen(const dg_agg_ticket *t) { return t && t->batch ? t->gen : 0; }
+
+namespace {
+struct GwCaller {
+    uint64_t next;  /* its next message */
+    uint64_t cur;   /* the message in flight */
+    uint64_t t0;    /* submit time (sampled messages) */
+    dg_agg_ticket t;
+    bool has;
+};
+struct alignas(64) GwQueue {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<uint32_t> v;
+};
+struct alignas(64) GwPark {
+    std::mutex mu;
+    std::vector<uint32_t> v;
+};
+}  // namespace
+
+/* The gateway shape (see include/dgj2t.h): `callers` logical callers, each
+ * with ONE call in flight at a time (a goroutine blocked in Do), multiplexed
+ * over `workers` OS threads the way the Go runtime runs goroutines on its Ms;
+ * a poller thread (the binding's one goroutine locked to an OS thread) blocks
+ * in dg_agg_wait_gen and makes the callers of each converted generation
+ * runnable again. Nothing blocks an OS thread per call. */
+int dg_agg_gateway_drive(dg_agg *a, const uint8_t *arena, const uint64_t *in_off, uint64_t n, int workers,
+                         int callers, uint8_t *out, const uint64_t *out_off, uint64_t *out_len, uint64_t *ret,
+                         uint32_t *lat_ns, double *seconds, uint64_t *stats)
+{
+    if (!a || !arena || !in_off || workers < 1 || callers < 1 || !out || !out_off || !out_len || !ret || !seconds)
+        return set_err(DG_E_INVALID, "bad args");
+    const uint32_t G = (uint32_t)std::min<uint64_t>((uint64_t)callers, std::max<uint64_t>(n, 1));
+    std::vector<GwCaller> cs(G);
+    for (uint32_t c = 0; c < G; c++) cs[c] = GwCaller{c, 0, 0, dg_agg_ticket{}, false};
+    std::vector<GwQueue> q(workers);
+    std::vector<GwPark> park(AGG_GEN_RING);
+    for (uint32_t c = 0; c < G; c++) q[c % workers].v.push_back(c);
+    std::atomic<uint64_t> processed{a->done_upto.load(std::memory_order_acquire)};
+    std::atomic<uint64_t> completed{0}, n_again{0}, n_park{0}, n_wake{0};
+    std::atomic<int> failed{0}, ready{0};
+    std::atomic<bool> go{false}, finished{false};
+    auto done_all = [&] { return completed.load(std::memory_order_acquire) >= n || failed.load() > 0; };
+    std::vector<std::thread> th;
+    for (int w = 0; w < workers; w++) {
+        th.emplace_back([&, w] {
+            std::vector<uint32_t> mine, retry, again;
+            ready.fetch_add(1);
+            while (!go.load(std::memory_order_acquire)) std::this_thread::yield();
+            uint64_t done_local = 0;
+            for (;;) {
+                {
+                    std::unique_lock<std::mutex> lk(q[w].mu);
+                    if (q[w].v.empty() && retry.empty() && !finished.load(std::memory_order_acquire))
+                        q[w].cv.wait_for(lk, std::chrono::milliseconds(1),
+                                         [&] { return !q[w].v.empty() || finished.load(std::memory_order_acquire); });
+                    mine.swap(q[w].v);
+                }
+                if (finished.load(std::memory_order_acquire) && mine.empty()) break;
+                const bool only_retry = mine.empty() && !retry.empty();
+                mine.insert(mine.end(), retry.begin(), retry.end());
+                retry.clear();
+                for (size_t k = 0; k < mine.size(); k++) {
+                    const uint32_t c = mine[k];
+                    GwCaller &C = cs[c];
+                    if (C.has) { /* resumed: its generation is converted, dg_agg_wait does not block */
+                        const uint64_t j = C.cur;
+                        size_t ol = 0;
+                        int rc = dg_agg_wait(a, &C.t, out + out_off[j], out_off[j + 1] - out_off[j], &ol, &ret[j]);
+                        out_len[j] = ol;
+                        if (rc) failed.fetch_add(1);
+                        if (lat_ns) lat_ns[j] = (j & (DRIVE_SAMPLE - 1)) == 0
+                                                    ? (uint32_t)std::min<uint64_t>(dg_agg::now_ns() - C.t0, 0xffffffffull)
+                                                    : 0;
+                        C.has = false;
+                        done_local++;
+                    }
+                    if (C.next >= n) continue;
+                    const uint64_t i = C.next;
+                    if ((i & (DRIVE_SAMPLE - 1)) == 0) C.t0 = dg_agg::now_ns();
+                    int rc = dg_agg_submit(a, arena + in_off[i], in_off[i + 1] - in_off[i], 1, &C.t);
+                    if (rc == DG_E_AGAIN) { /* no room in the open batch for this thread: later */
+                        retry.push_back(c);
+                        n_again.fetch_add(1, std::memory_order_relaxed);
+                        continue;
+                    }
+                    if (rc) {
+                        failed.fetch_add(1);
+                        continue;
+                    }
+                    C.cur = i;
+                    C.next = i + G;
+                    C.has = true;
+                    if (!C.t.batch) { /* converted alone by dg_agg_wait: runnable at once */
+                        retry.push_back(c);
+                        continue;
+                    }
+                    /* park on its generation (the goroutine's channel receive) */
+                    const uint64_t g = C.t.gen;
+                    GwPark &p = park[g % AGG_GEN_RING];
+                    bool now = false;
+                    {
+                        std::lock_guard<std::mutex> lk(p.mu);
+                        if (processed.load(std::memory_order_acquire) >= g) now = true;
+                        else p.v.push_back(c);
+                    }
+                    if (now) retry.push_back(c);
+                    else n_park.fetch_add(1, std::memory_order_relaxed);
+                }
+                mine.clear();
+                if (done_local) {
+                    completed.fetch_add(done_local, std::memory_order_acq_rel);
+                    done_local = 0;
+                }
+                if (only_retry) std::this_thread::yield();
+                if (done_all()) break;
+            }
+        });
+    }
+    while (ready.load() < workers) std::this_thread::yield();
+    const auto ts = Clock::now();
+    go.store(true, std::memory_order_release);
+    /* the poller */
+    uint64_t last = processed.load();
+    std::vector<uint32_t> woke;
+    uint32_t rr = 0;
+    while (!done_all()) {
+        uint64_t d = last;
+        dg_agg_wait_gen(a, last, 1000, &d);
+        for (uint64_t g = last + 1; g <= d; g++) {
+            GwPark &p = park[g % AGG_GEN_RING];
+            std::lock_guard<std::mutex> lk(p.mu);
+            processed.store(g, std::memory_order_release);
+            woke.insert(woke.end(), p.v.begin(), p.v.end());
+            p.v.clear();
+        }
+        last = d;
+        if (woke.empty()) continue;
+        n_wake.fetch_add(1, std::memory_order_relaxed);
+        /* spread over the workers, one lock per worker */
+        const size_t per = (woke.size() + workers - 1) / workers;
+        for (size_t k0 = 0; k0 < woke.size(); k0 += per) {
+            GwQueue &Q = q[rr++ % workers];
+            {
+                std::lock_guard<std::mutex> lk(Q.mu);
+                Q.v.insert(Q.v.end(), woke.begin() + k0, woke.begin() + std::min(woke.size(), k0 + per));
+            }
+            Q.cv.notify_one();
+        }
+        woke.clear();
+    }
+    finished.store(true, std::memory_order_release);
+    for (auto &Q : q) {
+        { std::lock_guard<std::mutex> lk(Q.mu); }
+        Q.cv.notify_all();
+    }
+    for (auto &x : th) x.join();
+    *seconds = std::chrono::duration<double>(Clock::now() - ts).count();
+    if (stats) {
+        stats[0] = n_park.load();
+        stats[1] = n_again.load();
+        stats[2] = n_wake.load();
+        stats[3] = G;
+    }
+    return failed.load() ? set_err(DG_E_HIP, "%d gateway calls failed", failed.load()) : DG_OK;
 }
 
 }  // extern "C"

@@ -109,8 +109,10 @@ uint32_t dg_desc_root(const dg_desc *desc);
  * stream is a blocking stream, so it is ordered with the legacy default
  * stream (handle 0) both ways. Launches
  * on different streams of one context may run concurrently: each stream gets
- * its own device scratch (lists, counters, workspaces), up to 8 streams per
- * context; beyond that a shared scratch orders the launches with events.
+ * its own device scratch (lists, counters, workspaces), up to 40 streams per
+ * context (an aggregator's ring of up to 24, the in-flight and pipeline
+ * streams); beyond that a shared scratch orders the launches with events, so
+ * launches on streams that share one run one after the other.
  * Equivalent, per message, to BinaryConv.Do(ctx, desc, jbytes)
  * (conv/j2t/conv.go:53-77) with the given flags.
  */
@@ -263,7 +265,13 @@ int dg_agg_do(dg_agg *agg, const uint8_t *json, size_t len, uint8_t *out, size_t
  * max_bytes is converted alone); a batch is sealed when one thread's part is
  * full, when a caller waits on it, or when its first message has waited
  * max_wait_us. dg_agg_create uses max_bytes = max(1 MiB, 512 B x max_batch).
- * Up to 256 threads take parts; calls from further threads convert alone. */
+ * The first 224 calling threads get a part each; further threads share the
+ * last 32 parts under a per-part lock (no thread count converts alone).
+ * Pinned host memory: every part that is in use holds ring x (8 x max_batch +
+ * max_bytes + 64) bytes (ring = DG_AGG_RING, default 16, at most 24), e.g. 16
+ * threads x 16 x (8 x 4096 + 2 MiB) = 520 MiB; plus per batch of the ring
+ * room for the largest batch the parts can make. Size max_batch / max_bytes
+ * for the caller threads the process runs. */
 int dg_agg_create2(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, uint64_t flags, uint32_t max_batch,
                    uint64_t max_bytes, uint32_t max_wait_us, dg_agg **out);
 /* Asynchronous form of dg_agg_do, for a caller with many requests in flight
@@ -298,8 +306,9 @@ int dg_agg_stats(dg_agg *agg, uint64_t *batches, uint64_t *msgs);
  * dg_j2t_do: longer than a part, or no part left for their thread; the
  * flusher's issue split in four: waiting for the parts' writers, buffers,
  * the gather launch, the conversion's launches).
- * A part (one of 256) belongs to a calling thread from its first call until
- * the thread exits; an exited thread's part goes to the next new thread. */
+ * An exclusive part (one of 224) belongs to a calling thread from its first
+ * call until the thread exits; an exited thread's part goes to the next new
+ * thread. */
 int dg_agg_profile(dg_agg *agg, uint64_t *out, int n);
 /* converts what is still queued, then stops the flusher (every ticket must
  * have been waited for) */
@@ -315,6 +324,32 @@ void dg_agg_destroy(dg_agg *agg);
 int dg_agg_drive(dg_agg *agg, const uint8_t *arena, const uint64_t *in_off, uint64_t n, int threads, int window,
                  uint8_t *out, const uint64_t *out_off, uint64_t *out_len, uint64_t *ret, uint32_t *lat_ns,
                  double *seconds);
+
+/* The gateway binding: goroutines do not hold an OS
+ * thread while their call converts. A Do submits without blocking
+ * (dg_agg_submit nonblock), takes the ticket's generation
+ * (dg_agg_ticket_gen) and parks on a Go channel for it; ONE poller thread
+ * blocks in dg_agg_wait_gen, which returns once batches up to a newer
+ * generation are converted (generations complete in order), and wakes the
+ * goroutines of every generation up to it; each then calls dg_agg_wait,
+ * which no longer blocks, to copy its result. Every ticket must be waited
+ * for, from any thread. */
+int dg_agg_wait_gen(dg_agg *agg, uint64_t after, uint32_t timeout_us, uint64_t *done);
+uint64_t dg_agg_ticket_gen(const dg_agg_ticket *t);
+/* aggregator knobs: "depth" (0 = off): also seal the open batch as soon as
+ * it holds a message and fewer than depth batches are converting -- for
+ * callers that park instead of blocking in dg_agg_wait, whose waits the
+ * aggregator cannot see; "max_wait_us": the seal timer of dg_agg_create. */
+int dg_agg_set_knob(dg_agg *agg, const char *name, int64_t value);
+/* Benchmark driver for the gateway shape: `callers` logical callers, each
+ * with ONE call in flight at a time (a goroutine in Do), multiplexed over
+ * `workers` OS threads (the Go runtime's Ms) with the dg_agg_wait_gen poller
+ * above; caller c converts messages c, c + callers, ... Outputs as
+ * dg_agg_drive; stats (optional, 4 u64): parks, submits retried for want of
+ * room, poller wake-ups, callers. */
+int dg_agg_gateway_drive(dg_agg *agg, const uint8_t *arena, const uint64_t *in_off, uint64_t n, int workers,
+                         int callers, uint8_t *out, const uint64_t *out_off, uint64_t *out_len, uint64_t *ret,
+                         uint32_t *lat_ns, double *seconds, uint64_t *stats);
 
 /* dg_j2t_batch_host for large host batches: the batch is streamed in
  * `chunks` pieces through 3 stream-private buffer sets, so the upload of

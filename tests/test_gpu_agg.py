@@ -234,3 +234,58 @@ def test_aggregator_fresh_contexts_first_batches():
         agg.close()
         assert [int(r) for r in rets] == [0] * len(msgs)
         assert outs == want, rep
+
+
+@pytest.mark.parametrize("callers,workers,depth", [(1024, 8, 2), (4096, 16, 3), (5, 3, 0), (300, 2, 1)])
+def test_gateway_drive_vs_oracle(callers, workers, depth):
+    """The gateway shape: many logical callers with ONE call
+    in flight each (goroutines in Do), multiplexed over a few OS threads and
+    woken per converted generation by one dg_agg_wait_gen poller -- no OS
+    thread blocks per call. Every result is the oracle's."""
+    td = W.nesting_i64_desc()
+    msgs = _mixed_msgs(6000, 21)
+    fl = T.flatten(td)
+    chk = oracle.RefOracle() or oracle.PortOracle()
+    want = [chk.j2t(fl, m, 1) for m in msgs]
+    agg = conv.Aggregator(td, conv.Options(), max_batch=512, max_wait_us=300, max_bytes=512 * 3000)
+    if depth:
+        agg.set_knob("depth", depth)
+    outs, rets, lat, secs, st = agg.gateway(msgs, callers=callers, workers=workers)
+    batches, n = agg.stats()
+    prof = agg.profile()
+    agg.close()
+    assert n == len(msgs) and prof[11] == 0
+    assert st[3] == min(callers, len(msgs))
+    assert [(int(r), o if int(r) == 0 else b"") for r, o in zip(rets, outs)] == \
+        [(r, o if r == 0 else b"") for r, o in want]
+    assert secs > 0 and int(lat.max()) > 0
+
+
+def test_aggregator_shared_parts_past_224_threads():
+    """More concurrent threads than exclusive parts: threads 225+ share the
+    last 32 parts under their lock instead of converting alone (the r4
+    256-thread cliff), and every result is the oracle's."""
+    td = W.nesting_i64_desc()
+    fl = T.flatten(td)
+    msgs = W.gen_nested_batch(random.Random(31), 900)
+    chk = oracle.RefOracle() or oracle.PortOracle()
+    want = [chk.j2t(fl, m, 1)[1] for m in msgs]
+    agg = conv.Aggregator(td, conv.Options(), max_batch=16, max_wait_us=200, max_bytes=64 * 1024)
+    got = [None] * len(msgs)
+    go = threading.Event()
+
+    def worker(k):
+        go.wait()
+        for i in range(k, len(msgs), 300):
+            got[i] = agg.do(msgs[i]) or b""
+
+    ths = [threading.Thread(target=worker, args=(k,)) for k in range(300)]
+    for t in ths:
+        t.start()
+    go.set()
+    for t in ths:
+        t.join(timeout=120)
+    prof = agg.profile()
+    agg.close()
+    assert prof[11] == 0, prof
+    assert got == want
