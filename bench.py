@@ -543,6 +543,11 @@ def bench_t2j(args, rank, world, dev, dist, backend, td, arena, off, meta):
 # of one device batch holds a quarter of its window, so a thread has calls in
 # four batches at once (one filling, three converting or coming back).
 AGG_RUNS = ((16, 8192), (64, 2048), (64, 1))
+# the gateway shape (dg_agg_gateway_drive): logical callers with ONE call in
+# flight each (goroutines in Do) over GATEWAY_WORKERS OS threads (the 16
+# CPUs a GPU gets) and one dg_agg_wait_gen poller; (callers, depth)
+GATEWAY_RUNS = ((1024, 2), (4096, 3), (16384, 4), (65536, 4))
+GATEWAY_WORKERS = 16
 
 
 def bench_agg(args, rank, world, dev, dist, backend, td, arena, off, meta):
@@ -644,6 +649,41 @@ def bench_agg(args, rank, world, dev, dist, backend, td, arena, off, meta):
                     bad += 1
             if bad:
                 raise RuntimeError(f"agg: {bad} calls differ from the oracle")
+    gw_runs = []
+    for callers, depth in GATEWAY_RUNS:
+        if os.environ.get("DG_BENCH_NO_GATEWAY"):
+            break
+        share = max(256, callers // GATEWAY_WORKERS)
+        h = C.c_void_p()
+        _lib.check(L.dg_agg_create2(ctx.h, dh, flat.root_type, flags, share, share * 256, max_wait_us, C.byref(h)))
+        _lib.check(L.dg_agg_set_knob(h, b"depth", depth))
+        secs = C.c_double(0)
+        st = np.zeros(4, dtype=np.uint64)
+        m = n
+
+        def gstep():
+            _lib.check(L.dg_agg_gateway_drive(h, arena.ctypes.data, off.ctypes.data, m, GATEWAY_WORKERS, callers,
+                                              out.ctypes.data, out_off.ctypes.data, out_len.ctypes.data,
+                                              rets.ctypes.data, lat.ctypes.data, C.byref(secs), st.ctypes.data))
+            return secs.value
+        gstep()
+        b0, tot0 = C.c_uint64(0), C.c_uint64(0)
+        _lib.check(L.dg_agg_stats(h, C.byref(b0), C.byref(tot0)))
+        gsteps = max(2, args.steps // 4)
+        ws = [gstep() for _ in range(gsteps)]
+        b, tot = C.c_uint64(0), C.c_uint64(0)
+        _lib.check(L.dg_agg_stats(h, C.byref(b), C.byref(tot)))
+        L.dg_agg_destroy(h)
+        u = meta.get("unique", n)
+        bad = int(sum(1 for i in range(0, m, 97) if int(rets[i]) != 0))
+        lt = lat[:m][lat[:m] > 0].astype(np.float64) / 1e3
+        gw_runs.append({"callers": callers, "os_threads": GATEWAY_WORKERS, "depth": depth, "per_thread_batch_share": share,
+                        "calls_per_step": m, "steps": gsteps, "msgs_per_s": round(m * gsteps / sum(ws)),
+                        "msgs_per_s_best": round(m / min(ws)),
+                        "lat_us_p50": round(float(np.percentile(lt, 50)), 1),
+                        "lat_us_p99": round(float(np.percentile(lt, 99)), 1),
+                        "avg_batch": round((tot.value - tot0.value) / max(1, b.value - b0.value), 1),
+                        "parks": int(st[0]), "retries": int(st[1]), "sampled_nonzero_status": bad})
     main = runs[0]
     json_bytes = int(off[-1])
     stats = torch.tensor([value_wall, float(json_bytes), float(n)], dtype=torch.float64,
@@ -673,6 +713,10 @@ def bench_agg(args, rank, world, dev, dist, backend, td, arena, off, meta):
                        "per_thread_batch_share": max_batch, "max_wait_us": max_wait_us, "batches_in_flight": int(os.environ.get("DG_AGG_RING", "8")),
                        "gbs_json_in": main["gbs_json_in"], "lat_us_p50": main["lat_us_p50"],
                        "lat_us_p99": main["lat_us_p99"], "runs": runs, "checked_vs_oracle": n,
+                       "gateway_runs": gw_runs,
+                       "gateway_note": "callers with one Do in flight each (goroutines) over 16 OS threads, woken per "
+                                       "converted generation by one dg_agg_wait_gen poller (INTEGRATION.md §2); "
+                                       "compare msgs_per_s with cpu_baseline.share.msgs_per_s (16 cores, same run)",
                        "reference_per_core_ns_per_op": (cpu or {}).get("one_core_ns_per_msg"),
                        "parallelism": f"dp{world} (one aggregator per rank), no data-path collective"},
             "roofline": None,

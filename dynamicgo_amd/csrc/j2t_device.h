@@ -314,7 +314,10 @@ DGI int64_t cvt64(double d)
     return (d >= -9223372036854775808.0 && d < 9223372036854775808.0) ? (int64_t)d : INT64_MIN;
 }
 
-DGI bool isspace_(uint8_t c) { return c == ' ' || c == '\r' || c == '\n' || c == '\t'; }
+/* ' ', '\t', '\n', '\r' as one shift of a 33-bit mask: no short-circuit
+ * branches (a chain of || compiled to a branch tree with exec-mask SALU per
+ * test, and sank the loads feeding it into the branches) */
+DGI bool isspace_(uint8_t c) { return ((0x100002600ull >> (c & 63)) & (uint64_t)(c < 33)) != 0; }
 
 /* advance_ns native/scanning.c:64-105 (+ lspace native/fastbytes.c:25-123):
  * 4 scalar probes, then a scan; note *p is left unchanged when the scan

@@ -80,6 +80,23 @@ constexpr uint32_t FL_MAXTASK = 512;             /* chunk tasks per block (more:
 #ifndef DG_FL_PERM
 #define DG_FL_PERM 0
 #endif
+/* -DDG_FLPROF_G: cycles per wave in the stages of a field's parse, summed
+ * over the fields (P.stats[2 + stage]): 0 separators from LDS, 1 delimiter
+ * bytes, 2 key, 3 value, 4 sizes, 5 bookkeeping after fl_field */
+#ifdef DG_FLPROF_G
+#define FLG_ARG , uint64_t *flg
+#define FLG_PASS , flg
+#define FLG(k)                                             \
+    do {                                                   \
+        const uint64_t now_ = __builtin_amdgcn_s_memtime(); \
+        flg[k] += now_ - flg[7];                           \
+        flg[7] = now_;                                     \
+    } while (0)
+#else
+#define FLG_ARG
+#define FLG_PASS
+#define FLG(k)
+#endif
 /* the field (within a round) wave w converts as its h-th: w + 4h, or with
  * DG_FL_PERM 1 a snake (w, then 7 - w) that pairs early with late fields */
 DGI uint32_t fl_slot(uint32_t w, uint32_t h)
@@ -144,6 +161,43 @@ struct LSrc {
         LSrc r;
         r.init(w8, off0 + s0, len);
         return r;
+    }
+};
+
+/* A number's bytes in registers: the 5 aligned staged words covering
+ * [p, p + 32) of the message, read together (one LDS round trip) instead of
+ * the parse loops' dependent word-at-a-time reads. Numbers up to RSL_MAX
+ * bytes use it (digits8 reads 8 bytes at i <= n: word index <= 4); longer
+ * ones parse from LDS. The stage has slack words past every message. */
+constexpr int32_t RSL_MAX = 24;
+struct RSrcL {
+    typedef int32_t idx;
+    uint64_t w0, w1, w2, w3, w4;
+    uint32_t sh; /* byte offset of the number's first byte in w0 */
+    int32_t n;
+    DGI void load(const LSrc &src, int32_t p, int32_t len)
+    {
+        const uint32_t b = (uint32_t)(src.off0 + p);
+        const __attribute__((address_space(3))) uint64_t *q = src.w8 + (b >> 3);
+        sh = b & 7;
+        n = len;
+        w0 = q[0];
+        w1 = q[1];
+        w2 = q[2];
+        w3 = q[3];
+        w4 = q[4];
+    }
+    DGI uint64_t word(uint32_t j) const { return j == 0 ? w0 : j == 1 ? w1 : j == 2 ? w2 : j == 3 ? w3 : w4; }
+    DGI uint8_t raw(int32_t i) const
+    {
+        const uint32_t b = sh + (uint32_t)i;
+        return (uint8_t)(word(b >> 3) >> ((b & 7) << 3));
+    }
+    DGI uint8_t at(int32_t i) const { return (uint32_t)i < (uint32_t)n ? raw(i) : 0; }
+    DGI uint64_t get8(int32_t i) const
+    {
+        const uint32_t b = sh + (uint32_t)i, j = b >> 3, s8 = (b & 7) << 3;
+        return (word(j) >> s8) | ((word(j + 1) << 1) << (63 - s8));
     }
 };
 
@@ -219,37 +273,58 @@ DGI int32_t fl_lookup(const DV &D, const dg_struct &sd, S &src, uint32_t k0, uin
  * is a string: the key and a string value are delimited without scanning. */
 template <class S, class DV>
 DGI bool fl_field(const DV &D, const dg_struct &sd, S &src, uint32_t sk, uint32_t ck, uint32_t ek, uint32_t nq,
-                  bool hasbs, uint32_t k, uint64_t flag, const FastTabs &tb, FField &F)
+                  bool hasbs, uint32_t k, uint64_t flag, const FastTabs &tb, FField &F FLG_ARG)
 {
     typedef typename S::idx SI;
-    /* the four delimiting bytes, read together; spaces around them take the loops */
+    /* Round 1 of LDS reads: the four delimiting bytes and the predicted
+     * field's record (field k in IDL order), issued together; every test is
+     * written without short-circuit branches, so the loads are not sunk into
+     * branches and chained one after another. Spaces around the delimiters
+     * take the loops. */
     const uint8_t d_s = src.raw((SI)sk), d_q = src.raw((SI)(ck - 1)), d_v = src.raw((SI)(ck + 1)),
                   d_e = src.raw((SI)(ek - 1));
+    const bool pred = k < sd.n_fields;
+    dg_field f = ldrec(&D.F[sd.field_begin + (pred ? k : 0u)]);
     uint32_t p = sk, q = ck, v0 = ck + 1, ve = ek;
-    if (isspace_(d_s) || isspace_(d_q) || isspace_(d_v) || isspace_(d_e) || ck + 1 >= ek) {
+    uint8_t cs = d_s, cq = d_q, c = d_v, ce = d_e;
+    if (isspace_(d_s) | isspace_(d_q) | isspace_(d_v) | isspace_(d_e) | (ck + 1 >= ek)) {
         p = skip_ws(src, sk);
         while (q > p && isspace_(src.raw((SI)(q - 1)))) q--;
         v0 = skip_ws(src, ck + 1);
         while (ve > v0 && isspace_(src.raw((SI)(ve - 1)))) ve--;
         if (v0 >= ve) return false;
+        cs = src.raw((SI)p);
+        cq = src.raw((SI)(q - 1));
+        c = src.raw((SI)v0);
+        ce = src.raw((SI)(ve - 1));
     }
-    if (q < p + 2 || src.raw((SI)p) != '"' || src.raw((SI)(q - 1)) != '"') return false;
+    if ((q < p + 2) | (cs != '"') | (cq != '"') | (nq != (c == '"' ? 4u : 2u))) return false;
     const uint32_t k0 = p + 1, kn = q - 1 - k0;
-    const uint8_t c = src.raw((SI)v0);
-    if (nq != (c == '"' ? 4u : 2u)) return false;
+    FLG(1);
     if (hasbs && has_byte(src, k0, kn, '\\')) return false; /* escaped key: unquoted before lookup -> the list pass */
-    /* the key (native/thrift.c:668-763): predicted (field k in IDL order), else the name table */
+    /* the key (native/thrift.c:668-763): predicted (field k in IDL order),
+     * else the name table. Round 2: a key of up to 16 bytes and the
+     * predicted key's pool words, compared in one step (the pool keys are
+     * zero-padded to 8 bytes, key_eq's semantics) */
     int32_t fi = -1;
-    dg_field f;
-    if (k < sd.n_fields) {
-        f = ldrec(&D.F[sd.field_begin + k]);
-        if ((f.flags & DG_FF_ALIAS_SELF) && f.key_len == kn && key_eq(src, (SI)k0, kn, (decltype(&D.R[0]))(&D.P[f.key_off])))
-            fi = (int32_t)(sd.field_begin + k);
+    {
+        const __attribute__((address_space(3))) uint64_t *pk = (decltype(&D.R[0]))(&D.P[f.key_off]);
+        bool hit;
+        if (kn <= 16) {
+            const uint64_t a0 = src.get8((SI)k0), a1 = src.get8((SI)(k0 + 8)), b0 = pk[0], b1 = pk[1];
+            const uint64_t m0 = kn >= 8 ? ~0ull : (1ull << (kn << 3)) - 1;
+            const uint64_t m1 = kn >= 16 ? ~0ull : kn <= 8 ? 0ull : (1ull << ((kn - 8) << 3)) - 1;
+            hit = ((a0 & m0) == b0) & ((kn <= 8) | ((a1 & m1) == b1));
+        } else {
+            hit = key_eq(src, (SI)k0, kn, pk);
+        }
+        if (pred & ((f.flags & DG_FF_ALIAS_SELF) != 0) & (f.key_len == kn) & hit) fi = (int32_t)(sd.field_begin + k);
     }
     if (fi < 0) {
         fi = fl_lookup(D, sd, src, k0, kn);
         if (fi >= 0) f = ldrec(&D.F[fi]);
     }
+    FLG(2);
     /* the value, [v0, ve) */
     F.defer = false;
     uint32_t vk;
@@ -258,7 +333,7 @@ DGI bool fl_field(const DV &D, const dg_struct &sd, S &src, uint32_t sk, uint32_
     int64_t iv = 0;
     double dv = 0.0;
     if (c == '"') {
-        if (ve - v0 < 2 || src.raw((SI)(ve - 1)) != '"') return false;
+        if ((ve - v0 < 2) | (ce != '"')) return false;
         vs0 = v0 + 1;
         vnb = ve - 1 - vs0;
         vesc = hasbs && has_byte(src, vs0, vnb, '\\');
@@ -271,8 +346,18 @@ DGI bool fl_field(const DV &D, const dg_struct &sd, S &src, uint32_t sk, uint32_
          * here, as the reference validates them before anything else */
         const bool later = DG_FL_DEFER_NUM && fi >= 0 && !((flag & DG_F_ENABLE_VM) && f.vm != DG_VM_NONE);
         if (!later) {
-            SI qq = (SI)v0;
-            if (!fast_vnumber(src, qq, tb, iv, dv, isint) || (uint32_t)qq != ve) return false;
+            const int32_t nl = (int32_t)(ve - v0);
+            bool okn;
+            if (nl <= RSL_MAX) { /* the number's words in registers: one LDS round trip */
+                RSrcL rs;
+                rs.load(src, (int32_t)v0, nl);
+                int32_t qq = 0;
+                okn = fast_vnumber(rs, qq, tb, iv, dv, isint) && qq == nl;
+            } else {
+                SI qq = (SI)v0;
+                okn = fast_vnumber(src, qq, tb, iv, dv, isint) && (uint32_t)qq == ve;
+            }
+            if (!okn) return false;
         }
         F.defer = later;
         vs0 = v0;
@@ -288,6 +373,7 @@ DGI bool fl_field(const DV &D, const dg_struct &sd, S &src, uint32_t sk, uint32_
     } else {
         return false; /* null, containers, garbage: the list pass */
     }
+    FLG(3);
     F.fi = fi;
     if (fi < 0 || ((f.flags & DG_FF_REQUEST_BASE) && (flag & DG_F_NO_WRITE_BASE))) {
         if (fi < 0 && !(flag & DG_F_ALLOW_UNKNOWN)) return false; /* ERR_UNKNOWN_FIELD */
@@ -360,6 +446,7 @@ DGI bool fl_field(const DV &D, const dg_struct &sd, S &src, uint32_t sk, uint32_
     F.iv = vk == FV_BOOL ? (int64_t)bv : iv;
     F.dv = dv;
     F.size = 3 + vsize;
+    FLG(4);
     return true;
 }
 
@@ -479,6 +566,24 @@ struct FlatParams {
 #define FLP(k)
 #define FLP_END()
 #endif
+/* -DDG_FLPROF_F: cycles per wave spent in each field slot's parse
+ * (P.stats[2 + slot]) and write (P.stats[8 + slot]), slots 0..5, 1 block in
+ * 32 sampled (tools/flprof.py --fields) */
+#ifdef DG_FLPROF_F
+#define FLF_DECL uint64_t flf[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#define FLF_T0() const uint64_t flf_t0 = __builtin_amdgcn_s_memtime()
+#define FLF_ADD(k) do { if ((k) < 12) flf[k] += __builtin_amdgcn_s_memtime() - flf_t0; } while (0)
+#define FLF_END()                                                                         \
+    do {                                                                                  \
+        if ((threadIdx.x & 63) == 0 && (blockIdx.x & 31) == 0)                            \
+            for (int k_ = 0; k_ < 12; k_++) atomicAdd(&P.stats[2 + k_], (unsigned long long)flf[k_]); \
+    } while (0)
+#else
+#define FLF_DECL
+#define FLF_T0()
+#define FLF_ADD(k)
+#define FLF_END()
+#endif
 
 /* per-message state of the block, one array per member (lane = message:
  * consecutive banks). ~36 KiB with a small descriptor: 4 blocks (16 waves)
@@ -513,6 +618,7 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
     __shared__ __attribute__((aligned(16))) FlatLds L;
     extern __shared__ __attribute__((aligned(16))) uint64_t s_fdesc[];
     FLP_DECL
+    FLF_DECL
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint64_t b0 = (uint64_t)blockIdx.x * FL_MPB;
     const uint64_t b1 = b0 + FL_MPB < P.n ? b0 + FL_MPB : P.n;
@@ -801,6 +907,9 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
         src.init((const __attribute__((address_space(3))) uint64_t *)(void *)&L.in[lwa >> 3], (int32_t)(lwa & 7), (int32_t)L.n[mm]);
         const uint32_t rounds = L.rounds;
         uint32_t nbytes = 0;
+#ifdef DG_FLPROF_G
+        uint64_t flg[8] = {0, 0, 0, 0, 0, 0, 0, __builtin_amdgcn_s_memtime()};
+#endif
         auto parse = [&](uint32_t k, FField &F) {
             F.size = 0;
             F.kind = FV_NONE;
@@ -814,15 +923,17 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
                     q1 = e1 >> 16;
                 }
                 const uint32_t ck = L.col[k * FL_MPB + mm];
-                if (!(ck >= sk && ck < ek && fl_field(D, sd, src, sk, ck, ek, q1 - q0, hasbs, k, P.flag, tb, F))) {
+                FLG(0);
+                if (!(ck >= sk && ck < ek && fl_field(D, sd, src, sk, ck, ek, q1 - q0, hasbs, k, P.flag, tb, F FLG_PASS))) {
                     L.ok[mm] = 0;
                     F.size = 0;
                     F.kind = FV_NONE;
                 } else if (F.fi >= 0) {
                     const uint32_t bit = (uint32_t)F.fi - sd.field_begin;
-                    if (bit < 32) atomicOr(&L.plo[mm], 1u << bit);
-                    else atomicOr(&L.phi[mm], 1u << (bit - 32));
+                    atomicOr(&L.plo[mm], bit < 32 ? 1u << (bit & 31) : 0u);
+                    atomicOr(&L.phi[mm], bit >= 32 ? 1u << (bit & 31) : 0u);
                 }
+                FLG(5);
             }
         };
         /* 0 = error, 1 = written, 2 = the body is left to chunk tasks */
@@ -840,8 +951,10 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
             uint16_t *sz = &L.size[(r & 1) * FL_SLOTS * FL_MPB];
 #pragma unroll
             for (uint32_t h = 0; h < FL_FPW; h++) {
+                FLF_T0();
                 parse(r * FL_SLOTS + fl_slot(wave, h), F[h]);
                 sz[fl_slot(wave, h) * FL_MPB + mm] = (uint16_t)F[h].size;
+                FLF_ADD(r * FL_SLOTS + fl_slot(wave, h));
             }
             FLP(4);
             __syncthreads();
@@ -863,7 +976,9 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
             uint32_t wr[FL_FPW], nch[FL_FPW], nsum = 0, good = 1;
 #pragma unroll
             for (uint32_t h = 0; h < FL_FPW; h++) {
+                FLF_T0();
                 wr[h] = write(F[h], off[h]);
+                FLF_ADD(6 + r * FL_SLOTS + fl_slot(wave, h));
                 nch[h] = wr[h] == 2 ? (F[h].nb + FL_CHUNK - 1) / FL_CHUNK : 0u;
                 nsum += nch[h];
                 good &= wr[h] != 0;
@@ -904,6 +1019,10 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
             FLP(6);
         }
         if (wave == 0) L.nbytes[mm] = nbytes;
+#ifdef DG_FLPROF_G
+        if (lane == 0 && (blockIdx.x & 31) == 0)
+            for (int k_ = 0; k_ < 6; k_++) atomicAdd(&P.stats[2 + k_], (unsigned long long)flg[k_]);
+#endif
     }
     FLP(6);
     __syncthreads();
@@ -974,6 +1093,7 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
         }
     }
     FLP_END();
+    FLF_END();
 }
 
 void launch_flat_kernel(dim3 grid, hipStream_t s, const Params &P, const FlatParams &S); /* LDS: + the blob */

@@ -949,12 +949,18 @@ DGI bool wave_run(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L
         }
         /* numbers: the map key's, then the value's, through ONE parser call
          * site; each becomes its Thrift bytes at once (fewer live VGPRs) */
+        /* round 0 parses each lane's key if it has a numeric one, else its
+         * value; round 1 only the values of lanes that had both (a numeric
+         * map key AND a numeric value): a page whose keys and values are
+         * numbers in different lanes (map<i64,struct> keys beside struct
+         * fields) pays ONE parser round, not two */
         bool kslow = false, vslow = false;
         for (uint32_t it = 0; it < 2; it++) {
-            const bool want = it == 0 ? kns >= 0 : ns >= 0;
+            const bool isk = it == 0 && kns >= 0;
+            const bool want = it == 0 ? (kns >= 0 || ns >= 0) : (kns >= 0 && ns >= 0);
             if (!ballot(want)) continue;
             if (want) {
-                const int32_t s0 = it == 0 ? kns : ns, n0 = it == 0 ? knn : nn;
+                const int32_t s0 = isk ? kns : ns, n0 = isk ? knn : nn;
                 int64_t q = 0, iv = 0;
                 double dv = 0.0;
                 bool isint = false;
@@ -970,9 +976,9 @@ DGI bool wave_run(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L
                 }
                 if (!okn) { /* long numbers (big decimals, long map keys), errors: the exact parser */
 #endif
-                    if (it == 0) kslow = true;
+                    if (isk) kslow = true;
                     else vslow = true;
-                } else if (it == 0) {
+                } else if (isk) {
                     num_le(ktt, isint, iv, dv, kb, kbn);
                 } else {
                     if (q != n0) bad = true;

@@ -382,6 +382,19 @@ def ref_lib_path() -> Optional[str]:
     return None
 
 
+def ref_utf8_validate(body: bytes) -> Optional[int]:
+    """The reference's utf8_validate (native/utf8.c:183-212) on body: -1 if
+    valid UTF-8, else the offset of the first invalid sequence; None when
+    oracle/_ref was not built."""
+    r = RefOracle()
+    if r is None:
+        return None
+    f = r.lib.dgref_utf8_validate
+    f.restype = C.c_long
+    f.argtypes = [C.c_char_p, C.c_size_t]
+    return int(f(body, len(body)))
+
+
 def RefOracle() -> Optional[_Base]:
     """The reference's own C engine, or None if oracle/_ref was not built."""
     global _ref_singleton

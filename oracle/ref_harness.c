@@ -1473,3 +1473,10 @@ int dgref_t2j_timed(const uint8_t *blob, const uint8_t *side, uint32_t root, con
     free(th);
     return 0;
 }
+
+/* The reference's UTF-8 validator, utf8_validate (native/utf8.c:183-212):
+ * -1 if s[0, n) is valid UTF-8, else the offset of the first invalid
+ * sequence. Not on the reference's j2t path; it pins the verdicts of the
+ * opt-in DG_F_VALIDATE_UTF8 extension (tests/test_oracle.py,
+ * tests/test_gpu_parity.py). */
+long dgref_utf8_validate(const uint8_t *s, size_t n) { return (long)utf8_validate((const char *)s, (ssize_t)n); }

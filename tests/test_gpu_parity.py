@@ -230,6 +230,33 @@ def test_utf8_validation_extension_vs_port_oracle():
             assert (int(r), o) == chk.j2t(fl, m, flags), m
 
 
+def test_utf8_validation_pinned_to_reference_validator():
+    """DG_F_VALIDATE_UTF8 verdicts of the GPU (fast paths and
+    the exact machine) against the reference's own validator, utf8_validate
+    (native/utf8.c:183-212, oracle/_ref), on 1 500 fuzz bodies as a string
+    value and as a STRING map key: rejected exactly when utf8_validate
+    returns an offset (ERR_INVAL at that byte), otherwise the reference's
+    flag-off bytes."""
+    from test_oracle import utf8_fuzz_bodies, UTF8_CASES_BODIES
+    ref = oracle.RefOracle()
+    if ref is None:
+        pytest.skip("oracle/_ref not built")
+    bodies = UTF8_CASES_BODIES + utf8_fuzz_bodies(62, 1500)
+    fs = T.flatten(W.simple_desc())
+    fn = T.flatten(W.nesting_i64_desc())
+    cases = [(fs, b'{"StringField":"', b'"}'), (fn, b'{"MapStringString":{"', b'":"v"}}')]
+    for fl, pre, post in cases:
+        msgs = [pre + b + post for b in bodies]
+        want = []
+        for b, m in zip(bodies, msgs):
+            bad = oracle.ref_utf8_validate(b)
+            want.append(ref.j2t(fl, m, 1) if bad < 0 else (((b[bad] << 40) | ((len(pre) + bad) << 8) | 2), b""))
+        for flags in (0x1 | 1 << 16, 0x1 | 1 << 16 | NO_FAST):
+            outs, rets = _raw_batch(fl, msgs, flags)
+            got = [(int(r), o if int(r) == 0 else b"") for r, o in zip(rets, outs)]
+            assert got == [(r, o if r == 0 else b"") for r, o in want], flags
+
+
 def test_pack_device_matches_slots():
     """dg_pack_device: the used prefix of every slot, back to back."""
     import torch

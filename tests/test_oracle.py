@@ -105,6 +105,53 @@ def test_utf8_validation_extension(body, bad):
     assert chk.j2t(fl, b'{"BinaryField":"\xff"}', 1 | UTF8_FLAG) == chk.j2t(fl, b'{"BinaryField":"\xff"}', 1)
 
 
+def utf8_fuzz_bodies(seed: int, n: int):
+    """JSON string bodies (no raw '"' or '\\') mixing valid UTF-8, ASCII,
+    escapes and invalid sequences: truncated, overlong, surrogate, out of
+    range, stray continuation bytes."""
+    rng = random.Random(seed)
+    pieces = [b"a", b"Z0", b" ", b"\\n", b"\\u00e9", "é".encode(), "中".encode(), "😀".encode(), b"\xc3", b"\xe4\xb8",
+              b"\xf0\x9f\x98", b"\x80", b"\xbf", b"\xc0\x80", b"\xc1\xbf", b"\xe0\x9f\xbf", b"\xed\xa0\x80",
+              b"\xf0\x8f\xbf\xbf", b"\xf4\x90\x80\x80", b"\xf5\x80\x80\x80", b"\xff", b"\x01\x1f", b"\xef\xbf\xbf",
+              b"\xf4\x8f\xbf\xbf", b"\xe0\xa0\x80", b"\xed\x9f\xbf", b"0123456789abcdefXYZ"]
+    out = []
+    for _ in range(n):
+        if rng.random() < 0.3:  # raw random bytes
+            b = bytes(rng.choice([c for c in range(256) if c not in (0x22, 0x5C)]) for _ in range(rng.randint(0, 40)))
+        else:
+            b = b"".join(rng.choice(pieces) for _ in range(rng.randint(0, 14)))
+        out.append(b)
+    return out
+
+
+def test_utf8_extension_pinned_to_reference_validator():
+    """the DG_F_VALIDATE_UTF8 verdicts pinned to the
+    reference's own validator, utf8_validate (native/utf8.c:183-212, compiled
+    from /root/reference into oracle/_ref): on the table above and 3 000
+    fuzz bodies, a string is rejected exactly when utf8_validate returns an
+    offset, with ERR_INVAL at that byte; otherwise the output is the
+    reference's flag-off output."""
+    if oracle.RefOracle() is None:
+        pytest.skip("oracle/_ref not built")
+    for body, bad in UTF8_CASES:
+        assert oracle.ref_utf8_validate(body) == (-1 if bad is None else bad), body
+    ref = oracle.RefOracle()
+    port = oracle.PortOracle()
+    fl = T.flatten(idl_desc("baseline.thrift", "SimpleMethod"))
+    pre = b'{"StringField":"'
+    n_bad = 0
+    for body in UTF8_CASES_BODIES + utf8_fuzz_bodies(61, 3000):
+        msg = pre + body + b'"}'
+        bad = oracle.ref_utf8_validate(body)
+        want = ref.j2t(fl, msg, 1) if bad < 0 else (_pack(2, body[bad], len(pre) + bad), b"")
+        n_bad += bad >= 0
+        assert port.j2t(fl, msg, 1 | UTF8_FLAG) == want, body
+    assert 300 < n_bad < 2900
+
+
+UTF8_CASES_BODIES = [b for b, _ in UTF8_CASES]
+
+
 def test_unterminated_string_block_tail():
     """The one malformed-input class where the reference's verdict is
     undefined: an unterminated string whose bytes after the opening quote end

@@ -13,6 +13,7 @@ from dynamicgo_amd import _lib, conv, workloads as W
 from dynamicgo_amd.thrift import flatten
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c2"
+fields = "--fields" in sys.argv  # a -DDG_FLPROF_F build: per field slot parse / write cycles
 td, msgs = {"c2": lambda: (W.simple_desc(), W.gen_flat_batch(random.Random(42), 65536)),
             "c2s": lambda: (W.simple_desc(), W.gen_flat_batch_shuffled(random.Random(42), 65536))}[cfg]()
 n = len(msgs)
@@ -39,6 +40,20 @@ _lib.check(L.dg_ctx_counters(ctx.h, cnt, 16, 1))
 reps = 5
 _lib.check(L.dg_bench_device(*args, reps, C.byref(ms)))
 _lib.check(L.dg_ctx_counters(ctx.h, cnt, 16, 1))
+if "--stages" in sys.argv:  # a -DDG_FLPROF_G build
+    c = list(cnt)[2:8]
+    waves = n // 64 // 32 * 4
+    print(f"{cfg}: {ms.value / reps * 1000:.1f} us/step (instrumented)")
+    for k, nm in enumerate(["separators", "delimiters", "key", "value", "sizes", "after"]):
+        print("  %-12s %8.0f cycles/wave" % (nm, c[k] / reps / waves))
+    sys.exit(0)
+if fields:
+    c = list(cnt)[2:14]
+    waves = n // 64 // 32 * 4
+    print(f"{cfg}: {ms.value / reps * 1000:.1f} us/step (instrumented), ok={(d_ret.cpu().numpy() == 0).sum()}")
+    for k in range(6):
+        print("  field slot %d: parse %8.0f  write %8.0f cycles/wave" % (k, c[k] / reps / waves * 4, c[6 + k] / reps / waves * 4))
+    sys.exit(0)
 c = list(cnt)[2:10]
 names = ["stage+desc+barrier", "classify+scan", "record", "open/close+barrier 1", "parse", "barrier 2", "write+tasks",
          "chunks+barrier 4"]
