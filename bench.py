@@ -204,6 +204,40 @@ def cpu_model() -> str:
     return "unknown"
 
 
+def _read(path: str):
+    try:
+        with open(path) as fh:
+            return fh.read().strip()
+    except OSError:
+        return None
+
+
+def host_cpu_env() -> dict:
+    """What bounds the CPU baseline on this host: the affinity mask, the
+    cgroup CPU quota (v2 cpu.max, or v1 cfs quota/period) and throttling
+    counters, and the load average. A quota below the threads the baseline
+    runs (e.g. 16 CPUs of quota under a 128-CPU affinity) throttles them in
+    every quota period: the all-core passes then swing by large factors."""
+    env = {"affinity_cpus": len(os.sched_getaffinity(0)), "os_cpu_count": os.cpu_count(),
+           "loadavg": [round(x, 2) for x in os.getloadavg()]}
+    v2 = _read("/sys/fs/cgroup/cpu.max")
+    if v2:
+        q, per = (v2.split() + ["100000"])[:2]
+        env["cgroup_cpu_max"] = v2
+        env["quota_cpus"] = None if q == "max" else round(int(q) / int(per), 2)
+    else:
+        q, per = _read("/sys/fs/cgroup/cpu/cpu.cfs_quota_us"), _read("/sys/fs/cgroup/cpu/cpu.cfs_period_us")
+        if q and per:
+            env["cgroup_cfs"] = f"{q} {per}"
+            env["quota_cpus"] = None if int(q) < 0 else round(int(q) / int(per), 2)
+    st = _read("/sys/fs/cgroup/cpu.stat") or _read("/sys/fs/cgroup/cpu/cpu.stat")
+    if st:
+        kv = dict(line.split()[:2] for line in st.splitlines() if len(line.split()) >= 2)
+        env["throttle"] = {k: int(kv[k]) for k in ("nr_periods", "nr_throttled", "throttled_usec", "throttled_time")
+                           if k in kv}
+    return env
+
+
 def cpu_baseline(flat, arena, off, flags, budget_s: float = 6.0):
     """The reference's own native/*.c (oracle/_ref, clang -O3 like the
     reference's build) on this host, outputs preallocated and first touched by
@@ -232,14 +266,20 @@ def cpu_baseline(flat, arena, off, flags, budget_s: float = 6.0):
         ref.j2t_timed(flat, a, o, flags, cpus, reps, times=ts)
         return float(np.median(ts)), ts
 
+    env0 = host_cpu_env()
     t_all, ts_all = timed(arena, off, phys[:cores_all])
+    env1 = host_cpu_env()
     t_share, ts_share = (t_all, ts_all) if cores == cores_all else timed(arena, off, phys[:cores])
     # one core: a prefix of at most ~64 MB / 65536 messages
     k = int(min(n, 65536, max(1, np.searchsorted(off, off[0] + 64 * 1024 * 1024))))
     a1, o1 = arena[:int(off[k]) + 64], off[:k + 1]
     t_one, ts_one = timed(a1, o1, phys[:1])
     one_bytes = int(o1[-1] - o1[0])
-    spread = lambda nb, ts: {"min": round(nb / max(ts) / 1e9, 4), "max": round(nb / min(ts) / 1e9, 4)}
+    spread = lambda nb, ts: {"min": round(nb / max(ts) / 1e9, 4), "max": round(nb / min(ts) / 1e9, 4),
+                             "best_of_5": round(nb / min(ts[:5]) / 1e9, 4)}
+    thr = None
+    if "throttle" in env0 and "throttle" in env1:
+        thr = {k: env1["throttle"][k] - env0["throttle"].get(k, 0) for k in env1["throttle"]}
     return {"value": round(nbytes / t_all / 1e9, 4), "unit": "GB/s", "cores": cores_all, "kind": "reference",
             "stat": "median of the passes", "range": spread(nbytes, ts_all),
             "cpu_model": cpu_model(), "msgs_per_s": round(n / t_all),
@@ -248,6 +288,7 @@ def cpu_baseline(flat, arena, off, flags, budget_s: float = 6.0):
             "one_core_gbs": round(one_bytes / t_one / 1e9, 4), "one_core_ns_per_msg": round(t_one / k * 1e9, 1),
             "one_core_range": spread(one_bytes, ts_one),
             "per_core_gbs": round(nbytes / t_all / 1e9 / cores_all, 4),
+            "host": env0, "all_core_throttling_delta": thr,
             "sample": f"all-core: the rank's whole batch ({n} msgs, {nbytes} B), median (min/max in range) of "
                       f"{len(ts_all)} passes, {cores_all} threads pinned to distinct physical cores of "
                       f"'{cpu_model()}' (affinity: {logical} logical CPUs = {len(phys)} physical cores); share: "

@@ -46,7 +46,26 @@ DG_ST_DEEP = 0xF1
 DG_ST_HM_END = 0xF2
 DG_ST_HM_ERR = 0xF3
 DG_ST_HM_END_AT = 0xF4
+DG_ST_CB_LIST = 0xF5  # DG_F_CB_COLLECT: every callback of one pass recorded (dgj2t_defs.h)
 E_VM_END = 24  # ERR_VM_END (native/native.h:70): a non-inline value mapping for the host
+F_CB_COLLECT = 1 << 22  # extension: record the callbacks of a pass and convert on (2 passes for k callbacks)
+_CB_CODES = (E_VM_END, DG_ST_HM_END_AT, DG_ST_CB_LIST)
+
+
+def _cb_records(rec: bytes, r: int):
+    """The callbacks a message stopped at, [(status, record)] in message
+    order: a DG_ST_CB_LIST slot holds every one of the pass (each behind the
+    status word its stop would have returned), the others one."""
+    if (r & 0xFF) != DG_ST_CB_LIST:
+        return [(r, rec)]
+    out, at = [], 0
+    for _ in range(r >> 40):
+        st = int.from_bytes(rec[at:at + 8], "big")
+        at += 8
+        n = 16 if (st & 0xFF) == E_VM_END else 8 + 8 * (st >> 40)
+        out.append((st, rec[at:at + n]))
+        at += n
+    return out
 
 # internal/types/types.go:107-131 ParsingError messages
 _ERR_MSG = {0: "ok", 1: "eof", 2: "invalid char", 3: "invalid escape char", 4: "invalid unicode escape",
@@ -341,6 +360,8 @@ class BinaryConv:
         requires words for DG_ST_HM_END, the 16-byte record for ERR_VM_END."""
         ctx = self._ctx()
         L = _lib.lib()
+        if flags & (F_VALUE_MAPPING | F_HM_SPLIT):
+            flags |= F_CB_COLLECT  # every callback of a pass at once (k callbacks: 2 passes)
         m = len(msgs)
         lens = np.fromiter((len(x) for x in msgs), dtype=np.uint64, count=m)
         in_off = np.zeros(m + 1, dtype=np.uint64)
@@ -401,48 +422,49 @@ class BinaryConv:
         In place on outs / rets / errs; a failing callback leaves the message
         its stop status and its error in errs."""
         answers = {}
-        todo = [i for i in range(len(msgs)) if (int(rets[i]) & 0xFF) in (E_VM_END, DG_ST_HM_END_AT)
-                and errs[i] is None]
+
+        def serve(i, r, rec):  # one callback -> its answer bytes, or raise
+            src = msgs[i]
+            if (r & 0xFF) == DG_ST_HM_END_AT:
+                si = _st.unpack(">Q", rec[:8])[0]
+                sd = flat.structs[si]
+                order = sorted(sd.fields, key=lambda f: f.id)
+                ids = []
+                for w in range(r >> 40):
+                    bits = _st.unpack(">Q", rec[8 + 8 * w:16 + 8 * w])[0]
+                    ids += [order[64 * w + b].id for b in range(64) if (bits >> b) & 1 and 64 * w + b < len(order)]
+                if hm_end is None:
+                    raise H.ConvError("ErrInvalidParam", "http request is nil")
+                return hm_end(i, sd, ids)
+            end = r >> 8
+            start, fidx = _st.unpack(">QQ", rec[:16])
+            f = flat.fields[fidx] if fidx < len(getattr(flat, "fields", [])) else None
+            if f is None:
+                raise H.ConvError("ErrConvert", "unknown field id for value-mapping")
+            if end >= len(src) or start > end:  # impl_amd64.go:132-134
+                raise H.ConvError("ErrConvert", "invalid value-mapping position")
+            try:
+                if f.value_mapping is None:
+                    raise ValueMappingError("no value mapping registered for type %d" % f.vm)
+                val = f.value_mapping.write(f, bytes(src[start:end]))
+            except Exception as e:  # any Write error (impl_amd64.go:137-139)
+                raise H.ConvError("ErrConvert", "failed to convert field '%s' value" % f.name, e)
+            return bytes([f.type.type]) + _st.pack(">h", f.id) + bytes(val)
+
+        todo = [i for i in range(len(msgs)) if (int(rets[i]) & 0xFF) in _CB_CODES and errs[i] is None]
         while todo:
             live = []
             for i in todo:
-                src, rec, r = msgs[i], outs[i], int(rets[i])
+                rec, r = outs[i], int(rets[i])
                 outs[i] = b""
-                if (r & 0xFF) == DG_ST_HM_END_AT:
-                    si = _st.unpack(">Q", rec[:8])[0]
-                    sd = flat.structs[si]
-                    order = sorted(sd.fields, key=lambda f: f.id)
-                    ids = []
-                    for w in range(r >> 40):
-                        bits = _st.unpack(">Q", rec[8 + 8 * w:16 + 8 * w])[0]
-                        ids += [order[64 * w + b].id for b in range(64) if (bits >> b) & 1 and 64 * w + b < len(order)]
-                    try:
-                        if hm_end is None:
-                            raise H.ConvError("ErrInvalidParam", "http request is nil")
-                        ans = hm_end(i, sd, ids)
-                    except H.ConvError as e:
-                        errs[i] = e
-                        continue
-                    answers.setdefault(i, []).append(ans)
-                    live.append(i)
-                    continue
-                end = r >> 8
-                start, fidx = _st.unpack(">QQ", rec[:16])
-                f = flat.fields[fidx] if fidx < len(getattr(flat, "fields", [])) else None
-                if f is None:
-                    errs[i] = H.ConvError("ErrConvert", "unknown field id for value-mapping")
-                    continue
-                if end >= len(src) or start > end:  # impl_amd64.go:132-134
-                    errs[i] = H.ConvError("ErrConvert", "invalid value-mapping position")
-                    continue
                 try:
-                    if f.value_mapping is None:
-                        raise ValueMappingError("no value mapping registered for type %d" % f.vm)
-                    val = f.value_mapping.write(f, bytes(src[start:end]))
-                except Exception as e:  # any Write error (impl_amd64.go:137-139)
-                    errs[i] = H.ConvError("ErrConvert", "failed to convert field '%s' value" % f.name, e)
+                    # served in the order the message meets them: a failing
+                    # callback is the error, as in the reference's Go loop
+                    for rk, reck in _cb_records(rec, r):
+                        answers.setdefault(i, []).append(serve(i, rk, reck))
+                except H.ConvError as e:
+                    errs[i] = e
                     continue
-                answers.setdefault(i, []).append(bytes([f.type.type]) + _st.pack(">h", f.id) + bytes(val))
                 live.append(i)
             if not live:
                 break
@@ -451,7 +473,7 @@ class BinaryConv:
                                    [answers[i] for i in live])
             for k, i in enumerate(live):
                 outs[i], rets[i] = o2[k], r2[k]
-            todo = [i for i in live if (int(rets[i]) & 0xFF) in (E_VM_END, DG_ST_HM_END_AT)]
+            todo = [i for i in live if (int(rets[i]) & 0xFF) in _CB_CODES]
 
     def do_batch_errors(self, desc, msgs: Sequence[bytes], extra_flags: int = 0):
         """BinaryConv.Do over a batch (conv/j2t/conv.go:53-77): (outputs,
@@ -624,6 +646,8 @@ class BinaryConv:
         need = C.c_uint64(0)
         L = _lib.lib()
         flags = to_flags(self.opts) | extra_flags
+        if flags & F_VALUE_MAPPING:
+            flags |= F_CB_COLLECT  # every value-mapping callback of a pass at once
 
         def call(out, cap):
             if chunks > 0:
@@ -642,7 +666,7 @@ class BinaryConv:
         outs = [out[int(out_off[i]):int(out_off[i + 1])].tobytes() for i in range(n)]
         rets = rets[:n]
         vm_errs = {}
-        if flags & F_VALUE_MAPPING and any((int(r) & 0xFF) == E_VM_END for r in rets):
+        if flags & F_VALUE_MAPPING and any((int(r) & 0xFF) in _CB_CODES for r in rets):
             errs = [None] * n
             self._serve_callbacks(flat, msgs, flags, outs, rets, errs)
             vm_errs = {i: e for i, e in enumerate(errs) if e is not None}

@@ -77,7 +77,7 @@ typedef const __attribute__((address_space(3))) double lds_f64;
  * machine does at such a struct (j2t_machine.h), so it is in too. */
 constexpr uint64_t FAST_FLAGS = DG_F_ALLOW_UNKNOWN | DG_F_WRITE_DEFAULT | DG_F_ENABLE_VM | DG_F_ENABLE_I2S |
                                 DG_F_WRITE_REQUIRE | DG_F_NO_BASE64 | DG_F_WRITE_OPTIONAL | DG_F_NO_WRITE_BASE |
-                                DG_F_ENABLE_HM | DG_F_HM_SPLIT;
+                                DG_F_ENABLE_HM | DG_F_HM_SPLIT | DG_F_CB_COLLECT;
 
 /* small power tables, copied to LDS by the kernel prologue */
 /* DG_POW10_M128[e + 348][1] for e in [EL_WLO, EL_WLO + EL_WN): the decimal

@@ -70,6 +70,16 @@ constexpr uint32_t FL_DESC = 16 * 1024;          /* descriptor bytes in LDS (dyn
 constexpr uint32_t FL_INLINE = DG_FL_INLINE;     /* longer string / base64 bodies are written as chunk tasks */
 constexpr uint32_t FL_CHUNK = DG_FL_CHUNK;       /* input bytes per chunk task (a multiple of 8) */
 constexpr uint32_t FL_MAXTASK = 512;             /* chunk tasks per block (more: the message declines) */
+#ifndef DG_FL_OSTAGE
+#define DG_FL_OSTAGE 0 /* measured slower (r5i: C2 kernel 62.8 vs 52.2 us): LDS writes share lgkmcnt with the
+                               * parse/unquote LDS reads, and the flush bunches every store at the end */
+#endif
+/* Output staging: a one-round block (every message <= FL_SLOTS fields)
+ * assembles each message's Thrift bytes in LDS (FL_OSTRIDE bytes per message,
+ * over the separator arrays, dead once the round's fields are parsed) and
+ * flushes them with contiguous stores. Field-major writes straight to global
+ * memory put 64 messages -- 64 lines -- in every store instruction. */
+constexpr uint32_t FL_OSTRIDE = 152; /* bytes per staged message: 8-aligned (word reads), 38 dwords (2-way banks) */
 #ifndef DG_FL_WPE
 #define DG_FL_WPE 4 /* waves per SIMD the register budget is cut for: 128 VGPRs; LDS allows 4 blocks (16 waves) per CU */
 #endif
@@ -602,14 +612,23 @@ struct FlatLds {
     uint32_t big[FL_MPB];                   /* listed for the wave kernel */
     uint32_t nbytes[FL_MPB];                /* Thrift bytes before STOP */
     uint32_t wid[FL_MPB];                   /* wrapped mode: 0x10000 | the outer field's id, 0 = not wrapped */
-    uint32_t sep[FL_MAXF * FL_MPB];         /* [k][m]: comma position | quotes before it << 16 */
+    uint32_t ostg[FL_MPB];                  /* the message's output is staged in LDS (ost) */
+    alignas(8) uint32_t sep[FL_MAXF * FL_MPB]; /* [k][m]: comma position | quotes before it << 16 */
     uint16_t col[FL_MAXF * FL_MPB];         /* [k][m]: colon position */
+    uint8_t ost_pad[FL_MPB * FL_OSTRIDE - (FL_MAXF * FL_MPB) * 6]; /* sep + col + this = the output stage */
     uint16_t size[2 * FL_SLOTS * FL_MPB];   /* [round & 1][slot][m] */
     uint32_t rounds, ntask;
     uint64_t p10u[20];
     double p10d[23];
     uint64_t pw[EL_WN];                     /* Eisel-Lemire powers window (j2t_fast.h) */
 };
+
+static_assert(offsetof(FlatLds, size) - offsetof(FlatLds, sep) >= FL_MPB * FL_OSTRIDE, "output stage");
+/* message m's output stage (valid after the round-0 size barrier) */
+DGI __attribute__((address_space(3))) uint8_t *fl_ost(FlatLds &L, uint32_t m)
+{
+    return (__attribute__((address_space(3))) uint8_t *)(void *)L.sep + m * FL_OSTRIDE;
+}
 
 template <int V>
 __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(DG_FL_WPE))) void j2t_flat_kernel(
@@ -629,10 +648,23 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
     const uint64_t base = lo & ~15ull;
     const bool staged = hi - base <= (uint64_t)FL_STAGEW * 8;
     if (staged) {
+        /* every thread's (up to 4) 16-byte loads issued before any is
+         * stored: one HBM round trip for the block's span, not one per
+         * loop trip */
         const uint4 *gs = (const uint4 *)(P.json + base); /* arena: 16 readable bytes past the end */
         uint4 *ls = (uint4 *)L.in;
         const uint32_t nw = (uint32_t)((hi - base + 15) >> 4);
-        for (uint32_t k = tid; k < nw; k += 64 * FL_WAVES) ls[k] = gs[k];
+        constexpr uint32_t NT = 64 * FL_WAVES;
+        static_assert(FL_STAGEW * 8 / 16 <= 4 * NT, "four 16-byte loads per thread cover the stage");
+        if (nw) { /* unconditional loads (clamped index), conditional stores: no branch between the loads */
+            const uint32_t l = nw - 1;
+            const uint4 v0 = gs[min(tid, l)], v1 = gs[min(tid + NT, l)], v2 = gs[min(tid + 2 * NT, l)],
+                        v3 = gs[min(tid + 3 * NT, l)];
+            if (tid < nw) ls[tid] = v0;
+            if (tid + NT < nw) ls[tid + NT] = v1;
+            if (tid + 2 * NT < nw) ls[tid + 2 * NT] = v2;
+            if (tid + 3 * NT < nw) ls[tid + 3 * NT] = v3;
+        }
     }
     {
         const uint4 *gd = (const uint4 *)S.blob;
@@ -696,9 +728,21 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
             const uint64_t a = P.in_off[b0 + m1];
             const uint32_t nw = (L.n[m1] + 7) >> 3, sh = (uint32_t)(a & 7) << 3;
             const glb_u64 *gsrc = (const glb_u64 *)(const void *)P.json + (a >> 3);
-            for (uint32_t w = g; w < nw; w += FL_G) {
-                const uint64_t lo = gsrc[w], hi = gsrc[w + 1];
-                L.in[(L.lw[m1] >> 3) + w] = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+            /* lane g: words g, g + 4, ... (<= 8 of them, 256 bytes); all its
+             * loads issued before the first use (indices clamped to the word
+             * past the message, inside the arena's 16 readable bytes) */
+            constexpr uint32_t NWL = FL_MAXLEN / 8 / FL_G;
+            uint64_t lo[NWL], hi[NWL];
+#pragma unroll
+            for (uint32_t j = 0; j < NWL; j++) {
+                const uint32_t w = g + FL_G * j;
+                lo[j] = gsrc[min(w, nw)];
+                hi[j] = gsrc[min(w + 1, nw)];
+            }
+#pragma unroll
+            for (uint32_t j = 0; j < NWL; j++) {
+                const uint32_t w = g + FL_G * j;
+                if (w < nw) L.in[(L.lw[m1] >> 3) + w] = sh ? (lo[j] >> sh) | (hi[j] << (64 - sh)) : lo[j];
             }
         }
         __syncthreads();
@@ -937,11 +981,21 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
             }
         };
         /* 0 = error, 1 = written, 2 = the body is left to chunk tasks */
-        auto write = [&](const FField &F, uint32_t off) -> uint32_t {
+        auto write = [&](const FField &F, uint32_t off, bool stg) -> uint32_t {
             if (!F.size) return 1;
             if (off + F.size >= cap) return 0; /* the slot holds the field and STOP */
+            if (stg) { /* into the message's LDS stage */
+                WOutT<3> o;
+                o.init(fl_ost(L, mm) + off);
+                const uint32_t wr = flat_write(src, F, tb, o);
+                o.finish();
+                return wr;
+            }
             WOut o;
             o.init(slot + off);
+#ifdef DG_FL_ABL_NOSTORE
+            o.dry = true; /* ablation (timing only): the field stores are not issued */
+#endif
             const uint32_t wr = flat_write(src, F, tb, o);
             o.finish();
             return wr;
@@ -973,11 +1027,15 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
                 tot += v;
             }
             nbytes += tot;
+            /* one round: the whole message (+ STOP, + the outer STOP when
+             * wrapped) fits its stage -- every wave decides the same */
+            const bool stg = DG_FL_OSTAGE && rounds == 1 && nbytes + 2 <= FL_OSTRIDE;
+            if (wave == 0) L.ostg[mm] = stg ? 1u : 0u;
             uint32_t wr[FL_FPW], nch[FL_FPW], nsum = 0, good = 1;
 #pragma unroll
             for (uint32_t h = 0; h < FL_FPW; h++) {
                 FLF_T0();
-                wr[h] = write(F[h], off[h]);
+                wr[h] = write(F[h], off[h], stg);
                 FLF_ADD(6 + r * FL_SLOTS + fl_slot(wave, h));
                 nch[h] = wr[h] == 2 ? (F[h].nb + FL_CHUNK - 1) / FL_CHUNK : 0u;
                 nsum += nch[h];
@@ -1036,12 +1094,23 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
             const uint32_t lwa = L.lw[m];
             LSrc src;
             src.init((const __attribute__((address_space(3))) uint64_t *)(void *)&L.in[lwa >> 3], (int32_t)(lwa & 7), (int32_t)L.n[m]);
-            WOut o;
-            o.init((gu8 *)(void *)(P.out + L.oa[m] + (uint32_t)(tk >> 32)));
             bool cok = true;
-            if ((tk >> 6) & 1) cok = body_b64(src, s0, cn, ((tk >> 7) & 1) != 0, o);
-            else body_copy(src, s0, cn, o);
-            o.finish();
+            if (L.ostg[m]) {
+                WOutT<3> o;
+                o.init(fl_ost(L, m) + (uint32_t)(tk >> 32));
+                if ((tk >> 6) & 1) cok = body_b64(src, s0, cn, ((tk >> 7) & 1) != 0, o);
+                else body_copy(src, s0, cn, o);
+                o.finish();
+            } else {
+                WOut o;
+                o.init((gu8 *)(void *)(P.out + L.oa[m] + (uint32_t)(tk >> 32)));
+#ifdef DG_FL_ABL_NOSTORE
+                o.dry = true;
+#endif
+                if ((tk >> 6) & 1) cok = body_b64(src, s0, cn, ((tk >> 7) & 1) != 0, o);
+                else body_copy(src, s0, cn, o);
+                o.finish();
+            }
             if (!cok) L.ok[m] = 0;
         }
     }
@@ -1072,23 +1141,66 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
                     }
                 }
             }
+            const bool stg = L.ostg[m] != 0;
+            uint32_t flen = 0; /* staged bytes to flush */
             if (good && wid) {
                 /* the outer field header, the inner STOP, the outer STOP */
                 gu8 *o = (gu8 *)(void *)P.out + L.oa[m];
                 o[-3] = DG_T_STRUCT;
                 o[-2] = (uint8_t)(wid >> 8);
                 o[-1] = (uint8_t)wid;
-                o[len - 1] = 0;
-                o[len] = 0;
+                if (stg) {
+                    fl_ost(L, m)[len - 1] = 0;
+                    fl_ost(L, m)[len] = 0;
+                    flen = len + 1;
+                } else {
+                    o[len - 1] = 0;
+                    o[len] = 0;
+                }
                 P.ret[i] = 0;
                 P.out_len[i] = len + 4;
             } else if (good) {
-                ((gu8 *)(void *)P.out)[L.oa[m] + len - 1] = 0; /* STOP */
+                if (stg) {
+                    fl_ost(L, m)[len - 1] = 0;
+                    flen = len;
+                } else {
+                    ((gu8 *)(void *)P.out)[L.oa[m] + len - 1] = 0; /* STOP */
+                }
                 P.ret[i] = 0;
                 P.out_len[i] = len;
             } else if (!L.big[m]) {
                 const uint32_t qq = atomicAdd(S.bail_count, 1u);
                 S.bail_list[qq] = (uint32_t)i;
+            }
+            L.nbytes[m] = flen;
+        } else {
+            L.nbytes[m] = 0;
+        }
+    }
+    /* ---- 5. flush the staged messages: 8 lanes per message, each an
+     *      8-byte destination word at a time (byte-exact at both ends), so
+     *      a wave's store covers 8 messages x 64 contiguous bytes ---- */
+    __syncthreads();
+    {
+        const uint32_t j = tid & 7;
+        for (uint32_t m = tid >> 3; m < FL_MPB; m += 64 * FL_WAVES / 8) {
+            const uint32_t flen = L.nbytes[m];
+            if (!flen) continue;
+            const uintptr_t d0 = (uintptr_t)(P.out + L.oa[m]), wb = d0 & ~(uintptr_t)7;
+            const uint32_t lead = (uint32_t)(d0 - wb), nw = (lead + flen + 7) >> 3;
+            const __attribute__((address_space(3))) uint64_t *sw =
+                (const __attribute__((address_space(3))) uint64_t *)fl_ost(L, m);
+            for (uint32_t k = j; k < nw; k += 8) {
+                /* stage bytes [8k - lead, 8k - lead + 8) */
+                const int32_t so = (int32_t)(8 * k) - (int32_t)lead;
+                uint64_t v;
+                if (so < 0) v = sw[0] << (8 * lead);
+                else if ((so & 7) == 0) v = sw[so >> 3];
+                else v = (sw[so >> 3] >> (8 * (so & 7))) | (sw[(so >> 3) + 1] << (64 - 8 * (so & 7)));
+                const uint32_t lo = k == 0 ? lead : 0u, hi = lead + flen - 8 * k < 8 ? lead + flen - 8 * k : 8u;
+                gu8 *w = (gu8 *)(void *)(wb + 8 * (uintptr_t)k);
+                if (lo == 0 && hi == 8) *(gu64 *)w = v;
+                else store_part(w, v, lo, hi);
             }
         }
     }

@@ -827,7 +827,7 @@ static int batch_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
     /* the packed bytes: failed and overflowed messages hold none */
     auto kept = [&](uint64_t i) {
         return ret[i] == 0 || (uint8_t)ret[i] == DG_ST_HM_END || (uint8_t)ret[i] == 24 /* ERR_VM_END's record */ ||
-               (uint8_t)ret[i] == DG_ST_HM_END_AT;
+               (uint8_t)ret[i] == DG_ST_HM_END_AT || (uint8_t)ret[i] == DG_ST_CB_LIST;
     };
     uint64_t packed = 0;
     for (uint64_t i = 0; i < n; i++)

@@ -146,6 +146,9 @@ struct Machine {
     const dg_cb_entry *ans_row; /* this message's value-mapping answers (Params::ans_tab), or NULL */
     uint32_t ans_seen;          /* non-inline value-mapping values met so far */
     uint64_t ans_at;            /* hm_bytes offset of the next answer */
+    uint32_t ncb;               /* DG_F_CB_COLLECT: callbacks recorded in this pass */
+    uint64_t slot_cap;          /* ... the slot's size (out.cap is 0 once one is: the output is dropped) */
+    Out rec;                    /* ... their records, from the slot's start */
     JState jt;
     PROF_DECL
 
@@ -265,6 +268,23 @@ struct Machine {
          * stop for it (dgj2t_defs.h dg_cb_entry) */
         field_cache_len = 0;
         if (take_answer()) return 0;
+        if (flag & DG_F_CB_COLLECT) {
+            if (!cb_room(16 + 8 * sd.req_words)) return pack(DG_ST_CB_LIST, ncb, 0);
+            rec.w64(pack(DG_ST_HM_END_AT, sd.req_words, (uint64_t)p));
+            rec.w64(si);
+            for (uint32_t w = 0; w < sd.req_words; w++) {
+                uint64_t bits = sd.req_words == 1 ? x.u : ws.reqarena[(uint32_t)x.u + w], m = 0;
+                while (bits) {
+                    const uint32_t b = __builtin_ctzll(bits);
+                    bits &= bits - 1;
+                    const dg_field f = ldrec(&D.F[sd.field_begin + w * 64 + b]);
+                    if (!(f.flags & DG_FF_REQUEST_BASE) && f.required == DG_REQ_REQUIRED) m |= 1ull << b;
+                }
+                rec.w64(m);
+            }
+            ncb++;
+            return 0;
+        }
         out.set_len(0);
         out.w64(si);
         for (uint32_t w = 0; w < sd.req_words; w++) {
@@ -278,6 +298,22 @@ struct Machine {
             out.w64(m);
         }
         return pack(DG_ST_HM_END_AT, sd.req_words, (uint64_t)p);
+    }
+
+    /* DG_F_CB_COLLECT: room for a callback record of `bytes` in the slot.
+     * The first one switches the output off (out.cap = 0: later writes are
+     * only counted) and starts the records at the slot's start. A callback's
+     * answer is output bytes only -- the reference's FSM resumes after the
+     * value or the struct either way (conv/j2t/impl_amd64.go:71-155) -- so
+     * converting on without it meets the same later callbacks and errors. */
+    DGI bool cb_room(uint32_t bytes)
+    {
+        if (ncb == 0) {
+            slot_cap = out.cap;
+            rec.init((uint8_t *)(void *)out.b, slot_cap);
+            out.cap = 0;
+        }
+        return rec.len + bytes <= slot_cap;
     }
 
     /* the host's next callback answer (dg_cb_entry), if it has one: written */
@@ -594,6 +630,14 @@ struct Machine {
             return 0;
         }
         if (take_answer()) return 0; /* the host's answer for this value (dg_cb_entry) */
+        if (flag & DG_F_CB_COLLECT) { /* recorded; the machine converts on */
+            if (!cb_room(24)) return pack(DG_ST_CB_LIST, ncb, 0);
+            rec.w64(pack0(E_VM_END, (uint64_t)p));
+            rec.w64((uint64_t)s0);
+            rec.w64((uint64_t)fidx);
+            ncb++;
+            return 0;
+        }
         /* ERR_VM_END for the host: the value's start and the field, in the slot */
         out.set_len(0);
         out.w64((uint64_t)s0);
@@ -900,6 +944,7 @@ DGI uint64_t convert_one(const Params &P, const DV &dv, uint64_t i, const S &src
     m.ans_row = P.ans_tab ? P.ans_tab + i : nullptr;
     m.ans_seen = 0;
     m.ans_at = m.ans_row ? m.ans_row->off : 0;
+    m.ncb = 0;
     uint64_t r;
     if (m.src.n == 0) { /* empty body -> STOP (conv/j2t/impl.go:52-82) */
         m.out.w8(0);
@@ -922,6 +967,13 @@ DGI uint64_t convert_one(const Params &P, const DV &dv, uint64_t i, const S &src
 #else
         r = m.run(P.root);
 #endif
+    }
+    if (m.ncb && (uint8_t)r != DG_ST_DEEP) {
+        /* DG_F_CB_COLLECT: the recorded callbacks, whatever came after them
+         * (an error there is met again once the host has served them) */
+        m.rec.finish();
+        olen = (uint32_t)m.rec.len;
+        return pack(DG_ST_CB_LIST, m.ncb < 0xFFFFFFu ? m.ncb : 0xFFFFFFu, 0);
     }
     /* HM_END: the host completes the output; VM_END / HM_END_AT: the callback's record */
     const bool keep = r == 0 || (uint8_t)r == DG_ST_HM_END || (uint8_t)r == E_VM_END || (uint8_t)r == DG_ST_HM_END_AT;

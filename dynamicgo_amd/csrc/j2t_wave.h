@@ -183,36 +183,47 @@ typedef __attribute__((address_space(1))) uint32_t gu32;
 typedef __attribute__((address_space(1))) uint16_t gu16;
 
 /* store bytes [lo, hi) of the little-endian word v at the 8-aligned w:
- * at most 6 naturally aligned stores, straight-line (no divergent loop) */
-DGI void store_part(gu8 *w, uint64_t v, uint32_t lo, uint32_t hi)
+ * at most 6 naturally aligned stores, straight-line (no divergent loop).
+ * AS: the address space written (1 = global, 3 = LDS) */
+template <int AS>
+DGI void store_part_as(__attribute__((address_space(AS))) uint8_t *w, uint64_t v, uint32_t lo, uint32_t hi)
 {
+    typedef __attribute__((address_space(AS))) uint16_t u16p;
+    typedef __attribute__((address_space(AS))) uint32_t u32p;
+    typedef __attribute__((address_space(AS))) uint64_t u64p;
     if (lo == 0 && hi == 8) {
-        *(gu64 *)w = v;
+        *(u64p *)w = v;
         return;
     }
     uint32_t i = lo;
     if ((i & 1) && i < hi) { w[i] = (uint8_t)(v >> (i * 8)); i += 1; }
-    if ((i & 2) && i + 2 <= hi) { *(gu16 *)(w + i) = (uint16_t)(v >> (i * 8)); i += 2; }
-    if ((i & 4) && i + 4 <= hi) { *(gu32 *)(w + i) = (uint32_t)(v >> (i * 8)); i += 4; }
-    if (i + 4 <= hi) { *(gu32 *)(w + i) = (uint32_t)(v >> (i * 8)); i += 4; }
-    if (i + 2 <= hi) { *(gu16 *)(w + i) = (uint16_t)(v >> (i * 8)); i += 2; }
+    if ((i & 2) && i + 2 <= hi) { *(u16p *)(w + i) = (uint16_t)(v >> (i * 8)); i += 2; }
+    if ((i & 4) && i + 4 <= hi) { *(u32p *)(w + i) = (uint32_t)(v >> (i * 8)); i += 4; }
+    if (i + 4 <= hi) { *(u32p *)(w + i) = (uint32_t)(v >> (i * 8)); i += 4; }
+    if (i + 2 <= hi) { *(u16p *)(w + i) = (uint16_t)(v >> (i * 8)); i += 2; }
     if (i < hi) w[i] = (uint8_t)(v >> (i * 8));
 }
+DGI void store_part(gu8 *w, uint64_t v, uint32_t lo, uint32_t hi) { store_part_as<1>(w, v, lo, hi); }
 
 /* A writer that owns exactly [start, start + written): whole aligned words
  * inside the range are stored as 8-byte words, the partial words at both
- * ends byte-exactly, so neighbouring tokens can write concurrently. */
-struct WOut {
-    gu8 *wa;       /* 8-aligned address of the current word */
+ * ends byte-exactly, so neighbouring tokens can write concurrently. AS: the
+ * address space written (WOut = global; the flat kernel also stages
+ * messages in LDS). */
+template <int AS>
+struct WOutT {
+    typedef __attribute__((address_space(AS))) uint8_t b8;
+    typedef __attribute__((address_space(AS))) uint64_t b64;
+    b8 *wa;        /* 8-aligned address of the current word */
     uint32_t lo;   /* first owned byte of the current word (first word only) */
     uint32_t used; /* bytes of the current word filled */
     uint64_t wbuf;
     uint64_t len;  /* bytes written */
     bool dry;      /* count only (lengths before the offsets are known) */
-    DGI void init(gu8 *p)
+    DGI void init(b8 *p)
     {
-        uintptr_t a = (uintptr_t)(void *)p;
-        wa = (gu8 *)(void *)(a & ~(uintptr_t)7);
+        const uintptr_t a = (uintptr_t)p;
+        wa = (b8 *)(a & ~(uintptr_t)7);
         lo = used = (uint32_t)(a & 7);
         wbuf = 0;
         len = 0;
@@ -238,8 +249,8 @@ struct WOut {
         uint64_t hi_w = used ? (v >> (64 - sh)) : 0;
         len += n;
         if (used + n >= 8) {
-            if (lo == 0) *(gu64 *)wa = lo_w;
-            else store_part(wa, lo_w, lo, 8);
+            if (lo == 0) *(b64 *)wa = lo_w;
+            else store_part_as<AS>(wa, lo_w, lo, 8);
             wa += 8;
             lo = 0;
             wbuf = hi_w;
@@ -255,9 +266,10 @@ struct WOut {
     DGI void w64(uint64_t v) { wle(__builtin_bswap64(v), 8); }
     DGI void finish()
     {
-        if (!dry && used > lo) store_part(wa, wbuf, lo, used);
+        if (!dry && used > lo) store_part_as<AS>(wa, wbuf, lo, used);
     }
 };
+typedef WOutT<1> WOut;
 
 /* big-endian u32 at an arbitrary byte address, byte-exact */
 DGI void put_be32(gu8 *p, uint32_t v)
@@ -1218,6 +1230,7 @@ __global__ __launch_bounds__(64 * WV_WAVES) __attribute__((amdgpu_waves_per_eu(D
     __shared__ uint64_t s_reqmask[WV_REQMASKS];
     __shared__ uint64_t s_p10u[20];
     __shared__ double s_p10d[23];
+    __shared__ uint64_t s_pw[EL_WN]; /* Eisel-Lemire powers of ordinary doubles: LDS, not the global table */
     const uint32_t tid = threadIdx.x;
     const uint64_t nh = W.list && W.huge_count
                             ? (uint64_t)__hip_atomic_load((uint32_t *)W.huge_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
@@ -1253,6 +1266,7 @@ __global__ __launch_bounds__(64 * WV_WAVES) __attribute__((amdgpu_waves_per_eu(D
         s_p10u[tid] = v;
     }
     if (tid < 23) s_p10d[tid] = P10[tid];
+    el_window_fill(s_pw, tid);
     __syncthreads();
     const auto dv = desc_view<3>((const __attribute__((address_space(3))) uint8_t *)(void *)s_desc, W.hdr);
     if (tid < WV_REQMASKS && tid < W.hdr.n_structs) {
@@ -1268,7 +1282,8 @@ __global__ __launch_bounds__(64 * WV_WAVES) __attribute__((amdgpu_waves_per_eu(D
     }
     __syncthreads();
     const uint32_t wave = tid >> 6, lane = tid & 63;
-    FastTabs tb{(const __attribute__((address_space(3))) uint64_t *)(void *)s_p10u, (lds_f64 *)(void *)s_p10d};
+    FastTabs tb{(const __attribute__((address_space(3))) uint64_t *)(void *)s_p10u, (lds_f64 *)(void *)s_p10d,
+                (const __attribute__((address_space(3))) uint64_t *)(void *)s_pw};
     const __attribute__((address_space(3))) uint8_t *cls = (const __attribute__((address_space(3))) uint8_t *)(void *)s_cls;
     __attribute__((address_space(3))) uint64_t *mbuf = (__attribute__((address_space(3))) uint64_t *)(void *)s_msg[wave];
     gu8 *dbuf = (gu8 *)(void *)(W.ws + ((uint64_t)blockIdx.x * WV_WAVES + wave) * DCAP);
@@ -1374,7 +1389,8 @@ __global__ __launch_bounds__(256) void dg_pack_scan_kernel(const uint8_t *out, c
         /* failed messages pack as nothing; an unframed DG_ST_HM_END keeps its
          * partial output and an ERR_VM_END its record for the host (dgj2t_defs.h) */
         const uint8_t c = (uint8_t)fr.ret[i];
-        return !fr.hdr && (c == DG_ST_HM_END || c == 24u || c == DG_ST_HM_END_AT) ? out_len[i] : 0u;
+        return !fr.hdr && (c == DG_ST_HM_END || c == 24u || c == DG_ST_HM_END_AT || c == DG_ST_CB_LIST) ? out_len[i]
+                                                                                                         : 0u;
     };
     /* bytes, and (ovf_out) overflowed slots in bits 44+ of the same sum */
     constexpr uint32_t OVF_SH = 44;

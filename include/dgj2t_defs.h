@@ -31,6 +31,10 @@
                                            mapped-field bytes in front. Nested structs with mapped fields still
                                            return ERR_HM. */
 #define DG_F_NO_FLAT_PATH (1ull << 21)  /* extension: lane-per-message small kernel even for a flat root (testing) */
+#define DG_F_CB_COLLECT (1ull << 22)    /* extension: at a callback the host must serve (ERR_VM_END, a nested
+                                           ERR_HM_END, see dg_cb_entry) the machine records it and converts on
+                                           instead of stopping; the message ends with DG_ST_CB_LIST and every
+                                           callback of one pass recorded, so k callbacks take 2 passes, not k + 1 */
 
 /* library-internal per-message statuses (code byte values the reference never
  * produces). The host entry points resolve them before returning; the device
@@ -43,6 +47,13 @@
                                     words (big-endian u64, `value` of them); the host appends the cached fields'
                                     bytes and the STOP */
 #define DG_ST_HM_END_AT 0xF4u    /* a nested struct's ERR_HM_END for the host (dg_cb_entry) */
+#define DG_ST_CB_LIST 0xF5u      /* DG_F_CB_COLLECT: `value` callbacks recorded in the slot, in the order the
+                                    message meets them (out_len bytes): each is the status word the stop would
+                                    have returned (big-endian u64: code 24 or DG_ST_HM_END_AT, its pos and value)
+                                    followed by that stop's record (dg_cb_entry). The host answers them in order
+                                    and converts the message again with the answers; an error met after a
+                                    callback is reported by that pass, as the reference reports it after Go
+                                    served the callback. */
 #define DG_ST_HM_ERR 0xF3u       /* DG_F_HM_SPLIT: the message opened a struct whose HTTP-mapping entry is an
                                     error (dg_hm_entry.len == DG_HM_ERR): handleHttpMappings failed for it on the
                                     host; value = the entry's slot, pos = the struct's '{' */

@@ -105,3 +105,35 @@ def test_vm_example3_fuzz():
     td = dynamic_struct()
     msgs = [fuzz.gen_message(rng, td) for _ in range(600)]
     _agree(td, msgs, conv.Options(EnableValueMapping=True, WriteRequireField=True))
+
+
+def test_many_callbacks_in_one_message_two_passes(monkeypatch):
+    """a message with k non-inline value-mapping callbacks
+    (ERR_VM_END, native/thrift.c:641-665) takes 2 device passes, not k + 1:
+    DG_F_CB_COLLECT records every callback of a pass and converts on, the
+    host serves them in message order, then one rerun writes the answers
+    (the reference resumes its FSM in place, conv/j2t/impl_amd64.go:169-247).
+    Messages with 64..400 callbacks -- list<struct> elements, duplicate root
+    keys, a nested struct's own, a failing callback in the middle, a JSON
+    error after the last callback -- agree with the reference FSM serving
+    the same callbacks one by one."""
+    td = vm_probe()
+    rng = random.Random(64)
+    msgs = [b'{"G":[' + b",".join(b'{"y":%d}' % rng.randint(-300, 300) for _ in range(n)) + b"]}"
+            for n in (64, 100, 257, 400)]
+    msgs.append(b"{" + b",".join(b'"A":"%d"' % k for k in range(80)) + b"}")
+    msgs.append(b'{"G":[' + b",".join(b'{"y":"%d","x":[%d]}' % (k, k) for k in range(70)) + b'],"D":2.5}')
+    bad = [b'{"y":%d}' % k for k in range(90)]
+    bad[45] = b'{"y":"4x"}'  # JSConv2 rejects it: the error of the 46th callback
+    msgs.append(b'{"G":[' + b",".join(bad) + b"]}")
+    msgs.append(b'{"G":[' + b",".join(b'{"y":%d}' % k for k in range(66)) + b'],"C":[1,}')  # JSON error after them
+    passes = []
+    orig = conv.BinaryConv._host_cb
+
+    def counted(self, *a, **kw):
+        passes.append(len(a[1]))
+        return orig(self, *a, **kw)
+    monkeypatch.setattr(conv.BinaryConv, "_host_cb", counted)
+    n_ok = _agree(td, msgs, conv.Options(EnableValueMapping=True))
+    assert n_ok == 6
+    assert len(passes) == 1, passes  # the main pass + ONE rerun for all callbacks of all messages

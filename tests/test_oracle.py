@@ -88,9 +88,9 @@ def _pack(code, value, pos):
 def test_utf8_validation_extension(body, bad):
     """DG_F_VALIDATE_UTF8 on the port oracle: valid strings convert exactly as
     without the flag; the first invalid sequence (utf8_validate semantics,
-    native/utf8.c:101-212) gives ERR_INVAL at its offset. Parity unpinned by
-    construction (the reference has no such flag): pinned to the definition
-    above and to the flag-off output on valid input."""
+    native/utf8.c:101-212) gives ERR_INVAL at its offset. The reference has no
+    such flag; the verdicts are pinned to its own validator by
+    test_utf8_extension_pinned_to_reference_validator below."""
     chk = oracle.PortOracle()
     fl = T.flatten(idl_desc("baseline.thrift", "SimpleMethod"))
     pre = b'{"StringField":"'
