@@ -69,17 +69,8 @@ constexpr uint32_t FL_DESC = 16 * 1024;          /* descriptor bytes in LDS (dyn
 #endif
 constexpr uint32_t FL_INLINE = DG_FL_INLINE;     /* longer string / base64 bodies are written as chunk tasks */
 constexpr uint32_t FL_CHUNK = DG_FL_CHUNK;       /* input bytes per chunk task (a multiple of 8) */
-constexpr uint32_t FL_MAXTASK = 512;             /* chunk tasks per block (more: the message declines) */
-#ifndef DG_FL_OSTAGE
-#define DG_FL_OSTAGE 0 /* measured slower (r5i: C2 kernel 62.8 vs 52.2 us): LDS writes share lgkmcnt with the
-                               * parse/unquote LDS reads, and the flush bunches every store at the end */
-#endif
-/* Output staging: a one-round block (every message <= FL_SLOTS fields)
- * assembles each message's Thrift bytes in LDS (FL_OSTRIDE bytes per message,
- * over the separator arrays, dead once the round's fields are parsed) and
- * flushes them with contiguous stores. Field-major writes straight to global
- * memory put 64 messages -- 64 lines -- in every store instruction. */
-constexpr uint32_t FL_OSTRIDE = 152; /* bytes per staged message: 8-aligned (word reads), 38 dwords (2-way banks) */
+constexpr uint32_t FL_MAXTASK = 320;             /* chunk tasks per block (more: the message declines; C2 ~160) */
+constexpr uint32_t FL_NESC = 4;                  /* escapes per message (more: the message declines) */
 #ifndef DG_FL_WPE
 #define DG_FL_WPE 4 /* waves per SIMD the register budget is cut for: 128 VGPRs; LDS allows 4 blocks (16 waves) per CU */
 #endif
@@ -211,13 +202,6 @@ struct RSrcL {
     }
 };
 
-/* counts bytes only (string sizes with escapes) */
-struct CountW {
-    uint64_t len = 0;
-    DGI void wle(uint64_t, uint32_t n) { len += n; }
-    DGI void w8(uint8_t) { len += 1; }
-};
-
 /* one parsed field */
 enum : uint32_t { FV_NONE = 0, FV_NUM, FV_STR, FV_BIN, FV_BOOL, FV_NUMSTR };
 struct FField {
@@ -242,18 +226,6 @@ DGI uint32_t skip_ws(S &s, uint32_t p)
     return p;
 }
 
-/* does src[s0, s0+nb) hold byte ch */
-template <class S>
-DGI bool has_byte(S &src, uint32_t s0, uint32_t nb, uint8_t ch)
-{
-    for (uint32_t j = 0; j < nb; j += 8) {
-        uint64_t m = eqbytes(src.get8((typename S::idx)(s0 + j)), ch);
-        if (nb - j < 8) m &= (1ull << ((nb - j) << 3)) - 1;
-        if (m) return true;
-    }
-    return false;
-}
-
 /* the name table of struct sd (native/thrift.c:449-468 j2t_find_field_key):
  * the global field index of key src[k0, k0+kn), or -1 */
 template <class S, class DV>
@@ -276,6 +248,64 @@ DGI int32_t fl_lookup(const DV &D, const dg_struct &sd, S &src, uint32_t k0, uin
     }
 }
 
+/* ---- escapes: decoded once, in the structure phase ----
+ * Every backslash of a flat message starts an escape (one before '"' or '\\'
+ * declines the message), so the structure phase decodes each one where it
+ * finds it (4 lanes per message, in parallel) into the message's escape
+ * table: position, JSON bytes (2 or 6), UTF-8 bytes (1..3) and their value.
+ * A string's Thrift size is then its length minus what its escapes shrink,
+ * and its body is written as runs copied around the escapes -- no serial
+ * unquote loop over the string on the field's wave, twice (size and write).
+ * unquote's semantics (native/parsing.c:702-945, flags 0) for everything
+ * the flat path keeps; a surrogate, an invalid escape or more than FL_NESC
+ * escapes decline the message to the list pass. */
+typedef const __attribute__((address_space(3))) uint64_t lds_esc;
+DGI bool fl_hex4(uint32_t w, uint32_t &v)
+{
+    uint32_t r = 0, ok = 1;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t b = (w >> (8 * k)) & 0xFF, d = b - '0', l = (b | 0x20) - 'a';
+        ok &= (uint32_t)(d < 10) | (uint32_t)(l < 6);
+        r = (r << 4) | (d < 10 ? d : (l + 10) & 0xF);
+    }
+    v = r;
+    return ok != 0;
+}
+/* the escape at message position p (e0: the 8 bytes from its backslash) ->
+ * its table entry, or 0 if the flat path leaves it to the exact machine */
+DGI uint64_t fl_escape(uint32_t p, uint64_t e0)
+{
+    const uint32_t c = (uint32_t)(e0 >> 8) & 0xFF;
+    if (c == 'u') {
+        uint32_t cp;
+        if (!fl_hex4((uint32_t)(e0 >> 16), cp) || (cp >= 0xd800 && cp <= 0xdfff)) return 0;
+        const uint32_t n = cp <= 0x7f ? 1u : cp <= 0x7ff ? 2u : 3u;
+        const uint32_t v = n == 1 ? cp
+                           : n == 2 ? (0xc0 | (cp >> 6)) | ((0x80 | (cp & 0x3f)) << 8)
+                                    : (0xe0 | (cp >> 12)) | ((0x80 | ((cp >> 6) & 0x3f)) << 8) | ((0x80 | (cp & 0x3f)) << 16);
+        return p | (6u << 12) | (n << 16) | ((uint64_t)v << 32);
+    }
+    /* _UnquoteTab native/parsing.c:565-575 */
+    const uint32_t cc = c == 'b' ? 8u : c == 'f' ? 12u : c == 'n' ? 10u : c == 'r' ? 13u : c == 't' ? 9u : c;
+    const bool ok = (c == '"') | (c == '\\') | (c == '/') | (c == 'b') | (c == 'f') | (c == 'n') | (c == 'r') | (c == 't');
+    return ok ? p | (2u << 12) | (1u << 16) | ((uint64_t)cc << 32) : 0;
+}
+/* escapes in [a, b): any, and the bytes they shrink the body by */
+DGI bool fl_esc_in(lds_esc *E, uint32_t ne, uint32_t a, uint32_t b, uint32_t &shrink)
+{
+    bool any = false;
+    shrink = 0;
+    for (uint32_t e = 0; e < ne; e++) {
+        const uint64_t x = E[e];
+        const uint32_t p = (uint32_t)x & 0xFFF;
+        const bool in = p >= a && p < b;
+        any |= in;
+        shrink += in ? ((uint32_t)(x >> 12) & 0xF) - ((uint32_t)(x >> 16) & 0x7) : 0u;
+    }
+    return any;
+}
+
 /* Field k: bytes (sk, ek) between its separators, its colon at ck, nq quotes
  * inside. Key lookup, value parse and Thrift size; false = decline the
  * message. Every quote of the message is a delimiter (phase 1 declined \" and
@@ -283,7 +313,8 @@ DGI int32_t fl_lookup(const DV &D, const dg_struct &sd, S &src, uint32_t k0, uin
  * is a string: the key and a string value are delimited without scanning. */
 template <class S, class DV>
 DGI bool fl_field(const DV &D, const dg_struct &sd, S &src, uint32_t sk, uint32_t ck, uint32_t ek, uint32_t nq,
-                  bool hasbs, uint32_t k, uint64_t flag, const FastTabs &tb, FField &F FLG_ARG)
+                  bool hasbs, lds_esc *E, uint32_t ne, uint32_t k, uint64_t flag, const FastTabs &tb,
+                  FField &F FLG_ARG)
 {
     typedef typename S::idx SI;
     /* Round 1 of LDS reads: the four delimiting bytes and the predicted
@@ -311,7 +342,8 @@ DGI bool fl_field(const DV &D, const dg_struct &sd, S &src, uint32_t sk, uint32_
     if ((q < p + 2) | (cs != '"') | (cq != '"') | (nq != (c == '"' ? 4u : 2u))) return false;
     const uint32_t k0 = p + 1, kn = q - 1 - k0;
     FLG(1);
-    if (hasbs && has_byte(src, k0, kn, '\\')) return false; /* escaped key: unquoted before lookup -> the list pass */
+    uint32_t shrink = 0;
+    if (hasbs && fl_esc_in(E, ne, k0, k0 + kn, shrink)) return false; /* escaped key: unquoted before lookup -> the list pass */
     /* the key (native/thrift.c:668-763): predicted (field k in IDL order),
      * else the name table. Round 2: a key of up to 16 bytes and the
      * predicted key's pool words, compared in one step (the pool keys are
@@ -346,7 +378,7 @@ DGI bool fl_field(const DV &D, const dg_struct &sd, S &src, uint32_t sk, uint32_
         if ((ve - v0 < 2) | (ce != '"')) return false;
         vs0 = v0 + 1;
         vnb = ve - 1 - vs0;
-        vesc = hasbs && has_byte(src, vs0, vnb, '\\');
+        vesc = hasbs && fl_esc_in(E, ne, vs0, vs0 + vnb, shrink); /* shrink: what its escapes take off */
         vk = FV_STR;
     } else if (c == '-' || (uint8_t)(c - '0') <= 9) {
         /* a known field without a value mapping: a number's Thrift size
@@ -424,9 +456,7 @@ DGI bool fl_field(const DV &D, const dg_struct &sd, S &src, uint32_t sk, uint32_
             vsize = 4 + vnb / 4 * 3 - (c3 == '=' ? (c2 == '=' ? 2 : 1) : 0);
             vk = FV_BIN;
         } else if (vesc) {
-            CountW cw;
-            if (!fast_unquote(src, (SI)vs0, (SI)vnb, cw)) return false;
-            vsize = 4 + (uint32_t)cw.len;
+            vsize = 4 + vnb - shrink;
         } else {
             vsize = 4 + vnb;
         }
@@ -503,7 +533,7 @@ DGI bool body_b64(S &src, uint32_t s0, uint32_t n, bool last, O &o)
  * 2 = header and length written, the body (> FL_INLINE bytes of a string
  * without escapes or of canonical base64) is left to chunk tasks. */
 template <class S, class O>
-DGI uint32_t flat_write(S &src, const FField &F, const FastTabs &tb, O &o)
+DGI uint32_t flat_write(S &src, const FField &F, const FastTabs &tb, O &o, lds_esc *E, uint32_t ne)
 {
     typedef typename S::idx SI;
     if (F.kind == FV_NONE) return 1;
@@ -527,7 +557,24 @@ DGI uint32_t flat_write(S &src, const FField &F, const FastTabs &tb, O &o)
     case FV_NUMSTR:
     case FV_STR:
         o.w32(F.kind == FV_NUMSTR ? F.nb : F.size - 7);
-        if (F.esc) return fast_unquote(src, (SI)F.s0, (SI)F.nb, o) ? 1u : 0u;
+        if (F.esc) { /* runs copied around the escapes (decoded in the structure phase), in position order */
+            uint32_t cur = F.s0;
+            const uint32_t end = F.s0 + F.nb;
+            for (uint32_t it = 0; it < FL_NESC; it++) {
+                uint64_t best = ~0ull;
+                for (uint32_t e = 0; e < ne; e++) {
+                    const uint32_t p = (uint32_t)E[e] & 0xFFF;
+                    if (p >= cur && p < end && p < ((uint32_t)best & 0xFFF)) best = E[e];
+                }
+                if (best == ~0ull) break;
+                const uint32_t p = (uint32_t)best & 0xFFF;
+                body_copy(src, cur, p - cur, o);
+                o.wle(best >> 32, (uint32_t)(best >> 16) & 0x7);
+                cur = p + ((uint32_t)(best >> 12) & 0xF);
+            }
+            body_copy(src, cur, end - cur, o);
+            return 1;
+        }
         if (F.nb > FL_INLINE) return 2;
         body_copy(src, F.s0, F.nb, o);
         return 1;
@@ -612,23 +659,16 @@ struct FlatLds {
     uint32_t big[FL_MPB];                   /* listed for the wave kernel */
     uint32_t nbytes[FL_MPB];                /* Thrift bytes before STOP */
     uint32_t wid[FL_MPB];                   /* wrapped mode: 0x10000 | the outer field's id, 0 = not wrapped */
-    uint32_t ostg[FL_MPB];                  /* the message's output is staged in LDS (ost) */
-    alignas(8) uint32_t sep[FL_MAXF * FL_MPB]; /* [k][m]: comma position | quotes before it << 16 */
+    uint32_t nesc[FL_MPB];                  /* escapes found in the message (phase 1) */
+    uint64_t esc[FL_MPB * FL_NESC];         /* [m][e]: position | in_len << 12 | out_len << 16 | UTF-8 bytes << 32 */
+    uint32_t sep[FL_MAXF * FL_MPB];         /* [k][m]: comma position | quotes before it << 16 */
     uint16_t col[FL_MAXF * FL_MPB];         /* [k][m]: colon position */
-    uint8_t ost_pad[FL_MPB * FL_OSTRIDE - (FL_MAXF * FL_MPB) * 6]; /* sep + col + this = the output stage */
     uint16_t size[2 * FL_SLOTS * FL_MPB];   /* [round & 1][slot][m] */
     uint32_t rounds, ntask;
     uint64_t p10u[20];
     double p10d[23];
     uint64_t pw[EL_WN];                     /* Eisel-Lemire powers window (j2t_fast.h) */
 };
-
-static_assert(offsetof(FlatLds, size) - offsetof(FlatLds, sep) >= FL_MPB * FL_OSTRIDE, "output stage");
-/* message m's output stage (valid after the round-0 size barrier) */
-DGI __attribute__((address_space(3))) uint8_t *fl_ost(FlatLds &L, uint32_t m)
-{
-    return (__attribute__((address_space(3))) uint8_t *)(void *)L.sep + m * FL_OSTRIDE;
-}
 
 template <int V>
 __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(DG_FL_WPE))) void j2t_flat_kernel(
@@ -716,6 +756,7 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
         L.phi[tid] = 0;
         L.oc[tid] = 0;
         L.nfq[tid] = 0;
+        L.nesc[tid] = 0;
     }
     __syncthreads();
     const uint32_t g = tid & 3, m1 = tid >> 2; /* phase 1: 4 lanes per message */
@@ -891,7 +932,22 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
             const uint64_t B = ((uint64_t)bh << 32 | bl) & vmask, QB = Q | B;
             const uint32_t nxt = g4_next((uint32_t)(QB & 1), g); /* the next lane's first byte */
             const uint64_t bb = B & ((QB >> 1) | ((uint64_t)nxt << 63));
-            bad = g4_sum(bb ? 1u : 0u);
+            /* decode this lane's escapes into the message's table (an escape
+             * may run into the next lane's bytes: read from the stage) */
+            uint32_t ebad = 0;
+            if (on && !bb && B) {
+                LSrc es;
+                es.init((const __attribute__((address_space(3))) uint64_t *)(void *)&L.in[lw], (int32_t)a7, (int32_t)n);
+                for (uint64_t eb = B; eb; eb &= eb - 1) {
+                    const uint32_t p = 64 * g + (uint32_t)__builtin_ctzll(eb);
+                    const uint64_t x = fl_escape(p, es.get8((int32_t)p));
+                    const uint32_t idx = atomicAdd(&L.nesc[m1], 1u);
+                    if (!x || p + ((uint32_t)(x >> 12) & 0xF) > n) ebad = 1;
+                    else if (idx < FL_NESC) L.esc[m1 * FL_NESC + idx] = x;
+                    else ebad = 1;
+                }
+            }
+            bad = g4_sum((bb ? 1u : 0u) | ebad);
         }
         if (on) {
             uint32_t ci = (pin & 0x3FF) - nc, ki = ((pin >> 10) & 0x3FF) - nk;
@@ -951,6 +1007,8 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
         src.init((const __attribute__((address_space(3))) uint64_t *)(void *)&L.in[lwa >> 3], (int32_t)(lwa & 7), (int32_t)L.n[mm]);
         const uint32_t rounds = L.rounds;
         uint32_t nbytes = 0;
+        lds_esc *E = (lds_esc *)(void *)&L.esc[mm * FL_NESC];
+        const uint32_t ne = min(L.nesc[mm], FL_NESC);
 #ifdef DG_FLPROF_G
         uint64_t flg[8] = {0, 0, 0, 0, 0, 0, 0, __builtin_amdgcn_s_memtime()};
 #endif
@@ -968,7 +1026,7 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
                 }
                 const uint32_t ck = L.col[k * FL_MPB + mm];
                 FLG(0);
-                if (!(ck >= sk && ck < ek && fl_field(D, sd, src, sk, ck, ek, q1 - q0, hasbs, k, P.flag, tb, F FLG_PASS))) {
+                if (!(ck >= sk && ck < ek && fl_field(D, sd, src, sk, ck, ek, q1 - q0, hasbs, E, ne, k, P.flag, tb, F FLG_PASS))) {
                     L.ok[mm] = 0;
                     F.size = 0;
                     F.kind = FV_NONE;
@@ -981,22 +1039,15 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
             }
         };
         /* 0 = error, 1 = written, 2 = the body is left to chunk tasks */
-        auto write = [&](const FField &F, uint32_t off, bool stg) -> uint32_t {
+        auto write = [&](const FField &F, uint32_t off) -> uint32_t {
             if (!F.size) return 1;
             if (off + F.size >= cap) return 0; /* the slot holds the field and STOP */
-            if (stg) { /* into the message's LDS stage */
-                WOutT<3> o;
-                o.init(fl_ost(L, mm) + off);
-                const uint32_t wr = flat_write(src, F, tb, o);
-                o.finish();
-                return wr;
-            }
             WOut o;
             o.init(slot + off);
 #ifdef DG_FL_ABL_NOSTORE
             o.dry = true; /* ablation (timing only): the field stores are not issued */
 #endif
-            const uint32_t wr = flat_write(src, F, tb, o);
+            const uint32_t wr = flat_write(src, F, tb, o, E, ne);
             o.finish();
             return wr;
         };
@@ -1027,15 +1078,11 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
                 tot += v;
             }
             nbytes += tot;
-            /* one round: the whole message (+ STOP, + the outer STOP when
-             * wrapped) fits its stage -- every wave decides the same */
-            const bool stg = DG_FL_OSTAGE && rounds == 1 && nbytes + 2 <= FL_OSTRIDE;
-            if (wave == 0) L.ostg[mm] = stg ? 1u : 0u;
             uint32_t wr[FL_FPW], nch[FL_FPW], nsum = 0, good = 1;
 #pragma unroll
             for (uint32_t h = 0; h < FL_FPW; h++) {
                 FLF_T0();
-                wr[h] = write(F[h], off[h], stg);
+                wr[h] = write(F[h], off[h]);
                 FLF_ADD(6 + r * FL_SLOTS + fl_slot(wave, h));
                 nch[h] = wr[h] == 2 ? (F[h].nb + FL_CHUNK - 1) / FL_CHUNK : 0u;
                 nsum += nch[h];
@@ -1094,23 +1141,15 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
             const uint32_t lwa = L.lw[m];
             LSrc src;
             src.init((const __attribute__((address_space(3))) uint64_t *)(void *)&L.in[lwa >> 3], (int32_t)(lwa & 7), (int32_t)L.n[m]);
-            bool cok = true;
-            if (L.ostg[m]) {
-                WOutT<3> o;
-                o.init(fl_ost(L, m) + (uint32_t)(tk >> 32));
-                if ((tk >> 6) & 1) cok = body_b64(src, s0, cn, ((tk >> 7) & 1) != 0, o);
-                else body_copy(src, s0, cn, o);
-                o.finish();
-            } else {
-                WOut o;
-                o.init((gu8 *)(void *)(P.out + L.oa[m] + (uint32_t)(tk >> 32)));
+            WOut o;
+            o.init((gu8 *)(void *)(P.out + L.oa[m] + (uint32_t)(tk >> 32)));
 #ifdef DG_FL_ABL_NOSTORE
-                o.dry = true;
+            o.dry = true;
 #endif
-                if ((tk >> 6) & 1) cok = body_b64(src, s0, cn, ((tk >> 7) & 1) != 0, o);
-                else body_copy(src, s0, cn, o);
-                o.finish();
-            }
+            bool cok = true;
+            if ((tk >> 6) & 1) cok = body_b64(src, s0, cn, ((tk >> 7) & 1) != 0, o);
+            else body_copy(src, s0, cn, o);
+            o.finish();
             if (!cok) L.ok[m] = 0;
         }
     }
@@ -1141,66 +1180,23 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
                     }
                 }
             }
-            const bool stg = L.ostg[m] != 0;
-            uint32_t flen = 0; /* staged bytes to flush */
             if (good && wid) {
                 /* the outer field header, the inner STOP, the outer STOP */
                 gu8 *o = (gu8 *)(void *)P.out + L.oa[m];
                 o[-3] = DG_T_STRUCT;
                 o[-2] = (uint8_t)(wid >> 8);
                 o[-1] = (uint8_t)wid;
-                if (stg) {
-                    fl_ost(L, m)[len - 1] = 0;
-                    fl_ost(L, m)[len] = 0;
-                    flen = len + 1;
-                } else {
-                    o[len - 1] = 0;
-                    o[len] = 0;
-                }
+                o[len - 1] = 0;
+                o[len] = 0;
                 P.ret[i] = 0;
                 P.out_len[i] = len + 4;
             } else if (good) {
-                if (stg) {
-                    fl_ost(L, m)[len - 1] = 0;
-                    flen = len;
-                } else {
-                    ((gu8 *)(void *)P.out)[L.oa[m] + len - 1] = 0; /* STOP */
-                }
+                ((gu8 *)(void *)P.out)[L.oa[m] + len - 1] = 0; /* STOP */
                 P.ret[i] = 0;
                 P.out_len[i] = len;
             } else if (!L.big[m]) {
                 const uint32_t qq = atomicAdd(S.bail_count, 1u);
                 S.bail_list[qq] = (uint32_t)i;
-            }
-            L.nbytes[m] = flen;
-        } else {
-            L.nbytes[m] = 0;
-        }
-    }
-    /* ---- 5. flush the staged messages: 8 lanes per message, each an
-     *      8-byte destination word at a time (byte-exact at both ends), so
-     *      a wave's store covers 8 messages x 64 contiguous bytes ---- */
-    __syncthreads();
-    {
-        const uint32_t j = tid & 7;
-        for (uint32_t m = tid >> 3; m < FL_MPB; m += 64 * FL_WAVES / 8) {
-            const uint32_t flen = L.nbytes[m];
-            if (!flen) continue;
-            const uintptr_t d0 = (uintptr_t)(P.out + L.oa[m]), wb = d0 & ~(uintptr_t)7;
-            const uint32_t lead = (uint32_t)(d0 - wb), nw = (lead + flen + 7) >> 3;
-            const __attribute__((address_space(3))) uint64_t *sw =
-                (const __attribute__((address_space(3))) uint64_t *)fl_ost(L, m);
-            for (uint32_t k = j; k < nw; k += 8) {
-                /* stage bytes [8k - lead, 8k - lead + 8) */
-                const int32_t so = (int32_t)(8 * k) - (int32_t)lead;
-                uint64_t v;
-                if (so < 0) v = sw[0] << (8 * lead);
-                else if ((so & 7) == 0) v = sw[so >> 3];
-                else v = (sw[so >> 3] >> (8 * (so & 7))) | (sw[(so >> 3) + 1] << (64 - 8 * (so & 7)));
-                const uint32_t lo = k == 0 ? lead : 0u, hi = lead + flen - 8 * k < 8 ? lead + flen - 8 * k : 8u;
-                gu8 *w = (gu8 *)(void *)(wb + 8 * (uintptr_t)k);
-                if (lo == 0 && hi == 8) *(gu64 *)w = v;
-                else store_part(w, v, lo, hi);
             }
         }
     }

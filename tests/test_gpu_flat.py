@@ -237,3 +237,39 @@ def test_flat_task_cap_path():
         assert len(m) <= 256
         msgs.append(m)
     assert not _compare(fl, msgs, 0x1 | FLAT)
+
+
+def test_flat_escape_table_vs_oracle():
+    """The structure phase's escape table (j2t_flat.h fl_escape): every simple
+    escape, \\u of 1, 2 and 3 UTF-8 bytes (upper/lower-case hex), escapes at
+    a string's start and end, next to each other, up to FL_NESC (4) per
+    message and beyond it, in keys, in numbers' js_conv text, in binary
+    fields, invalid ones and surrogates (declined to the list pass): the
+    bytes and status words of the reference. Escapes the table keeps stay on
+    the flat kernel (no bail)."""
+    rng = random.Random(77)
+    td = W.simple_desc()
+    fl = T.flatten(td)
+    pieces = ["a", "Z9", "\\n", "\\t", "\\r", "\\b", "\\f", "\\/", "\\u0041", "\\u00e9", "\\u00E9", "\\u07ff",
+              "\\u0800", "\\u4e2d", "\\uFFFF", "\\u0000", "é"]
+    keep = []
+    for _ in range(3000):
+        body = "".join(rng.choice(pieces) for _ in range(rng.randint(0, 7)))
+        keep.append(('{"ByteField":%d,"StringField":"%s","I32Field":%d}' %
+                     (rng.randint(-128, 127), body, rng.randint(-2**31, 2**31 - 1))).encode())
+    ok = [m for m in keep if m.count(b"\\") <= 4]
+    ctx = conv.default_context()
+    ctx.stats(reset=True)
+    outs, rets = _raw_batch(fl, ok, 0x1 | FLAT)
+    bails, _ = ctx.stats(reset=True)
+    assert bails == 0, bails
+    assert not _compare(fl, ok, 0x1 | FLAT)
+    odd = [b'{"StringField":"\\ud83d\\ude00"}', b'{"StringField":"\\ud83d"}', b'{"StringField":"\\x"}',
+           b'{"StringField":"\\u12"}', b'{"StringField":"\\u12G4"}', b'{"StringField":"ab\\',
+           b'{"Str\\u0069ngField":"k"}', b'{"StringField":"\\n\\n\\n\\n\\n"}', b'{"BinaryField":"QQ\\u003d="}',
+           b'{"I32Field":1\\n}', b'{"StringField":"\\u002"}', b'{"StringField":"\\n","StringField":"\\t\\b\\f\\r"}',
+           b'{"StringField":"' + b"\\u00e9" * 4 + b'"}', b'{"StringField":"' + b"\\u00e9" * 5 + b'"}']
+    for flags in (0x1, 0x11, 0x7):
+        for extra in (FLAT, NO_FLAT):
+            bad = _compare(fl, keep + odd, flags | extra)
+            assert not bad, (hex(flags), extra, bad[:4])
