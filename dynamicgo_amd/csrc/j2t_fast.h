@@ -153,10 +153,16 @@ DGI uint64_t swar_val(uint64_t x, uint32_t t)
  * `if (man_nd < 19)` digit cap); returns t */
 DGI uint32_t acc_digits(uint64_t &man, int &nd, uint64_t x, uint32_t k, const FastTabs &tb)
 {
+    (void)tb;
     uint32_t room = (uint32_t)(19 - nd);
     uint32_t t = k < room ? k : room;
     if (t) {
-        man = man * tb.p10u[t] + swar_val(x, t);
+        /* 10^t (t <= 8) in registers: 32-bit, so man * p is one 64x32 product */
+        uint32_t p = (t & 1) ? 10u : 1u;
+        p = (t & 2) ? p * 100u : p;
+        p = (t & 4) ? p * 10000u : p;
+        p = (t & 8) ? 100000000u : p;
+        man = man * (uint64_t)p + swar_val(x, t);
         nd += (int)t;
     }
     return t;
@@ -232,14 +238,16 @@ DGI bool fast_vnumber(S &src, SI &p, const FastTabs &tb, int64_t &iv, double &dv
         }
         nd = 0;
     }
-    while (nd < 19) { /* fraction digits up to the cap */
+    /* without a '.', the integer loop stopped at a non-digit: the two loops
+     * below would read no digit */
+    while (dbl && nd < 19) { /* fraction digits up to the cap */
         uint32_t k = digits8(src, i, x);
         uint32_t t = acc_digits(man, nd, x, k, tb);
         exp10 -= (int)t;
         i += t;
         if (t < 8) break;
     }
-    for (;;) { /* digits beyond the cap */
+    while (dbl) { /* digits beyond the cap */
         uint32_t k = digits8(src, i, x);
         if (k) trunc = true;
         i += k;

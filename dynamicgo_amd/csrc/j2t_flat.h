@@ -664,7 +664,7 @@ struct FlatLds {
     uint32_t sep[FL_MAXF * FL_MPB];         /* [k][m]: comma position | quotes before it << 16 */
     uint16_t col[FL_MAXF * FL_MPB];         /* [k][m]: colon position */
     uint16_t size[2 * FL_SLOTS * FL_MPB];   /* [round & 1][slot][m] */
-    uint32_t rounds, ntask;
+    uint32_t rounds, ntask, tgrab;
     uint64_t p10u[20];
     double p10d[23];
     uint64_t pw[EL_WN];                     /* Eisel-Lemire powers window (j2t_fast.h) */
@@ -721,6 +721,7 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
     if (tid == 0) {
         L.rounds = 0;
         L.ntask = 0;
+        L.tgrab = 0;
     }
     if (tid < FL_MPB) {
         uint32_t ok = 0, n = 0, lw = 0, big = 0, cap = 0;
@@ -1078,19 +1079,22 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
                 tot += v;
             }
             nbytes += tot;
-            uint32_t wr[FL_FPW], nch[FL_FPW], nsum = 0, good = 1;
+            /* bodies of more than FL_INLINE bytes (a string without escapes,
+             * canonical base64) are left to chunk tasks of FL_CHUNK input
+             * bytes: reserved before the writes (one LDS atomic per wave,
+             * lane 63 reserves the wave's total), so that after the last
+             * round's barrier every wave takes tasks as soon as its own
+             * writes are done -- no barrier between the writes and the
+             * tasks (a task owns its body bytes, the header's wave the rest) */
+            uint32_t nch[FL_FPW], nsum = 0, good = 1;
 #pragma unroll
             for (uint32_t h = 0; h < FL_FPW; h++) {
-                FLF_T0();
-                wr[h] = write(F[h], off[h]);
-                FLF_ADD(6 + r * FL_SLOTS + fl_slot(wave, h));
-                nch[h] = wr[h] == 2 ? (F[h].nb + FL_CHUNK - 1) / FL_CHUNK : 0u;
+                const FField &G = F[h];
+                const bool body = G.kind == FV_BIN || ((G.kind == FV_STR || G.kind == FV_NUMSTR) && !G.esc);
+                nch[h] = body && G.nb > FL_INLINE && off[h] + G.size < cap ? (G.nb + FL_CHUNK - 1) / FL_CHUNK : 0u;
                 nsum += nch[h];
-                good &= wr[h] != 0;
             }
             {
-                /* bodies left to chunk tasks of FL_CHUNK input bytes: one LDS
-                 * atomic per wave (lane 63 reserves the wave's total) */
                 const uint32_t incl = wave_incl_sum(nsum, lane);
                 const uint32_t wtot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
                 if (wtot) {
@@ -1120,6 +1124,14 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
                     }
                 }
             }
+            if (r + 1 == rounds) __syncthreads(); /* the task list is complete */
+#pragma unroll
+            for (uint32_t h = 0; h < FL_FPW; h++) {
+                FLF_T0();
+                const uint32_t wr = write(F[h], off[h]);
+                FLF_ADD(6 + r * FL_SLOTS + fl_slot(wave, h));
+                good &= wr != 0;
+            }
             if (!good) L.ok[mm] = 0;
             FLP(6);
         }
@@ -1130,13 +1142,18 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
 #endif
     }
     FLP(6);
-    __syncthreads();
-    /* ---- 3b. chunk tasks: long string / base64 bodies, spread over the block ---- */
+    /* ---- 3b. chunk tasks: long string / base64 bodies, taken 64 at a time
+     *      by the waves as they finish their writes ---- */
     {
         const uint32_t nt = min(L.ntask, FL_MAXTASK);
-        for (uint32_t t = tid; t < nt; t += 64 * FL_WAVES) {
-            const uint64_t tk = L.task[t];
-            if (tk == ~0ull) continue; /* a declined message's slot */
+        for (;;) {
+            uint32_t t0 = 0;
+            if (lane == 0) t0 = atomicAdd(&L.tgrab, 64u);
+            t0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)t0);
+            if (t0 >= nt) break;
+            const uint32_t t = t0 + lane;
+            const uint64_t tk = t < nt ? L.task[t] : ~0ull;
+            if (tk == ~0ull) continue; /* past the list, or a declined message's slot */
             const uint32_t m = (uint32_t)tk & 63, s0 = (uint32_t)(tk >> 8) & 0xFFF, cn = (uint32_t)(tk >> 20) & 0xFFF;
             const uint32_t lwa = L.lw[m];
             LSrc src;

@@ -205,6 +205,90 @@ DGI void store_part_as(__attribute__((address_space(AS))) uint8_t *w, uint64_t v
 }
 DGI void store_part(gu8 *w, uint64_t v, uint32_t lo, uint32_t hi) { store_part_as<1>(w, v, lo, hi); }
 
+#ifndef DG_UNALIGNED_OUT
+#define DG_UNALIGNED_OUT 1
+#endif
+#if DG_UNALIGNED_OUT
+/* A writer that owns exactly [start, start + written): every 8 bytes as one
+ * unaligned 8-byte store (the HSA code object runs the memory pipeline in
+ * unaligned mode: a dwordx2 store at any byte address writes exactly those
+ * 8 bytes), the last 1..7 as 4/2/1-byte stores. No aligned-word edge
+ * bookkeeping, and neighbouring tokens written by other lanes or waves are
+ * never touched, so they can write concurrently. AS: the address space. */
+typedef uint64_t __attribute__((aligned(1))) u64_a1;
+typedef uint32_t __attribute__((aligned(1))) u32_a1;
+typedef uint16_t __attribute__((aligned(1))) u16_a1;
+template <int AS>
+DGI void store_tail_as(__attribute__((address_space(AS))) uint8_t *p, uint64_t v, uint32_t n) /* n < 8 bytes */
+{
+    if (n & 4) {
+        *(__attribute__((address_space(AS))) u32_a1 *)p = (uint32_t)v;
+        p += 4;
+        v >>= 32;
+    }
+    if (n & 2) {
+        *(__attribute__((address_space(AS))) u16_a1 *)p = (uint16_t)v;
+        p += 2;
+        v >>= 16;
+    }
+    if (n & 1) *p = (uint8_t)v;
+}
+template <int AS>
+struct WOutT {
+    typedef __attribute__((address_space(AS))) uint8_t b8;
+    typedef __attribute__((address_space(AS))) u64_a1 b64u;
+    b8 *p;         /* the next byte stored */
+    uint32_t used; /* bytes held in wbuf */
+    uint64_t wbuf;
+    uint64_t len;  /* bytes written */
+    bool dry;      /* count only (lengths before the offsets are known) */
+    DGI void init(b8 *q)
+    {
+        p = q;
+        used = 0;
+        wbuf = 0;
+        len = 0;
+        dry = false;
+    }
+    DGI void init_dry()
+    {
+        p = nullptr;
+        used = 0;
+        wbuf = 0;
+        len = 0;
+        dry = true;
+    }
+    DGI void wle(uint64_t v, uint32_t n)
+    {
+        if (dry) {
+            len += n;
+            return;
+        }
+        if (n < 8) v &= (1ull << (n << 3)) - 1;
+        const uint32_t sh = used << 3;
+        const uint64_t lo_w = wbuf | (v << sh);
+        const uint64_t hi_w = used ? (v >> (64 - sh)) : 0;
+        len += n;
+        if (used + n >= 8) {
+            *(b64u *)p = lo_w;
+            p += 8;
+            wbuf = hi_w;
+            used = used + n - 8;
+        } else {
+            wbuf = lo_w;
+            used += n;
+        }
+    }
+    DGI void w8(uint8_t v) { wle(v, 1); }
+    DGI void w16(uint16_t v) { wle(__builtin_bswap16(v), 2); }
+    DGI void w32(uint32_t v) { wle(__builtin_bswap32(v), 4); }
+    DGI void w64(uint64_t v) { wle(__builtin_bswap64(v), 8); }
+    DGI void finish()
+    {
+        if (!dry && used) store_tail_as<AS>(p, wbuf, used);
+    }
+};
+#else
 /* A writer that owns exactly [start, start + written): whole aligned words
  * inside the range are stored as 8-byte words, the partial words at both
  * ends byte-exactly, so neighbouring tokens can write concurrently. AS: the
@@ -269,6 +353,7 @@ struct WOutT {
         if (!dry && used > lo) store_part_as<AS>(wa, wbuf, lo, used);
     }
 };
+#endif
 typedef WOutT<1> WOut;
 
 /* big-endian u32 at an arbitrary byte address, byte-exact */
@@ -365,10 +450,21 @@ DGI int32_t wv_lookup(const DV &D, const dg_struct &sd, S &src, int64_t k0, uint
 }
 
 /* src[s0, s0+nb) -> dst, by the 64 lanes of the wave: lane l stores the
- * 8-aligned destination words l, l+64, ... (partial end words byte-exactly) */
+ * destination bytes [8l, 8l+8), [8l+512, ...) (unaligned 8-byte stores, the
+ * last partial one byte-exactly) */
 template <class S>
 DGI void coop_copy(S &src, int64_t s0, int64_t nb, gu8 *dst, uint32_t lane)
 {
+#if DG_UNALIGNED_OUT
+    const int64_t nw = (nb + 7) >> 3;
+    for (int64_t k = lane; k < nw; k += 64) {
+        const int64_t off = k * 8, rem = nb - off;
+        const uint64_t v = src.get8(s0 + off);
+        gu8 *w = dst + off;
+        if (rem >= 8) *(__attribute__((address_space(1))) u64_a1 *)w = v;
+        else store_tail_as<1>(w, v, (uint32_t)rem);
+    }
+#else
     const uintptr_t da = (uintptr_t)(void *)dst, wb = da & ~(uintptr_t)7;
     const uint32_t lead = (uint32_t)(da - wb);
     const int64_t nw = (int64_t)(lead + nb + 7) >> 3;
@@ -382,6 +478,7 @@ DGI void coop_copy(S &src, int64_t s0, int64_t nb, gu8 *dst, uint32_t lane)
         if (lo == 0 && hi == 8) *(gu64 *)w = v;
         else store_part(w, v, lo, hi);
     }
+#endif
 }
 
 

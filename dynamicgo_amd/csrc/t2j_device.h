@@ -384,6 +384,130 @@ DGI int32_t t2j_field(const DV &D, const dg_struct &sd, uint32_t hint, uint16_t 
     return -1;
 }
 
+#ifndef DG_T2J_GROUPS
+#define DG_T2J_GROUPS 0
+#endif
+#if DG_T2J_GROUPS
+/* JSON output of one lane: Out's 8-byte word assembly, completed words held
+ * in registers until the 64-byte aligned group they belong to is complete,
+ * then stored as four 16-byte stores issued together. 64 lanes writing 64
+ * slots 16 bytes at a time left L2 lines partly written long enough to be
+ * written back more than once (t2j-c2: 24.5 MB written for 13.6 MB of JSON
+ * and status words); whole groups staged through LDS wrote 16.6 MB but cost
+ * 14 % of the kernel (r4o/r4p). Here the group is 8 named registers shifted
+ * one word per completed word (constant register indices: no scratch). */
+struct JOut {
+    typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+    gu8 *b;
+    uint64_t cap;
+    uint64_t len;
+    uint64_t wbuf;  /* the word holding position len */
+    uint64_t g0, g1, g2, g3, g4, g5, g6, g7; /* the open group's completed words, newest in g7 */
+    uint32_t gb;    /* the slot's first word's position in its 64-byte group (0..7) */
+    bool wide;      /* slot base 8-aligned: word and 16-byte stores allowed */
+
+    DGI void init(uint8_t *base, uint64_t c)
+    {
+        b = (gu8 *)(void *)base;
+        cap = c;
+        len = 0;
+        wbuf = 0;
+        g0 = g1 = g2 = g3 = g4 = g5 = g6 = g7 = 0;
+        wide = ((uintptr_t)base & 7) == 0;
+        gb = wide ? (uint32_t)(((uintptr_t)base >> 3) & 7) : 0u;
+    }
+    DGI void store_word(uint64_t wi, uint64_t v)
+    {
+        const uint64_t a = wi << 3;
+        if (wide && a + 8 <= cap) *(gu64 *)(b + a) = v;
+        else if (a < cap) Out::store_bytes(b, a, cap, v);
+    }
+    DGI uint64_t load_word(uint64_t wi) const
+    {
+        const uint64_t a = wi << 3;
+        if (wide && a + 8 <= cap) return *(const gu64 *)(b + a);
+        return a < cap ? Out::load_bytes(b, a, cap) : 0;
+    }
+    /* the open group's newest k words (k <= 8) end at word e (exclusive):
+     * word e - k + m = g_{8-k+m}; words before the slot or past cap are not
+     * written */
+    static __device__ __noinline__ void group_edge(gu8 *b, uint64_t cap, bool wide, int64_t e, uint32_t k,
+                                                   uint64_t x0, uint64_t x1, uint64_t x2, uint64_t x3, uint64_t x4,
+                                                   uint64_t x5, uint64_t x6, uint64_t x7)
+    {
+        const uint64_t g[8] = {x0, x1, x2, x3, x4, x5, x6, x7};
+        for (uint32_t m = 8 - k; m < 8; m++) {
+            const int64_t wi = e - 8 + (int64_t)m;
+            if (wi < 0) continue;
+            const uint64_t a = (uint64_t)wi << 3;
+            if (wide && a + 8 <= cap) *(gu64 *)(b + a) = g[m];
+            else if (a < cap) Out::store_bytes(b, a, cap, g[m]);
+        }
+    }
+    DGI void wle(uint64_t v, uint32_t n)
+    {
+        const uint32_t used = (uint32_t)(len & 7);
+        const uint32_t sh = used << 3;
+        if (n < 8) v &= (1ull << (n << 3)) - 1;
+        const uint64_t lo = (wbuf & ((1ull << sh) - 1)) | (v << sh);
+        const uint64_t hi = used ? (v >> (64 - sh)) : 0;
+        const uint64_t wi = len >> 3;
+        len += n;
+        if (used + n >= 8) {
+            g0 = g1;
+            g1 = g2;
+            g2 = g3;
+            g3 = g4;
+            g4 = g5;
+            g5 = g6;
+            g6 = g7;
+            g7 = lo;
+            if (((gb + (uint32_t)wi) & 7) == 7) { /* the group is complete */
+                if (wide && wi >= 7 && (wi + 1) * 8 <= cap) {
+                    __attribute__((address_space(1))) u64x2 *q =
+                        (__attribute__((address_space(1))) u64x2 *)(void *)(b + (wi - 7) * 8); /* 64-byte aligned */
+                    u64x2 p0, p1, p2, p3;
+                    p0.x = g0; p0.y = g1;
+                    p1.x = g2; p1.y = g3;
+                    p2.x = g4; p2.y = g5;
+                    p3.x = g6; p3.y = g7;
+                    q[0] = p0;
+                    q[1] = p1;
+                    q[2] = p2;
+                    q[3] = p3;
+                } else {
+                    group_edge(b, cap, wide, (int64_t)wi + 1, 8, g0, g1, g2, g3, g4, g5, g6, g7);
+                }
+            }
+            wbuf = hi;
+        } else {
+            wbuf = lo;
+        }
+    }
+    DGI void w8(uint8_t v) { wle(v, 1); }
+    /* truncate to x; the converter only ever truncates to 0 (a stop's
+     * record or an exception's JSON replaces the output) */
+    DGI void set_len(uint64_t x)
+    {
+        if (x == 0) {
+            len = 0;
+            wbuf = 0;
+            return;
+        }
+        finish(); /* general case (unused): flush, then read the partial word back */
+        len = x;
+        wbuf = (x & 7) ? load_word(x >> 3) : 0;
+    }
+    /* the open group's completed words, and the partial word */
+    DGI void finish()
+    {
+        const uint64_t lw = len >> 3;
+        const uint32_t k = (gb + (uint32_t)lw) & 7; /* completed words of the open group */
+        if (k) group_edge(b, cap, wide, (int64_t)lw, k, g0, g1, g2, g3, g4, g5, g6, g7);
+        if (len & 7) store_word(lw, wbuf);
+    }
+};
+#else
 /* JSON output of one lane: Out's 8-byte word assembly, with completed words
  * stored in aligned 16-byte pairs (one dwordx4 store per lane per 16 bytes,
  * the width the L2 write counters and write-back handle whole; 8-byte stores
@@ -478,6 +602,8 @@ struct JOut {
         if (len & 7) store_word(lw, wbuf);
     }
 };
+
+#endif
 
 /* side-table bytes [off, off+len) (8-aligned, 16 readable past the end) */
 DGI void emit_side(JOut &o, const T2JSide &X, uint32_t off, uint32_t len)

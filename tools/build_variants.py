@@ -12,7 +12,7 @@ for spec in sys.argv[1:]:
     out = os.path.join(b.ROOT, "dynamicgo_amd", f"libdgj2t_{name}.so")
     if all(f.startswith("-DDG_FL_") for f in fl):
         units = ("j2t_kern_flat.hip", "j2t_host.hip")
-    elif all(f.startswith("-DDG_T2W") for f in fl):
+    elif all(f.startswith(("-DDG_T2W", "-DDG_T2J")) for f in fl):
         units = ("t2j_kern.hip",)
     else:
         units = ("j2t_kern_wave.hip", "j2t_kern_wave5.hip", "j2t_host.hip", "j2t_kern_flat.hip")

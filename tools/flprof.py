@@ -40,6 +40,9 @@ _lib.check(L.dg_ctx_counters(ctx.h, cnt, 16, 1))
 reps = 5
 _lib.check(L.dg_bench_device(*args, reps, C.byref(ms)))
 _lib.check(L.dg_ctx_counters(ctx.h, cnt, 16, 1))
+if "--plain" in sys.argv:  # any build: the time only (e.g. under rocprofv3 --pmc)
+    print(f"{cfg}: {ms.value / reps * 1000:.1f} us/step")
+    sys.exit(0)
 if "--stages" in sys.argv:  # a -DDG_FLPROF_G build
     c = list(cnt)[2:8]
     waves = n // 64 // 32 * 4
