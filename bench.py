@@ -588,7 +588,25 @@ AGG_RUNS = ((16, 8192), (64, 2048), (64, 1))
 # flight each (goroutines in Do) over GATEWAY_WORKERS OS threads (the 16
 # CPUs a GPU gets) and one dg_agg_wait_gen poller; (callers, depth)
 GATEWAY_RUNS = ((1024, 2), (4096, 3), (16384, 4), (65536, 4))
+GATEWAY_FILL_DIV = 8  # min_fill = callers / 8: a batch waits for an eighth of the callers (or max_wait)
 GATEWAY_WORKERS = 16
+
+
+def agg_profile(pr, pr0, nbatches, ncalls):
+    """dg_agg_profile's counters over a run: us per batch in each stage, ns per call"""
+    pr = [pr[i] - pr0[i] for i in range(16)]
+    nb_ = max(1, nbatches)
+    prof = {k: round(pr[i] / nb_ / 1e3, 1) for i, k in enumerate(
+        ("flusher_wait_seal", "flusher_wait_free", "flusher_issue", "completer_wait_hdr", "completer_wait_data",
+         "seal_to_issued", "issued_to_done", "callers_blocked"))}
+    ncalls = max(1, ncalls)
+    prof["ns_per_call_in_submit"] = round(pr[8] / ncalls, 1)
+    prof["ns_per_call_in_wait"] = round(pr[9] / ncalls, 1)
+    prof["submits_without_open_batch"] = int(pr[10])
+    prof["calls_converted_alone"] = int(pr[11])
+    for i, k in enumerate(("issue_wait_writers", "issue_buffers", "issue_gather", "issue_convert")):
+        prof[k] = round(pr[12 + i] / nb_ / 1e3, 1)
+    return prof
 
 
 def bench_agg(args, rank, world, dev, dist, backend, td, arena, off, meta):
@@ -652,18 +670,7 @@ def bench_agg(args, rank, world, dev, dist, backend, td, arena, off, meta):
         _lib.check(L.dg_agg_stats(h, C.byref(b), C.byref(tot)))
         pr = (C.c_uint64 * 16)()
         _lib.check(L.dg_agg_profile(h, pr, 16))
-        pr = [pr[i] - pr0[i] for i in range(16)]
-        nb_ = max(1, b.value - b0.value)
-        prof = {k: round(pr[i] / nb_ / 1e3, 1) for i, k in enumerate(
-            ("flusher_wait_seal", "flusher_wait_free", "flusher_issue", "completer_wait_hdr", "completer_wait_data",
-             "seal_to_issued", "issued_to_done", "callers_blocked"))}
-        ncalls = max(1, tot.value - tot0.value)
-        prof["ns_per_call_in_submit"] = round(pr[8] / ncalls, 1)
-        prof["ns_per_call_in_wait"] = round(pr[9] / ncalls, 1)
-        prof["submits_without_open_batch"] = int(pr[10])
-        prof["calls_converted_alone"] = int(pr[11])
-        for i, k in enumerate(("issue_wait_writers", "issue_buffers", "issue_gather", "issue_convert")):
-            prof[k] = round(pr[12 + i] / nb_ / 1e3, 1)
+        prof = agg_profile(pr, pr0, b.value - b0.value, tot.value - tot0.value)
         L.dg_agg_destroy(h)
         lt = lat[:m][lat[:m] > 0].astype(np.float64) / 1e3  # every 8th call is timed (dg_agg_drive)
         runs.append({"threads": threads, "in_flight_per_thread": window, "per_thread_batch_share": per_thread,
@@ -672,7 +679,7 @@ def bench_agg(args, rank, world, dev, dist, backend, td, arena, off, meta):
                      "ms_per_step": round(wall / steps * 1e3, 3),
                      "lat_us_p50": round(float(np.percentile(lt, 50)), 1),
                      "lat_us_p99": round(float(np.percentile(lt, 99)), 1),
-                     "avg_batch": round((tot.value - tot0.value) / nb_, 1), "wall_s": round(wall, 3),
+                     "avg_batch": round((tot.value - tot0.value) / max(1, b.value - b0.value), 1), "wall_s": round(wall, 3),
                      "us_per_batch": prof})
         if ri == 0:
             value_wall, value_steps = wall, steps
@@ -698,8 +705,11 @@ def bench_agg(args, rank, world, dev, dist, backend, td, arena, off, meta):
         h = C.c_void_p()
         _lib.check(L.dg_agg_create2(ctx.h, dh, flat.root_type, flags, share, share * 256, max_wait_us, C.byref(h)))
         _lib.check(L.dg_agg_set_knob(h, b"depth", depth))
+        fill = int(os.environ.get("DG_BENCH_GW_FILL_DIV", GATEWAY_FILL_DIV))
+        if fill > 0:
+            _lib.check(L.dg_agg_set_knob(h, b"min_fill", callers // fill))
         secs = C.c_double(0)
-        st = np.zeros(4, dtype=np.uint64)
+        st = np.zeros(8, dtype=np.uint64)
         m = n
 
         def gstep():
@@ -708,23 +718,30 @@ def bench_agg(args, rank, world, dev, dist, backend, td, arena, off, meta):
                                               rets.ctypes.data, lat.ctypes.data, C.byref(secs), st.ctypes.data))
             return secs.value
         gstep()
-        b0, tot0 = C.c_uint64(0), C.c_uint64(0)
+        b0, tot0, pr0 = C.c_uint64(0), C.c_uint64(0), (C.c_uint64 * 16)()
         _lib.check(L.dg_agg_stats(h, C.byref(b0), C.byref(tot0)))
+        _lib.check(L.dg_agg_profile(h, pr0, 16))
         gsteps = max(2, args.steps // 4)
         ws = [gstep() for _ in range(gsteps)]
-        b, tot = C.c_uint64(0), C.c_uint64(0)
+        b, tot, pr = C.c_uint64(0), C.c_uint64(0), (C.c_uint64 * 16)()
         _lib.check(L.dg_agg_stats(h, C.byref(b), C.byref(tot)))
+        _lib.check(L.dg_agg_profile(h, pr, 16))
+        gprof = agg_profile(pr, pr0, b.value - b0.value, tot.value - tot0.value)
         L.dg_agg_destroy(h)
         u = meta.get("unique", n)
         bad = int(sum(1 for i in range(0, m, 97) if int(rets[i]) != 0))
         lt = lat[:m][lat[:m] > 0].astype(np.float64) / 1e3
         gw_runs.append({"callers": callers, "os_threads": GATEWAY_WORKERS, "depth": depth, "per_thread_batch_share": share,
+                        "min_fill": callers // fill if fill > 0 else 0,
                         "calls_per_step": m, "steps": gsteps, "msgs_per_s": round(m * gsteps / sum(ws)),
                         "msgs_per_s_best": round(m / min(ws)),
                         "lat_us_p50": round(float(np.percentile(lt, 50)), 1),
                         "lat_us_p99": round(float(np.percentile(lt, 99)), 1),
                         "avg_batch": round((tot.value - tot0.value) / max(1, b.value - b0.value), 1),
-                        "parks": int(st[0]), "retries": int(st[1]), "sampled_nonzero_status": bad})
+                        "parks": int(st[0]), "retries": int(st[1]), "sampled_nonzero_status": bad,
+                        "worker_ns_per_call": {k: round(int(st[4 + i]) / max(1, m), 1) for i, k in
+                                               enumerate(("in_wait", "in_submit", "idle", "all"))},
+                        "us_per_batch": gprof})
     main = runs[0]
     json_bytes = int(off[-1])
     stats = torch.tensor([value_wall, float(json_bytes), float(n)], dtype=torch.float64,

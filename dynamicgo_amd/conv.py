@@ -776,7 +776,8 @@ class Aggregator:
         with one call in flight each -- goroutines in Do -- multiplexed over
         `workers` OS threads, woken per converted generation by one poller
         (dg_agg_wait_gen). Returns (outputs, statuses, latency ns of every 8th
-        message, wall seconds, stats [parks, retries, wake-ups, callers])."""
+        message, wall seconds, stats [parks, retries, wake-ups, callers, worker ns in
+        wait, in submit, idle, in all])."""
         n = len(msgs)
         lens = np.fromiter((len(m) for m in msgs), dtype=np.uint64, count=n)
         in_off = np.zeros(n + 1, dtype=np.uint64)
@@ -788,7 +789,7 @@ class Aggregator:
         out_len = np.zeros(max(n, 1), dtype=np.uint64)
         rets = np.zeros(max(n, 1), dtype=np.uint64)
         lat = np.zeros(max(n, 1), dtype=np.uint32)
-        st = np.zeros(4, dtype=np.uint64)
+        st = np.zeros(8, dtype=np.uint64)
         secs = C.c_double(0)
         _lib.check(_lib.lib().dg_agg_gateway_drive(self.h, arena.ctypes.data, in_off.ctypes.data, n, workers, callers,
                                                    out.ctypes.data, out_off.ctypes.data, out_len.ctypes.data,

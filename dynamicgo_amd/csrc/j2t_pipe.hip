@@ -256,7 +256,7 @@ constexpr int AGG_SHARED = 32;  /* the last AGG_SHARED parts are shared: a threa
 constexpr int AGG_EXCL = AGG_SLOTS - AGG_SHARED;
 constexpr int AGG_GEN_RING = 64; /* dg_agg_gateway_drive: parked callers by generation (> AGG_RING_MAX + 2) */
 constexpr int AGG_EAGER_INFLIGHT = 1;
-constexpr uint64_t AGG_EXACT_MAX = 64ull << 20; /* launch(): per-batch buffers sized for the parts' caps up to this */
+constexpr uint64_t AGG_EXACT_MAX = 512ull << 20; /* launch(): per-batch buffers sized for the parts' caps up to this (64 MiB: gateway parts of 4096 calls grew buffers batch after batch, 332 us per batch, r5y) */
 
 /* one caller thread's part of one batch (its own cache lines) */
 struct alignas(128) Sub {
@@ -326,6 +326,20 @@ struct dg_agg {
      * are converting -- the policy for callers that do not block in
      * dg_agg_wait (goroutines parked on a channel, an event loop) */
     std::atomic<int> depth{0};
+    /* min_fill > 0 (knob "min_fill"): the depth rule seals only a batch that
+     * holds at least this many calls (else max_wait or a full part does);
+     * many callers with one call each refill a batch over a pipeline round
+     * trip, and sealing at once made batches too small to fill the ring's
+     * round trip (r5y: 65536 callers, 4428-call batches, the flusher waiting
+     * 536 us a batch for a free one) */
+    std::atomic<uint32_t> min_fill{0};
+    uint64_t open_calls(const Batch *x) const
+    {
+        uint64_t k = 0;
+        const int ns = nparts();
+        for (int s = 0; s < ns; s++) k += x->sub[s].n.load(std::memory_order_relaxed);
+        return k;
+    }
     /* every generation <= done_upto is converted and readable (the completer
      * finishes batches in generation order); dg_agg_wait_gen blocks on it */
     std::atomic<uint64_t> done_upto{0};
@@ -541,7 +555,12 @@ void dg_agg::run_flusher()
                 if (x->seal_req.load(std::memory_order_acquire)) break;
                 const uint64_t t0 = x->t_first.load(std::memory_order_acquire);
                 const int dp = depth.load(std::memory_order_relaxed);
-                if (dp > 0 && t0 && !stop && busy_batches.load(std::memory_order_seq_cst) < dp) break;
+                bool poll = false; /* the depth rule waits for min_fill calls: look again shortly */
+                if (dp > 0 && t0 && !stop && busy_batches.load(std::memory_order_seq_cst) < dp) {
+                    const uint32_t mf = min_fill.load(std::memory_order_relaxed);
+                    if (!mf || open_calls(x) >= mf) break;
+                    poll = true;
+                }
                 if (stop) {
                     if (!t0) {
                         inflight.push_back(nullptr); /* the completer's exit marker */
@@ -554,7 +573,8 @@ void dg_agg::run_flusher()
                 if (t0) {
                     const uint64_t now = now_ns();
                     if (now - t0 >= (uint64_t)max_wait.count()) break;
-                    cv_flush.wait_for(lk, std::chrono::nanoseconds(max_wait.count() - (int64_t)(now - t0)));
+                    const int64_t left = max_wait.count() - (int64_t)(now - t0);
+                    cv_flush.wait_for(lk, std::chrono::nanoseconds(poll ? std::min<int64_t>(left, 10000) : left));
                 } else {
                     cv_flush.wait_for(lk, std::chrono::milliseconds(20));
                 }
@@ -1283,6 +1303,8 @@ int dg_agg_set_knob(dg_agg *a, const char *name, int64_t value)
     if (!a || !name) return set_err(DG_E_INVALID, "bad args");
     if (!strcmp(name, "depth")) {
         a->depth.store((int)std::max<int64_t>(0, std::min<int64_t>(value, a->ring - 2)), std::memory_order_relaxed);
+    } else if (!strcmp(name, "min_fill")) {
+        a->min_fill.store((uint32_t)std::max<int64_t>(0, std::min<int64_t>(value, 1ll << 30)), std::memory_order_relaxed);
     } else if (!strcmp(name, "max_wait_us")) {
         if (value < 0) return set_err(DG_E_INVALID, "max_wait_us < 0");
         std::lock_guard<std::mutex> g(a->mu);
@@ -1316,23 +1338,22 @@ struct GwCaller {
     dg_agg_ticket t;
     bool has;
 };
-struct alignas(64) GwQueue {
+struct alignas(64) GwWorker {
     std::mutex mu;
     std::condition_variable cv;
-    std::vector<uint32_t> v;
-};
-struct alignas(64) GwPark {
-    std::mutex mu;
-    std::vector<uint32_t> v;
+    std::atomic<bool> idle{false};
 };
 }  // namespace
 
 /* The gateway shape (see include/dgj2t.h): `callers` logical callers, each
  * with ONE call in flight at a time (a goroutine blocked in Do), multiplexed
- * over `workers` OS threads the way the Go runtime runs goroutines on its Ms;
- * a poller thread (the binding's one goroutine locked to an OS thread) blocks
- * in dg_agg_wait_gen and makes the callers of each converted generation
- * runnable again. Nothing blocks an OS thread per call. */
+ * over `workers` OS threads the way the Go runtime runs goroutines on its Ms
+ * (each with its own run queue, a P); a poller thread (the binding's one
+ * goroutine locked to an OS thread) blocks in dg_agg_wait_gen and publishes
+ * each converted generation. A caller parks in its worker's own ring by the
+ * generation of its call (no lock shared between workers: a shared park list
+ * serialised the 16 workers at ~1.4 M calls/s, r5w) and is runnable again
+ * once that generation is published. Nothing blocks an OS thread per call. */
 int dg_agg_gateway_drive(dg_agg *a, const uint8_t *arena, const uint64_t *in_off, uint64_t n, int workers,
                          int callers, uint8_t *out, const uint64_t *out_off, uint64_t *out_len, uint64_t *ret,
                          uint32_t *lat_ns, double *seconds, uint64_t *stats)
@@ -1342,40 +1363,61 @@ int dg_agg_gateway_drive(dg_agg *a, const uint8_t *arena, const uint64_t *in_off
     const uint32_t G = (uint32_t)std::min<uint64_t>((uint64_t)callers, std::max<uint64_t>(n, 1));
     std::vector<GwCaller> cs(G);
     for (uint32_t c = 0; c < G; c++) cs[c] = GwCaller{c, 0, 0, dg_agg_ticket{}, false};
-    std::vector<GwQueue> q(workers);
-    std::vector<GwPark> park(AGG_GEN_RING);
-    for (uint32_t c = 0; c < G; c++) q[c % workers].v.push_back(c);
+    std::vector<GwWorker> wk(workers);
     std::atomic<uint64_t> processed{a->done_upto.load(std::memory_order_acquire)};
     std::atomic<uint64_t> completed{0}, n_again{0}, n_park{0}, n_wake{0};
+    std::atomic<uint64_t> t_wait{0}, t_submit{0}, t_idle{0}, t_all{0}; /* ns summed over the workers */
     std::atomic<int> failed{0}, ready{0};
-    std::atomic<bool> go{false}, finished{false};
+    std::atomic<bool> go{false};
     auto done_all = [&] { return completed.load(std::memory_order_acquire) >= n || failed.load() > 0; };
     std::vector<std::thread> th;
     for (int w = 0; w < workers; w++) {
         th.emplace_back([&, w] {
-            std::vector<uint32_t> mine, retry, again;
+            std::vector<uint32_t> run, retry;
+            std::vector<std::vector<uint32_t>> parked(AGG_GEN_RING);
+            uint32_t nparked = 0;
+            for (uint32_t c = (uint32_t)w; c < G; c += (uint32_t)workers) run.push_back(c);
             ready.fetch_add(1);
             while (!go.load(std::memory_order_acquire)) std::this_thread::yield();
-            uint64_t done_local = 0;
+            uint64_t seen = processed.load(std::memory_order_acquire), done_local = 0;
+            uint64_t tw = 0, ts_ = 0, ti = 0;
+            const uint64_t tw0 = dg_agg::now_ns();
             for (;;) {
-                {
-                    std::unique_lock<std::mutex> lk(q[w].mu);
-                    if (q[w].v.empty() && retry.empty() && !finished.load(std::memory_order_acquire))
-                        q[w].cv.wait_for(lk, std::chrono::milliseconds(1),
-                                         [&] { return !q[w].v.empty() || finished.load(std::memory_order_acquire); });
-                    mine.swap(q[w].v);
-                }
-                if (finished.load(std::memory_order_acquire) && mine.empty()) break;
-                const bool only_retry = mine.empty() && !retry.empty();
-                mine.insert(mine.end(), retry.begin(), retry.end());
+                /* the callers of the generations published since the last look */
+                const uint64_t pg = processed.load(std::memory_order_acquire);
+                if (nparked)
+                    for (uint64_t g = seen + 1; g <= pg && g <= seen + AGG_GEN_RING; g++) {
+                        std::vector<uint32_t> &v = parked[g % AGG_GEN_RING];
+                        run.insert(run.end(), v.begin(), v.end());
+                        nparked -= (uint32_t)v.size();
+                        v.clear();
+                    }
+                seen = pg;
+                const bool only_retry = run.empty() && !retry.empty();
+                run.insert(run.end(), retry.begin(), retry.end());
                 retry.clear();
-                for (size_t k = 0; k < mine.size(); k++) {
-                    const uint32_t c = mine[k];
+                if (run.empty()) {
+                    if (done_all() || !nparked) break; /* !nparked: every caller of this worker is through */
+                    const uint64_t i0 = dg_agg::now_ns();
+                    {
+                        std::unique_lock<std::mutex> lk(wk[w].mu);
+                        wk[w].idle.store(true); /* seq_cst against the poller's store of processed, then load of idle */
+                        wk[w].cv.wait_for(lk, std::chrono::milliseconds(1),
+                                          [&] { return processed.load() > seen || done_all(); });
+                        wk[w].idle.store(false, std::memory_order_relaxed);
+                    }
+                    ti += dg_agg::now_ns() - i0;
+                    continue;
+                }
+                for (size_t k = 0; k < run.size(); k++) {
+                    const uint32_t c = run[k];
                     GwCaller &C = cs[c];
                     if (C.has) { /* resumed: its generation is converted, dg_agg_wait does not block */
                         const uint64_t j = C.cur;
                         size_t ol = 0;
+                        const uint64_t q0 = dg_agg::now_ns();
                         int rc = dg_agg_wait(a, &C.t, out + out_off[j], out_off[j + 1] - out_off[j], &ol, &ret[j]);
+                        tw += dg_agg::now_ns() - q0;
                         out_len[j] = ol;
                         if (rc) failed.fetch_add(1);
                         if (lat_ns) lat_ns[j] = (j & (DRIVE_SAMPLE - 1)) == 0
@@ -1387,7 +1429,9 @@ int dg_agg_gateway_drive(dg_agg *a, const uint8_t *arena, const uint64_t *in_off
                     if (C.next >= n) continue;
                     const uint64_t i = C.next;
                     if ((i & (DRIVE_SAMPLE - 1)) == 0) C.t0 = dg_agg::now_ns();
+                    const uint64_t q1 = dg_agg::now_ns();
                     int rc = dg_agg_submit(a, arena + in_off[i], in_off[i + 1] - in_off[i], 1, &C.t);
+                    ts_ += dg_agg::now_ns() - q1;
                     if (rc == DG_E_AGAIN) { /* no room in the open batch for this thread: later */
                         retry.push_back(c);
                         n_again.fetch_add(1, std::memory_order_relaxed);
@@ -1406,17 +1450,15 @@ int dg_agg_gateway_drive(dg_agg *a, const uint8_t *arena, const uint64_t *in_off
                     }
                     /* park on its generation (the goroutine's channel receive) */
                     const uint64_t g = C.t.gen;
-                    GwPark &p = park[g % AGG_GEN_RING];
-                    bool now = false;
-                    {
-                        std::lock_guard<std::mutex> lk(p.mu);
-                        if (processed.load(std::memory_order_acquire) >= g) now = true;
-                        else p.v.push_back(c);
+                    if (g <= processed.load(std::memory_order_acquire) || g > seen + AGG_GEN_RING) {
+                        retry.push_back(c);
+                    } else {
+                        parked[g % AGG_GEN_RING].push_back(c);
+                        nparked++;
+                        n_park.fetch_add(1, std::memory_order_relaxed);
                     }
-                    if (now) retry.push_back(c);
-                    else n_park.fetch_add(1, std::memory_order_relaxed);
                 }
-                mine.clear();
+                run.clear();
                 if (done_local) {
                     completed.fetch_add(done_local, std::memory_order_acq_rel);
                     done_local = 0;
@@ -1424,44 +1466,33 @@ int dg_agg_gateway_drive(dg_agg *a, const uint8_t *arena, const uint64_t *in_off
                 if (only_retry) std::this_thread::yield();
                 if (done_all()) break;
             }
+            t_wait.fetch_add(tw);
+            t_submit.fetch_add(ts_);
+            t_idle.fetch_add(ti);
+            t_all.fetch_add(dg_agg::now_ns() - tw0);
         });
     }
     while (ready.load() < workers) std::this_thread::yield();
     const auto ts = Clock::now();
     go.store(true, std::memory_order_release);
-    /* the poller */
+    /* the poller: publish each converted generation, wake the idle workers */
     uint64_t last = processed.load();
-    std::vector<uint32_t> woke;
-    uint32_t rr = 0;
     while (!done_all()) {
         uint64_t d = last;
         dg_agg_wait_gen(a, last, 1000, &d);
-        for (uint64_t g = last + 1; g <= d; g++) {
-            GwPark &p = park[g % AGG_GEN_RING];
-            std::lock_guard<std::mutex> lk(p.mu);
-            processed.store(g, std::memory_order_release);
-            woke.insert(woke.end(), p.v.begin(), p.v.end());
-            p.v.clear();
-        }
+        if (d <= last) continue;
+        processed.store(d);
         last = d;
-        if (woke.empty()) continue;
         n_wake.fetch_add(1, std::memory_order_relaxed);
-        /* spread over the workers, one lock per worker */
-        const size_t per = (woke.size() + workers - 1) / workers;
-        for (size_t k0 = 0; k0 < woke.size(); k0 += per) {
-            GwQueue &Q = q[rr++ % workers];
-            {
-                std::lock_guard<std::mutex> lk(Q.mu);
-                Q.v.insert(Q.v.end(), woke.begin() + k0, woke.begin() + std::min(woke.size(), k0 + per));
+        for (auto &W : wk)
+            if (W.idle.load()) {
+                { std::lock_guard<std::mutex> lk(W.mu); }
+                W.cv.notify_one();
             }
-            Q.cv.notify_one();
-        }
-        woke.clear();
     }
-    finished.store(true, std::memory_order_release);
-    for (auto &Q : q) {
-        { std::lock_guard<std::mutex> lk(Q.mu); }
-        Q.cv.notify_all();
+    for (auto &W : wk) {
+        { std::lock_guard<std::mutex> lk(W.mu); }
+        W.cv.notify_all();
     }
     for (auto &x : th) x.join();
     *seconds = std::chrono::duration<double>(Clock::now() - ts).count();
@@ -1470,6 +1501,10 @@ int dg_agg_gateway_drive(dg_agg *a, const uint8_t *arena, const uint64_t *in_off
         stats[1] = n_again.load();
         stats[2] = n_wake.load();
         stats[3] = G;
+        stats[4] = t_wait.load(); /* ns in dg_agg_wait, summed over the workers */
+        stats[5] = t_submit.load();
+        stats[6] = t_idle.load();
+        stats[7] = t_all.load();
     }
     return failed.load() ? set_err(DG_E_HIP, "%d gateway calls failed", failed.load()) : DG_OK;
 }

@@ -339,14 +339,18 @@ uint64_t dg_agg_ticket_gen(const dg_agg_ticket *t);
 /* aggregator knobs: "depth" (0 = off): also seal the open batch as soon as
  * it holds a message and fewer than depth batches are converting -- for
  * callers that park instead of blocking in dg_agg_wait, whose waits the
- * aggregator cannot see; "max_wait_us": the seal timer of dg_agg_create. */
+ * aggregator cannot see; "min_fill" (0 = off): the depth rule seals only a
+ * batch of at least this many calls (many parked callers refill a batch
+ * over a round trip: sealing at once keeps batches small); "max_wait_us":
+ * the seal timer of dg_agg_create. */
 int dg_agg_set_knob(dg_agg *agg, const char *name, int64_t value);
 /* Benchmark driver for the gateway shape: `callers` logical callers, each
  * with ONE call in flight at a time (a goroutine in Do), multiplexed over
  * `workers` OS threads (the Go runtime's Ms) with the dg_agg_wait_gen poller
  * above; caller c converts messages c, c + callers, ... Outputs as
- * dg_agg_drive; stats (optional, 4 u64): parks, submits retried for want of
- * room, poller wake-ups, callers. */
+ * dg_agg_drive; stats (optional, 8 u64): parks, submits retried for want of
+ * room, poller wake-ups, callers, then ns summed over the workers in
+ * dg_agg_wait, in dg_agg_submit, idle, and in all. */
 int dg_agg_gateway_drive(dg_agg *agg, const uint8_t *arena, const uint64_t *in_off, uint64_t n, int workers,
                          int callers, uint8_t *out, const uint64_t *out_off, uint64_t *out_len, uint64_t *ret,
                          uint32_t *lat_ns, double *seconds, uint64_t *stats);

@@ -236,8 +236,8 @@ def test_aggregator_fresh_contexts_first_batches():
         assert outs == want, rep
 
 
-@pytest.mark.parametrize("callers,workers,depth", [(1024, 8, 2), (4096, 16, 3), (5, 3, 0), (300, 2, 1)])
-def test_gateway_drive_vs_oracle(callers, workers, depth):
+@pytest.mark.parametrize("callers,workers,depth,fill", [(1024, 8, 2, 0), (4096, 16, 3, 512), (5, 3, 0, 0), (300, 2, 1, 64)])
+def test_gateway_drive_vs_oracle(callers, workers, depth, fill):
     """The gateway shape: many logical callers with ONE call
     in flight each (goroutines in Do), multiplexed over a few OS threads and
     woken per converted generation by one dg_agg_wait_gen poller -- no OS
@@ -250,12 +250,14 @@ def test_gateway_drive_vs_oracle(callers, workers, depth):
     agg = conv.Aggregator(td, conv.Options(), max_batch=512, max_wait_us=300, max_bytes=512 * 3000)
     if depth:
         agg.set_knob("depth", depth)
+    if fill:
+        agg.set_knob("min_fill", fill)
     outs, rets, lat, secs, st = agg.gateway(msgs, callers=callers, workers=workers)
     batches, n = agg.stats()
     prof = agg.profile()
     agg.close()
     assert n == len(msgs) and prof[11] == 0
-    assert st[3] == min(callers, len(msgs))
+    assert st[3] == min(callers, len(msgs)) and st[7] > 0
     assert [(int(r), o if int(r) == 0 else b"") for r, o in zip(rets, outs)] == \
         [(r, o if r == 0 else b"") for r, o in want]
     assert secs > 0 and int(lat.max()) > 0
