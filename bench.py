@@ -588,8 +588,8 @@ AGG_RUNS = ((16, 8192), (64, 2048), (64, 1))
 # flight each (goroutines in Do) over GATEWAY_WORKERS OS threads (the 16
 # CPUs a GPU gets) and one dg_agg_wait_gen poller; (callers, depth)
 GATEWAY_RUNS = ((1024, 2), (4096, 3), (16384, 4), (65536, 4))
-GATEWAY_FILL_DIV = 8  # min_fill = callers / 8: a batch waits for an eighth of the callers (or max_wait)
-GATEWAY_WORKERS = 16
+GATEWAY_FILL_DIV = 4  # min_fill = callers / 4: a batch waits for a quarter of the callers (or max_wait); r5y8: 4 > 8 > 16 at 16384
+GATEWAY_WORKERS = int(os.environ.get("DG_BENCH_GW_WORKERS", "16"))
 
 
 def agg_profile(pr, pr0, nbatches, ncalls):

@@ -546,10 +546,28 @@ void dg_agg::run_flusher()
     for (;;) {
         const uint64_t g = open.load(std::memory_order_acquire);
         Batch *x = &b[g % ring];
+        /* the next batch of the ring, once its callers have taken their
+         * results -- waited for first, while x still fills, so that a free
+         * slot and the seal are awaited together, not one after the other
+         * (r5y: 65536 gateway callers, 244 us seal + 186-536 us free a batch) */
+        Batch *y = &b[(g + 1) % ring];
         uint64_t t0 = now_ns();
         {
+            std::unique_lock<std::mutex> lk(mu);
+            cv_flush.wait(lk, [&] { return y->free_ || (stop && !x->t_first.load(std::memory_order_acquire)); });
+            if (!y->free_) { /* stopping with nothing to convert (y's callers never came back) */
+                inflight.push_back(nullptr);
+                lk.unlock();
+                cv_done.notify_one();
+                return;
+            }
+            y->free_ = false;
+        }
+        uint64_t t1 = now_ns();
+        prof[1].fetch_add(t1 - t0, std::memory_order_relaxed);
+        {
             /* until a caller asks for the seal (its sub-batch is full), the
-             * first message has waited max_wait, or stop */
+             * first message has waited max_wait, the depth rule, or stop */
             std::unique_lock<std::mutex> lk(mu);
             for (;;) {
                 if (x->seal_req.load(std::memory_order_acquire)) break;
@@ -563,6 +581,7 @@ void dg_agg::run_flusher()
                 }
                 if (stop) {
                     if (!t0) {
+                        y->free_ = true; /* not taken after all */
                         inflight.push_back(nullptr); /* the completer's exit marker */
                         lk.unlock();
                         cv_done.notify_one();
@@ -580,15 +599,9 @@ void dg_agg::run_flusher()
                 }
             }
         }
-        /* the next batch of the ring, once its callers have taken their results */
-        Batch *y = &b[(g + 1) % ring];
-        uint64_t t1 = now_ns();
-        prof[0].fetch_add(t1 - t0, std::memory_order_relaxed);
-        {
-            std::unique_lock<std::mutex> lk(mu);
-            cv_flush.wait(lk, [&] { return y->free_; });
-            y->free_ = false;
-        }
+        const uint64_t t1s = now_ns();
+        prof[0].fetch_add(t1s - t1, std::memory_order_relaxed);
+        t1 = t1s;
         const int ns = nparts();
         for (int s = 0; s < ns; s++) {
             y->sub[s].n.store(0, std::memory_order_relaxed);
@@ -1331,6 +1344,7 @@ int dg_agg_wait_gen(dg_agg *a, uint64_t after, uint32_t timeout_us, uint64_t *do
 uint64_t dg_agg_ticket_gen(const dg_agg_ticket *t) { return t && t->batch ? t->gen : 0; }
 
 namespace {
+constexpr size_t GW_PREFETCH = 8; /* dg_agg_gateway_drive: results prefetched this many callers ahead */
 struct GwCaller {
     uint64_t next;  /* its next message */
     uint64_t cur;   /* the message in flight */
@@ -1377,10 +1391,16 @@ int dg_agg_gateway_drive(dg_agg *a, const uint8_t *arena, const uint64_t *in_off
             std::vector<std::vector<uint32_t>> parked(AGG_GEN_RING);
             uint32_t nparked = 0;
             for (uint32_t c = (uint32_t)w; c < G; c += (uint32_t)workers) run.push_back(c);
+            /* requests arrive at this worker in arena order: a runnable caller
+             * takes the next one (a goroutine serving the next request), so
+             * consecutive calls read consecutive JSON -- not message c, c + G,
+             * ... of one caller, a cache miss per call */
+            uint64_t nxt = n * (uint64_t)w / (uint64_t)workers;
+            const uint64_t lim = n * (uint64_t)(w + 1) / (uint64_t)workers;
             ready.fetch_add(1);
             while (!go.load(std::memory_order_acquire)) std::this_thread::yield();
             uint64_t seen = processed.load(std::memory_order_acquire), done_local = 0;
-            uint64_t tw = 0, ts_ = 0, ti = 0;
+            uint64_t tw = 0, ts_ = 0, ti = 0, np_ = 0, na_ = 0; /* counted locally: no shared line per call */
             const uint64_t tw0 = dg_agg::now_ns();
             for (;;) {
                 /* the callers of the generations published since the last look */
@@ -1412,6 +1432,15 @@ int dg_agg_gateway_drive(dg_agg *a, const uint8_t *arena, const uint64_t *in_off
                 for (size_t k = 0; k < run.size(); k++) {
                     const uint32_t c = run[k];
                     GwCaller &C = cs[c];
+                    if (k + GW_PREFETCH < run.size()) { /* a later caller's result: status, offsets (pinned, DMA-written: not in cache) */
+                        const GwCaller &D = cs[run[k + GW_PREFETCH]];
+                        if (D.has && D.t.batch) {
+                            const Batch *x = (const Batch *)D.t.batch;
+                            const uint64_t i = x->sub[D.t.idx >> 24].gbase + (D.t.idx & 0xFFFFFFu);
+                            __builtin_prefetch(x->ret() + i);
+                            __builtin_prefetch(x->pack_off() + i);
+                        }
+                    }
                     if (C.has) { /* resumed: its generation is converted, dg_agg_wait does not block */
                         const uint64_t j = C.cur;
                         size_t ol = 0;
@@ -1426,23 +1455,23 @@ int dg_agg_gateway_drive(dg_agg *a, const uint8_t *arena, const uint64_t *in_off
                         C.has = false;
                         done_local++;
                     }
-                    if (C.next >= n) continue;
-                    const uint64_t i = C.next;
+                    if (nxt >= lim) continue;
+                    const uint64_t i = nxt;
                     if ((i & (DRIVE_SAMPLE - 1)) == 0) C.t0 = dg_agg::now_ns();
                     const uint64_t q1 = dg_agg::now_ns();
                     int rc = dg_agg_submit(a, arena + in_off[i], in_off[i + 1] - in_off[i], 1, &C.t);
                     ts_ += dg_agg::now_ns() - q1;
                     if (rc == DG_E_AGAIN) { /* no room in the open batch for this thread: later */
                         retry.push_back(c);
-                        n_again.fetch_add(1, std::memory_order_relaxed);
+                        na_++;
                         continue;
                     }
                     if (rc) {
                         failed.fetch_add(1);
                         continue;
                     }
+                    nxt++;
                     C.cur = i;
-                    C.next = i + G;
                     C.has = true;
                     if (!C.t.batch) { /* converted alone by dg_agg_wait: runnable at once */
                         retry.push_back(c);
@@ -1455,7 +1484,7 @@ int dg_agg_gateway_drive(dg_agg *a, const uint8_t *arena, const uint64_t *in_off
                     } else {
                         parked[g % AGG_GEN_RING].push_back(c);
                         nparked++;
-                        n_park.fetch_add(1, std::memory_order_relaxed);
+                        np_++;
                     }
                 }
                 run.clear();
@@ -1466,6 +1495,8 @@ int dg_agg_gateway_drive(dg_agg *a, const uint8_t *arena, const uint64_t *in_off
                 if (only_retry) std::this_thread::yield();
                 if (done_all()) break;
             }
+            n_park.fetch_add(np_);
+            n_again.fetch_add(na_);
             t_wait.fetch_add(tw);
             t_submit.fetch_add(ts_);
             t_idle.fetch_add(ti);

@@ -347,7 +347,8 @@ int dg_agg_set_knob(dg_agg *agg, const char *name, int64_t value);
 /* Benchmark driver for the gateway shape: `callers` logical callers, each
  * with ONE call in flight at a time (a goroutine in Do), multiplexed over
  * `workers` OS threads (the Go runtime's Ms) with the dg_agg_wait_gen poller
- * above; caller c converts messages c, c + callers, ... Outputs as
+ * above; worker w serves messages [w n / workers, (w + 1) n / workers) in
+ * order, each runnable caller taking the next one. Outputs as
  * dg_agg_drive; stats (optional, 8 u64): parks, submits retried for want of
  * room, poller wake-ups, callers, then ns summed over the workers in
  * dg_agg_wait, in dg_agg_submit, idle, and in all. */
