@@ -191,11 +191,73 @@ DGI bool atof_exact_l(uint64_t man, int exp, int sgn, double &val, const FastTab
     return false;
 }
 
+/* A whole token that is a plain integer, -?(0|[1-9][0-9]{0,18}), from a
+ * register source (RSrc / RSrcL: the token's first 24 bytes in registers,
+ * src.n its exact length): its value in a fixed number of steps -- three
+ * 8-digit SWAR chunks, no data-dependent loop -- so a wave whose lanes hold
+ * integers of different lengths runs one path. Anything else (a '.', an
+ * exponent, a sign without digits, a leading zero before digits, 20+ digits,
+ * a 19-digit value past int64) returns false and takes fast_vnumber's
+ * general loop, whose results these are (native/scanning.c:958-1083 on this
+ * shape: is_overflow false, iv = man * sgn, dv = (double)man with the sign). */
+template <class S>
+DGI bool fast_int_regs(const S &src, int64_t &iv, double &dv, int32_t &end)
+{
+    const int32_t n = (int32_t)src.n;
+    if (n < 1 || n > 20) return false;
+    const uint64_t a0 = src.get8(0), a1 = src.get8(8), a2 = src.get8(16);
+    const uint32_t neg = (uint8_t)a0 == '-' ? 1u : 0u;
+    const uint32_t nd = (uint32_t)n - neg;
+    /* the digits from byte 0 */
+    const uint64_t d0 = neg ? (a0 >> 8) | (a1 << 56) : a0, d1 = neg ? (a1 >> 8) | (a2 << 56) : a1,
+                   d2 = neg ? a2 >> 8 : a2;
+    const uint64_t x0 = d0 ^ 0x3030303030303030ull, x1 = d1 ^ 0x3030303030303030ull, x2 = d2 ^ 0x3030303030303030ull;
+    auto nondig = [](uint64_t x) { return (((x & 0x7F7F7F7F7F7F7F7Full) + 0x7676767676767676ull) | x) & 0x8080808080808080ull; };
+    auto upto = [](uint32_t k) { return k >= 8 ? ~0ull : (1ull << (k << 3)) - 1; }; /* the first k bytes */
+    const uint32_t t0 = nd < 8 ? nd : 8u, t1 = nd <= 8 ? 0u : nd - 8 < 8 ? nd - 8 : 8u, t2 = nd <= 16 ? 0u : nd - 16;
+    const uint64_t bad = (nondig(x0) & upto(t0)) | (nondig(x1) & upto(t1)) | (nondig(x2) & upto(t2));
+    const uint32_t f = (uint32_t)(x0 & 0xFF); /* first digit's value */
+    if (nd < 1 || nd > 19 || bad || (f == 0 && nd > 1)) return false;
+    auto p10 = [](uint32_t t) {
+        uint32_t p = (t & 1) ? 10u : 1u;
+        p = (t & 2) ? p * 100u : p;
+        p = (t & 4) ? p * 10000u : p;
+        return (t & 8) ? 100000000u : p;
+    };
+    uint64_t man = swar_val(x0, t0);
+    man = man * (uint64_t)p10(t1) + swar_val(x1, t1);
+    man = man * (uint64_t)p10(t2) + swar_val(x2, t2);
+    if ((man >> 63) && !(neg && man == (1ull << 63))) return false; /* is_overflow: the double path */
+    const int sgn = neg ? -1 : 1;
+    iv = (int64_t)(man * (uint64_t)(int64_t)sgn);
+    dv = man ? with_sign((double)man, sgn) : 0.0; /* "-0": the general path's +0.0 */
+    end = n;
+    return true;
+}
+
+/* register sources (RSrc, RSrcL: kRegs) take fast_int_regs first */
+template <class S, class = void>
+struct is_regsrc {
+    static constexpr bool value = false;
+};
+template <class S>
+struct is_regsrc<S, decltype((void)S::kRegs)> {
+    static constexpr bool value = S::kRegs;
+};
+
 /* vnumber (native/scanning.c:958-1083) on the success paths; false = the
  * reference would error or need atof_native -> bail. */
 template <class S>
 DGI bool fast_vnumber(S &src, SI &p, const FastTabs &tb, int64_t &iv, double &dv, bool &isint)
 {
+    if constexpr (is_regsrc<S>::value) {
+        int32_t e;
+        if (p == 0 && fast_int_regs(src, iv, dv, e)) {
+            isint = true;
+            p = (SI)e;
+            return true;
+        }
+    }
     SI i = p;
     uint8_t c = src.at(i);
     int sgn = 1;

@@ -70,7 +70,7 @@ constexpr uint32_t FL_DESC = 16 * 1024;          /* descriptor bytes in LDS (dyn
 constexpr uint32_t FL_INLINE = DG_FL_INLINE;     /* longer string / base64 bodies are written as chunk tasks */
 constexpr uint32_t FL_CHUNK = DG_FL_CHUNK;       /* input bytes per chunk task (a multiple of 8) */
 constexpr uint32_t FL_MAXTASK = 320;             /* chunk tasks per block (more: the message declines; C2 ~160) */
-constexpr uint32_t FL_NESC = 4;                  /* escapes per message (more: the message declines) */
+constexpr uint32_t FL_NESC = 8;                  /* escapes per message (more: the message declines; C1's string has 8) */
 #ifndef DG_FL_WPE
 #define DG_FL_WPE 4 /* waves per SIMD the register budget is cut for: 128 VGPRs; LDS allows 4 blocks (16 waves) per CU */
 #endif
@@ -173,6 +173,7 @@ struct LSrc {
 constexpr int32_t RSL_MAX = 24;
 struct RSrcL {
     typedef int32_t idx;
+    static constexpr bool kRegs = true; /* fast_vnumber: the fixed-step integer path */
     uint64_t w0, w1, w2, w3, w4;
     uint32_t sh; /* byte offset of the number's first byte in w0 */
     int32_t n;
@@ -259,7 +260,19 @@ DGI int32_t fl_lookup(const DV &D, const dg_struct &sd, S &src, uint32_t k0, uin
  * unquote's semantics (native/parsing.c:702-945, flags 0) for everything
  * the flat path keeps; a surrogate, an invalid escape or more than FL_NESC
  * escapes decline the message to the list pass. */
-typedef const __attribute__((address_space(3))) uint64_t lds_esc;
+typedef const __attribute__((address_space(3))) uint32_t lds_esc;
+/* an entry: bit 31 set | position (12 bits) | \u form << 12 | code point << 13 */
+DGI uint32_t esc_pos(uint32_t x) { return x & 0xFFF; }
+DGI uint32_t esc_in(uint32_t x) { return (x >> 12) & 1 ? 6u : 2u; }           /* JSON bytes */
+DGI uint32_t esc_cp(uint32_t x) { return (x >> 13) & 0xFFFF; }
+DGI uint32_t esc_out(uint32_t x) { const uint32_t cp = esc_cp(x); return cp <= 0x7f ? 1u : cp <= 0x7ff ? 2u : 3u; }
+DGI uint32_t esc_utf8(uint32_t x) /* its UTF-8 bytes, first byte lowest */
+{
+    const uint32_t cp = esc_cp(x);
+    return cp <= 0x7f ? cp
+           : cp <= 0x7ff ? (0xc0 | (cp >> 6)) | ((0x80 | (cp & 0x3f)) << 8)
+                         : (0xe0 | (cp >> 12)) | ((0x80 | ((cp >> 6) & 0x3f)) << 8) | ((0x80 | (cp & 0x3f)) << 16);
+}
 DGI bool fl_hex4(uint32_t w, uint32_t &v)
 {
     uint32_t r = 0, ok = 1;
@@ -274,22 +287,18 @@ DGI bool fl_hex4(uint32_t w, uint32_t &v)
 }
 /* the escape at message position p (e0: the 8 bytes from its backslash) ->
  * its table entry, or 0 if the flat path leaves it to the exact machine */
-DGI uint64_t fl_escape(uint32_t p, uint64_t e0)
+DGI uint32_t fl_escape(uint32_t p, uint64_t e0)
 {
     const uint32_t c = (uint32_t)(e0 >> 8) & 0xFF;
     if (c == 'u') {
         uint32_t cp;
         if (!fl_hex4((uint32_t)(e0 >> 16), cp) || (cp >= 0xd800 && cp <= 0xdfff)) return 0;
-        const uint32_t n = cp <= 0x7f ? 1u : cp <= 0x7ff ? 2u : 3u;
-        const uint32_t v = n == 1 ? cp
-                           : n == 2 ? (0xc0 | (cp >> 6)) | ((0x80 | (cp & 0x3f)) << 8)
-                                    : (0xe0 | (cp >> 12)) | ((0x80 | ((cp >> 6) & 0x3f)) << 8) | ((0x80 | (cp & 0x3f)) << 16);
-        return p | (6u << 12) | (n << 16) | ((uint64_t)v << 32);
+        return 0x80000000u | p | (1u << 12) | (cp << 13);
     }
     /* _UnquoteTab native/parsing.c:565-575 */
     const uint32_t cc = c == 'b' ? 8u : c == 'f' ? 12u : c == 'n' ? 10u : c == 'r' ? 13u : c == 't' ? 9u : c;
     const bool ok = (c == '"') | (c == '\\') | (c == '/') | (c == 'b') | (c == 'f') | (c == 'n') | (c == 'r') | (c == 't');
-    return ok ? p | (2u << 12) | (1u << 16) | ((uint64_t)cc << 32) : 0;
+    return ok ? 0x80000000u | p | (cc << 13) : 0u;
 }
 /* escapes in [a, b): any, and the bytes they shrink the body by */
 DGI bool fl_esc_in(lds_esc *E, uint32_t ne, uint32_t a, uint32_t b, uint32_t &shrink)
@@ -297,11 +306,11 @@ DGI bool fl_esc_in(lds_esc *E, uint32_t ne, uint32_t a, uint32_t b, uint32_t &sh
     bool any = false;
     shrink = 0;
     for (uint32_t e = 0; e < ne; e++) {
-        const uint64_t x = E[e];
-        const uint32_t p = (uint32_t)x & 0xFFF;
+        const uint32_t x = E[e];
+        const uint32_t p = esc_pos(x);
         const bool in = p >= a && p < b;
         any |= in;
-        shrink += in ? ((uint32_t)(x >> 12) & 0xF) - ((uint32_t)(x >> 16) & 0x7) : 0u;
+        shrink += in ? esc_in(x) - esc_out(x) : 0u;
     }
     return any;
 }
@@ -561,16 +570,16 @@ DGI uint32_t flat_write(S &src, const FField &F, const FastTabs &tb, O &o, lds_e
             uint32_t cur = F.s0;
             const uint32_t end = F.s0 + F.nb;
             for (uint32_t it = 0; it < FL_NESC; it++) {
-                uint64_t best = ~0ull;
+                uint32_t best = 0xFFFFFFFFu; /* position 0xFFF: none */
                 for (uint32_t e = 0; e < ne; e++) {
-                    const uint32_t p = (uint32_t)E[e] & 0xFFF;
-                    if (p >= cur && p < end && p < ((uint32_t)best & 0xFFF)) best = E[e];
+                    const uint32_t x = E[e], p = esc_pos(x);
+                    if (p >= cur && p < end && p < esc_pos(best)) best = x;
                 }
-                if (best == ~0ull) break;
-                const uint32_t p = (uint32_t)best & 0xFFF;
+                if (best == 0xFFFFFFFFu) break;
+                const uint32_t p = esc_pos(best);
                 body_copy(src, cur, p - cur, o);
-                o.wle(best >> 32, (uint32_t)(best >> 16) & 0x7);
-                cur = p + ((uint32_t)(best >> 12) & 0xF);
+                o.wle(esc_utf8(best), esc_out(best));
+                cur = p + esc_in(best);
             }
             body_copy(src, cur, end - cur, o);
             return 1;
@@ -660,7 +669,7 @@ struct FlatLds {
     uint32_t nbytes[FL_MPB];                /* Thrift bytes before STOP */
     uint32_t wid[FL_MPB];                   /* wrapped mode: 0x10000 | the outer field's id, 0 = not wrapped */
     uint32_t nesc[FL_MPB];                  /* escapes found in the message (phase 1) */
-    uint64_t esc[FL_MPB * FL_NESC];         /* [m][e]: position | in_len << 12 | out_len << 16 | UTF-8 bytes << 32 */
+    uint32_t esc[FL_MPB * FL_NESC];         /* [m][e]: fl_escape's entries */
     uint32_t sep[FL_MAXF * FL_MPB];         /* [k][m]: comma position | quotes before it << 16 */
     uint16_t col[FL_MAXF * FL_MPB];         /* [k][m]: colon position */
     uint16_t size[2 * FL_SLOTS * FL_MPB];   /* [round & 1][slot][m] */
@@ -941,9 +950,9 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
                 es.init((const __attribute__((address_space(3))) uint64_t *)(void *)&L.in[lw], (int32_t)a7, (int32_t)n);
                 for (uint64_t eb = B; eb; eb &= eb - 1) {
                     const uint32_t p = 64 * g + (uint32_t)__builtin_ctzll(eb);
-                    const uint64_t x = fl_escape(p, es.get8((int32_t)p));
+                    const uint32_t x = fl_escape(p, es.get8((int32_t)p));
                     const uint32_t idx = atomicAdd(&L.nesc[m1], 1u);
-                    if (!x || p + ((uint32_t)(x >> 12) & 0xF) > n) ebad = 1;
+                    if (!x || p + esc_in(x) > n) ebad = 1;
                     else if (idx < FL_NESC) L.esc[m1 * FL_NESC + idx] = x;
                     else ebad = 1;
                 }

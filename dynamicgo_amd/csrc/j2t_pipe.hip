@@ -1441,6 +1441,16 @@ int dg_agg_gateway_drive(dg_agg *a, const uint8_t *arena, const uint64_t *in_off
                             __builtin_prefetch(x->pack_off() + i);
                         }
                     }
+                    if (k + GW_PREFETCH / 2 < run.size()) { /* ... and, its offsets now cached, its packed bytes */
+                        const GwCaller &D = cs[run[k + GW_PREFETCH / 2]];
+                        if (D.has && D.t.batch) {
+                            const Batch *x = (const Batch *)D.t.batch;
+                            const uint64_t i = x->sub[D.t.idx >> 24].gbase + (D.t.idx & 0xFFFFFFu);
+                            const uint8_t *q = x->h_packed + x->pack_off()[i];
+                            __builtin_prefetch(q);
+                            __builtin_prefetch(q + 64);
+                        }
+                    }
                     if (C.has) { /* resumed: its generation is converted, dg_agg_wait does not block */
                         const uint64_t j = C.cur;
                         size_t ol = 0;

@@ -522,6 +522,7 @@ DGI bool chunk_b64(S &src, int64_t s0, int64_t n, bool last, O &o)
 constexpr int64_t RS_MAX = 24;
 struct RSrc {
     typedef int64_t idx;
+    static constexpr bool kRegs = true; /* fast_vnumber: the fixed-step integer path */
     uint64_t w0, w1, w2, w3, w4;
     uint32_t sh; /* byte offset of the token's first byte in w0 */
     int64_t n;

@@ -242,8 +242,8 @@ def test_flat_task_cap_path():
 def test_flat_escape_table_vs_oracle():
     """The structure phase's escape table (j2t_flat.h fl_escape): every simple
     escape, \\u of 1, 2 and 3 UTF-8 bytes (upper/lower-case hex), escapes at
-    a string's start and end, next to each other, up to FL_NESC (4) per
-    message and beyond it, in keys, in numbers' js_conv text, in binary
+    a string's start and end, next to each other, up to FL_NESC (8) per
+    message and beyond it (C1's string has 8), in keys, in numbers' js_conv text, in binary
     fields, invalid ones and surrogates (declined to the list pass): the
     bytes and status words of the reference. Escapes the table keeps stay on
     the flat kernel (no bail)."""
@@ -254,13 +254,13 @@ def test_flat_escape_table_vs_oracle():
               "\\u0800", "\\u4e2d", "\\uFFFF", "\\u0000", "é"]
     keep = []
     for _ in range(3000):
-        body = "".join(rng.choice(pieces) for _ in range(rng.randint(0, 7)))
+        body = "".join(rng.choice(pieces) for _ in range(rng.randint(0, 10)))
         keep.append(('{"ByteField":%d,"StringField":"%s","I32Field":%d}' %
                      (rng.randint(-128, 127), body, rng.randint(-2**31, 2**31 - 1))).encode())
-    ok = [m for m in keep if m.count(b"\\") <= 4]
+    ok = [m for m in keep if m.count(b"\\") <= 8]
     ctx = conv.default_context()
     ctx.stats(reset=True)
-    outs, rets = _raw_batch(fl, ok, 0x1 | FLAT)
+    outs, rets = _raw_batch(fl, ok + [W.c1_simple_json()] * 256, 0x1 | FLAT)
     bails, _ = ctx.stats(reset=True)
     assert bails == 0, bails
     assert not _compare(fl, ok, 0x1 | FLAT)
@@ -268,8 +268,39 @@ def test_flat_escape_table_vs_oracle():
            b'{"StringField":"\\u12"}', b'{"StringField":"\\u12G4"}', b'{"StringField":"ab\\',
            b'{"Str\\u0069ngField":"k"}', b'{"StringField":"\\n\\n\\n\\n\\n"}', b'{"BinaryField":"QQ\\u003d="}',
            b'{"I32Field":1\\n}', b'{"StringField":"\\u002"}', b'{"StringField":"\\n","StringField":"\\t\\b\\f\\r"}',
-           b'{"StringField":"' + b"\\u00e9" * 4 + b'"}', b'{"StringField":"' + b"\\u00e9" * 5 + b'"}']
+           b'{"StringField":"' + b"\\u00e9" * 8 + b'"}', b'{"StringField":"' + b"\\u00e9" * 9 + b'"}',
+           W.c1_simple_json()]
     for flags in (0x1, 0x11, 0x7):
         for extra in (FLAT, NO_FLAT):
             bad = _compare(fl, keep + odd, flags | extra)
             assert not bad, (hex(flags), extra, bad[:4])
+
+
+INT_TOKENS = ["0", "-0", "7", "-7", "00", "01", "-01", "-", "--1", "+1", "1-", "12a", "1.", "1.5", "-1.25", "1e5", "1E+2",
+              "-0.0", "0e0", "127", "-128", "128", "32767", "-32768", "2147483647", "-2147483648", "2147483648",
+              "9223372036854775807", "-9223372036854775808", "9223372036854775808", "-9223372036854775809",
+              "9999999999999999999", "18446744073709551615", "18446744073709551616", "12345678901234567890",
+              "123456789012345678901", "1234567", "12345678", "123456789", "1234567890123456", "12345678901234567",
+              "000000000000000000001", "99999999", "100000000", "4294967296"]
+
+
+@pytest.mark.parametrize("route", ["flat", "small", "wave"])
+def test_integer_tokens_vs_oracle(route):
+    """fast_vnumber's fixed-step integer path (j2t_fast.h fast_int_regs,
+    register sources: the flat kernel's RSrcL, the wave kernel's RSrc) and
+    its fall-backs: every integer shape, the int64 edges, 19- and 20-digit
+    values, "-0", leading zeros and non-integers, in every numeric field
+    type, against the reference; "wave" pads the message past the wave
+    kernel's 512-byte threshold."""
+    td = flat_desc()
+    fl = T.flatten(td)
+    msgs = []
+    for v in INT_TOKENS:
+        for f in ("y", "s16", "s32", "s64", "d", "vm64", "vm16"):
+            pad = ',"Str":"' + "p" * 600 + '"' if route == "wave" else ""
+            msgs.append(('{"req":1,"%s":%s%s}' % (f, v, pad)).encode())
+            msgs.append(('{"%s":%s,"req":%s%s}' % (f, v, v, pad)).encode())
+    extra = {"flat": FLAT, "small": NO_FLAT, "wave": NO_FLAT}[route]
+    for flags in (0x1, 0x41, 0x5):
+        bad = _compare(fl, msgs, flags | extra)
+        assert not bad, (route, hex(flags), bad[:4])
