@@ -70,6 +70,7 @@ constexpr uint32_t FL_DESC = 16 * 1024;          /* descriptor bytes in LDS (dyn
 constexpr uint32_t FL_INLINE = DG_FL_INLINE;     /* longer string / base64 bodies are written as chunk tasks */
 constexpr uint32_t FL_CHUNK = DG_FL_CHUNK;       /* input bytes per chunk task (a multiple of 8) */
 constexpr uint32_t FL_MAXTASK = 320;             /* chunk tasks per block (more: the message declines; C2 ~160) */
+constexpr uint32_t FL_KEYS = 32;                  /* name-table slots of the flat struct kept as a key table (larger: name table) */
 constexpr uint32_t FL_NESC = 8;                  /* escapes per message (more: the message declines; C1's string has 8) */
 #ifndef DG_FL_WPE
 #define DG_FL_WPE 4 /* waves per SIMD the register budget is cut for: 128 VGPRs; LDS allows 4 blocks (16 waves) per CU */
@@ -81,6 +82,10 @@ constexpr uint32_t FL_NESC = 8;                  /* escapes per message (more: t
 #ifndef DG_FL_PERM
 #define DG_FL_PERM 0
 #endif
+#ifndef DG_FL_REMAP
+#define DG_FL_REMAP 1 /* the field remap (phase 2a) */
+#endif
+
 /* -DDG_FLPROF_G: cycles per wave in the stages of a field's parse, summed
  * over the fields (P.stats[2 + stage]): 0 separators from LDS, 1 delimiter
  * bytes, 2 key, 3 value, 4 sizes, 5 bookkeeping after fl_field */
@@ -320,10 +325,11 @@ DGI bool fl_esc_in(lds_esc *E, uint32_t ne, uint32_t a, uint32_t b, uint32_t &sh
  * message. Every quote of the message is a delimiter (phase 1 declined \" and
  * \\), so a field holds exactly the key's two quotes, plus two when the value
  * is a string: the key and a string value are delimited without scanning. */
-template <class S, class DV>
+template <bool KO = false, class S, class DV>
 DGI bool fl_field(const DV &D, const dg_struct &sd, S &src, uint32_t sk, uint32_t ck, uint32_t ek, uint32_t nq,
-                  bool hasbs, lds_esc *E, uint32_t ne, uint32_t k, uint64_t flag, const FastTabs &tb,
-                  FField &F FLG_ARG)
+                  bool hasbs, lds_esc *E, uint32_t ne, const __attribute__((address_space(3))) uint64_t *KW,
+                  const __attribute__((address_space(3))) uint32_t *KM, uint32_t nk, uint32_t k, uint64_t flag,
+                  const FastTabs &tb, FField &F FLG_ARG)
 {
     typedef typename S::idx SI;
     /* Round 1 of LDS reads: the four delimiting bytes and the predicted
@@ -358,6 +364,7 @@ DGI bool fl_field(const DV &D, const dg_struct &sd, S &src, uint32_t sk, uint32_
      * predicted key's pool words, compared in one step (the pool keys are
      * zero-padded to 8 bytes, key_eq's semantics) */
     int32_t fi = -1;
+    uint64_t a0m = 0, a1m = 0; /* a key of up to 16 bytes, zero-padded like the pool's */
     {
         const __attribute__((address_space(3))) uint64_t *pk = (decltype(&D.R[0]))(&D.P[f.key_off]);
         bool hit;
@@ -365,15 +372,33 @@ DGI bool fl_field(const DV &D, const dg_struct &sd, S &src, uint32_t sk, uint32_
             const uint64_t a0 = src.get8((SI)k0), a1 = src.get8((SI)(k0 + 8)), b0 = pk[0], b1 = pk[1];
             const uint64_t m0 = kn >= 8 ? ~0ull : (1ull << (kn << 3)) - 1;
             const uint64_t m1 = kn >= 16 ? ~0ull : kn <= 8 ? 0ull : (1ull << ((kn - 8) << 3)) - 1;
-            hit = ((a0 & m0) == b0) & ((kn <= 8) | ((a1 & m1) == b1));
+            a0m = a0 & m0;
+            a1m = a1 & m1;
+            hit = (a0m == b0) & ((kn <= 8) | (a1m == b1));
         } else {
             hit = key_eq(src, (SI)k0, kn, pk);
         }
         if (pred & ((f.flags & DG_FF_ALIAS_SELF) != 0) & (f.key_len == kn) & hit) fi = (int32_t)(sd.field_begin + k);
     }
     if (fi < 0) {
-        fi = fl_lookup(D, sd, src, k0, kn);
+        if (nk && kn <= 16) {
+            /* the struct's names from the key table (phase 1): every lane
+             * scans the same entries (uniform addresses, broadcast reads),
+             * no byte-serial hash and no probe chain -- the shuffled-key
+             * case (c2s) misses the predicted field on most fields */
+#pragma unroll 4
+            for (uint32_t e = 0; e < nk; e++) {
+                const uint32_t mt = KM[e];
+                if (((mt >> 24) == kn) & (KW[2 * e] == a0m) & (KW[2 * e + 1] == a1m)) fi = (int32_t)(mt & 0xFFFFFFu);
+            }
+        } else {
+            fi = fl_lookup(D, sd, src, k0, kn);
+        }
         if (fi >= 0) f = ldrec(&D.F[fi]);
+    }
+    if constexpr (KO) { /* the key pass (field remap): the field only */
+        F.fi = fi;
+        return true;
     }
     FLG(2);
     /* the value, [v0, ve) */
@@ -670,10 +695,14 @@ struct FlatLds {
     uint32_t wid[FL_MPB];                   /* wrapped mode: 0x10000 | the outer field's id, 0 = not wrapped */
     uint32_t nesc[FL_MPB];                  /* escapes found in the message (phase 1) */
     uint32_t esc[FL_MPB * FL_NESC];         /* [m][e]: fl_escape's entries */
+    uint64_t kw[2 * FL_KEYS];               /* key table: the flat struct's names up to 16 bytes, zero-padded */
+    uint32_t km[FL_KEYS];                   /* ... field | key_len << 24 (0xFF << 24: empty slot, longer key) */
+    uint32_t fkm[FL_SLOTS];                 /* field j's own key length (the order check; 0xFF: not predictable) */
     uint32_t sep[FL_MAXF * FL_MPB];         /* [k][m]: comma position | quotes before it << 16 */
     uint16_t col[FL_MAXF * FL_MPB];         /* [k][m]: colon position */
     uint16_t size[2 * FL_SLOTS * FL_MPB];   /* [round & 1][slot][m] */
-    uint32_t rounds, ntask, tgrab;
+    uint32_t fseen[FL_MPB];                 /* key pass: the fields found in the message (bit = field index) */
+    uint32_t rounds, ntask, tgrab, noremap;
     uint64_t p10u[20];
     double p10d[23];
     uint64_t pw[EL_WN];                     /* Eisel-Lemire powers window (j2t_fast.h) */
@@ -731,6 +760,7 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
         L.rounds = 0;
         L.ntask = 0;
         L.tgrab = 0;
+        L.noremap = 0;
     }
     if (tid < FL_MPB) {
         uint32_t ok = 0, n = 0, lw = 0, big = 0, cap = 0;
@@ -767,7 +797,9 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
         L.oc[tid] = 0;
         L.nfq[tid] = 0;
         L.nesc[tid] = 0;
+        L.fseen[tid] = 0;
     }
+    if (tid < FL_SLOTS * FL_MPB / 4) ((uint32_t *)(void *)L.task)[tid] = 0xFFFFFFFFu; /* the field map (in the task area): none */
     __syncthreads();
     const uint32_t g = tid & 3, m1 = tid >> 2; /* phase 1: 4 lanes per message */
     if (!staged) {
@@ -804,6 +836,31 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
                       (const __attribute__((address_space(3))) uint64_t *)(void *)L.pw};
     const dg_type rt = ldrec(&D.T[S.wrap ? S.wrap_inner : P.root]);
     const dg_struct sd = ldrec(&D.S[rt.st]);
+    /* the key table: the name table's slots (read by phase 2, after phase 1's barrier) */
+    const uint32_t nk = sd.name_mask + 1 <= FL_KEYS ? sd.name_mask + 1 : 0u;
+    if (tid < nk) {
+        const dg_name nm = ldrec(&D.N[sd.name_begin + tid]);
+        uint32_t mt = 0xFF000000u;
+        uint64_t w0 = 0, w1 = 0;
+        if (nm.field != DG_NONE && nm.key_len <= 16) {
+            const __attribute__((address_space(3))) uint64_t *pk = (decltype(&D.R[0]))(&D.P[nm.key_off]);
+            w0 = nm.key_len ? pk[0] : 0ull; /* the pool pads keys with zeros to 8 bytes */
+            w1 = nm.key_len > 8 ? pk[1] : 0ull;
+            mt = nm.field | (nm.key_len << 24);
+        }
+        L.km[tid] = mt;
+        L.kw[2 * tid] = w0;
+        L.kw[2 * tid + 1] = w1;
+    }
+    if (tid >= 64 && tid < 64 + FL_SLOTS) { /* the predicted keys' lengths, for the order check */
+        const uint32_t j = tid - 64;
+        uint32_t len = 0xFF;
+        if (j < sd.n_fields) {
+            const dg_field f = ldrec(&D.F[sd.field_begin + j]);
+            if (f.flags & DG_FF_ALIAS_SELF) len = f.key_len;
+        }
+        L.fkm[j] = len;
+    }
     if (S.wrap) {
         /* ---- 0b. wrapped mode: ws '{' ws "key" ws ':' ws {inner} ws '}' ws
          *      with the key a wrap_ok field of R: the inner object becomes
@@ -1018,6 +1075,8 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
         const uint32_t rounds = L.rounds;
         uint32_t nbytes = 0;
         lds_esc *E = (lds_esc *)(void *)&L.esc[mm * FL_NESC];
+        const __attribute__((address_space(3))) uint64_t *KW = (const __attribute__((address_space(3))) uint64_t *)(void *)L.kw;
+        const __attribute__((address_space(3))) uint32_t *KM = (const __attribute__((address_space(3))) uint32_t *)(void *)L.km;
         const uint32_t ne = min(L.nesc[mm], FL_NESC);
 #ifdef DG_FLPROF_G
         uint64_t flg[8] = {0, 0, 0, 0, 0, 0, 0, __builtin_amdgcn_s_memtime()};
@@ -1036,7 +1095,7 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
                 }
                 const uint32_t ck = L.col[k * FL_MPB + mm];
                 FLG(0);
-                if (!(ck >= sk && ck < ek && fl_field(D, sd, src, sk, ck, ek, q1 - q0, hasbs, E, ne, k, P.flag, tb, F FLG_PASS))) {
+                if (!(ck >= sk && ck < ek && fl_field(D, sd, src, sk, ck, ek, q1 - q0, hasbs, E, ne, KW, KM, nk, k, P.flag, tb, F FLG_PASS))) {
                     L.ok[mm] = 0;
                     F.size = 0;
                     F.kind = FV_NONE;
@@ -1061,14 +1120,83 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
             o.finish();
             return wr;
         };
+        /* ---- 2a. field remap: a wave converts the same FIELD of its 64
+         *      messages, not the same position. With the keys in IDL order
+         *      (C2) that is the same thing; with shuffled keys (c2s) a
+         *      position holds a different field, type and code path in every
+         *      lane, and the wave ran the union of all of them (VALU 4.8 K vs
+         *      2.9 K per wave, r6c). A key pass finds each position's field
+         *      (fmap[field][message] = position, in the task area, unused
+         *      until the tasks); the block remaps only when every message
+         *      fits one round and every key is a known field once. ---- */
+        uint8_t *fmap = (uint8_t *)(void *)L.task;
+        bool remap_try = DG_FL_REMAP && rounds == 1 && sd.n_fields <= FL_SLOTS && nk != 0;
+        if (remap_try) {
+            /* the order check: a key's length at every position equals the
+             * predicted (IDL-order) field's. Keys in IDL order (C2) pass and
+             * skip the key pass (a key pass on every block cost C2 4 %, r6f);
+             * a false pass only keeps the positional assignment, which is
+             * always correct */
+            uint32_t mis = 0;
+#pragma unroll
+            for (uint32_t h = 0; h < FL_FPW; h++) {
+                const uint32_t k = fl_slot(wave, h);
+                if (ok0 && k < nf) {
+                    const uint32_t sk = k ? (L.sep[(k - 1) * FL_MPB + mm] & 0xFFFF) + 1 : (oc & 0xFFFF) + 1;
+                    const uint32_t ck = L.col[k * FL_MPB + mm];
+                    mis |= (k >= sd.n_fields || L.fkm[k] != ck - sk - 2) ? 1u : 0u;
+                }
+            }
+            if (ballot(mis != 0) && lane == 0) atomicOr(&L.noremap, 2u);
+            __syncthreads();
+            remap_try = (L.noremap & 2u) != 0;
+        }
+        if (remap_try) {
+            uint32_t fail = 0;
+#pragma unroll
+            for (uint32_t h = 0; h < FL_FPW; h++) {
+                const uint32_t k = fl_slot(wave, h);
+                if (ok0 && k < nf) {
+                    const uint32_t e0 = k ? L.sep[(k - 1) * FL_MPB + mm] : 0;
+                    const uint32_t sk = k ? (e0 & 0xFFFF) + 1 : (oc & 0xFFFF) + 1, q0 = e0 >> 16;
+                    uint32_t ek = oc >> 16, q1 = qtot;
+                    if (k + 1 < nf) {
+                        const uint32_t e1 = L.sep[k * FL_MPB + mm];
+                        ek = e1 & 0xFFFF;
+                        q1 = e1 >> 16;
+                    }
+                    const uint32_t ck = L.col[k * FL_MPB + mm];
+                    FField G;
+                    G.fi = -1;
+                    if (!(ck >= sk && ck < ek &&
+                          fl_field<true>(D, sd, src, sk, ck, ek, q1 - q0, hasbs, E, ne, KW, KM, nk, k, P.flag, tb, G FLG_PASS)) ||
+                        G.fi < 0) {
+                        fail = 1;
+                    } else {
+                        const uint32_t j = (uint32_t)G.fi - sd.field_begin;
+                        if (atomicOr(&L.fseen[mm], 1u << j) & (1u << j)) fail = 1; /* a duplicate key */
+                        else fmap[j * FL_MPB + mm] = (uint8_t)k;
+                    }
+                }
+            }
+            if (ballot(fail != 0) && lane == 0) atomicOr(&L.noremap, 1u);
+            __syncthreads();
+        }
+        const bool remap = remap_try && (L.noremap & 1u) == 0; /* block-uniform */
         for (uint32_t r = 0; r < rounds; r++) {
             FField F[FL_FPW];
+            uint32_t kslot[FL_FPW]; /* the position of F[h] in the message */
             uint16_t *sz = &L.size[(r & 1) * FL_SLOTS * FL_MPB];
 #pragma unroll
             for (uint32_t h = 0; h < FL_FPW; h++) {
                 FLF_T0();
-                parse(r * FL_SLOTS + fl_slot(wave, h), F[h]);
-                sz[fl_slot(wave, h) * FL_MPB + mm] = (uint16_t)F[h].size;
+                const uint32_t j = fl_slot(wave, h);
+                const uint32_t k = remap ? (uint32_t)fmap[j * FL_MPB + mm] : r * FL_SLOTS + j; /* 0xFF: no such field */
+                const uint32_t si = remap ? k : j; /* its position within the round */
+                kslot[h] = si;
+                parse(k, F[h]);
+                if (si < FL_SLOTS) sz[si * FL_MPB + mm] = (uint16_t)F[h].size;
+                if (remap && j >= nf) sz[j * FL_MPB + mm] = 0; /* positions past the message's fields */
                 FLF_ADD(r * FL_SLOTS + fl_slot(wave, h));
             }
             FLP(4);
@@ -1084,7 +1212,7 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
             for (uint32_t f = 0; f < FL_SLOTS; f++) {
                 const uint32_t v = sz[f * FL_MPB + mm];
 #pragma unroll
-                for (uint32_t h = 0; h < FL_FPW; h++) off[h] += f < fl_slot(wave, h) ? v : 0u;
+                for (uint32_t h = 0; h < FL_FPW; h++) off[h] += f < kslot[h] ? v : 0u;
                 tot += v;
             }
             nbytes += tot;

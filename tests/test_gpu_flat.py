@@ -304,3 +304,33 @@ def test_integer_tokens_vs_oracle(route):
     for flags in (0x1, 0x41, 0x5):
         bad = _compare(fl, msgs, flags | extra)
         assert not bad, (route, hex(flags), bad[:4])
+
+
+def test_flat_field_remap_shuffled_keys():
+    """Shuffled key order (c2s): the key pass maps each position to its
+    field and every wave converts one FIELD of its 64 messages
+    (j2t_flat.h 2a). No message leaves the flat kernel, and the bytes are
+    the small kernel's and the reference's; blocks with a duplicate key, an
+    unknown key or a malformed field fall back to positions."""
+    ctx = conv.default_context()
+    rng = random.Random(9)
+    td = W.simple_desc()
+    fl = T.flatten(td)
+    msgs = W.gen_flat_batch_shuffled(rng, 12000)
+    ctx.stats(reset=True)
+    o1, r1 = _raw_batch(fl, msgs, 0x1 | FLAT)
+    bails, _ = ctx.stats(reset=True)
+    o2, r2 = _raw_batch(fl, msgs, 0x1 | NO_FLAT)
+    assert o1 == o2 and list(r1) == list(r2)
+    assert bails == 0, bails
+    assert not _compare(fl, msgs[:3000], 0x1 | FLAT)
+    mixed = list(msgs[:640])
+    for i in range(0, 640, 67):
+        mixed[i] = mixed[i].replace(b'"I32Field"', b'"ByteField"', 1)  # a duplicate key
+    for i in range(5, 640, 131):
+        mixed[i] = mixed[i].replace(b'"I64Field"', b'"Nope"', 1)  # an unknown key
+    for i in range(9, 640, 97):
+        mixed[i] = mixed[i].replace(b'":', b'" :', 1)
+    for flags in (0x1, 0x11, 0x7):
+        bad = _compare(fl, mixed, flags | FLAT)
+        assert not bad, (hex(flags), bad[:4])
