@@ -126,7 +126,15 @@ struct WaveLds {
 #ifndef DG_WV_CH
 #define DG_WV_CH 8
 #endif
-constexpr uint32_t WV_CH = DG_WV_CH; /* input bytes per body chunk task (a multiple of 8) */
+constexpr uint32_t WV_CH = DG_WV_CH; /* input bytes per string-copy chunk task (a multiple of 8) */
+#ifndef DG_WV_CHB
+#define DG_WV_CHB 16
+#endif
+constexpr uint32_t WV_CHB = DG_WV_CHB; /* base64 characters per chunk task of a body longer than WV_CHB_MIN (a multiple
+                                        * of 8; r6i: C4's 48 KiB bodies 0.828 ms at 16 vs 0.863 at 8; C3's short ones
+                                        * prefer 8: 1.313 vs 1.329 ms) */
+constexpr uint32_t WV_CHB_MIN = 256;
+DGI uint32_t wv_task_bytes(bool bin, uint32_t n) { return bin && n > WV_CHB_MIN ? WV_CHB : WV_CH; }
 
 struct WaveParams {
     const uint8_t *blob; /* descriptor blob (device) */
@@ -1205,7 +1213,8 @@ DGI bool wave_run(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L
          * (task c belongs to the first lane whose inclusive chunk count
          * exceeds c), so the page's longest string does not set the time */
         {
-            const uint32_t nch = chunked ? (uint32_t)((cn + WV_CH - 1) / WV_CH) : 0u;
+            const uint32_t csz = wv_task_bytes(isbin, (uint32_t)cn);
+            const uint32_t nch = chunked ? (uint32_t)((cn + csz - 1) / csz) : 0u;
             const uint32_t cinc = wave_incl_sum(nch, lane);
             const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)cinc, 63);
             if (T) {
@@ -1214,23 +1223,31 @@ DGI bool wave_run(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L
                 L.cbd[lane] = opos + khead + 4;
                 L.cbn[lane] = (uint32_t)cn | (isbin ? 0x80000000u : 0u);
                 __builtin_amdgcn_wave_barrier();
+                uint32_t l = 0, lend = 0; /* the owner of this lane's previous task, its inclusive count */
 #if defined(DG_WV_ABL) && (DG_WV_ABL & 8)
                 for (uint32_t c = lane; c < 0; c += 64) { /* ablation: no body tasks */
 #else
                 for (uint32_t c = lane; c < T; c += 64) {
 #endif
-                    uint32_t l = 0;
+                    /* c only grows: a body longer than 64 tasks (C4's base64)
+                     * keeps its owner, checked with one LDS read instead of a
+                     * 6-read binary search per task */
+                    if (c >= lend) {
+                        l = 0;
 #pragma unroll
-                    for (uint32_t step = 32; step; step >>= 1)
-                        if (L.cinc[l + step - 1] <= c) l += step;
+                        for (uint32_t step = 32; step; step >>= 1)
+                            if (L.cinc[l + step - 1] <= c) l += step;
+                        lend = L.cinc[l];
+                    }
                     const uint32_t bn = L.cbn[l], blen = bn & 0x7FFFFFFFu;
-                    const uint32_t lch = (blen + WV_CH - 1) / WV_CH;
-                    const uint32_t k = c - (L.cinc[l] - lch);
-                    const int64_t s0 = (int64_t)L.cbs[l] + (int64_t)k * WV_CH;
-                    const int64_t n = (int64_t)min(WV_CH, blen - k * WV_CH);
+                    const uint32_t tsz = wv_task_bytes((bn >> 31) != 0, blen);
+                    const uint32_t lch = (blen + tsz - 1) / tsz;
+                    const uint32_t k = c - (lend - lch);
+                    const int64_t s0 = (int64_t)L.cbs[l] + (int64_t)k * tsz;
+                    const int64_t n = (int64_t)min(tsz, blen - k * tsz);
                     WOut w;
                     if (bn >> 31) {
-                        w.init(ob + L.cbd[l] + (uint64_t)k * (WV_CH / 4 * 3));
+                        w.init(ob + L.cbd[l] + (uint64_t)k * (tsz / 4 * 3));
                         if (!chunk_b64(src, s0, n, k + 1 == lch, w)) bad = true;
                     } else {
                         w.init(ob + L.cbd[l] + (uint64_t)k * WV_CH);
