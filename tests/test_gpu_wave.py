@@ -130,7 +130,8 @@ def test_wave_path_bails_are_exact():
 
 
 def test_wave_vs_lane_kernel_on_mixed_batch():
-    """C5-style mixed batch (flat + nested + large) through both kernels."""
+    """C5-style mixed batch (flat + nested + large) through both kernels,
+    and against the reference (not a self-comparison only)."""
     fl = T.flatten(W.mixed_desc())
     msgs = W.gen_mixed_batch(random.Random(45), 3000, large_scale=0.1)
     o1, r1, b1 = _run(fl, msgs, 1)
@@ -138,3 +139,6 @@ def test_wave_vs_lane_kernel_on_mixed_batch():
     assert list(r1) == list(r2)
     assert o1 == o2
     assert b1 == 0
+    er, eo = _checker().j2t_batch(fl, msgs, 1)
+    assert [int(r) for r in r1] == [int(r) for r in er]
+    assert list(o1) == list(eo)
