@@ -1344,7 +1344,11 @@ int dg_agg_wait_gen(dg_agg *a, uint64_t after, uint32_t timeout_us, uint64_t *do
 uint64_t dg_agg_ticket_gen(const dg_agg_ticket *t) { return t && t->batch ? t->gen : 0; }
 
 namespace {
-constexpr size_t GW_PREFETCH = 8; /* dg_agg_gateway_drive: results prefetched this many callers ahead */
+#ifndef DG_GW_PREFETCH
+#define DG_GW_PREFETCH 16
+#endif
+constexpr size_t GW_PREFETCH = DG_GW_PREFETCH; /* dg_agg_gateway_drive: results prefetched this many callers ahead
+                                                * (r6: 16 vs 8) */
 struct GwCaller {
     uint64_t next;  /* its next message */
     uint64_t cur;   /* the message in flight */
@@ -1432,6 +1436,7 @@ int dg_agg_gateway_drive(dg_agg *a, const uint8_t *arena, const uint64_t *in_off
                 for (size_t k = 0; k < run.size(); k++) {
                     const uint32_t c = run[k];
                     GwCaller &C = cs[c];
+                    if (k + 2 * GW_PREFETCH < run.size()) __builtin_prefetch(&cs[run[k + 2 * GW_PREFETCH]]);
                     if (k + GW_PREFETCH < run.size()) { /* a later caller's result: status, offsets (pinned, DMA-written: not in cache) */
                         const GwCaller &D = cs[run[k + GW_PREFETCH]];
                         if (D.has && D.t.batch) {

@@ -14,6 +14,8 @@ for spec in sys.argv[1:]:
         units = ("j2t_kern_flat.hip", "j2t_host.hip")
     elif all(f.startswith(("-DDG_T2W", "-DDG_T2J")) for f in fl):
         units = ("t2j_kern.hip",)
+    elif all(f.startswith("-DDG_GW") for f in fl):
+        units = ("j2t_pipe.hip",)
     else:
         units = ("j2t_kern_wave.hip", "j2t_kern_wave5.hip", "j2t_host.hip", "j2t_kern_flat.hip")
     b.build_hip(out=out, unit_flags={u: fl for u in units})
