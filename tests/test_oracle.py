@@ -6,7 +6,7 @@ import pytest
 
 import oracle
 import fuzz
-from dynamicgo_amd import thrift as T
+from dynamicgo_amd import thrift as T, workloads as W
 from schemas import probe, idl_desc
 
 
@@ -170,3 +170,19 @@ def test_unterminated_string_block_tail():
         assert r & 0xFF == 1 and (r >> 8) & 0xFFFFFFFF == len(m), (k, hex(r))  # ERR_EOF at len
         if ref is not None and k % 32:
             assert ref.j2t(fl, m, 1)[0] == r, k
+
+
+def test_batch_wrapper_redoes_outputs_larger_than_their_slot():
+    """j2t_batch sizes slots at 4x the message + 64; default writes of a tiny
+    message outgrow that ("{}" of NestingI64 with WRITE_DEFAULT: 120 bytes),
+    and the harness then reports the full length without the bytes. The
+    wrapper converts such messages again alone (found by tools/fuzz_sweep.py:
+    the batch checker returned zeros where the GPU was right)."""
+    fl = T.flatten(W.nesting_i64_desc())
+    msgs = [b"{}", b'{"I32":5}', b"{}"]
+    for o in [x for x in (oracle.RefOracle(), oracle.PortOracle()) if x]:
+        for flags in (0x2, 0x3, 0x7):
+            er, eo = o.j2t_batch(fl, msgs, flags)
+            want = [o.j2t(fl, m, flags) for m in msgs]
+            assert [(int(r), b) for r, b in zip(er, eo)] == want
+            assert all(len(b) > 4 * 2 + 64 for b in eo)

@@ -1,0 +1,40 @@
+"""A longer GPU fuzz sweep than the test suite (more seeds, every route):
+python tools/fuzz_sweep.py [seeds]  -> mismatches vs the oracle, per route"""
+import os
+import random
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+import fuzz  # noqa: E402
+import oracle  # noqa: E402
+from dynamicgo_amd import thrift as T, workloads as W  # noqa: E402
+from test_gpu_parity import _raw_batch  # noqa: E402
+from test_gpu_flat import flat_desc  # noqa: E402
+
+FLAT, NO_FLAT, NO_WAVE = 1 << 19, 1 << 21, 1 << 20
+chk = oracle.RefOracle() or oracle.PortOracle()
+seeds = int(sys.argv[1]) if len(sys.argv) > 1 else 12
+descs = {"flat": flat_desc(), "simple": W.simple_desc(), "nesting": W.nesting_i64_desc(), "mixed": W.mixed_desc()}
+total_bad = 0
+for name, td in descs.items():
+    fl = T.flatten(td)
+    for seed in range(seeds):
+        rng = random.Random(7000 + seed)
+        msgs = [fuzz.gen_message(rng, td, mutate_p=rng.random() < 0.3) for _ in range(800)]
+        if name == "simple":
+            msgs += W.gen_flat_batch_shuffled(rng, 400) + [fuzz.spacify(random.Random(k), m.decode()).encode()
+                                                        for k, m in enumerate(W.gen_flat_batch(rng, 200))]
+        for flags in (0x1, 0x0, 0x7, 0x41, 0x11):
+            er, eo = chk.j2t_batch(fl, msgs, flags & 0xFFFF)
+            for route, extra in (("default", 0), ("flat", FLAT), ("noflat", NO_FLAT)):
+                outs, rets = _raw_batch(fl, msgs, flags | extra)
+                bad = [i for i in range(len(msgs)) if int(rets[i]) != int(er[i]) or outs[i] != eo[i]]
+                if bad:
+                    total_bad += len(bad)
+                    print(f"MISMATCH {name} seed={seed} flags={flags:#x} route={route}: {len(bad)} e.g. {msgs[bad[0]][:200]!r} "
+                          f"got {int(rets[bad[0]]):#x} want {int(er[bad[0]]):#x}", flush=True)
+    print(f"{name}: done", flush=True)
+print("total mismatches", total_bad)
+sys.exit(1 if total_bad else 0)
