@@ -15,22 +15,34 @@ from test_gpu_flat import flat_desc  # noqa: E402
 
 FLAT, NO_FLAT, NO_WAVE = 1 << 19, 1 << 21, 1 << 20
 chk = oracle.RefOracle() or oracle.PortOracle()
+port = oracle.PortOracle()
 seeds = int(sys.argv[1]) if len(sys.argv) > 1 else 12
+FLAGS = [int(x, 0) for x in os.environ.get("FUZZ_FLAGS", "0x1,0x0,0x7,0x41,0x11").split(",")]
+SEED0 = int(os.environ.get("FUZZ_SEED0", "7000"))
 descs = {"flat": flat_desc(), "simple": W.simple_desc(), "nesting": W.nesting_i64_desc(), "mixed": W.mixed_desc()}
 total_bad = 0
 for name, td in descs.items():
     fl = T.flatten(td)
     for seed in range(seeds):
-        rng = random.Random(7000 + seed)
+        rng = random.Random(SEED0 + seed)
         msgs = [fuzz.gen_message(rng, td, mutate_p=rng.random() < 0.3) for _ in range(800)]
         if name == "simple":
             msgs += W.gen_flat_batch_shuffled(rng, 400) + [fuzz.spacify(random.Random(k), m.decode()).encode()
                                                         for k, m in enumerate(W.gen_flat_batch(rng, 200))]
-        for flags in (0x1, 0x0, 0x7, 0x41, 0x11):
+        for flags in FLAGS:
             er, eo = chk.j2t_batch(fl, msgs, flags & 0xFFFF)
             for route, extra in (("default", 0), ("flat", FLAT), ("noflat", NO_FLAT)):
                 outs, rets = _raw_batch(fl, msgs, flags | extra)
                 bad = [i for i in range(len(msgs)) if int(rets[i]) != int(er[i]) or outs[i] != eo[i]]
+                # DESIGN.md §4's one documented exception: an unterminated string
+                # ending on a 32-byte block boundary, where the reference reads a
+                # stale register and reports a position past the end; the port
+                # (and the GPU) report ERR_EOF at the end
+                ub = [i for i in bad if (int(er[i]) >> 8) & 0xFFFFFFFF > len(msgs[i]) and
+                      port.j2t(fl, msgs[i], flags & 0xFFFF) == (int(rets[i]), outs[i])]
+                if ub:
+                    print(f"documented reference exception {name} seed={seed} flags={flags:#x} route={route}: {len(ub)}", flush=True)
+                bad = [i for i in bad if i not in ub]
                 if bad:
                     total_bad += len(bad)
                     print(f"MISMATCH {name} seed={seed} flags={flags:#x} route={route}: {len(bad)} e.g. {msgs[bad[0]][:200]!r} "
