@@ -68,6 +68,7 @@ T2J_METRIC = "conv/t2j GB/s Thrift in + msgs/s, 64K-batch device-resident"
 # faster or equal: C5's 1M batch (4.45 vs 4.73 ms), t2j-c3 (1.48 vs 1.50 ms;
 # its wave kernel's workspace is ordered across streams)
 DEFAULT_INFLIGHT = {"c5": 1, "t2j-c3": 1}
+KERNEL_NAMES = (("j2t_flat_kernel", "j2t_small_kernel"), "j2t_wave_kernel")  # first launch (flat | small), wave
 FLAGS = {"c2x": 0x7}  # default: conv.Options{} -> F_ALLOW_UNKNOWN (conv/j2t/conv.go:102-104)
 
 
@@ -241,12 +242,13 @@ def host_cpu_env() -> dict:
 def cpu_baseline(flat, arena, off, flags, budget_s: float = 6.0):
     """The reference's own native/*.c (oracle/_ref, clang -O3 like the
     reference's build) on this host, outputs preallocated and first touched by
-    an untimed pass, best of reps, byte-balanced shards, threads pinned to
+    an untimed pass, median of reps, byte-balanced shards, threads pinned to
     distinct physical cores:
-      * value: ALL physical cores this process may use (one
-        thread per physical core);
-      * share: min(CPU_SHARE, physical) cores, the host CPUs the GPU box
-        grants per GPU;
+      * value: the cores that can actually run at once, i.e. the physical
+        cores of the affinity mask capped by the cgroup CPU quota (16 on the
+        GPU box: more threads than the quota only throttle);
+      * all_affinity: one thread per physical core of the affinity mask
+        (SURVEY.md §8(d)), reported beside it with the quota's throttling;
       * one core over a bounded prefix."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # reported baseline only
@@ -255,7 +257,8 @@ def cpu_baseline(flat, arena, off, flags, budget_s: float = 6.0):
         return None
     phys, logical = oracle.physical_cpus()
     cores_all = max(1, len(phys))
-    cores = max(1, min(CPU_SHARE, len(phys)))
+    quota = host_cpu_env().get("quota_cpus")
+    cores = max(1, min(CPU_SHARE, len(phys), int(quota) if quota else len(phys)))
     n = len(off) - 1
     nbytes = int(off[-1] - off[0])
 
@@ -266,34 +269,48 @@ def cpu_baseline(flat, arena, off, flags, budget_s: float = 6.0):
         ref.j2t_timed(flat, a, o, flags, cpus, reps, times=ts)
         return float(np.median(ts)), ts
 
+    env_s = host_cpu_env()
+    t_share, ts_share = timed(arena, off, phys[:cores])
     env0 = host_cpu_env()
-    t_all, ts_all = timed(arena, off, phys[:cores_all])
+    t_all, ts_all = (t_share, ts_share) if cores == cores_all else timed(arena, off, phys[:cores_all])
     env1 = host_cpu_env()
-    t_share, ts_share = (t_all, ts_all) if cores == cores_all else timed(arena, off, phys[:cores])
     # one core: a prefix of at most ~64 MB / 65536 messages
     k = int(min(n, 65536, max(1, np.searchsorted(off, off[0] + 64 * 1024 * 1024))))
     a1, o1 = arena[:int(off[k]) + 64], off[:k + 1]
     t_one, ts_one = timed(a1, o1, phys[:1])
     one_bytes = int(o1[-1] - o1[0])
     spread = lambda nb, ts: {"min": round(nb / max(ts) / 1e9, 4), "max": round(nb / min(ts) / 1e9, 4),
+                             "p5": round(nb / float(np.percentile(ts, 95)) / 1e9, 4),
+                             "p95": round(nb / float(np.percentile(ts, 5)) / 1e9, 4),
                              "best_of_5": round(nb / min(ts[:5]) / 1e9, 4)}
-    thr = None
-    if "throttle" in env0 and "throttle" in env1:
-        thr = {k: env1["throttle"][k] - env0["throttle"].get(k, 0) for k in env1["throttle"]}
-    return {"value": round(nbytes / t_all / 1e9, 4), "unit": "GB/s", "cores": cores_all, "kind": "reference",
-            "stat": "median of the passes", "range": spread(nbytes, ts_all),
-            "cpu_model": cpu_model(), "msgs_per_s": round(n / t_all),
-            "share": {"cores": cores, "value": round(nbytes / t_share / 1e9, 4), "msgs_per_s": round(n / t_share),
-                      "range": spread(nbytes, ts_share), "note": f"the {CPU_SHARE} CPUs per GPU the box grants"},
+    def throttled(a, b):
+        if "throttle" in a and "throttle" in b:
+            return {k: b["throttle"][k] - a["throttle"].get(k, 0) for k in b["throttle"]}
+        return None
+
+    v_share = nbytes / t_share / 1e9
+    return {"value": round(v_share, 4), "unit": "GB/s", "cores": cores, "kind": "reference",
+            "stat": "median of the passes", "range": spread(nbytes, ts_share),
+            "range_ratio": round(max(ts_share) / min(ts_share), 3),
+            "range_ratio_p5_p95": round(float(np.percentile(ts_share, 95) / np.percentile(ts_share, 5)), 3),
+            "cpu_model": cpu_model(), "msgs_per_s": round(n / t_share),
+            "per_core_gbs": round(v_share / cores, 4), "throttling_delta": throttled(env_s, env0),
+            "cores_rule": f"min({CPU_SHARE} CPUs per GPU, physical cores in affinity {len(phys)}, "
+                          f"cgroup quota {quota})",
+            "all_affinity": {"cores": cores_all, "value": round(nbytes / t_all / 1e9, 4),
+                             "msgs_per_s": round(n / t_all), "range": spread(nbytes, ts_all),
+                             "throttling_delta": throttled(env0, env1),
+                             "note": "one thread per physical core of the affinity mask; above the quota the "
+                                     "threads only share the quota's CPU time"},
             "one_core_gbs": round(one_bytes / t_one / 1e9, 4), "one_core_ns_per_msg": round(t_one / k * 1e9, 1),
             "one_core_range": spread(one_bytes, ts_one),
-            "per_core_gbs": round(nbytes / t_all / 1e9 / cores_all, 4),
-            "host": env0, "all_core_throttling_delta": thr,
-            "sample": f"all-core: the rank's whole batch ({n} msgs, {nbytes} B), median (min/max in range) of "
-                      f"{len(ts_all)} passes, {cores_all} threads pinned to distinct physical cores of "
-                      f"'{cpu_model()}' (affinity: {logical} logical CPUs = {len(phys)} physical cores); share: "
-                      f"{cores} cores, {len(ts_share)} passes; one-core: first {k} msgs ({one_bytes} B), "
-                      f"{len(ts_one)} passes; reference native.c built by oracle/Makefile (clang -O3 -mavx2)"}
+            "host": env_s,
+            "sample": f"the rank's whole batch ({n} msgs, {nbytes} B), median (min/max in range) of "
+                      f"{len(ts_share)} passes, {cores} threads pinned to distinct physical cores of "
+                      f"'{cpu_model()}' (affinity: {logical} logical CPUs = {len(phys)} physical cores, quota "
+                      f"{quota} CPUs); all_affinity: {cores_all} threads, {len(ts_all)} passes; one-core: first "
+                      f"{k} msgs ({one_bytes} B), {len(ts_one)} passes; reference native.c built by "
+                      f"oracle/Makefile (clang -O3 -mavx2)"}
 
 
 # ---------------------------------------------------------------- end to end
@@ -920,6 +937,16 @@ def main(argv=None):
     json_bytes = int(off[-1])
     thrift_bytes = int(d_ol.to(torch.int64).sum().item())
     alg_bytes = json_bytes + thrift_bytes + PER_MSG_META * n
+    # the algorithmic bytes of the messages each kernel converts: the wave
+    # kernel takes messages longer than the wave_min knob, the first kernel
+    # (flat / small / lane) the rest (declines to the list pass are counted
+    # with the kernel that listed them: exact_path_msgs_per_step is ~0)
+    wmin = C.c_int64(0)
+    _lib.check(L.dg_ctx_get_knob(ctx.h, b"wave_min", C.byref(wmin)))
+    big = lens > wmin.value
+    ol_np = d_ol.cpu().numpy().astype(np.int64)
+    route_bytes = [int(lens[~big].sum() + ol_np[~big].sum() + PER_MSG_META * int((~big).sum())),
+                   int(lens[big].sum() + ol_np[big].sum() + PER_MSG_META * int(big.sum()))]
 
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
@@ -931,6 +958,14 @@ def main(argv=None):
     ev1.record(stream)
     torch.cuda.synchronize()
     gpu_ms = ev0.elapsed_time(ev1) / args.steps
+    # per-kernel leg: the same serial steps with HIP events around each launch
+    # of the step (on the launch stream), for the dominant kernel's roofline
+    kms = (C.c_double * 3)()
+    _lib.check(L.dg_j2t_batch_device_ktime(ctx.h, dh, flat.root_type, d_json.data_ptr(), d_in.data_ptr(), n, flags,
+                                           d_out.data_ptr(), d_oo.data_ptr(), d_ol.data_ptr(), d_ret.data_ptr(),
+                                           d_pend.data_ptr(), stream.cuda_stream, max_len, args.steps, kms))
+    kernel_ms = list(kms)
+    dom = int(np.argmax(kernel_ms[:2]))
     if depth > 1:  # warm the in-flight streams and check every set converted the batch
         step_inflight(args.warmup * depth)
         torch.cuda.synchronize()
@@ -964,6 +999,8 @@ def main(argv=None):
     total_msgs = sum(p[2] for p in per_rank)
     value = total_json / wall_max * args.steps / 1e9
     achieved = alg_bytes / (gpu_ms / 1e3) / 1e9
+    dom_achieved = route_bytes[dom] / (kernel_ms[dom] / 1e3) / 1e9 if kernel_ms[dom] > 0 else 0.0
+    flat_route = args.config in ("c1", "c2", "c2x", "c2s", "c5")  # flat root, or C5's wrapped flat members
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -1011,11 +1048,20 @@ def main(argv=None):
                        "inflight": depth,
                        "per_rank_inflight_step_ms": [round(p[4], 5) for p in per_rank],
                        "serial_gbs": round(total_json / max(p[3] for p in per_rank) / 1e6, 3)},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+            "roofline": {"bound": "hbm", "achieved": round(dom_achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(dom_achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "traffic_source": f"profiles/traffic_{args.config}.json (PMC, committed)" if traffic else None,
-                         "kernel_ms": round(gpu_ms, 5), "kernel_ms_note": "one batch at a time (serial leg), every launch of the step",
-                         "alg_bytes_per_launch": alg_bytes},
+                         "kernel": KERNEL_NAMES[dom][0 if flat_route else 1] if dom == 0 else KERNEL_NAMES[1],
+                         "kernel_ms": round(kernel_ms[dom], 5),
+                         "alg_bytes_per_launch": route_bytes[dom],
+                         "kernel_ms_note": "the dominant kernel's average launch, HIP events on its launch stream "
+                                           "(dg_j2t_batch_device_ktime, serial leg); alg bytes = JSON + Thrift + 28 "
+                                           "per message it converts",
+                         "per_kernel_ms": {"first": round(kernel_ms[0], 5), "wave": round(kernel_ms[1], 5),
+                                           "list_pass": round(kernel_ms[2], 5)},
+                         "step": {"achieved": round(achieved, 2), "frac": round(achieved / HBM_PEAK_GBS, 5),
+                                  "ms": round(gpu_ms, 5), "alg_bytes": alg_bytes,
+                                  "note": "every launch of the serial step (incl. list pass and launch gaps)"}},
             "cpu_baseline": cpu,
         }
         if e2e is not None:

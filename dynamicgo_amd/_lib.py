@@ -16,7 +16,7 @@ EXPORTS = ["dg_last_error", "dg_build_info", "dg_ctx_create", "dg_ctx_destroy", 
            "dg_desc_create",
            "dg_desc_create_device", "dg_desc_destroy", "dg_desc_root", "dg_j2t_batch_device",
            "dg_j2t_batch_device_ml", "dg_j2t_batch_device_hm", "dg_j2t_batch_device_cb", "dg_j2t_batch_device_iters",
-           "dg_j2t_batch_device_inflight",
+           "dg_j2t_batch_device_inflight", "dg_j2t_batch_device_ktime",
            "dg_slot_bound", "dg_j2t_batch_host", "dg_j2t_batch_host_hm", "dg_j2t_batch_host_cb", "dg_j2t_do", "dg_pack_device", "dg_pack_device_scan", "dg_pack_device_framed", "dg_agg_create", "dg_agg_create2", "dg_agg_do",
            "dg_agg_submit", "dg_agg_wait", "dg_agg_ready", "dg_agg_stats", "dg_agg_profile", "dg_agg_destroy", "dg_agg_drive", "dg_agg_wait_gen", "dg_agg_ticket_gen", "dg_agg_set_knob",
            "dg_agg_gateway_drive", "dg_j2t_pipeline_host", "dg_bench_device", "dg_desc_attach_t2j", "dg_t2j_slot_bound", "dg_t2j_batch_device", "dg_t2j_batch_device_ml",
@@ -68,6 +68,8 @@ def lib() -> C.CDLL:
         "dg_j2t_batch_device_cb": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, vp, vp, vp, vp, vp, vp, u64]),
         "dg_j2t_batch_host_cb": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, vp, u64, vp, vp, P64]),
         "dg_j2t_batch_device_iters": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, vp, vp, vp, vp, vp, u64, C.c_int]),
+        "dg_j2t_batch_device_ktime": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, vp, vp, vp, vp, vp, u64, C.c_int,
+                                           C.POINTER(C.c_double)]),
         "dg_j2t_batch_device_inflight": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, vp, C.c_int, vp, u64, C.c_int]),
         "dg_slot_bound": (u64, [u64]),
         "dg_j2t_batch_host": (i32, [vp, vp, u32, vp, vp, u64, u64, vp, u64, vp, vp, P64]),

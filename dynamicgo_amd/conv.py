@@ -458,9 +458,12 @@ class BinaryConv:
                 rec, r = outs[i], int(rets[i])
                 outs[i] = b""
                 try:
+                    recs = _cb_records(rec, r)
+                    if not recs:  # an empty record list would rerun the message unchanged forever
+                        raise H.ConvError("ErrConvert", "callback record list is empty")
                     # served in the order the message meets them: a failing
                     # callback is the error, as in the reference's Go loop
-                    for rk, reck in _cb_records(rec, r):
+                    for rk, reck in recs:
                         answers.setdefault(i, []).append(serve(i, rk, reck))
                 except H.ConvError as e:
                     errs[i] = e

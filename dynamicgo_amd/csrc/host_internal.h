@@ -137,6 +137,10 @@ struct dg_ctx {
     std::vector<hipStream_t> side;
     std::vector<hipEvent_t> side_ev;
     hipEvent_t fork_ev = nullptr;
+    /* dg_j2t_batch_device_ktime: while set, enqueue() records kt[0] before the
+     * batch's first kernel, kt[1] after it, kt[2] after the wave kernel and
+     * kt[3] after the list pass (timing events, on the launch stream) */
+    hipEvent_t *kt = nullptr;
 };
 
 /* frees the context's pipeline buffers (j2t_pipe.hip) */

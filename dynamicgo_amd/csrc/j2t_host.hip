@@ -454,6 +454,9 @@ static int enqueue(dg_ctx *c, Scratch *x, const dg_desc *d, uint32_t root, const
                                       : (flags & DG_F_FLAT_PATH) != 0 ||
                                             (!(flags & DG_F_NO_FLAT_PATH) && (max_len == 0 || max_len <= FL_MAXLEN));
     const bool no_flat = (flags & DG_F_NO_FLAT_PATH) != 0 || K.flat == 0;
+    auto mark = [&](int i) {
+        if (c->kt) (void)hipEventRecord(c->kt[i], s);
+    };
     flags &= ~(DG_F_NO_WAVE_PATH | DG_F_FLAT_PATH | DG_F_NO_FLAT_PATH);
     Params P;
     P.root = root;
@@ -550,12 +553,15 @@ static int enqueue(dg_ctx *c, Scratch *x, const dg_desc *d, uint32_t root, const
             FP.wrap = wrap_ok ? 1u : 0u;
             FP.wrap_inner = wrap_ok ? inner : 0u;
             FP.wrap_ok = wrap_ok;
+            mark(0);
             launch_flat_kernel(dim3((uint32_t)((n + FL_MPB - 1) / FL_MPB)), s, P1, FP);
         } else {
             const uint64_t mpb = (uint64_t)SM_WAVES * (uint64_t)(mpw >= 64 ? 64 : mpw == 16 ? 16 : 32);
+            mark(0);
             launch_small_kernel(mpw, dim3((uint32_t)((n + mpb - 1) / mpb)), s, P1, S);
         }
         HIPCHK(hipGetLastError());
+        mark(1);
         if (need_wave) {
             WaveParams W;
             W.blob = d->d_blob;
@@ -571,14 +577,20 @@ static int enqueue(dg_ctx *c, Scratch *x, const dg_desc *d, uint32_t root, const
             wave_launch(s, P, W);
             HIPCHK(hipGetLastError());
         }
+        mark(2);
         Params P3 = P;
         P3.list = x->d_bail_list;
         P3.list_count = x->d_counts;
         P3.reset2 = x->d_counts + 1; /* P3.fast stays set: the small kernel's declines try the full fast path */
         const uint64_t lb = (uint64_t)std::max<int64_t>(1, K.list_blocks); /* list-pass grid */
         lane_launch(dim3((uint32_t)std::min<uint64_t>(blocks, lb)), P3);
+        mark(3);
     } else if (!wave) {
+        mark(0);
         lane_launch(dim3((uint32_t)blocks), P);
+        mark(1);
+        mark(2);
+        mark(3);
     } else {
         /* 1. lane kernel: small messages (lane fast path + exact machine);
          *    messages longer than big_max are listed for the wave kernel
@@ -591,8 +603,10 @@ static int enqueue(dg_ctx *c, Scratch *x, const dg_desc *d, uint32_t root, const
         P1.big_count = x->d_counts + 1;
         P1.big_max = big_max;
         P1.huge_count = x->d_counts + 3;
+        mark(0);
         lane_launch(dim3((uint32_t)blocks), P1);
         HIPCHK(hipGetLastError());
+        mark(1);
         WaveParams W;
         W.blob = d->d_blob;
         W.hdr = d->hdr;
@@ -606,12 +620,14 @@ static int enqueue(dg_ctx *c, Scratch *x, const dg_desc *d, uint32_t root, const
         W.queue = x->d_counts + 2;
         wave_launch(s, P, W);
         HIPCHK(hipGetLastError());
+        mark(2);
         Params P3 = P;
         P3.list = x->d_bail_list;
         P3.list_count = x->d_counts;
         P3.reset2 = x->d_counts + 1;
         P3.fast = 0;
         lane_launch(dim3((uint32_t)std::min<uint64_t>(blocks, 32)), P3);
+        mark(3);
     }
     HIPCHK(hipGetLastError());
     return DG_OK;
@@ -702,6 +718,38 @@ int dg_j2t_batch_device_iters(dg_ctx *c, const dg_desc *d, uint32_t root, const 
         if (rc) return rc;
     }
     return DG_OK;
+}
+
+int dg_j2t_batch_device_ktime(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *d_json,
+                              const uint64_t *d_in_off, uint64_t n, uint64_t flags, uint8_t *d_out,
+                              const uint64_t *d_out_off, uint32_t *d_out_len, uint64_t *d_ret, uint32_t *d_pending,
+                              void *stream, uint64_t max_len, int iters, double *ms)
+{
+    if (!c || !d || iters < 1 || !ms) return set_err(DG_E_INVALID, "bad args");
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    std::vector<hipEvent_t> ev((size_t)iters * 4, nullptr);
+    int rc = DG_OK;
+    for (auto &e : ev)
+        if (hipEventCreate(&e) != hipSuccess) rc = set_err(DG_E_HIP, "hipEventCreate");
+    for (int k = 0; k < iters && !rc; k++) {
+        c->kt = &ev[(size_t)k * 4];
+        rc = launch(c, d, root, d_json, d_in_off, n, flags, d_out, d_out_off, d_out_len, d_ret, d_pending, s, max_len);
+    }
+    c->kt = nullptr;
+    ms[0] = ms[1] = ms[2] = 0;
+    if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = set_err(DG_E_HIP, "hipStreamSynchronize");
+    for (int k = 0; k < iters && !rc; k++)
+        for (int i = 0; i < 3; i++) {
+            float t = 0;
+            if (hipEventElapsedTime(&t, ev[(size_t)k * 4 + i], ev[(size_t)k * 4 + i + 1]) != hipSuccess)
+                rc = set_err(DG_E_HIP, "hipEventElapsedTime");
+            ms[i] += t / iters;
+        }
+    for (auto &e : ev)
+        if (e) (void)hipEventDestroy(e);
+    return rc;
 }
 
 int dg_j2t_batch_device_inflight(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *d_json,

@@ -147,6 +147,7 @@ struct Machine {
     uint32_t ans_seen;          /* non-inline value-mapping values met so far */
     uint64_t ans_at;            /* hm_bytes offset of the next answer */
     uint32_t ncb;               /* DG_F_CB_COLLECT: callbacks recorded in this pass */
+    uint32_t cb_need;           /* ... the slot bytes the first record needs when it does not fit */
     uint64_t slot_cap;          /* ... the slot's size (out.cap is 0 once one is: the output is dropped) */
     Out rec;                    /* ... their records, from the slot's start */
     JState jt;
@@ -269,7 +270,7 @@ struct Machine {
         field_cache_len = 0;
         if (take_answer()) return 0;
         if (flag & DG_F_CB_COLLECT) {
-            if (!cb_room(16 + 8 * sd.req_words)) return pack(DG_ST_CB_LIST, ncb, 0);
+            if (!cb_room(16 + 8 * sd.req_words)) return cb_full(16 + 8 * sd.req_words);
             rec.w64(pack(DG_ST_HM_END_AT, sd.req_words, (uint64_t)p));
             rec.w64(si);
             for (uint32_t w = 0; w < sd.req_words; w++) {
@@ -314,6 +315,18 @@ struct Machine {
             out.cap = 0;
         }
         return rec.len + bytes <= slot_cap;
+    }
+
+    /* a record does not fit the slot: the records so far go to the host, or,
+     * when there are none, the slot is too small even for the first one and
+     * the host reruns the message with a slot of the bytes needed (as for
+     * any output overflow) instead of getting an empty record list */
+    DGI uint64_t cb_full(uint32_t bytes)
+    {
+        if (ncb) return pack(DG_ST_CB_LIST, ncb, 0);
+        out.cap = slot_cap;
+        cb_need = bytes;
+        return pack(DG_ST_OUT_OVERFLOW, bytes, 0);
     }
 
     /* the host's next callback answer (dg_cb_entry), if it has one: written */
@@ -631,7 +644,7 @@ struct Machine {
         }
         if (take_answer()) return 0; /* the host's answer for this value (dg_cb_entry) */
         if (flag & DG_F_CB_COLLECT) { /* recorded; the machine converts on */
-            if (!cb_room(24)) return pack(DG_ST_CB_LIST, ncb, 0);
+            if (!cb_room(24)) return cb_full(24);
             rec.w64(pack0(E_VM_END, (uint64_t)p));
             rec.w64((uint64_t)s0);
             rec.w64((uint64_t)fidx);
@@ -945,6 +958,7 @@ DGI uint64_t convert_one(const Params &P, const DV &dv, uint64_t i, const S &src
     m.ans_seen = 0;
     m.ans_at = m.ans_row ? m.ans_row->off : 0;
     m.ncb = 0;
+    m.cb_need = 0;
     uint64_t r;
     if (m.src.n == 0) { /* empty body -> STOP (conv/j2t/impl.go:52-82) */
         m.out.w8(0);
@@ -974,6 +988,10 @@ DGI uint64_t convert_one(const Params &P, const DV &dv, uint64_t i, const S &src
         m.rec.finish();
         olen = (uint32_t)m.rec.len;
         return pack(DG_ST_CB_LIST, m.ncb < 0xFFFFFFu ? m.ncb : 0xFFFFFFu, 0);
+    }
+    if (m.cb_need && (uint8_t)r == DG_ST_OUT_OVERFLOW) { /* cb_full: no room for the first record */
+        olen = m.cb_need;
+        return r;
     }
     /* HM_END: the host completes the output; VM_END / HM_END_AT: the callback's record */
     const bool keep = r == 0 || (uint8_t)r == DG_ST_HM_END || (uint8_t)r == E_VM_END || (uint8_t)r == DG_ST_HM_END_AT;

@@ -256,7 +256,13 @@ constexpr int AGG_SHARED = 32;  /* the last AGG_SHARED parts are shared: a threa
 constexpr int AGG_EXCL = AGG_SLOTS - AGG_SHARED;
 constexpr int AGG_GEN_RING = 64; /* dg_agg_gateway_drive: parked callers by generation (> AGG_RING_MAX + 2) */
 constexpr int AGG_EAGER_INFLIGHT = 1;
-constexpr uint64_t AGG_EXACT_MAX = 512ull << 20; /* launch(): per-batch buffers sized for the parts' caps up to this (64 MiB: gateway parts of 4096 calls grew buffers batch after batch, 332 us per batch, r5y) */
+/* launch(): each batch's buffers are sized for the registered parts' caps
+ * summed (no regrowth mid-run: gateway parts of 4096 calls grew buffers batch
+ * after batch, 332 us per batch, r5y) while that exact size times the ring
+ * stays within this budget of packed output (knob "exact_total"); above it a
+ * batch grows lazily to twice what it needed. Every batch of the ring holds
+ * about 1x the packed size in pinned host memory and ~5x in device memory. */
+constexpr uint64_t AGG_EXACT_TOTAL = 4ull << 30;
 
 /* one caller thread's part of one batch (its own cache lines) */
 struct alignas(128) Sub {
@@ -333,6 +339,7 @@ struct dg_agg {
      * round trip (r5y: 65536 callers, 4428-call batches, the flusher waiting
      * 536 us a batch for a free one) */
     std::atomic<uint32_t> min_fill{0};
+    std::atomic<uint64_t> exact_total{AGG_EXACT_TOTAL}; /* knob "exact_total" (bytes), see AGG_EXACT_TOTAL */
     uint64_t open_calls(const Batch *x) const
     {
         uint64_t k = 0;
@@ -506,10 +513,10 @@ int dg_agg::launch(Batch *x)
     /* Buffers for the largest batch the registered parts can make (their
      * caps summed), so a batch never grows them again until a new thread
      * registers: hipFree / hipHostFree wait for the whole device, every batch
-     * in flight. Above AGG_EXACT_MAX bytes of packed output, growth is for
-     * twice the batch that needed it instead. */
+     * in flight. When that size over the whole ring exceeds exact_total
+     * bytes, growth is for twice the batch that needed it instead. */
     const uint64_t Nx = (uint64_t)ns * cap_n, Bx = (uint64_t)ns * cap_b;
-    const bool exact = slot_off(Bx, Nx) <= AGG_EXACT_MAX;
+    const bool exact = slot_off(Bx, Nx) * (uint64_t)ring <= exact_total.load(std::memory_order_relaxed);
     const uint64_t Ng = exact ? Nx : 2 * N + 64, Bg = exact ? Bx : 2 * B + 4096;
     if ((rc = x->dv.reserve(exact ? Nx : N, exact ? Bx : B, exact))) return rc;
     if (x->h_hdr_cap < 16 * N + 8 && (rc = grow_pinned(x->h_hdr, x->h_hdr_cap, 16 * Ng + 8))) return rc;
@@ -1318,6 +1325,9 @@ int dg_agg_set_knob(dg_agg *a, const char *name, int64_t value)
         a->depth.store((int)std::max<int64_t>(0, std::min<int64_t>(value, a->ring - 2)), std::memory_order_relaxed);
     } else if (!strcmp(name, "min_fill")) {
         a->min_fill.store((uint32_t)std::max<int64_t>(0, std::min<int64_t>(value, 1ll << 30)), std::memory_order_relaxed);
+    } else if (!strcmp(name, "exact_total")) {
+        if (value < 0) return set_err(DG_E_INVALID, "exact_total < 0");
+        a->exact_total.store((uint64_t)value, std::memory_order_relaxed);
     } else if (!strcmp(name, "max_wait_us")) {
         if (value < 0) return set_err(DG_E_INVALID, "max_wait_us < 0");
         std::lock_guard<std::mutex> g(a->mu);
@@ -1379,6 +1389,10 @@ int dg_agg_gateway_drive(dg_agg *a, const uint8_t *arena, const uint64_t *in_off
     if (!a || !arena || !in_off || workers < 1 || callers < 1 || !out || !out_off || !out_len || !ret || !seconds)
         return set_err(DG_E_INVALID, "bad args");
     const uint32_t G = (uint32_t)std::min<uint64_t>((uint64_t)callers, std::max<uint64_t>(n, 1));
+    /* every worker owns a range of the messages and must have callers to
+     * serve it: with fewer callers (or messages) than workers, the extra
+     * workers would own messages nobody submits and the drive never ends */
+    workers = (int)std::min<uint64_t>((uint64_t)workers, G);
     std::vector<GwCaller> cs(G);
     for (uint32_t c = 0; c < G; c++) cs[c] = GwCaller{c, 0, 0, dg_agg_ticket{}, false};
     std::vector<GwWorker> wk(workers);
@@ -1438,8 +1452,11 @@ int dg_agg_gateway_drive(dg_agg *a, const uint8_t *arena, const uint64_t *in_off
                     GwCaller &C = cs[c];
                     if (k + 2 * GW_PREFETCH < run.size()) __builtin_prefetch(&cs[run[k + 2 * GW_PREFETCH]]);
                     if (k + GW_PREFETCH < run.size()) { /* a later caller's result: status, offsets (pinned, DMA-written: not in cache) */
+                        /* only callers of published generations: a retried
+                         * caller's batch may still be filling (its header and
+                         * offsets not written yet, or being regrown) */
                         const GwCaller &D = cs[run[k + GW_PREFETCH]];
-                        if (D.has && D.t.batch) {
+                        if (D.has && D.t.batch && D.t.gen <= seen) {
                             const Batch *x = (const Batch *)D.t.batch;
                             const uint64_t i = x->sub[D.t.idx >> 24].gbase + (D.t.idx & 0xFFFFFFu);
                             __builtin_prefetch(x->ret() + i);
@@ -1448,7 +1465,7 @@ int dg_agg_gateway_drive(dg_agg *a, const uint8_t *arena, const uint64_t *in_off
                     }
                     if (k + GW_PREFETCH / 2 < run.size()) { /* ... and, its offsets now cached, its packed bytes */
                         const GwCaller &D = cs[run[k + GW_PREFETCH / 2]];
-                        if (D.has && D.t.batch) {
+                        if (D.has && D.t.batch && D.t.gen <= seen) {
                             const Batch *x = (const Batch *)D.t.batch;
                             const uint64_t i = x->sub[D.t.idx >> 24].gbase + (D.t.idx & 0xFFFFFFu);
                             const uint8_t *q = x->h_packed + x->pack_off()[i];

@@ -164,6 +164,17 @@ int dg_j2t_batch_device_iters(dg_ctx *ctx, const dg_desc *desc, uint32_t root_ty
                               const uint64_t *d_out_off, uint32_t *d_out_len, uint64_t *d_ret,
                               uint32_t *d_pending, void *stream, uint64_t max_len, int iters);
 
+/* dg_j2t_batch_device_iters with HIP timing events around each of the batch's
+ * launches (measurement only: the events add a few microseconds between
+ * kernels). ms[0] = the first kernel (flat, small or lane), ms[1] = the wave
+ * kernel, ms[2] = the list pass (exact machine), each averaged over `iters`
+ * serial conversions; 0 for a launch the route does not make. Returns after
+ * the stream has drained. */
+int dg_j2t_batch_device_ktime(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, const uint8_t *d_json,
+                              const uint64_t *d_in_off, uint64_t n, uint64_t flags, uint8_t *d_out,
+                              const uint64_t *d_out_off, uint32_t *d_out_len, uint64_t *d_ret,
+                              uint32_t *d_pending, void *stream, uint64_t max_len, int iters, double *ms);
+
 /* One in-flight batch's outputs (dg_j2t_batch_device_inflight). */
 typedef struct dg_out_set {
     uint8_t *d_out;      /* slot arena, laid out by the shared d_out_off */
@@ -269,9 +280,15 @@ int dg_agg_do(dg_agg *agg, const uint8_t *json, size_t len, uint8_t *out, size_t
  * last 32 parts under a per-part lock (no thread count converts alone).
  * Pinned host memory: every part that is in use holds ring x (8 x max_batch +
  * max_bytes + 64) bytes (ring = DG_AGG_RING, default 16, at most 24), e.g. 16
- * threads x 16 x (8 x 4096 + 2 MiB) = 520 MiB; plus per batch of the ring
- * room for the largest batch the parts can make. Size max_batch / max_bytes
- * for the caller threads the process runs. */
+ * threads x 16 x (8 x 4096 + 2 MiB) = 520 MiB. On top of that, every batch
+ * of the ring keeps buffers for the largest batch the registered parts can
+ * make, P = 4 x (parts x max_bytes) + 128 x (parts x max_batch) bytes of
+ * packed output: about P of pinned host memory and 5 P of device memory per
+ * batch, ring x that in all. They are sized exactly (never regrown mid-run)
+ * while ring x P <= 4 GiB (knob "exact_total"), else grown lazily to twice
+ * the batch that needed them. E.g. 16 threads, max_batch 4096, max_bytes
+ * 1 MiB: P = 72 MiB, ring 16: 1.15 GiB pinned + 5.8 GiB device. Size
+ * max_batch / max_bytes for the caller threads the process runs. */
 int dg_agg_create2(dg_ctx *ctx, const dg_desc *desc, uint32_t root_type, uint64_t flags, uint32_t max_batch,
                    uint64_t max_bytes, uint32_t max_wait_us, dg_agg **out);
 /* Asynchronous form of dg_agg_do, for a caller with many requests in flight
@@ -342,13 +359,15 @@ uint64_t dg_agg_ticket_gen(const dg_agg_ticket *t);
  * aggregator cannot see; "min_fill" (0 = off): the depth rule seals only a
  * batch of at least this many calls (many parked callers refill a batch
  * over a round trip: sealing at once keeps batches small); "max_wait_us":
- * the seal timer of dg_agg_create. */
+ * the seal timer of dg_agg_create; "exact_total" (bytes, default 4 GiB):
+ * the ring-wide budget for sizing batch buffers exactly (dg_agg_create2). */
 int dg_agg_set_knob(dg_agg *agg, const char *name, int64_t value);
 /* Benchmark driver for the gateway shape: `callers` logical callers, each
  * with ONE call in flight at a time (a goroutine in Do), multiplexed over
  * `workers` OS threads (the Go runtime's Ms) with the dg_agg_wait_gen poller
  * above; worker w serves messages [w n / workers, (w + 1) n / workers) in
- * order, each runnable caller taking the next one. Outputs as
+ * order, each runnable caller taking the next one (workers is clamped to
+ * min(workers, callers, n): a worker needs callers for its range). Outputs as
  * dg_agg_drive; stats (optional, 8 u64): parks, submits retried for want of
  * room, poller wake-ups, callers, then ns summed over the workers in
  * dg_agg_wait, in dg_agg_submit, idle, and in all. */

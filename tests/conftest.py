@@ -60,3 +60,29 @@ def knob():
     yield set_
     for k, v in saved.items():
         ctx.set_knob(k, v)
+
+
+# The full C5 batch (1 048 576 messages, seed 45) for tests/test_gpu_full.py:
+# generated with a fork pool right after collection, before any test has
+# touched the GPU (a process that initialised HIP must not fork workers).
+_C5 = {}
+
+
+def pytest_collection_finish(session):
+    if not any("test_full_c5_batch" in it.nodeid for it in session.items):
+        return
+    from dynamicgo_amd import workloads as W
+    try:
+        cpus = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cpus = os.cpu_count() or 1
+    _C5["arena"], _C5["off"] = W.gen_mixed_arena(1 << 20, 45, workers=max(1, min(16, cpus)))
+
+
+@pytest.fixture(scope="session")
+def c5_batch():
+    """(arena, offsets) of the benched C5 batch (bench.py --config c5)."""
+    if "arena" not in _C5:
+        from dynamicgo_amd import workloads as W
+        _C5["arena"], _C5["off"] = W.gen_mixed_arena(1 << 20, 45, workers=1)
+    return _C5["arena"], _C5["off"]

@@ -263,6 +263,26 @@ def test_gateway_drive_vs_oracle(callers, workers, depth, fill):
     assert secs > 0 and int(lat.max()) > 0
 
 
+@pytest.mark.parametrize("n,callers,workers", [(10, 64, 16), (600, 3, 16), (2, 1, 16)])
+def test_gateway_drive_fewer_callers_or_messages_than_workers(n, callers, workers):
+    """worker w owns messages [n w / W, n (w+1) / W) but only the
+    callers c = w (mod W); with fewer callers (or messages) than workers some
+    workers owned messages no caller submitted and the drive never ended.
+    Workers are clamped to min(workers, callers, n); every result is the
+    oracle's."""
+    td = W.nesting_i64_desc()
+    msgs = W.gen_nested_batch(random.Random(23), n)
+    fl = T.flatten(td)
+    chk = oracle.RefOracle() or oracle.PortOracle()
+    want = [chk.j2t(fl, m, 1) for m in msgs]
+    agg = conv.Aggregator(td, conv.Options(), max_batch=256, max_wait_us=200, max_bytes=512 * 3000)
+    outs, rets, lat, secs, st = agg.gateway(msgs, callers=callers, workers=workers)
+    agg.close()
+    assert st[3] == min(callers, n)
+    assert [(int(r), o if int(r) == 0 else b"") for r, o in zip(rets, outs)] == \
+        [(r, o if r == 0 else b"") for r, o in want]
+
+
 def test_aggregator_shared_parts_past_224_threads():
     """More concurrent threads than exclusive parts: threads 225+ share the
     last 32 parts under their lock instead of converting alone (the r4
