@@ -235,6 +235,62 @@ DGI bool fast_int_regs(const S &src, int64_t &iv, double &dv, int32_t &end)
     return true;
 }
 
+/* A whole token that is a plain decimal, -?[0-9]+\.[0-9]+ with at most 19
+ * digits in all, from a register source: its mantissa (every digit, the
+ * point removed) and exponent (minus the fraction digits) in a fixed number
+ * of steps, as fast_int_regs. These are exactly the (man, exp10) that
+ * vnumber's digit loops (native/scanning.c:958-1083, fast_vnumber's general
+ * path) build for such a token: leading zeros add nothing to man, and 19
+ * digits never reach the 19-digit cap, so nothing is truncated. A leading
+ * zero before more integer digits, an exponent, a second point or anything
+ * else returns false and takes the general path. */
+template <class S>
+DGI bool fast_dec_regs(const S &src, uint64_t &man, int &exp10, int &sgn)
+{
+    const int32_t n = (int32_t)src.n;
+    if (n < 3 || n > 21) return false;
+    const uint64_t a0 = src.get8(0), a1 = src.get8(8), a2 = src.get8(16);
+    const uint32_t neg = (uint8_t)a0 == '-' ? 1u : 0u;
+    const uint32_t len = (uint32_t)n - neg; /* digits and the point */
+    const uint64_t d0 = neg ? (a0 >> 8) | (a1 << 56) : a0, d1 = neg ? (a1 >> 8) | (a2 << 56) : a1,
+                   d2 = neg ? a2 >> 8 : a2;
+    auto upto = [](uint32_t k) { return k >= 8 ? ~0ull : (1ull << (k << 3)) - 1; }; /* the first k bytes */
+    auto eqdot = [](uint64_t x) {
+        const uint64_t y = x ^ 0x2E2E2E2E2E2E2E2Eull;
+        return ~(((y & 0x7F7F7F7F7F7F7F7Full) + 0x7F7F7F7F7F7F7F7Full) | y | 0x7F7F7F7F7F7F7F7Full);
+    };
+    const uint32_t u0 = len < 8 ? len : 8u, u1 = len <= 8 ? 0u : len - 8 < 8 ? len - 8 : 8u,
+                   u2 = len <= 16 ? 0u : len - 16;
+    const uint64_t m0 = eqdot(d0) & upto(u0), m1 = eqdot(d1) & upto(u1), m2 = eqdot(d2) & upto(u2);
+    if (__builtin_popcountll(m0) + __builtin_popcountll(m1) + __builtin_popcountll(m2) != 1) return false;
+    const uint32_t pd = m0 ? (uint32_t)__builtin_ctzll(m0) >> 3
+                       : m1 ? 8u + ((uint32_t)__builtin_ctzll(m1) >> 3) : 16u + ((uint32_t)__builtin_ctzll(m2) >> 3);
+    if (pd < 1 || pd + 2 > len) return false; /* a digit on both sides */
+    /* the point removed: bytes above it move down one */
+    const uint64_t s0 = (d0 >> 8) | (d1 << 56), s1 = (d1 >> 8) | (d2 << 56), s2 = d2 >> 8;
+    const uint64_t k0 = upto(pd), k1 = pd <= 8 ? 0ull : upto(pd - 8), k2 = pd <= 16 ? 0ull : upto(pd - 16);
+    const uint64_t r0 = (d0 & k0) | (s0 & ~k0), r1 = (d1 & k1) | (s1 & ~k1), r2 = (d2 & k2) | (s2 & ~k2);
+    const uint32_t nd = len - 1;
+    const uint64_t x0 = r0 ^ 0x3030303030303030ull, x1 = r1 ^ 0x3030303030303030ull, x2 = r2 ^ 0x3030303030303030ull;
+    auto nondig = [](uint64_t x) { return (((x & 0x7F7F7F7F7F7F7F7Full) + 0x7676767676767676ull) | x) & 0x8080808080808080ull; };
+    const uint32_t t0 = nd < 8 ? nd : 8u, t1 = nd <= 8 ? 0u : nd - 8 < 8 ? nd - 8 : 8u, t2 = nd <= 16 ? 0u : nd - 16;
+    const uint64_t bad = (nondig(x0) & upto(t0)) | (nondig(x1) & upto(t1)) | (nondig(x2) & upto(t2));
+    if (nd > 19 || bad || ((x0 & 0xFF) == 0 && pd > 1)) return false;
+    auto p10 = [](uint32_t t) {
+        uint32_t p = (t & 1) ? 10u : 1u;
+        p = (t & 2) ? p * 100u : p;
+        p = (t & 4) ? p * 10000u : p;
+        return (t & 8) ? 100000000u : p;
+    };
+    uint64_t m = swar_val(x0, t0);
+    m = m * (uint64_t)p10(t1) + swar_val(x1, t1);
+    m = m * (uint64_t)p10(t2) + swar_val(x2, t2);
+    man = m;
+    exp10 = -(int)(nd - pd);
+    sgn = neg ? -1 : 1;
+    return true;
+}
+
 /* register sources (RSrc, RSrcL: kRegs) take fast_int_regs first */
 template <class S, class = void>
 struct is_regsrc {
@@ -250,6 +306,10 @@ struct is_regsrc<S, decltype((void)S::kRegs)> {
 template <class S>
 DGI bool fast_vnumber(S &src, SI &p, const FastTabs &tb, int64_t &iv, double &dv, bool &isint)
 {
+    SI i = p;
+    uint64_t man = 0;
+    int exp10 = 0, sgn = 1;
+    bool trunc = false, regdec = false;
     if constexpr (is_regsrc<S>::value) {
         int32_t e;
         if (p == 0 && fast_int_regs(src, iv, dv, e)) {
@@ -257,10 +317,13 @@ DGI bool fast_vnumber(S &src, SI &p, const FastTabs &tb, int64_t &iv, double &dv
             p = (SI)e;
             return true;
         }
+        if (p == 0 && fast_dec_regs(src, man, exp10, sgn)) {
+            regdec = true;
+            i = (SI)src.n;
+        }
     }
-    SI i = p;
+    if (!regdec) {
     uint8_t c = src.at(i);
-    int sgn = 1;
     if (c == '-') {
         sgn = -1;
         c = src.at(++i);
@@ -276,9 +339,8 @@ DGI bool fast_vnumber(S &src, SI &p, const FastTabs &tb, int64_t &iv, double &dv
             return true;
         }
     }
-    uint64_t man = 0;
-    int nd = 0, exp10 = 0;
-    bool trunc = false, dbl = false;
+    int nd = 0;
+    bool dbl = false;
     uint64_t x;
     for (;;) { /* integer digits */
         uint32_t k = digits8(src, i, x);
@@ -340,6 +402,7 @@ DGI bool fast_vnumber(S &src, SI &p, const FastTabs &tb, int64_t &iv, double &dv
             return true;
         }
     }
+    } /* !regdec */
     /* atof_fast native/scanning.c:928-948; atof_native -> bail */
     double val;
     if (!atof_exact_l(man, exp10, sgn, val, tb)) {

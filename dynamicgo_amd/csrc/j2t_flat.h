@@ -831,6 +831,9 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
         __syncthreads();
     }
     FLP(0);
+#if defined(DG_FL_STOP) && DG_FL_STOP == 9
+    return; /* ablation: launch, staging and the block's tables only */
+#endif
     const auto D = desc_view<3>((const __attribute__((address_space(3))) uint8_t *)(void *)s_fdesc, S.hdr);
     const FastTabs tb{(const __attribute__((address_space(3))) uint64_t *)(void *)L.p10u, (lds_f64 *)(void *)L.p10d,
                       (const __attribute__((address_space(3))) uint64_t *)(void *)L.pw};

@@ -683,14 +683,28 @@ DGI bool scan_chunk(uint32_t x, int64_t head, int64_t len, uint32_t chunk, ScanS
     }
     /* backslashes inside a string mark the open string: the last entry
      * started before them (after every entry write of the chunk; a wave's
-     * LDS operations complete in order) */
+     * LDS operations complete in order). An escape's backslash (one not
+     * itself escaped) also counts what the escape takes off the string's
+     * unquoted length in bits 16+ of the string's separator word: 1 for
+     * \" \\ \/ \b \f \n \r \t; anything else (\u, an invalid escape, an
+     * escape whose letter is in the next chunk) sets bit 31 and the page
+     * sizes that string with unquote (native/parsing.c:702-945) */
     const uint32_t bsi = bs & instr;
+    const uint32_t xn = (uint32_t)__shfl_down((int)x, 1); /* the next lane's bytes (converged) */
     if (bsi) {
+        const uint32_t ei = bsi & ~escaped;
 #pragma unroll
         for (uint32_t j = 0; j < 4; j++) {
             if ((bsi >> j) & 1) {
                 uint32_t kb = st.produced + pre + (uint32_t)__builtin_popcount(tok & ((1u << j) - 1));
                 L.tbs[(kb - 1) & WV_RMASK] = 1;
+                if ((ei >> j) & 1) {
+                    const uint32_t c = j < 3 ? (x >> (8 * (j + 1))) & 0xFF : lane < 63 ? xn & 0xFF : 0u;
+                    const bool simple = c == '"' || c == '\\' || c == '/' || c == 'b' || c == 'f' || c == 'n' ||
+                                        c == 'r' || c == 't';
+                    if (simple) atomicAdd(&L.tsep[(kb - 1) & WV_RMASK], 1u << 16);
+                    else atomicOr(&L.tsep[(kb - 1) & WV_RMASK], 1u << 31);
+                }
             }
         }
     }
@@ -703,7 +717,11 @@ DGI bool scan_chunk(uint32_t x, int64_t head, int64_t len, uint32_t chunk, ScanS
         if ((term >> j) & 1) L.tend[(kb - 1) & WV_RMASK] = (uint32_t)(p0 + j);
         if ((seps >> j) & 1) {
             if (kb == 0) badsep = true;
-            else atomicAdd(&L.tsep[(kb - 1) & WV_RMASK], ((sepc >> j) & 1) ? 1u : 256u);
+            /* a second separator after one entry is always a grammar error
+             * (the exact machine reports it): every separator word then holds
+             * at most one colon or comma, and no count carries into the next
+             * field (256 colons read as one comma, 256 commas as escapes) */
+            else if (atomicAdd(&L.tsep[(kb - 1) & WV_RMASK], ((sepc >> j) & 1) ? 1u : 256u) & 0xFFFFu) badsep = true;
         }
     }
     if (ballot(badsep)) st.bad = 1;
@@ -844,7 +862,7 @@ DGI bool wave_run(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L
         uint32_t kend = 0, ksep = 0, kq = K_NONE, sq = 0;
         bool qkey = false;
         if (alive && t >= 1) {
-            const uint32_t a = L.tpos[(t - 1) & WV_RMASK], sa = L.tsep[(t - 1) & WV_RMASK];
+            const uint32_t a = L.tpos[(t - 1) & WV_RMASK], sa = L.tsep[(t - 1) & WV_RMASK] & 0xFFFFu;
             if ((a >> 29) == K_STRING && (sa & 0xFFu)) {
                 haskey = true;
                 ksep = sa;
@@ -854,7 +872,7 @@ DGI bool wave_run(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L
                 if (t >= 2) {
                     const uint32_t b = L.tpos[(t - 2) & WV_RMASK];
                     kq = b >> 29;
-                    sq = L.tsep[(t - 2) & WV_RMASK];
+                    sq = L.tsep[(t - 2) & WV_RMASK] & 0xFFFFu;
                     qkey = kq == K_STRING && (sq & 0xFFu);
                 }
             } else {
@@ -1133,10 +1151,17 @@ DGI bool wave_run(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L
                 if (bl < 0) bad = true;
                 vln = (uint32_t)bl;
             } else if (esc) {
-                WOut co;
-                co.init_dry();
-                if (!fast_unquote(src, cs, cn, co)) bad = true;
-                vln = (uint32_t)co.len;
+                /* the escapes the scan counted (bits 16+ of the separator
+                 * word), else unquote without output */
+                const uint32_t shr = L.tsep[t & WV_RMASK] >> 16;
+                if (!(shr & 0x8000u) && cn < 32768) {
+                    vln = (uint32_t)cn - shr;
+                } else {
+                    WOut co;
+                    co.init_dry();
+                    if (!fast_unquote(src, cs, cn, co)) bad = true;
+                    vln = (uint32_t)co.len;
+                }
             } else {
                 vln = (uint32_t)cn;
             }
@@ -1200,9 +1225,16 @@ DGI bool wave_run(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L
             if (live && kn > 0) fast_copy(src, ks, kn, w); /* string map key (no escapes) */
             if (live && cl && vbn == 1 && reqs) unset_fields(D, ldrec(&D.S[sidx]), reqs, flag, w); /* before the STOP */
             if (live && vbn) w.wle(vb, vbn);
+#if defined(DG_WV_ABL) && (DG_WV_ABL & 64)
+            if (0) /* ablation: escaped strings not written */
+#endif
             if (live && !chunked && esc && kind == K_STRING) fast_unquote(src, cs, cn, w);
             w.finish();
+#if defined(DG_WV_ABL) && (DG_WV_ABL & 96)
+            if (live && !op && !chunked && !esc && w.len != ln) bad = true;
+#else
             if (live && !op && !chunked && w.len != ln) bad = true;
+#endif
         }
         if (alive && cl) {
             if (!(pflags & CF_SKIP) && !(pflags & CF_STRUCT))

@@ -306,6 +306,58 @@ def test_integer_tokens_vs_oracle(route):
         assert not bad, (route, hex(flags), bad[:4])
 
 
+DEC_TOKENS = ["0.0", "-0.0", "0.5", "-0.5", "1.5", "-1.25", "00.5", "01.5", "-01.5", "1.", "-1.", ".5", "-.5", "1.2.3",
+              "1..2", "1.5e3", "1.5E-3", "1.5x", "1.x5", "-", "0.000123", "-0.000000000000000001", "0.0000000000000000001",
+              "0.00000000000000000001", "123456789.0123456789", "1234567890.123456789", "12345678901234567.89",
+              "1234567890123456789.0", "9007199254740993.0", "9007199254740993.5", "-510378.14969714754",
+              "722205.81933333166", "-6890.4", "3422.05", "1.7976931348623157", "4.9406564584124654", "2.2250738585072014",
+              "0.1", "0.2", "0.3", "123.456", "99999999999999999.9", "1.00000000000000000", "1.000000000000000000",
+              "5e-324", "1e309", "-1e309", "1.5.", "12345678901234567890.5"]
+
+
+@pytest.mark.parametrize("route", ["flat", "small", "wave"])
+def test_decimal_tokens_vs_oracle(route):
+    """fast_vnumber's fixed-step decimal path (j2t_fast.h fast_dec_regs:
+    -?D+.D+ with at most 19 digits, mantissa and exponent without the digit
+    loops) and its fall-backs to the general path: leading zeros, a point at
+    either end, two points, exponents, 19/20/21 digits, the doubles next to
+    2^53 and the range edges, in every numeric field type, against the
+    reference; "wave" pads the message past the wave kernel's threshold."""
+    td = flat_desc()
+    fl = T.flatten(td)
+    msgs = []
+    for v in DEC_TOKENS:
+        for f in ("y", "s16", "s32", "s64", "d", "vm64", "vm16", "far"):
+            pad = ',"Str":"' + "p" * 600 + '"' if route == "wave" else ""
+            msgs.append(('{"req":1,"%s":%s%s}' % (f, v, pad)).encode())
+            msgs.append(('{"%s":%s,"req":2%s}' % (f, v, pad)).encode())
+    extra = {"flat": FLAT, "small": NO_FLAT, "wave": NO_FLAT}[route]
+    for flags in (0x1, 0x41, 0x5):
+        bad = _compare(fl, msgs, flags | extra)
+        assert not bad, (route, hex(flags), bad[:4])
+
+
+def test_decimal_map_keys_and_values_vs_oracle(knob):
+    """Decimal tokens as numeric map keys (parsed as a prefix: trailing text
+    after the number is ignored) and as map/list values, on the wave kernel
+    (wave_min 0) and the lane kernel, against the reference."""
+    td = T.struct_type("M", [
+        T.FieldDescriptor(1, "md", T.map_of(T.builtin("i64"), T.builtin("double")), T.OPTIONAL),
+        T.FieldDescriptor(2, "ld", T.list_of(T.builtin("double")), T.OPTIONAL),
+        T.FieldDescriptor(3, "mi", T.map_of(T.builtin("double"), T.builtin("i32")), T.OPTIONAL),
+    ])
+    fl = T.flatten(td)
+    msgs = []
+    for v in DEC_TOKENS:
+        msgs.append(('{"md":{"%s":%s,"7":1.25},"ld":[%s,0.5]}' % (v, v, v)).encode())
+        msgs.append(('{"mi":{"%s":1,"%s7":2},"ld":[1.5,%s]}' % (v, v, v)).encode())
+    for wm in (0, 512):
+        knob("wave_min", wm)
+        for flags in (0x1, 0x41):
+            bad = _compare(fl, msgs, flags)
+            assert not bad, (wm, hex(flags), bad[:4])
+
+
 def test_flat_field_remap_shuffled_keys():
     """Shuffled key order (c2s): the key pass maps each position to its
     field and every wave converts one FIELD of its 64 messages

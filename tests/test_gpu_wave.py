@@ -57,6 +57,10 @@ def _must_wave_cases():
         cases.append(b'{"ByteField":2,"BinaryField":"' + (b"QUJD" * 40)[:n - 4] + b'QQ==","I32Field":1}')
     for n in (7, 8, 9, 31, 32, 33, 63, 64, 65, 100):                          # copy chunk-task boundaries
         cases.append(b'{"StringField":"' + bytes(97 + (i % 26) for i in range(n)) + b'","ByteField":4}')
+    for k in range(240, 262):                                                 # escapes counted by the scan:
+        cases.append(b'{"StringField":"' + b"z" * k + b'\\n\\t\\"\\\\\\/\\b\\f\\r end","I32Field":3}')  # letter in the next chunk
+    cases.append(b'{"StringField":"' + b"\\n" * 300 + b'","ByteField":1}')   # 300 escapes in one string
+    cases.append(b'{"StringField":"\\u0041\\n","BinaryField":"QUI="}')          # \u with a simple one
     cases.append(b'{"DoubleField":-0,"I64Field":-9223372036854775808,"I32Field":1.9,"ByteField":-129}')
     cases.append(b'{"DoubleField":1e22,"I64Field":123456789012345678,"I32Field":2147483648}')
     cases.append(b'{"DoubleField":0.1e-5,"I64Field":99999999999999999999}')   # overflow -> double -> cvt
@@ -91,6 +95,11 @@ def _may_bail_cases():
         b'{"BinaryField":"QQ=A"}', b'{"BinaryField":"' + b"QUJD" * 20 + b'QQ=A"}',   # '=' then a letter: decode error
         b'{"StringField":"\\ud800"}', b'{"StringField":"\\x"}', b"[1]", b"", b"null", b"  {}  ", b"{",
         b'{"ByteField":1]', b'{"a":[1,2}', b'{"ByteField":1e2}', b'{"I32Field":"12"}',
+        b'{"ByteField":1,,"I32Field":2}', b'{"ByteField"::1}', b'{"ByteField":1,:"I32Field":2}',  # two separators
+        b'{"ByteField":1' + b":" * 256 + b'"I32Field":2}',                  # 256 colons (not one comma)
+        b'{"StringField":"a\\n"' + b"," * 256 + b'}',                       # 256 commas after an escaped string
+        b'{"StringField":"a\\n"' + b"," * 255 + b'"I32Field":2}',
+        b'{"StringField":"\\q\\n"}', b'{"StringField":"\\n\\u12"}',
     ]
 
 

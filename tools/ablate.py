@@ -12,6 +12,10 @@ def main():
     dev = torch.device("cuda:0")
     if cfg == "c2":
         td, msgs = W.simple_desc(), W.gen_flat_batch(random.Random(42), 65536)
+    elif cfg in ("c3small", "c3big"):  # C3 messages that fit the wave kernel's LDS stage, or not
+        td, msgs = W.nesting_i64_desc(), W.gen_nested_batch(random.Random(43), 3 * 65536)
+        msgs = [m for m in msgs if (len(m) <= 1900) == (cfg == "c3small")][:32768]
+        print("%s: %d msgs, %d bytes" % (cfg, len(msgs), sum(map(len, msgs))))
     else:
         td, msgs = W.nesting_i64_desc(), W.gen_nested_batch(random.Random(43), 65536)
     flat = flatten(td)
