@@ -1068,6 +1068,14 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
      *      straight into the slots, byte-exact at the shared edge words ---- */
     {
         const uint32_t mm = lane;
+        /* the field slots wave w converts rotate with the block: the waves
+         * of one SIMD (wave w of each resident block) then hold different
+         * fields -- a double beside a byte -- instead of the same heavy or
+         * light one in every block, so no SIMD carries all the heavy slots */
+#ifndef DG_FL_ROT
+#define DG_FL_ROT 1
+#endif
+        const uint32_t fwave = DG_FL_ROT ? (wave + blockIdx.x) % FL_WAVES : wave;
         const uint32_t ok0 = L.ok[mm], lwa = L.lw[mm], oc = L.oc[mm], nfq = L.nfq[mm];
         const uint32_t nf = nfq & 0xFF, qtot = (nfq >> 8) & 0x3FF;
         const bool hasbs = (nfq >> 31) != 0;
@@ -1143,7 +1151,7 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
             uint32_t mis = 0;
 #pragma unroll
             for (uint32_t h = 0; h < FL_FPW; h++) {
-                const uint32_t k = fl_slot(wave, h);
+                const uint32_t k = fl_slot(fwave, h);
                 if (ok0 && k < nf) {
                     const uint32_t sk = k ? (L.sep[(k - 1) * FL_MPB + mm] & 0xFFFF) + 1 : (oc & 0xFFFF) + 1;
                     const uint32_t ck = L.col[k * FL_MPB + mm];
@@ -1158,7 +1166,7 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
             uint32_t fail = 0;
 #pragma unroll
             for (uint32_t h = 0; h < FL_FPW; h++) {
-                const uint32_t k = fl_slot(wave, h);
+                const uint32_t k = fl_slot(fwave, h);
                 if (ok0 && k < nf) {
                     const uint32_t e0 = k ? L.sep[(k - 1) * FL_MPB + mm] : 0;
                     const uint32_t sk = k ? (e0 & 0xFFFF) + 1 : (oc & 0xFFFF) + 1, q0 = e0 >> 16;
@@ -1193,14 +1201,14 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
 #pragma unroll
             for (uint32_t h = 0; h < FL_FPW; h++) {
                 FLF_T0();
-                const uint32_t j = fl_slot(wave, h);
+                const uint32_t j = fl_slot(fwave, h);
                 const uint32_t k = remap ? (uint32_t)fmap[j * FL_MPB + mm] : r * FL_SLOTS + j; /* 0xFF: no such field */
                 const uint32_t si = remap ? k : j; /* its position within the round */
                 kslot[h] = si;
                 parse(k, F[h]);
                 if (si < FL_SLOTS) sz[si * FL_MPB + mm] = (uint16_t)F[h].size;
                 if (remap && j >= nf) sz[j * FL_MPB + mm] = 0; /* positions past the message's fields */
-                FLF_ADD(r * FL_SLOTS + fl_slot(wave, h));
+                FLF_ADD(r * FL_SLOTS + fl_slot(fwave, h));
             }
             FLP(4);
             __syncthreads();
@@ -1269,7 +1277,7 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
             for (uint32_t h = 0; h < FL_FPW; h++) {
                 FLF_T0();
                 const uint32_t wr = write(F[h], off[h]);
-                FLF_ADD(6 + r * FL_SLOTS + fl_slot(wave, h));
+                FLF_ADD(6 + r * FL_SLOTS + fl_slot(fwave, h));
                 good &= wr != 0;
             }
             if (!good) L.ok[mm] = 0;

@@ -1090,6 +1090,8 @@ int dg_j2t_pipeline_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8
      * next chunk's reads overlap the previous chunk's copy-out */
     void *dv_json = nullptr, *dv_end = nullptr, *dv_in = nullptr, *dv_in_end = nullptr;
     const uint64_t jend = in_off[n] + 15;
+    void *dv_in0 = nullptr;
+    const bool in_pinned = host_pinned(in_off, &dv_in0);
     const bool zc = host_pinned(json, &dv_json) && host_pinned(json + jend, &dv_end) &&
                     (uint8_t *)dv_end - (uint8_t *)dv_json == (ptrdiff_t)jend && host_pinned(in_off, &dv_in) &&
                     host_pinned(in_off + n, &dv_in_end) && (uint64_t *)dv_in_end - (uint64_t *)dv_in == (ptrdiff_t)n &&
@@ -1105,11 +1107,11 @@ int dg_j2t_pipeline_host(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8
         PipeBuf &p = *(PipeBuf *)c->pipe[k % nb];
         const uint64_t a = cb[k], m = cb[k + 1] - a, base = in_off[a], jb = base & ~15ull;
         /* the longest message picks the kernels; unknown (0) when the
-         * offsets are pinned: CPU reads of pinned memory run at ~10 GB/s (a
-         * 64K batch's offsets cost 50 us), and the kernels route long
-         * messages themselves */
+         * offsets are pinned (read in place or uploaded): CPU reads of pinned
+         * memory run at ~10 GB/s (a 64K batch's offsets cost 50 us), and the
+         * kernels route long messages themselves */
         uint64_t max_len = 0;
-        if (!zc) {
+        if (!zc && !in_pinned) {
             max_len = 1;
             for (uint64_t j = a; j < a + m; j++) max_len = std::max<uint64_t>(max_len, in_off[j + 1] - in_off[j]);
         }

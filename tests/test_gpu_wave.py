@@ -61,6 +61,22 @@ def _must_wave_cases():
         cases.append(b'{"StringField":"' + b"z" * k + b'\\n\\t\\"\\\\\\/\\b\\f\\r end","I32Field":3}')  # letter in the next chunk
     cases.append(b'{"StringField":"' + b"\\n" * 300 + b'","ByteField":1}')   # 300 escapes in one string
     cases.append(b'{"StringField":"\\u0041\\n","BinaryField":"QUI="}')          # \u with a simple one
+    # long-string mode (bodies past WV_LONG = 1024 bytes are written while the
+    # scan reads them): lengths around the threshold and every 4-byte phase
+    # of the quote, base64 with and without padding, plain strings, two long
+    # strings in one message, a long value after many entries
+    for n in (1016, 1020, 1024, 1028, 1280, 4096, 20000):
+        for ph in range(4):
+            cases.append(b'{' + b' ' * ph + b'"BinaryField":"' + (b"QUJD" * (n // 4))[:n - 4] + b'QQ==",'
+                         b'"StringField":"' + bytes(97 + (i * 7 + ph) % 26 for i in range(n + ph)) + b'","ByteField":3}')
+    cases.append(b'{"BinaryField":"' + b"QUJD" * 700 + b'"}')                     # no padding
+    cases.append(b'{"BinaryField":"' + b"QUJD" * 700 + b'QUI="}')
+    cases.append(b'{"ByteField":1' + b"".join(b',"K%d":%d' % (i, i) for i in range(100)) + b',"StringField":"' +
+                 b"w" * 3000 + b'"}')
+    cases.append(b'{"StringField":"' + b"s" * 1500 + b'","StringField2":"' + b"t" * 1500 + b'"}')  # unknown key: skipped
+    cases.append(("nest", b'{"ListString":["' + b"l" * 3000 + b'"],"String":"' + b"m" * 2000 + b'",'
+                  b'"MapStringString":{"k":"' + b"v" * 2500 + b'"},"SimpleStruct":{"BinaryField":"'
+                  + b"QUJD" * 600 + b'","StringField":"' + b"q" * 1200 + b'"},"Binary":"' + b"QUJD" * 400 + b'"}'))
     cases.append(b'{"DoubleField":-0,"I64Field":-9223372036854775808,"I32Field":1.9,"ByteField":-129}')
     cases.append(b'{"DoubleField":1e22,"I64Field":123456789012345678,"I32Field":2147483648}')
     cases.append(b'{"DoubleField":0.1e-5,"I64Field":99999999999999999999}')   # overflow -> double -> cvt
@@ -100,6 +116,16 @@ def _may_bail_cases():
         b'{"StringField":"a\\n"' + b"," * 256 + b'}',                       # 256 commas after an escaped string
         b'{"StringField":"a\\n"' + b"," * 255 + b'"I32Field":2}',
         b'{"StringField":"\\q\\n"}', b'{"StringField":"\\n\\u12"}',
+        # long-string mode: errors and escapes after the stream started
+        b'{"BinaryField":"' + b"QUJD" * 500 + b'Q!JD' + b"QUJD" * 100 + b'"}',   # a bad character
+        b'{"BinaryField":"' + b"QUJD" * 500 + b'QQ==' + b"QUJD" * 100 + b'"}',   # padding in the middle
+        b'{"BinaryField":"' + b"QUJD" * 500 + b'QQ=A"}', b'{"BinaryField":"' + b"QUJD" * 500 + b'QUJ"}',
+        b'{"BinaryField":"' + b"QUJD" * 500 + b'\\n"}',
+        b'{"StringField":"' + b"e" * 1800 + b'\\n\\t' + b"f" * 900 + b'","ByteField":2}',  # escapes: page writes it
+        b'{"StringField":"' + b"e" * 1800 + b'\\u00e9' + b"f" * 900 + b'"}',
+        b'{"StringField":"' + b"x" * 3000,                                     # unterminated
+        b'{"ByteField":1,"ByteField":2,"StringField":"' + b"d" * 2000 + b'"}',  # duplicate before it
+        b'{"StringField":"' + b"d" * 2000 + b'","StringField":"z"}',           # duplicate after it
     ]
 
 
