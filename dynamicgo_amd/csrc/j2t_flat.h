@@ -62,7 +62,7 @@ constexpr uint32_t FL_SLACKW = FL_G * FL_LW + 2; /* reads past the last message 
 constexpr uint32_t FL_MAXF = 24;                 /* fields per message (top-level commas + 1) */
 constexpr uint32_t FL_DESC = 16 * 1024;          /* descriptor bytes in LDS (dynamic) */
 #ifndef DG_FL_INLINE
-#define DG_FL_INLINE 16
+#define DG_FL_INLINE 8 /* r7p: 8 vs 16 bytes, the flat kernel 2 % faster on C2, c2s, c2x; C1 even */
 #endif
 #ifndef DG_FL_CHUNK
 #define DG_FL_CHUNK 32
@@ -703,6 +703,13 @@ struct FlatLds {
     uint16_t size[2 * FL_SLOTS * FL_MPB];   /* [round & 1][slot][m] */
     uint32_t fseen[FL_MPB];                 /* key pass: the fields found in the message (bit = field index) */
     uint32_t rounds, ntask, tgrab, noremap;
+    /* kernel arguments used only by the writes and the finish, read from
+     * here where they are needed instead of held in SGPRs through the parse
+     * (the kernel is at the SGPR limit: uniform values spill to VGPR lanes) */
+    uint8_t *a_out;
+    uint64_t *a_ret;
+    uint32_t *a_out_len, *a_bail_count, *a_bail_list;
+    uint32_t a_nb, a_wrap; /* messages in the block; S.wrap */
     uint64_t p10u[20];
     double p10d[23];
     uint64_t pw[EL_WN];                     /* Eisel-Lemire powers window (j2t_fast.h) */
@@ -761,6 +768,13 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
         L.ntask = 0;
         L.tgrab = 0;
         L.noremap = 0;
+        L.a_out = P.out;
+        L.a_ret = P.ret;
+        L.a_out_len = P.out_len;
+        L.a_bail_count = S.bail_count;
+        L.a_bail_list = S.bail_list;
+        L.a_nb = (uint32_t)(b1 - b0);
+        L.a_wrap = S.wrap;
     }
     if (tid < FL_MPB) {
         uint32_t ok = 0, n = 0, lw = 0, big = 0, cap = 0;
@@ -1080,7 +1094,7 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
         const uint32_t nf = nfq & 0xFF, qtot = (nfq >> 8) & 0x3FF;
         const bool hasbs = (nfq >> 31) != 0;
         const uint32_t cap = L.cap[mm];
-        gu8 *const slot = (gu8 *)(void *)(P.out + L.oa[mm]);
+        gu8 *const slot = (gu8 *)(void *)(L.a_out + L.oa[mm]);
         LSrc src;
         src.init((const __attribute__((address_space(3))) uint64_t *)(void *)&L.in[lwa >> 3], (int32_t)(lwa & 7), (int32_t)L.n[mm]);
         const uint32_t rounds = L.rounds;
@@ -1307,7 +1321,7 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
             LSrc src;
             src.init((const __attribute__((address_space(3))) uint64_t *)(void *)&L.in[lwa >> 3], (int32_t)(lwa & 7), (int32_t)L.n[m]);
             WOut o;
-            o.init((gu8 *)(void *)(P.out + L.oa[m] + (uint32_t)(tk >> 32)));
+            o.init((gu8 *)(void *)(L.a_out + L.oa[m] + (uint32_t)(tk >> 32)));
 #ifdef DG_FL_ABL_NOSTORE
             o.dry = true;
 #endif
@@ -1324,10 +1338,10 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
     /* ---- 4. per message (a lane): unset fields, then STOP and the result ---- */
     if (tid < FL_MPB) {
         const uint32_t m = tid;
-        const uint64_t i = b0 + m;
-        if (i < b1) {
+        const uint64_t i = (uint64_t)blockIdx.x * FL_MPB + m;
+        if (m < L.a_nb) {
             const uint32_t len = L.nbytes[m] + 1;
-            const uint32_t wid = S.wrap ? L.wid[m] : 0u;
+            const uint32_t wid = L.a_wrap ? L.wid[m] : 0u;
             bool good = L.ok[m] && len <= L.cap[m];
             if (good) {
                 const uint64_t present = (uint64_t)L.plo[m] | ((uint64_t)L.phi[m] << 32);
@@ -1347,21 +1361,21 @@ __global__ __launch_bounds__(64 * FL_WAVES) __attribute__((amdgpu_waves_per_eu(D
             }
             if (good && wid) {
                 /* the outer field header, the inner STOP, the outer STOP */
-                gu8 *o = (gu8 *)(void *)P.out + L.oa[m];
+                gu8 *o = (gu8 *)(void *)L.a_out + L.oa[m];
                 o[-3] = DG_T_STRUCT;
                 o[-2] = (uint8_t)(wid >> 8);
                 o[-1] = (uint8_t)wid;
                 o[len - 1] = 0;
                 o[len] = 0;
-                P.ret[i] = 0;
-                P.out_len[i] = len + 4;
+                L.a_ret[i] = 0;
+                L.a_out_len[i] = len + 4;
             } else if (good) {
-                ((gu8 *)(void *)P.out)[L.oa[m] + len - 1] = 0; /* STOP */
-                P.ret[i] = 0;
-                P.out_len[i] = len;
+                ((gu8 *)(void *)L.a_out)[L.oa[m] + len - 1] = 0; /* STOP */
+                L.a_ret[i] = 0;
+                L.a_out_len[i] = len;
             } else if (!L.big[m]) {
-                const uint32_t qq = atomicAdd(S.bail_count, 1u);
-                S.bail_list[qq] = (uint32_t)i;
+                const uint32_t qq = atomicAdd(L.a_bail_count, 1u);
+                L.a_bail_list[qq] = (uint32_t)i;
             }
         }
     }
