@@ -109,6 +109,7 @@ struct CRec {
     uint64_t nulldr; /* struct: DEFAULT/REQUIRED fields that occurred as null */
 };
 constexpr uint32_t CF_SKIP = 1, CF_OBJ = 2, CF_STRUCT = 4, CF_MAP = 8, CF_LIST = 16;
+constexpr uint32_t CF_ST_SHIFT = 8; /* struct: its dg_struct index above the CF_* bits (no dg_type read per round) */
 
 struct WaveLds {
     uint32_t tpos[WV_RING]; /* kind << 29 | position */
@@ -934,7 +935,7 @@ DGI bool wave_run(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L
                     } else if (pflags & CF_SKIP) {
                         skip = true;
                     } else if (pflags & CF_STRUCT) { /* j2t_key native/thrift.c:668-763 */
-                        const dg_struct sd = ldrec(&D.S[ldrec(&D.T[ptype]).st]);
+                        const dg_struct sd = ldrec(&D.S[pflags >> CF_ST_SHIFT]);
                         const int32_t f = kesc ? -2 : wv_lookup(D, sd, src, kpos + 1, kend - (uint32_t)kpos - 1, khash);
                         if (f == -2) {
                             bad = true; /* escaped key: exact machine */
@@ -967,10 +968,18 @@ DGI bool wave_run(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L
                             const dg_type ct = ldrec(&D.T[ty]);
                             if (kind == K_LBRACE) {
                                 if (ct.ttype == DG_T_STRUCT) {
-                                    c.flags |= CF_STRUCT;
-                                    const dg_struct csd = ldrec(&D.S[ct.st]);
-                                    if (csd.req_words != 1) bad = true;
-                                    if ((flag & DG_F_ENABLE_HM) && (csd.flags & DG_SF_HTTP_MAPPING)) bad = true;
+                                    c.flags |= CF_STRUCT | (ct.st << CF_ST_SHIFT);
+                                    /* bit 0: more than 64 fields, bit 1: HTTP-mapped fields
+                                     * (the block's struct table; the record past it) */
+                                    uint32_t sf;
+                                    if (ct.st < WV_REQMASKS) {
+                                        sf = ((const __attribute__((address_space(3))) uint8_t *)(reqmask + WV_REQMASKS))[ct.st];
+                                    } else {
+                                        const dg_struct csd = ldrec(&D.S[ct.st]);
+                                        sf = (csd.req_words != 1 ? 1u : 0u) | ((csd.flags & DG_SF_HTTP_MAPPING) ? 2u : 0u);
+                                    }
+                                    if (sf & 1u) bad = true;
+                                    if ((flag & DG_F_ENABLE_HM) && (sf & 2u)) bad = true;
                                 } else if (ct.ttype == DG_T_MAP) {
                                     c.flags |= CF_MAP;
                                 } else {
@@ -1180,7 +1189,7 @@ DGI bool wave_run(const Params &P, const DV &D, uint32_t D_nf, uint64_t m, LW &L
         uint32_t uln = 0;  /* bytes of the unset fields */
         if (alive && cl) {
             if (!(pflags & CF_SKIP) && (pflags & CF_STRUCT)) {
-                sidx = ldrec(&D.T[ptype]).st;
+                sidx = pflags >> CF_ST_SHIFT;
                 const dg_struct csd = ldrec(&D.S[sidx]);
                 reqs = (D.R[csd.req_begin] & ~L.crec[ci].seen) | L.crec[ci].nulldr;
                 if (!(flag & (DG_F_WRITE_REQUIRE | DG_F_WRITE_DEFAULT | DG_F_WRITE_OPTIONAL)) && sidx < WV_REQMASKS) {
@@ -1374,7 +1383,7 @@ __global__ __launch_bounds__(64 * WV_WAVES) __attribute__((amdgpu_waves_per_eu(D
     __shared__ __attribute__((aligned(16))) uint64_t s_msg[WV_WAVES][WV_MSG / 8];
     extern __shared__ __attribute__((aligned(16))) uint64_t s_desc[]; /* the blob, rounded to 16 B (launch size) */
     __shared__ uint8_t s_cls[256];
-    __shared__ uint64_t s_reqmask[WV_REQMASKS];
+    __shared__ uint64_t s_reqmask[WV_REQMASKS + WV_REQMASKS / 8]; /* REQUIRED-field masks, then a flags byte per struct */
     __shared__ uint64_t s_p10u[20];
     __shared__ double s_p10d[23];
     __shared__ uint64_t s_pw[EL_WN]; /* Eisel-Lemire powers of ordinary doubles: LDS, not the global table */
@@ -1426,6 +1435,8 @@ __global__ __launch_bounds__(64 * WV_WAVES) __attribute__((amdgpu_waves_per_eu(D
             if (f.required == DG_REQ_REQUIRED && !(f.flags & DG_FF_REQUEST_BASE)) mk |= 1ull << k;
         }
         s_reqmask[tid] = mk;
+        ((uint8_t *)(s_reqmask + WV_REQMASKS))[tid] =
+            (uint8_t)((sd.req_words != 1 ? 1u : 0u) | ((sd.flags & DG_SF_HTTP_MAPPING) ? 2u : 0u));
     }
     __syncthreads();
     const uint32_t wave = tid >> 6, lane = tid & 63;
