@@ -262,17 +262,30 @@ def cpu_baseline(flat, arena, off, flags, budget_s: float = 6.0):
     n = len(off) - 1
     nbytes = int(off[-1] - off[0])
 
-    def timed(a, o, cpus):
+    def timed(a, o, cpus, per=1):
         t1 = ref.j2t_timed(flat, a, o, flags, cpus, 1)
         reps = int(max(5, min(200, budget_s / 2 / max(t1, 1e-6))))
         ts = []
         ref.j2t_timed(flat, a, o, flags, cpus, reps, times=ts)
+        ts = [t / per for t in ts]
         return float(np.median(ts)), ts
 
+    # a pass of a small batch takes ~1 ms on 16 cores, where one descheduled
+    # thread doubles it (r7z C2: passes spread 4x); the timed passes convert
+    # the batch `rep` times over (the same messages, a >= 64 MB arena), and
+    # the times are per batch
+    rep = int(max(1, min(16, (64 << 20) // max(nbytes, 1))))
+    if rep > 1:
+        body = np.asarray(arena[int(off[0]):int(off[-1])])
+        arena_r = np.concatenate([body] * rep + [np.zeros(64, dtype=np.uint8)])
+        off_r = np.concatenate([(off[:n] - off[0]) + k * nbytes for k in range(rep)] +
+                               [np.array([rep * nbytes], dtype=off.dtype)]).astype(np.uint64)
+    else:
+        arena_r, off_r = arena, off
     env_s = host_cpu_env()
-    t_share, ts_share = timed(arena, off, phys[:cores])
+    t_share, ts_share = timed(arena_r, off_r, phys[:cores], rep)
     env0 = host_cpu_env()
-    t_all, ts_all = (t_share, ts_share) if cores == cores_all else timed(arena, off, phys[:cores_all])
+    t_all, ts_all = (t_share, ts_share) if cores == cores_all else timed(arena_r, off_r, phys[:cores_all], rep)
     env1 = host_cpu_env()
     # one core: a prefix of at most ~64 MB / 65536 messages
     k = int(min(n, 65536, max(1, np.searchsorted(off, off[0] + 64 * 1024 * 1024))))
@@ -305,7 +318,8 @@ def cpu_baseline(flat, arena, off, flags, budget_s: float = 6.0):
             "one_core_gbs": round(one_bytes / t_one / 1e9, 4), "one_core_ns_per_msg": round(t_one / k * 1e9, 1),
             "one_core_range": spread(one_bytes, ts_one),
             "host": env_s,
-            "sample": f"the rank's whole batch ({n} msgs, {nbytes} B), median (min/max in range) of "
+            "sample": f"the rank's whole batch ({n} msgs, {nbytes} B; {rep} copies per timed pass, times per "
+                      f"batch), median (min/max in range) of "
                       f"{len(ts_share)} passes, {cores} threads pinned to distinct physical cores of "
                       f"'{cpu_model()}' (affinity: {logical} logical CPUs = {len(phys)} physical cores, quota "
                       f"{quota} CPUs); all_affinity: {cores_all} threads, {len(ts_all)} passes; one-core: first "
