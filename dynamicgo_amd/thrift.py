@@ -40,6 +40,7 @@ VM_BODY_DYNAMIC = 257  # thrift/annotation/value_mapping.go:51
 HTTP_MAPPING_KEYS = ("api.query", "api.path", "api.header", "api.cookie", "api.body",
                      "api.http_code", "api.raw_body", "api.form", "api.raw_uri",
                      "api.no_body_struct")  # thrift/annotation/register.go:28-37
+ANNO_DEPRECATED = "dynamicgo.deprecated"  # AnnoKeyDynamicGoDeprecated, thrift/annotation.go:248
 
 
 class TypeDescriptor:
@@ -190,6 +191,22 @@ class StructDescriptor:
 
     def field_by_id(self, fid: int) -> Optional[FieldDescriptor]:
         return self.ids.get(fid)
+
+    def requires_bitmap(self) -> List[int]:
+        """The RequiresBitmap words (thrift/utils.go:45-79): bit id%64 of word
+        id//64, set for Required/Default, clear for Optional; max id//64+1 words."""
+        words = [0] * (max(self.requires, default=0) // 64 + 1)
+        for fid, on in self.requires.items():
+            if on:
+                words[fid // 64] |= 1 << (fid % 64)
+        return words
+
+    def requires_is_set(self, fid: int) -> bool:
+        """RequiresBitmap.IsSet (thrift/utils.go:64-71), out of range raises."""
+        w = self.requires_bitmap()
+        if fid // 64 >= len(w):
+            raise IndexError("bitmap id out of range")
+        return bool(w[fid // 64] >> (fid % 64) & 1)
 
 
 # ---- builtins (thrift/idl.go:540-551) ----
@@ -748,10 +765,14 @@ class _Compiler:
         self.opts = opts
 
     def resolve(self, f: IDLFile, name: str):
-        if "." in name:
-            pkg, rest = name.split(".", 1)
-            if pkg in f.includes:
-                return f.includes[pkg], rest
+        """An include's prefix is its file name less ".thrift", dots included
+        ("deep/deep.ref.thrift" -> "deep.ref."): the longest matching prefix wins."""
+        best = None
+        for pkg in f.includes:
+            if name.startswith(pkg + ".") and (best is None or len(pkg) > len(best)):
+                best = pkg
+        if best is not None:
+            return f.includes[best], name[len(best) + 1:]
         return f, name
 
     def const_default(self, f: IDLFile, t: TypeDescriptor, cv) -> Optional[bytes]:
@@ -804,6 +825,8 @@ class _Compiler:
         td = TypeDescriptor(STRUCT, pt.name, struct=sd)
         cache[ck] = td
         for pf in ff.structs[name]:
+            if any(k == ANNO_DEPRECATED for k, _ in pf.annos):
+                continue  # handleNativeFieldAnnotation (thrift/annotation.go:399-404): field dropped
             alias = pf.name
             vm = VM_NONE
             vmap = None
