@@ -662,3 +662,27 @@ def test_reference_http_mapping_cases(chk, monkeypatch, name):
             fn(chk, v)
     else:
         fn(chk)
+
+
+def test_reference_known_answers_more(chk):
+    """conv/t2j/conv_test.go's TestAPIBody (:288-308), TestUnknowFields
+    (:472-518) and TestSimpleArgs (:711-733) through BinaryConv on the GPU,
+    each also against the checker."""
+    from test_t2j_oracle import API_BODY_JSON, _example3_resp_bin, _example3_svc, api_body_thrift
+    fns = _example3_svc().functions()
+    td = fns["ApiBodyMethod"].response().struct.fields[0].type
+    assert t2j.BinaryConv(conv.Options(EnableValueMapping=True)).do(td, api_body_thrift()) == API_BODY_JSON
+    assert not compare(chk, T.flatten(td), [api_body_thrift()], VM)
+    src = _example3_resp_bin()
+    for td in (fns["PartialMethod"].response().struct.fields[0].type,
+               fns["PartialMethod"].request().struct.fields[0].type):
+        with pytest.raises(t2j.T2JError) as ei:
+            t2j.BinaryConv(conv.Options(DisallowUnknownField=True)).do(td, src)
+        assert ei.value.behavior == "ErrUnknownField"
+        t2j.BinaryConv(conv.Options()).do(td, src)
+        assert not compare(chk, T.flatten(td), [src], DISALLOW)
+        assert not compare(chk, T.flatten(td), [src], 0)
+    for name, src, want in (("String", struct.pack(">i", 5) + b"hello", b'"hello"'),
+                            ("I64", struct.pack(">q", 2**63 - 1), b"9223372036854775807")):
+        td = fns[name].response().struct.fields[0].type
+        assert t2j.BinaryConv(conv.Options()).do(td, src) == want

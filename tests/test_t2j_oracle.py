@@ -169,3 +169,65 @@ def test_response_base_skipped(chk):
     want = json.loads(js0)["BaseResp"]
     assert (br.StatusMessage, br.StatusCode) == (want["StatusMessage"], want["StatusCode"])
     assert (br.Extra or {}) == (want.get("Extra") or {})
+
+
+# ---- more of conv/t2j/conv_test.go's known answers, through the checker ----
+T2J_DISALLOW_UNKNOWN = 1 << 4
+
+
+def api_body_thrift():
+    """example3.ExampleApiBody{Code: 1, Code2: 2, InnerCode: {C1: 31, C2: 32,
+    C3: [{C1: 41, C2: 42}]}} as FastWriteNocopy writes it (id order; the
+    inner element's nil C3 is a default-requiredness list, written empty)."""
+    def inner(c1, c2, elems):
+        b = b"\x0a\x00\x01" + struct.pack(">q", c1) + b"\x06\x00\x02" + struct.pack(">h", c2)
+        return b + b"\x0f\x00\x03\x0c" + struct.pack(">i", len(elems)) + b"".join(elems) + b"\x00"
+    return (b"\x0a\x00\x01" + struct.pack(">q", 1) + b"\x06\x00\x02" + struct.pack(">h", 2) +
+            b"\x0c\x00\x03" + inner(31, 32, [inner(41, 42, [])]) + b"\x00")
+
+
+API_BODY_JSON = b'{"Code":1,"code":2,"InnerCode":{"C1":31,"code":32,"C3":[{"C1":41,"code":42,"C3":[]}]}}'
+
+
+def test_api_body(chk):
+    """TestAPIBody (conv/t2j/conv_test.go:288-308): api.body keys are not
+    JSON keys on this path; go.tag json names are."""
+    td = _example3_svc().functions()["ApiBodyMethod"].response().struct.fields[0].type
+    fl = T.flatten(td)
+    side = T.flatten_t2j(fl)
+    assert chk.t2j(fl, side, api_body_thrift(), T2J_ENABLE_VM) == (0, API_BODY_JSON)
+
+
+def _example3_resp_bin():
+    import os
+    from schemas import IDL_DIR
+    return open(os.path.join(os.path.dirname(IDL_DIR), "example3resp.bin"), "rb").read()
+
+
+@pytest.mark.parametrize("which", ["top", "nested"])
+def test_unknown_fields(chk, which):
+    """TestUnknowFields (conv/t2j/conv_test.go:472-518): example3resp.bin read
+    as PartialMethod's response (top) or request (nested) struct: ErrUnknownField
+    with DisallowUnknownField, no error without it."""
+    fn = _example3_svc().functions()["PartialMethod"]
+    td = (fn.response() if which == "top" else fn.request()).struct.fields[0].type
+    fl = T.flatten(td)
+    side = T.flatten_t2j(fl)
+    src = _example3_resp_bin()
+    r, _ = chk.t2j(fl, side, src, T2J_DISALLOW_UNKNOWN)
+    assert r & 0xFF == 2  # DG_T2J_E_UNKNOWN_FIELD
+    r, js = chk.t2j(fl, side, src, 0)
+    assert r == 0
+    import json
+    json.loads(js)
+
+
+def test_simple_args(chk):
+    """TestSimpleArgs (conv/t2j/conv_test.go:711-733): a string and an i64
+    response root."""
+    fns = _example3_svc().functions()
+    for name, src, want in (("String", struct.pack(">i", 5) + b"hello", b'"hello"'),
+                            ("I64", struct.pack(">q", 2**63 - 1), b"9223372036854775807")):
+        td = fns[name].response().struct.fields[0].type
+        fl = T.flatten(td)
+        assert chk.t2j(fl, T.flatten_t2j(fl), src, 0) == (0, want)
