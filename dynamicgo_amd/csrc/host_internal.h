@@ -39,7 +39,7 @@ struct Scratch {
     hipStream_t owner = nullptr;   /* the stream it was created for */
     hipStream_t last = nullptr;    /* stream of the last launch that used it */
     bool used = false;
-    hipEvent_t done = nullptr;     /* recorded after every launch that used it */
+    hipEvent_t done = nullptr;     /* recorded after every launch that used it (no system-scope fence: ordering only) */
     uint8_t *ws_fast = nullptr;
     uint64_t ws_fast_lanes = 0;
     uint64_t *d_deep_list = nullptr;

@@ -63,7 +63,15 @@ static int scratch_new(dg_ctx *c, hipStream_t owner, Scratch **out)
 {
     Scratch *x = new Scratch();
     x->owner = owner;
-    hipError_t e = hipEventCreateWithFlags(&x->done, hipEventDisableTiming);
+    /* `done` orders execution only: the host frees or overwrites a scratch
+     * buffer after it, and a launch on another stream that takes the scratch
+     * over waits for it. No host reads data through it, and a kernel's own
+     * dispatch fences already publish its writes to the kernels after it (as
+     * between the batch's kernels on one stream), so it carries no
+     * system-scope fence: that fence cost every batch a 5-6 us gap before the
+     * stream's next kernel (r8g trace; r8h/r8i: C2 in flight 336 -> 353 GB/s;
+     * a device-scope release instead gained nothing). */
+    hipError_t e = hipEventCreateWithFlags(&x->done, hipEventDisableTiming | hipEventDisableSystemFence);
     if (e == hipSuccess) e = hipMalloc(&x->d_counts, DG_NCOUNTS * 4);
     /* ordered before the owner stream's launches: a plain hipMemset runs on
      * the null stream, which a non-blocking stream (the aggregator's) does

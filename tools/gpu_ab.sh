@@ -22,6 +22,6 @@ rows=list(csv.DictReader(open(sys.argv[1])))
 print(sys.argv[2], sys.argv[3], " ".join("%s=%.2fus" % (r["Name"].split("(")[0].split("<")[0][-22:], float(r["AverageNs"])/1e3) for r in rows if "j2t" in r["Name"] or "t2j" in r["Name"]))' $O/${v}_${c}_$rep/run_kernel_stats.csv $v $c
   else
     DG_ALLOW_STALE=1 DG_LIB_PATH=dynamicgo_amd/$v.so timeout -k 10 300 python -u bench.py --config $c --no-cpu-baseline --no-e2e > $O/${v}_${c}_$rep.json 2> $O/${v}_${c}_$rep.err || { tail -5 $O/${v}_${c}_$rep.err; exit 1; }
-    python -c 'import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]);print(sys.argv[2],sys.argv[3],d["value"],d["roofline"]["kernel_ms"])' $O/${v}_${c}_$rep.json $v $c
+    python -c 'import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]);print(sys.argv[2],sys.argv[3],d["value"],d["ms_per_step"],d["config"].get("serial_gbs"),d["roofline"]["kernel_ms"])' $O/${v}_${c}_$rep.json $v $c
   fi
 done; done; done
