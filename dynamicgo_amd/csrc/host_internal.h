@@ -32,7 +32,7 @@ __attribute__((visibility("hidden"))) int set_err(int code, const char *fmt, ...
  * on `done`), which keeps the ordering rule true in every case. */
 constexpr int DG_MAX_SCRATCH = 40; /* an aggregator ring (<= AGG_RING_MAX = 24 streams) + the context's stream
                                     * + the in-flight side streams (<= 7) + the host pipeline's 3 */
-constexpr uint32_t DG_NCOUNTS = 16;
+constexpr uint32_t DG_NCOUNTS = 24;
 constexpr uint32_t DG_J2T_COUNTS_BYTES = 6 * 4;
 constexpr uint32_t DG_T2J_DEEP_COUNT = 8;
 struct Scratch {
@@ -51,8 +51,10 @@ struct Scratch {
      * pack: [6] arrivals, [7] departures of dg_pack_device_scan, [12] its
      *      slot-overflow count (MsgFrame::ovf_out) -- self-reset;
      * t2j: [8] deep-pass queue length, [9] long messages, [10] the wave
-     *      kernel's queue, [11] its bails (reset by a stream memset after the
-     *      t2j launch). */
+     *      kernel's queue, [11] its bails; launches alternate between this
+     *      set and [16..19] (t2j_set), and each launch's deep pass zeroes the
+     *      other set, the one the previous launch used (no memset per
+     *      launch). */
     uint32_t *d_counts = nullptr;
     uint32_t *d_bail_list = nullptr;
     uint64_t bail_cap = 0;
@@ -69,6 +71,7 @@ struct Scratch {
     uint64_t t2j_big_cap = 0;
     uint32_t *t2j_bail = nullptr;  /* t2j: the wave kernel's bails ([11] counts them) */
     uint64_t t2j_bail_cap = 0;
+    uint32_t t2j_set = 0;          /* t2j: the counter set of the next launch (0: [8..11], 1: [16..19]) */
     /* a second stream of this scratch's launches (created on first use): the
      * t2j wave kernel runs on it beside the lane pass (Knobs::t2j_overlap) */
     hipStream_t side = nullptr;

@@ -1230,7 +1230,8 @@ struct T2JParams {
     const dg_cb_entry *ans_tab; /* DG_T2J_HM: per message the host's writeHttpValue answers (or NULL) */
     const uint8_t *ans_bytes;
     uint32_t *deep_list;      /* messages nested beyond the LDS frames */
-    uint32_t *deep_count;     /* their number (reset by the host after the deep pass) */
+    uint32_t *deep_count;     /* their number */
+    uint32_t *reset_counts;   /* the deep pass zeroes these 4 counters: the set the previous launch used */
     uint8_t *ws;              /* deep pass: T2J_DEEP_DEPTH frames per lane */
     /* the wave path (t2j_wave.h): the lane pass lists messages longer than
      * big_min (when big_list is set) instead of converting them; list mode

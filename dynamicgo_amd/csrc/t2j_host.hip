@@ -28,7 +28,8 @@ static uint32_t t2j_spread(const dg_ctx *c, uint64_t max_len)
  * messages that may be long): the lane pass converts the short messages and
  * lists the long ones, the wave kernel converts those (t2j_wave.h), the lane
  * pass in list mode converts the wave kernel's bails. Then the deep pass over
- * what the lane passes queued, and the counter reset; the scratch's `done`
+ * what the lane passes queued (it also zeroes the counter set the previous
+ * launch used); the scratch's `done`
  * event after. */
 static int t2j_launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t *src, const uint64_t *in_off,
                       uint64_t n, uint64_t opts, uint8_t *out, const uint64_t *out_off, uint32_t *out_len,
@@ -45,7 +46,8 @@ static int t2j_launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
     if ((rc = grow_x(x, x->t2j_list, x->t2j_list_cap, n))) return rc;
     if (!c->ws_t2j) {
         HIPCHK(hipMalloc(&c->ws_t2j, T2J_DEEP_WS));
-        HIPCHK(hipEventCreateWithFlags(&c->ws_t2j_done, hipEventDisableTiming));
+        /* ordering only (the next deep pass on another stream): no system-scope fence */
+        HIPCHK(hipEventCreateWithFlags(&c->ws_t2j_done, hipEventDisableTiming | hipEventDisableSystemFence));
     }
     const uint64_t wmin = (uint64_t)c->knobs.t2j_wave_min;
     /* the root-level Go-side options run on the lane kernel only */
@@ -72,6 +74,9 @@ static int t2j_launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
          * pass on another stream waits for the previous one */
         if (c->ws_t2w_last && c->ws_t2w_last != ws) HIPCHK(hipStreamWaitEvent(ws, c->ws_t2w_done, 0));
     }
+    /* this launch's counter set; its deep pass zeroes the other one */
+    uint32_t *const cnt = x->d_counts + (x->t2j_set ? 16u : DG_T2J_DEEP_COUNT);
+    uint32_t *const cnt_next = x->d_counts + (x->t2j_set ? DG_T2J_DEEP_COUNT : 16u);
     T2JParams P;
     memset(&P, 0, sizeof P);
     P.root = root;
@@ -87,7 +92,8 @@ static int t2j_launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
     P.hdr = d->hdr;
     P.side = d->d_side;
     P.deep_list = x->t2j_list;
-    P.deep_count = x->d_counts + DG_T2J_DEEP_COUNT;
+    P.deep_count = cnt;
+    P.reset_counts = cnt_next;
     P.ws = c->ws_t2j;
     P.stats = c->d_stats;
     P.aux = (opts & DG_T2J_SKIP_RESP_BASE) ? aux : nullptr;
@@ -97,7 +103,7 @@ static int t2j_launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
     if (wave) {
         T2JParams P1 = P;
         P1.big_list = x->t2j_big;
-        P1.big_count = x->d_counts + DG_T2J_DEEP_COUNT + 1;
+        P1.big_count = cnt + 1;
         P1.big_min = wmin;
         if (ovl) {
             launch_t2j_route(n, s, P1); /* the long ones, by length */
@@ -110,10 +116,10 @@ static int t2j_launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
         if (e == hipSuccess) launch_t2j_pass(n, s, P1, 1); /* the short ones: full waves */
         T2WParams W;
         W.list = x->t2j_big;
-        W.count = x->d_counts + DG_T2J_DEEP_COUNT + 1;
-        W.queue = x->d_counts + DG_T2J_DEEP_COUNT + 2;
+        W.count = cnt + 1;
+        W.queue = cnt + 2;
         W.bail_list = x->t2j_bail;
-        W.bail_count = x->d_counts + DG_T2J_DEEP_COUNT + 3;
+        W.bail_count = cnt + 3;
         const uint32_t wblocks = (uint32_t)c->n_cu * T2W_BPC; /* the token regions are sized for it */
         W.tok = c->ws_t2w;
         W.side_len = (uint32_t)d->side_len;
@@ -129,7 +135,7 @@ static int t2j_launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
             e = hipGetLastError();
         }
         if (e == hipSuccess) {
-            if (!c->ws_t2w_done) e = hipEventCreateWithFlags(&c->ws_t2w_done, hipEventDisableTiming);
+            if (!c->ws_t2w_done) e = hipEventCreateWithFlags(&c->ws_t2w_done, hipEventDisableTiming | hipEventDisableSystemFence);
             if (e == hipSuccess) e = hipEventRecord(c->ws_t2w_done, ws);
             if (e == hipSuccess) c->ws_t2w_last = ws;
         }
@@ -151,7 +157,12 @@ static int t2j_launch(dg_ctx *c, const dg_desc *d, uint32_t root, const uint8_t 
     }
     if (e == hipSuccess) e = hipEventRecord(c->ws_t2j_done, s);
     if (e == hipSuccess) c->ws_t2j_last = s;
-    (void)hipMemsetAsync(x->d_counts + DG_T2J_DEEP_COUNT, 0, 16, s);
+    if (e == hipSuccess) {
+        x->t2j_set ^= 1u;
+    } else { /* the deep pass may not have run: both sets cleared */
+        (void)hipMemsetAsync(cnt, 0, 16, s);
+        (void)hipMemsetAsync(cnt_next, 0, 16, s);
+    }
     HIPCHK(hipEventRecord(x->done, s));
     x->used = true;
     x->last = s;

@@ -120,6 +120,7 @@ __global__ __launch_bounds__(T2J_BLOCK) void t2j_deep_kernel(T2JParams P)
 {
     const uint32_t cnt = *(volatile uint32_t *)P.deep_count;
     const uint32_t lane = blockIdx.x * T2J_BLOCK + threadIdx.x;
+    if (lane < 4 && P.reset_counts) P.reset_counts[lane] = 0; /* the next launch's counters */
     const auto D = desc_view<1>((const __attribute__((address_space(1))) uint8_t *)(const void *)P.blob, P.hdr);
     const T2JSide X = t2j_side(P.side);
     T2JFrame *fr = (T2JFrame *)(void *)(P.ws + (uint64_t)lane * T2J_DEEP_DEPTH * sizeof(T2JFrame));
