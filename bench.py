@@ -839,7 +839,10 @@ def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    # 100 steps: the timed region's fixed cost (the synchronize on each side,
+    # the first launch, the in-flight ramp) is ~40-100 us; C2 (r8m, one box):
+    # 348.8 / 380.7 / 401.7 GB/s at 20 / 50 / 100 steps of ~32 us
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -773,11 +773,13 @@ int dg_j2t_batch_device_inflight(dg_ctx *c, const dg_desc *d, uint32_t root, con
         hipStream_t x;
         hipEvent_t e;
         HIPCHK(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
-        HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence)); /* ordering only */
         c->side.push_back(x);
         c->side_ev.push_back(e);
     }
-    if (!c->fork_ev) HIPCHK(hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
+    /* fork / join events order the streams only (no host reads through them):
+     * no system-scope fence, like the scratch's `done` */
+    if (!c->fork_ev) HIPCHK(hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming | hipEventDisableSystemFence));
     if (used > 1) { /* fork: the side streams start after what `stream` holds */
         HIPCHK(hipEventRecord(c->fork_ev, s0));
         for (int j = 0; j < used - 1; j++) HIPCHK(hipStreamWaitEvent(c->side[j], c->fork_ev, 0));
