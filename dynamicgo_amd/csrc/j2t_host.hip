@@ -739,8 +739,11 @@ int dg_j2t_batch_device_ktime(dg_ctx *c, const dg_desc *d, uint32_t root, const 
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     std::vector<hipEvent_t> ev((size_t)iters * 4, nullptr);
     int rc = DG_OK;
+    /* timing events without the system-scope fence (HIP's flag for events
+     * that only measure): with it each mark added the fence's L2 writeback to
+     * the kernel before it (C2 flat kernel ~35.0 us against 33.1 under rocprof) */
     for (auto &e : ev)
-        if (hipEventCreate(&e) != hipSuccess) rc = set_err(DG_E_HIP, "hipEventCreate");
+        if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) rc = set_err(DG_E_HIP, "hipEventCreate");
     for (int k = 0; k < iters && !rc; k++) {
         c->kt = &ev[(size_t)k * 4];
         rc = launch(c, d, root, d_json, d_in_off, n, flags, d_out, d_out_off, d_out_len, d_ret, d_pending, s, max_len);
