@@ -1036,8 +1036,26 @@ def main(argv=None):
             t0 = time.perf_counter()
             cv.do(flat, m)
             t.append(time.perf_counter() - t0)
+        # the same call straight through the C ABI a cgo binding uses
+        # (dg_j2t_do, preallocated output), without the Python mirror's
+        # per-call array building
+        obuf = C.create_string_buffer(4 * len(m) + 256)
+        olen = C.c_size_t(0)
+        oret = C.c_uint64(0)
+        tc = []
+        for k in range(220):
+            t0 = time.perf_counter()
+            _lib.check(L.dg_j2t_do(ctx.h, dh, flat.root_type, m, len(m), flags, obuf, len(obuf), C.byref(olen),
+                                   C.byref(oret)))
+            if k >= 20:
+                tc.append(time.perf_counter() - t0)
+        if oret.value != 0 or obuf.raw[:olen.value] != cv.do(flat, m):
+            raise SystemExit("dg_j2t_do differs from BinaryConv.do")
         c1 = {"do_latency_us_median": round(float(np.median(t)) * 1e6, 1),
-              "note": "one message through dg_j2t_do (H2D, kernels, D2H, synchronous) from Python"}
+              "do_latency_c_abi_us_median": round(float(np.median(tc)) * 1e6, 1),
+              "note": "one message, host in -> host out, synchronous: BinaryConv.do (the Python mirror: "
+                      "dg_j2t_batch_host) and dg_j2t_do called directly through ctypes (the C ABI a cgo binding "
+                      "calls: one pinned upload, the kernels, the packing, one download)"}
 
     traffic = None
     tp = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
