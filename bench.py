@@ -405,14 +405,20 @@ def same_outputs(d_oo, d_ol, a, b) -> bool:
     tails are never written)."""
     import torch
     n = d_ol.numel()
-    total = int(d_oo[-1].item())
-    if n == 0 or total == 0:
+    if n == 0 or int(d_oo[-1].item()) == 0:
         return True
-    seg = torch.repeat_interleave(torch.arange(n, device=d_oo.device), d_oo[1:] - d_oo[:-1])
-    pos = torch.arange(total, device=d_oo.device) - d_oo[:-1][seg]
-    valid = pos < d_ol.to(torch.int64)[seg]
-    del seg, pos
-    return bool(torch.equal(a[:total][valid], b[:total][valid]))
+    step = 1 << 16  # messages per pass: the masks stay a few hundred MB at C5's slot sizes
+    for i in range(0, n, step):
+        j = min(n, i + step)
+        lo, hi = int(d_oo[i].item()), int(d_oo[j].item())
+        oo = d_oo[i:j + 1] - lo
+        seg = torch.repeat_interleave(torch.arange(j - i, device=d_oo.device), oo[1:] - oo[:-1])
+        pos = torch.arange(hi - lo, device=d_oo.device) - oo[:-1][seg]
+        valid = pos < d_ol[i:j].to(torch.int64)[seg]
+        del seg, pos
+        if not torch.equal(a[lo:hi][valid], b[lo:hi][valid]):
+            return False
+    return True
 
 
 # ---------------------------------------------------------------- t2j
