@@ -15,7 +15,9 @@ from dynamicgo_amd.thrift import flatten
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c2"
 fields = "--fields" in sys.argv  # a -DDG_FLPROF_F build: per field slot parse / write cycles
 td, msgs = {"c2": lambda: (W.simple_desc(), W.gen_flat_batch(random.Random(42), 65536)),
-            "c2s": lambda: (W.simple_desc(), W.gen_flat_batch_shuffled(random.Random(42), 65536))}[cfg]()
+            "c2s": lambda: (W.simple_desc(), W.gen_flat_batch_shuffled(random.Random(42), 65536)),
+            # one block alone (64 messages): the block's latency chain with nothing beside it
+            "c2one": lambda: (W.simple_desc(), W.gen_flat_batch(random.Random(42), 64))}[cfg]()
 n = len(msgs)
 flat = flatten(td)
 a, off = W.arena(msgs)
@@ -45,14 +47,14 @@ if "--plain" in sys.argv:  # any build: the time only (e.g. under rocprofv3 --pm
     sys.exit(0)
 if "--stages" in sys.argv:  # a -DDG_FLPROF_G build
     c = list(cnt)[2:8]
-    waves = n // 64 // 32 * 4
+    waves = max(1, n // 64 // 32) * 4
     print(f"{cfg}: {ms.value / reps * 1000:.1f} us/step (instrumented)")
     for k, nm in enumerate(["separators", "delimiters", "key", "value", "sizes", "after"]):
         print("  %-12s %8.0f cycles/wave" % (nm, c[k] / reps / waves))
     sys.exit(0)
 if fields:
     c = list(cnt)[2:14]
-    waves = n // 64 // 32 * 4
+    waves = max(1, n // 64 // 32) * 4
     print(f"{cfg}: {ms.value / reps * 1000:.1f} us/step (instrumented), ok={(d_ret.cpu().numpy() == 0).sum()}")
     for k in range(6):
         print("  field slot %d: parse %8.0f  write %8.0f cycles/wave" % (k, c[k] / reps / waves * 4, c[6 + k] / reps / waves * 4))
@@ -60,7 +62,7 @@ if fields:
 c = list(cnt)[2:10]
 names = ["stage+desc+barrier", "classify+scan", "record", "open/close+barrier 1", "parse", "barrier 2", "write+tasks",
          "chunks+barrier 4"]
-waves = n // 64 // 32 * 4  # 4 waves per 64-message block; 1 block in 32 sampled
+waves = max(1, n // 64 // 32) * 4  # 4 waves per 64-message block; 1 block in 32 sampled
 tot = sum(c)
 print(f"{cfg}: {ms.value / reps * 1000:.1f} us/step (instrumented), ok={(d_ret.cpu().numpy() == 0).sum()}")
 for k, nm in enumerate(names):
