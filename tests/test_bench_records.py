@@ -43,3 +43,26 @@ def test_cpu_baseline_cores_are_the_quota_bounded_ones(monkeypatch):
     monkeypatch.setattr(bench, "host_cpu_env", lambda: dict(real(), quota_cpus=2.0))
     cb2 = bench.cpu_baseline(fl, arena, off, 1, budget_s=0.05)
     assert cb2["cores"] == min(2, len(phys))
+
+
+def test_same_outputs_compares_slot_prefixes_in_passes():
+    """The in-flight check (bench.same_outputs): every message's slot prefix
+    of out_len bytes is compared, the slot tails are not, over more messages
+    than one pass takes (C5's 1M messages at depth 2 once ran its masks out
+    of memory)."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(5)
+    n = (1 << 16) * 2 + 123
+    lens = rng.integers(0, 40, n)
+    oo = np.zeros(n + 1, np.int64)
+    np.cumsum((lens + 64 + 7) // 8 * 8, out=oo[1:])
+    d_oo, d_ol = torch.from_numpy(oo), torch.from_numpy(lens.astype(np.int32))
+    a = torch.from_numpy(rng.integers(0, 256, int(oo[-1]) + 64, dtype=np.uint8))
+    b = a.clone()
+    assert bench.same_outputs(d_oo, d_ol, a, b)
+    k = n - 7
+    b[int(oo[k]) + int(lens[k]) + 3] ^= 1  # a slot tail: not compared
+    assert bench.same_outputs(d_oo, d_ol, a, b)
+    k = int(np.nonzero(lens[(1 << 16) + 5:])[0][0]) + (1 << 16) + 5  # a prefix byte in the second pass
+    b[int(oo[k])] ^= 1
+    assert not bench.same_outputs(d_oo, d_ol, a, b)
